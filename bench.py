@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CDSSM-300d training throughput (pairs/sec, whole job) + Recall@10.
+
+Config (BASELINE.json config 2): CDSSM with 2 x 150 conv filters
+(k = 3, 4 -> 300-d pooled) -> Dense 150, 30k hashed letter-trigram ids, query 45 /
+page 2000 tokens (reference ngram lengths, dssm_cnn_v2/config.py:88-91), J = 3 explicit
+negatives per query (reference), bf16 MFMA compute with fp32 master weights, per-GPU
+batch 4096 (weak scaling), cross-GPU in-batch negatives: every query is scored against
+ALL W * 4096 * (1 + J) page vectors of the step (all-gathered over RCCL).  Synthetic
+data: a device-resident pool of pre-featurized batches (no dataset/network available),
+random-init weights.  Each timed step = forward + backward + gradient all-reduce +
+Adam update.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
+
+Rank 0 prints ONE JSON line (driver contract).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (queries)")
+    ap.add_argument("--loss", default="cross_gpu", choices=["cross_gpu", "explicit", "in_batch"])
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
+                    help="torch = eager PyTorch-ROCm implementation of the same model (baseline stand-in)")
+    ap.add_argument("--recall", type=int, default=2048, help="held-out pairs for Recall@10 (0 = skip)")
+    ap.add_argument("--pool", type=int, default=4, help="pre-featurized batches kept in HBM")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.eval.retrieval import recall_at_k
+    from dnn_page_vectors_amd.models.cdssm import CDSSM, cdssm_flops_per_sample
+    from dnn_page_vectors_amd.ops._common import set_backend
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    info = pdist.init_distributed()
+    if a.backend == "torch":
+        set_backend("torch")
+    cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=a.batch, loss_mode=a.loss)
+    V = cfg.vocab_hash_size
+    dev = info.device
+    model = CDSSM(cfg, V)
+    trainer = Trainer(cfg, model, dev)
+
+    spec = spec_from_config(cfg, V, num_pages=16384)
+    data = SyntheticPairs(spec, dev, seed=1337 + info.rank)
+    pool = [data.batch(a.batch) for _ in range(max(1, a.pool))]
+    torch.cuda.synchronize()
+
+    def step(i):
+        q, d = pool[i % len(pool)]
+        return trainer.train_step(q, d)
+
+    for i in range(a.warmup):
+        m = step(i)
+    torch.cuda.synchronize()
+    pdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        m = step(a.warmup + i)
+    torch.cuda.synchronize()
+    pdist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    pdist.all_reduce_max_(t)
+    dt = float(t[0])
+    final_loss = float(m["loss"])
+
+    recall = None
+    if a.recall > 0:
+        qe, pe = data.eval_set(a.recall)
+        qv = model.encode(qe, "query")
+        pv = model.encode(pe, "doc")
+        recall = recall_at_k(qv, pv, torch.arange(a.recall, device=dev), k=10)
+
+    W = info.world_size
+    pairs = a.batch * W * a.steps
+    value = pairs / dt
+    flops = 3.0 * cdssm_flops_per_sample(cfg) * a.batch * W * a.steps / dt  # fwd + ~2x bwd (dense-equivalent)
+    if info.is_main:
+        out = {
+            "metric": "pairs/sec (whole node) + Recall@10, DSSM-300d",
+            "value": round(value, 1),
+            "unit": "pairs/s",
+            "n_gpus": W,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (device-resident pre-featurized Zipf trigram-id pages; random-init weights)",
+            "config": {"model": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
+                       "global_batch": a.batch * W, "seq_len": cfg.document_length,
+                       "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend},
+            "recall_at_10": None if recall is None else round(recall, 4),
+            "final_loss": round(final_loss, 4),
+            "dense_equiv_tflops": round(flops / 1e12, 1),
+        }
+        print(json.dumps(out), flush=True)
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+"""In-tree native build: HIP kernels (hipcc, gfx950) + C++ host runtime (g++).
+
+Outputs go to ``dnn_page_vectors_amd/lib/`` so they travel with the repo
+snapshot to the GPU box (``*.so`` is git-ignored, not gpurun-ignored).
+Rebuilds are incremental: each object is keyed by a hash of its source, the
+shared headers and the compile flags.
+
+    python -m dnn_page_vectors_amd._build          # build everything
+    python -m dnn_page_vectors_amd._build --hip    # kernels only
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Sequence
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+OBJ = os.path.join(PKG, "lib", "obj")
+
+HIP_LIB = os.path.join(LIB, "libpagevec_hip.so")
+RT_LIB = os.path.join(LIB, "libpagevec_rt.so")
+
+ARCH = os.environ.get("PAGEVEC_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-ffp-contract=fast"]
+RT_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-sign-compare"]
+
+
+def _digest(paths: Sequence[str], flags: Sequence[str]) -> str:
+    h = hashlib.sha1()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()[:16]
+
+
+def _headers(d: str) -> List[str]:
+    out = []
+    for root, _, files in os.walk(d):
+        for fn in sorted(files):
+            if fn.endswith((".h", ".hpp", ".cuh", ".inc")):
+                out.append(os.path.join(root, fn))
+    return sorted(out)
+
+
+def _sources(d: str, ext: str) -> List[str]:
+    if not os.path.isdir(d):
+        return []
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(ext))
+
+
+def _run(cmd: List[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build command failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+    if verbose and r.stdout.strip():
+        print(r.stdout)
+
+
+def _compile_all(srcs: List[str], compiler: str, flags: List[str], incdir: str, tag: str,
+                 jobs: int, verbose: bool) -> List[str]:
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _headers(incdir)
+    objs = []
+    todo = []
+    for s in srcs:
+        key = _digest([s] + hdrs, flags + [compiler])
+        o = os.path.join(OBJ, f"{tag}_{os.path.splitext(os.path.basename(s))[0]}_{key}.o")
+        objs.append(o)
+        if not os.path.exists(o):
+            todo.append((s, o))
+    def one(so):
+        s, o = so
+        tmp = o + ".tmp.o"
+        _run([compiler] + flags + ["-I", incdir, "-c", s, "-o", tmp], verbose)
+        os.replace(tmp, o)
+    if todo:
+        with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            list(ex.map(one, todo))
+    return objs
+
+
+def _link(objs: List[str], out: str, linker: List[str], verbose: bool) -> bool:
+    stamp = out + ".stamp"
+    key = hashlib.sha1("\n".join(objs).encode()).hexdigest()
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return False
+    tmp = out + ".tmp"
+    _run(linker + ["-shared", "-o", tmp] + objs, verbose)
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(key)
+    return True
+
+
+def build_runtime(verbose: bool = False, jobs: int = 4) -> str:
+    srcs = _sources(os.path.join(CSRC, "runtime"), ".cpp")
+    objs = _compile_all(srcs, CXX, RT_FLAGS, os.path.join(CSRC, "runtime"), "rt", jobs, verbose)
+    _link(objs, RT_LIB, [CXX, "-pthread"], verbose)
+    return RT_LIB
+
+
+def build_hip(verbose: bool = False, jobs: int = 4) -> str:
+    if not os.path.exists(HIPCC):
+        raise RuntimeError(f"hipcc not found at {HIPCC}")
+    srcs = _sources(os.path.join(CSRC, "kernels"), ".hip")
+    flags = list(HIP_FLAGS)
+    if os.environ.get("PAGEVEC_DEBUG_KERNELS"):
+        flags += ["-DPAGEVEC_DEBUG=1"]
+    objs = _compile_all(srcs, HIPCC, flags, os.path.join(CSRC, "kernels"), "hip", jobs, verbose)
+    _link(objs, HIP_LIB, [HIPCC, f"--offload-arch={ARCH}", "-fPIC"], verbose)
+    return HIP_LIB
+
+
+def build_all(verbose: bool = False, jobs: int = 0) -> None:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    build_runtime(verbose, jobs)
+    build_hip(verbose, jobs)
+
+
+def clean() -> None:
+    shutil.rmtree(LIB, ignore_errors=True)
+
+
+def main(argv: Sequence[str] = ()) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hip", action="store_true")
+    ap.add_argument("--rt", action="store_true")
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=0)
+    a = ap.parse_args(list(argv) or sys.argv[1:])
+    if a.clean:
+        clean()
+    jobs = a.jobs or min(8, os.cpu_count() or 4)
+    if a.hip or not a.rt:
+        if not a.hip:
+            build_runtime(a.verbose, jobs)
+        build_hip(a.verbose, jobs)
+    elif a.rt:
+        build_runtime(a.verbose, jobs)
+
+
+if __name__ == "__main__":
+    main()

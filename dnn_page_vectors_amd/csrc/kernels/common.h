@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 kernels (wave64, CDNA4 MFMA).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PV_API extern "C" __attribute__((visibility("default")))
+
+namespace pv {
+
+constexpr int WAVE = 64;
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 bf16)
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16;  // 32x32 accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) {
+  return __uint_as_float(((unsigned)h) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (NaN stays NaN via the quiet bit).
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+// lowbias32 finaliser — the counter-based RNG shared with ops/reference.py.
+__host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ unsigned dropout_row_hash(unsigned seed, unsigned row) {
+  return mix32(seed ^ mix32(row));
+}
+
+// Keep-bits for columns 4g..4g+3 of a row (byte b of the group hash >= thr).
+__device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
+  return mix32(hrow + g * 0x9E3779B9u);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5 T1).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  int q = nwg / nx, r = nwg % nx;
+  int x = bid % nx, i = bid / nx;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+}  // namespace pv
+
+#define PV_LAUNCH_CHECK() \
+  do {                    \
+    hipError_t e__ = hipGetLastError(); \
+    if (e__ != hipSuccess) return (int)e__; \
+  } while (0)

@@ -1,0 +1,359 @@
+// K1+K2+K3: fused embedding gather -> dropout -> Conv1D(k=3,4; 150 filters each, valid)
+//           -> global max-pool over time (+argmax) -> bias -> ReLU.
+//
+// Reference op chain: dssm_cnn_v2/cnn_dssm_th.py:86-109 (Convolution1D + MaxPooling1D
+// + Flatten + concat) preceded by Embedding + Dropout(0.25) (:111-134).
+//
+// MI355X design (gfx950, wave64, v_mfma_f32_16x16x32_bf16):
+//  * Implicit GEMM with rows = window start t, cols = filters, K = k*EP where each
+//    embedding row is stored with a padded stride EP=104 (cols 100..103 are zero in
+//    the bf16 table copy AND in the packed weights), so window t is the *contiguous*
+//    LDS span X[t*EP, (t+k)*EP): no im2col, and the A fragment of K-step s is one
+//    16-byte-aligned ds_read_b128 at byte 208*t + 64*s + 16*(lane>>4).  Both widths
+//    share the A fragments of steps 0..9; k=4 adds steps 10..12.
+//  * All 2 x 150 filters (padded to 2 x 160 = 20 tiles of 16 columns) live in
+//    REGISTERS for the whole persistent workgroup: 4 waves (one per SIMD) own
+//    {3 k3 + 2 k4} or {2 k3 + 3 k4} tiles => 56/59 MFMAs per 16-row block per wave
+//    (97.5% balance).  Weights are loaded once per workgroup, not per sample.
+//  * Conv activations never leave registers: each lane keeps a running max and the
+//    argmax row for its 4 accumulator rows; the cross-lane reduction happens once per
+//    sample.  ReLU(max + bias) == max(ReLU(conv + bias)) because ReLU is monotone.
+//  * Dropout: counter-based hash of (seed, row, column) applied while staging the
+//    gathered rows into LDS (mask only, exact in bf16); the 1/(1-p) scale is applied
+//    to the pooled maximum (max(s*y) = s*max(y), s > 0).  The backward regenerates
+//    the same mask at the argmax windows only.
+//  * Staging is register-prefetched one chunk ahead (T14: issue loads before the
+//    MFMA phase, write LDS after the barrier) and token ids two chunks ahead, so the
+//    id->row dependent loads never sit on the critical path.
+#include "common.h"
+
+namespace pv {
+namespace convpool {
+
+constexpr int EP = 104;            // padded embedding stride (elements)
+constexpr int ROWB = EP * 2;       // bytes per LDS row (208 = 13 * 16)
+constexpr int PIECES = ROWB / 16;  // 16-byte pieces per row
+constexpr int S3 = 10;             // K-steps of 32 for k=3 (K = 312 -> 320)
+constexpr int S4 = 13;             // K-steps of 32 for k=4 (K = 416)
+constexpr int NT = 10;             // 16-column tiles per width (150 -> 160 filters)
+constexpr int FW = 150;            // real filters per width
+constexpr int R = 64;              // window rows per chunk
+constexpr int CROWS = R + 3;       // LDS rows per chunk
+constexpr int NTHREADS = 256;
+constexpr int PPT = (CROWS * PIECES + NTHREADS - 1) / NTHREADS;  // pieces per thread (4)
+constexpr int IDS_PT = (CROWS + NTHREADS - 1) / NTHREADS;        // ids per thread (1)
+
+struct Params {
+  const int* ids;              // (N, L)
+  const unsigned short* table; // (V, EP) bf16
+  const bf16x8* wpack;         // [tile][step][lane] fragments
+  const float* bias;           // (2*FW)
+  float* pooled;               // (N, 2*FW)
+  int* argmax;                 // (N, 2*FW)
+  int N, L, V;
+  unsigned seed, row_offset;
+  int thr;                     // dropout byte threshold (0 = off)
+  int token_mode;              // 1: one keep decision per row
+  float scale;                 // 1/(1-p)
+};
+
+// fragment base index of tile T in wpack (tiles 0..9 k3 with S3 steps, 10..19 k4 with S4)
+__device__ __forceinline__ int tile_base(int T) {
+  return T < NT ? T * S3 : NT * S3 + (T - NT) * S4;
+}
+
+struct Cursor {
+  int n, c, nchunks;
+};
+
+__device__ __forceinline__ void advance(Cursor& cu) {
+  if (++cu.c >= cu.nchunks) {
+    cu.c = 0;
+    cu.n += gridDim.x;
+  }
+}
+
+// Load the token ids of chunk (n,c) row `r` for this thread.
+__device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int (&tok)[IDS_PT]) {
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) {
+    int r = threadIdx.x + i * NTHREADS;
+    int t = cu.c * R + r;
+    tok[i] = (cu.n < p.N && r < CROWS && t < p.L) ? p.ids[(size_t)cu.n * p.L + t] : -1;
+  }
+}
+
+// Issue the 16-byte table loads for this thread's pieces of chunk (n,c).
+// tok_of_row(r) reads another thread's id through LDS scratch (ids_lds).
+__device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u32x4 (&v)[PPT]) {
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    int q = threadIdx.x + i * NTHREADS;
+    int r = q / PIECES, pc = q - r * PIECES;
+    int tok = (q < CROWS * PIECES) ? ids_lds[r] : -1;
+    if (tok >= 0 && tok < p.V) {
+      v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)tok * EP + pc * 8);
+    } else {
+      v[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned keep_bits_mask(unsigned h, int thr) {
+  // 2 bf16 lanes per dword: returns AND-mask for the dword pair (bytes b0,b1 of h)
+  unsigned m = 0;
+  if ((int)(h & 0xFF) >= thr) m |= 0x0000FFFFu;
+  if ((int)((h >> 8) & 0xFF) >= thr) m |= 0xFFFF0000u;
+  return m;
+}
+
+// Apply dropout to the staged pieces and write them into the LDS chunk buffer.
+__device__ __forceinline__ void store_rows(const Params& p, const Cursor& cu, char* xl, u32x4 (&v)[PPT]) {
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    int q = threadIdx.x + i * NTHREADS;
+    if (q < CROWS * PIECES) {
+      int r = q / PIECES, pc = q - r * PIECES;
+      u32x4 x = v[i];
+      if (p.thr > 0) {
+        unsigned row = p.row_offset + (unsigned)(cu.n * p.L + cu.c * R + r);
+        unsigned hr = dropout_row_hash(p.seed, row);
+        if (p.token_mode) {
+          unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
+          x = x & u32x4{m, m, m, m};
+        } else {
+          unsigned h0 = dropout_group_hash(hr, 2 * pc), h1 = dropout_group_hash(hr, 2 * pc + 1);
+          x.x &= keep_bits_mask(h0, p.thr);
+          x.y &= keep_bits_mask(h0 >> 16, p.thr);
+          x.z &= keep_bits_mask(h1, p.thr);
+          x.w &= keep_bits_mask(h1 >> 16, p.thr);
+        }
+      }
+      *reinterpret_cast<u32x4*>(xl + r * ROWB + pc * 16) = x;
+    }
+  }
+}
+
+template <int N3, int N4>
+__device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base, char* xl, int* ids_lds) {
+  const int lane = threadIdx.x & 63;
+  // ---- weights for this wave's tiles: resident for the whole workgroup lifetime
+  bf16x8 w3[N3][S3];
+  bf16x8 w4[N4][S4];
+#pragma unroll
+  for (int i = 0; i < N3; ++i)
+#pragma unroll
+    for (int s = 0; s < S3; ++s) w3[i][s] = p.wpack[(tile_base(t3base + i) + s) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < N4; ++i)
+#pragma unroll
+    for (int s = 0; s < S4; ++s) w4[i][s] = p.wpack[(tile_base(NT + t4base + i) + s) * 64 + lane];
+
+  const int nchunks = (p.L - 3 + 1 + R - 1) / R;  // covers windows 0..L-3 (k=3)
+  Cursor cur{(int)blockIdx.x, 0, nchunks};
+  Cursor nxt = cur;
+  advance(nxt);
+  Cursor nxt2 = nxt;
+  advance(nxt2);
+
+  int tok[IDS_PT];
+  u32x4 stage[PPT];
+  // prologue: ids of chunk 0 -> LDS, rows of chunk 0 -> regs, ids of chunk 1 -> regs
+  load_ids(p, cur, tok);
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) {
+    int r = threadIdx.x + i * NTHREADS;
+    if (r < CROWS) ids_lds[r] = tok[i];
+  }
+  __syncthreads();
+  load_rows(p, ids_lds, stage);
+  load_ids(p, nxt, tok);
+
+  const int nw3 = p.L - 2, nw4 = p.L - 3;  // valid windows per width
+  f32x4 m3[N3], m4[N4];
+  int a3[N3][4], a4[N4][4];
+  auto reset_state = [&]() {
+#pragma unroll
+    for (int i = 0; i < N3; ++i) {
+      m3[i] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a3[i][r] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < N4; ++i) {
+      m4[i] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a4[i][r] = 0;
+    }
+  };
+  reset_state();
+  const int rsub = lane & 15, kq = lane >> 4;
+
+  while (cur.n < p.N) {
+    __syncthreads();  // previous chunk's LDS reads are complete
+    store_rows(p, cur, xl, stage);
+#pragma unroll
+    for (int i = 0; i < IDS_PT; ++i) {
+      int r = threadIdx.x + i * NTHREADS;
+      if (r < CROWS) ids_lds[CROWS + r] = tok[i];  // ids of `nxt` into the second id slot
+    }
+    __syncthreads();
+    // prefetch: rows of nxt (ids already in LDS slot 2), ids of nxt2
+    load_rows(p, ids_lds + CROWS, stage);
+    load_ids(p, nxt2, tok);
+
+    // ---- MFMA phase over the 4 row blocks of this chunk
+    const int tc = cur.c * R;
+#pragma unroll 1
+    for (int blk = 0; blk < R / 16; ++blk) {
+      const int t0 = tc + blk * 16;
+      if (t0 >= nw3) break;
+      f32x4 c3[N3], c4[N4];
+#pragma unroll
+      for (int i = 0; i < N3; ++i) c3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* abase = xl + (blk * 16 + rsub) * ROWB + kq * 16;
+      bf16x8 anext = *reinterpret_cast<const bf16x8*>(abase);
+#pragma unroll
+      for (int s = 0; s < S4; ++s) {
+        bf16x8 a = anext;  // software-pipelined A fragment (one K-step ahead)
+        if (s + 1 < S4) anext = *reinterpret_cast<const bf16x8*>(abase + (s + 1) * 64);
+        if (s < S3) {
+#pragma unroll
+          for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
+      }
+      // running max / argmax; rows of this lane: t0 + 4*kq + r
+      const int rowb = t0 + 4 * kq;
+      const bool full = (t0 + 16 <= nw4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rowb + r;
+        const bool v3 = full || row < nw3, v4 = full || row < nw4;
+#pragma unroll
+        for (int i = 0; i < N3; ++i) {
+          float x = c3[i][r];
+          bool gt = v3 && x > m3[i][r];
+          m3[i][r] = gt ? x : m3[i][r];
+          a3[i][r] = gt ? row : a3[i][r];
+        }
+#pragma unroll
+        for (int i = 0; i < N4; ++i) {
+          float x = c4[i][r];
+          bool gt = v4 && x > m4[i][r];
+          m4[i][r] = gt ? x : m4[i][r];
+          a4[i][r] = gt ? row : a4[i][r];
+        }
+      }
+    }
+
+    // ---- sample epilogue: reduce over 4 regs and the 4 lane groups, write out
+    if (cur.c == cur.nchunks - 1) {
+      auto finish = [&](f32x4& m, int (&a)[4], int colbase) {
+        float bv = m[0];
+        int bi = a[0];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          bool take = m[r] > bv || (m[r] == bv && a[r] < bi);
+          bv = take ? m[r] : bv;
+          bi = take ? a[r] : bi;
+        }
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+          float ov = __shfl_xor(bv, o, 64);
+          int oi = __shfl_xor(bi, o, 64);
+          bool take = ov > bv || (ov == bv && oi < bi);
+          bv = take ? ov : bv;
+          bi = take ? oi : bi;
+        }
+        int col = colbase + rsub;  // filter index within width
+        if (kq == 0 && (col % 160) < FW) {
+          int f = (col / 160) * FW + (col % 160);
+          float y = bv * p.scale + p.bias[f];
+          p.pooled[(size_t)cur.n * (2 * FW) + f] = y > 0.f ? y : 0.f;
+          p.argmax[(size_t)cur.n * (2 * FW) + f] = bi;
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < N3; ++i) finish(m3[i], a3[i], (t3base + i) * 16);
+#pragma unroll
+      for (int i = 0; i < N4; ++i) finish(m4[i], a4[i], 160 + (t4base + i) * 16);
+      reset_state();
+    }
+    cur = nxt;
+    nxt = nxt2;
+    advance(nxt2);
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS, 1) void conv_pool_fwd_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[CROWS * ROWB + 2 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave == 0) run_wave<3, 2>(p, 0, 0, xl, ids_lds);
+  else if (wave == 1) run_wave<3, 2>(p, 3, 2, xl, ids_lds);
+  else if (wave == 2) run_wave<2, 3>(p, 6, 4, xl, ids_lds);
+  else run_wave<2, 3>(p, 8, 7, xl, ids_lds);
+}
+
+}  // namespace convpool
+}  // namespace pv
+
+using namespace pv;
+
+// Pack conv weights (fp32, [F][k][E] per width) into MFMA B fragments (bf16).
+// w3: (150,3,E) ; w4: (150,4,E). out: 20 tiles' fragments (NT*S3 + NT*S4) * 64 lanes * 8.
+__global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E, bf16x8* out) {
+  using namespace pv::convpool;
+  int frag = blockIdx.x;  // fragment index
+  int lane = threadIdx.x;
+  int T, s;
+  if (frag < NT * S3) { T = frag / S3; s = frag % S3; }
+  else { T = NT + (frag - NT * S3) / S4; s = (frag - NT * S3) % S4; }
+  int k = (T < NT) ? 3 : 4;
+  const float* w = (T < NT) ? w3 : w4;
+  int col = (T % NT) * 16 + (lane & 15);
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int kk = s * 32 + (lane >> 4) * 8 + j;  // window element
+    int jj = kk / EP, e = kk % EP;
+    float x = 0.f;
+    if (col < FW && jj < k && e < E) x = w[((size_t)col * k + jj) * E + e];
+    v[j] = (short)f32_to_bf16(x);
+  }
+  out[(size_t)frag * 64 + lane] = v;
+}
+
+PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* out, void* stream) {
+  using namespace pv::convpool;
+  if (E > EP) return -1;
+  int nfrag = NT * S3 + NT * S4;
+  hipLaunchKernelGGL(pack_conv_weights_kernel, dim3(nfrag), dim3(64), 0, (hipStream_t)stream, w3, w4, E,
+                     (bf16x8*)out);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_conv_packed_size() {
+  using namespace pv::convpool;
+  return (NT * S3 + NT * S4) * 64 * 8;  // bf16 elements
+}
+
+PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack, const float* bias,
+                            float* pooled, int* argmax, int N, int L, int V, unsigned seed, unsigned row_offset,
+                            int thr, int token_mode, float scale, int grid, void* stream) {
+  using namespace pv::convpool;
+  if (L < 4 || N <= 0) return -1;
+  Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
+           seed, row_offset, thr, token_mode, scale};
+  if (grid <= 0) grid = 256;
+  if (grid > N) grid = N;
+  hipLaunchKernelGGL(conv_pool_fwd_kernel, dim3(grid), dim3(NTHREADS), 0, (hipStream_t)stream, p);
+  PV_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,140 @@
+// K8: fused flat-buffer Adam + helper elementwise kernels.
+//
+// Reference optimizer: model.compile(optimizer="adam") (cnn_dssm_th.py:182) = Keras-1
+// Adam(lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-8):
+//   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
+//   p   -= lr_t * m / (sqrt(v) + eps)
+// All parameters of a model live in ONE fp32 flat buffer (params / grads / m / v are
+// parallel flat buffers), so the whole update is a single vectorised streaming launch
+// (7 x 4 B per parameter) and the DP all-reduce works on the same flat gradient buffer.
+// The same launch can emit a bf16 shadow copy of selected ranges (e.g. the embedding
+// tables the fused conv kernel gathers from), with a row-padded layout.
+#include "common.h"
+
+namespace pv {
+namespace optim {
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
+                                                   float b1, float b2, float eps, float wd, int torch_style,
+                                                   float bc2_sqrt_inv, const float* __restrict__ skip) {
+  if (skip && *skip != 0.f) return;  // non-finite guard: skip the whole step
+  long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x);
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long n4 = n / 4;
+  for (long i = i4; i < n4; i += stride) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gg[k] + wd * pp[k];
+      mm[k] = b1 * mm[k] + (1.f - b1) * gk;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
+      float den = torch_style ? (sqrtf(vv[k]) * bc2_sqrt_inv + eps) : (sqrtf(vv[k]) + eps);
+      pp[k] -= lr_t * mm[k] / den;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pp;
+    reinterpret_cast<f32x4*>(m)[i] = mm;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  for (long i = n4 * 4 + i4; i < n; i += stride) {
+    float gk = g[i] + wd * p[i];
+    m[i] = b1 * m[i] + (1.f - b1) * gk;
+    v[i] = b2 * v[i] + (1.f - b2) * gk * gk;
+    float den = torch_style ? (sqrtf(v[i]) * bc2_sqrt_inv + eps) : (sqrtf(v[i]) + eps);
+    p[i] -= lr_t * m[i] / den;
+  }
+}
+
+// fp32 (rows, cols) -> bf16 (rows, ldo) with zero padding of columns cols..ldo-1
+__global__ void cast_pad_bf16_kernel(const float* __restrict__ in, unsigned short* __restrict__ out, long rows, int cols,
+                                     int ldo) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  long total = rows * ldo;
+  for (; i < total; i += stride) {
+    long r = i / ldo;
+    int c = (int)(i - r * ldo);
+    out[i] = c < cols ? f32_to_bf16(in[r * cols + c]) : (unsigned short)0;
+  }
+}
+
+// sum of squares + non-finite flag over a flat buffer (block partials -> atomics)
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ out2) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  float s = 0.f, bad = 0.f;
+  for (; i < n; i += stride) {
+    float v = x[i];
+    if (!isfinite(v)) bad = 1.f;
+    else s += v * v;
+  }
+  s = wave_sum(s);
+  bad = wave_max(bad);
+  __shared__ float ws[4], wb[4];
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { ws[w] = s; wb[w] = bad; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = ws[0] + ws[1] + ws[2] + ws[3];
+    float b = fmaxf(fmaxf(wb[0], wb[1]), fmaxf(wb[2], wb[3]));
+    atomicAdd(&out2[0], t);
+    if (b != 0.f) atomicExch(&out2[1], 1.f);
+  }
+}
+
+__global__ void scale_kernel(float* __restrict__ x, long n, float s) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) x[i] *= s;
+}
+
+}  // namespace optim
+}  // namespace pv
+
+using namespace pv;
+
+static unsigned grid_for(long n, int per_thread) {
+  long b = (n / per_thread + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int step, float lr, float b1, float b2,
+                   float eps, float wd, int torch_style, const float* skip, void* stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+  float lr_t, bc2i = 1.f;
+  if (torch_style) {
+    lr_t = (float)(lr / bc1);
+    bc2i = (float)(1.0 / sqrt(bc2));
+  } else {
+    lr_t = (float)(lr * sqrt(bc2) / bc1);
+  }
+  hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_cast_pad_bf16(const float* in, void* out, long rows, int cols, int ldo, void* stream) {
+  hipLaunchKernelGGL(pv::optim::cast_pad_bf16_kernel, dim3(grid_for(rows * ldo, 4)), dim3(256), 0,
+                     (hipStream_t)stream, in, (unsigned short*)out, rows, cols, ldo);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_sumsq(const float* x, long n, float* out2, void* stream) {
+  hipLaunchKernelGGL(pv::optim::sumsq_kernel, dim3(grid_for(n, 8)), dim3(256), 0, (hipStream_t)stream, x, n, out2);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_scale(float* x, long n, float s, void* stream) {
+  hipLaunchKernelGGL(pv::optim::scale_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, x, n, s);
+  PV_LAUNCH_CHECK();
+  return 0;
+}

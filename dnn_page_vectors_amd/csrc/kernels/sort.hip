@@ -1,0 +1,20 @@
+// Stable LSD radix sort of (uint32 key, uint32 value) pairs on the device (rocPRIM via hipCUB).
+// Used to bucket sparse-gradient entries by destination row (deterministic order within
+// a bucket = emission order, so the segment sums are reproducible run to run).
+#include <hipcub/hipcub.hpp>
+#include "common.h"
+
+PV_API long pv_sort_pairs_temp_bytes(long n, int end_bit) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
+                                     (const unsigned*)nullptr, (unsigned*)nullptr, (int)n, 0, end_bit);
+  return (long)bytes;
+}
+
+PV_API int pv_sort_pairs_u32(void* temp, long temp_bytes, const unsigned* keys_in, unsigned* keys_out,
+                             const unsigned* vals_in, unsigned* vals_out, long n, int end_bit, void* stream) {
+  size_t bytes = (size_t)temp_bytes;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0,
+                                                    end_bit, (hipStream_t)stream);
+  return (int)e;
+}

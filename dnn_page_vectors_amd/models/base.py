@@ -1,0 +1,91 @@
+"""Two-tower model base class.
+
+Every model maps token ids to vectors with a *query tower* and a *document tower*
+(reference: ``query_model = model(Lq)``, ``doc_model = model(Ld)``, the doc tower
+shared by the positive and the J negatives, dssm_cnn_v2/cnn_dssm_th.py:147-156).
+
+Subclasses implement ``tower_forward(tower, ids, training, seed)``.  The base
+class provides ``forward`` (raw tower outputs for a training batch), ``encode``
+(L2-normalised vectors, no dropout; the page-vector extraction API the reference
+never had — its only pattern is reading weights, old_scripts/simple_rnn.py:51) and
+the compute-cache refresh hook used after optimizer steps.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops import dense as dops
+
+_GENERATION = [0]
+
+
+def bump_generation() -> None:
+    """Invalidate derived compute copies (bf16 tables, packed weights) of all models."""
+    _GENERATION[0] += 1
+
+
+class TwoTowerModel(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        self._cache_gen = -1
+        self._cache: Dict[str, object] = {}
+
+    # ---- to implement ----------------------------------------------------------
+    def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int,
+                      slot: int = 0) -> torch.Tensor:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    @property
+    def out_dim(self) -> int:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def build_cache(self) -> Dict[str, object]:
+        """Derived low-precision copies of the parameters used by the fused kernels."""
+        return {}
+
+    # ---- shared ------------------------------------------------------------------
+    def compute_cache(self) -> Dict[str, object]:
+        if self._cache_gen != _GENERATION[0] or not self._cache:
+            with torch.no_grad():
+                self._cache = self.build_cache()
+            self._cache_gen = _GENERATION[0]
+        return self._cache
+
+    def forward(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """q_ids (B, Lq); d_ids (B, S, Ld) with S = 1+J docs per query (positive first).
+
+        Returns raw (unnormalised) q (B, D) and d (B, S, D).
+        """
+        B, S, Ld = d_ids.shape
+        training = self.training
+        q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
+        if getattr(self.cfg, "share_doc_tower", True):
+            d = self.tower_forward("doc", d_ids.reshape(B * S, Ld), training, seed * 2 + 2).view(B, S, -1)
+        else:  # v1: independent towers per document slot (dssm_cnn/cnn_dssm.py:160-164)
+            d = torch.stack([self.tower_forward("doc", d_ids[:, s], training, seed * 2 + 2 + 1000 * s, slot=s)
+                             for s in range(S)], dim=1)
+        return q, d
+
+    @torch.no_grad()
+    def encode(self, ids: torch.Tensor, tower: str = "doc", batch_size: int = 4096,
+               normalize: bool = True) -> torch.Tensor:
+        """Vectors for ``ids`` (N, L) from one tower, evaluated without dropout."""
+        was = self.training
+        self.eval()
+        outs = []
+        try:
+            for i in range(0, ids.shape[0], batch_size):
+                v = self.tower_forward(tower, ids[i:i + batch_size], False, 0)
+                outs.append(dops.l2_normalize(v) if normalize else v)
+        finally:
+            self.train(was)
+        return torch.cat(outs, 0) if outs else torch.empty(0, self.out_dim, device=ids.device)
+
+    def architecture(self) -> Dict[str, object]:
+        """JSON-able description (the cnn_dssm_model_only.json analogue)."""
+        return {"class": type(self).__name__, "config": self.cfg.to_dict(),
+                "params": {n: list(p.shape) for n, p in self.named_parameters()}}

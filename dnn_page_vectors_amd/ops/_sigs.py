@@ -1,0 +1,49 @@
+"""ctypes prototypes of the HIP launcher ABI (csrc/kernels/*.hip).
+
+Codes: p = pointer, i = int32, u = uint32, l = int64, f = float32.
+Every launcher returns an int status (0 = ok, >0 hipError_t, <0 argument error).
+"""
+import ctypes
+
+_T = {"p": ctypes.c_void_p, "i": ctypes.c_int, "u": ctypes.c_uint, "l": ctypes.c_long, "f": ctypes.c_float}
+
+SIGS = {
+    # conv_pool_fwd.hip
+    "pv_conv_pack_weights": "ppipp",
+    "pv_conv_packed_size": "",
+    "pv_conv_pool_fwd": "pppppp" "iii" "uu" "ii" "f" "i" "p",
+    # conv_pool_bwd.hip
+    "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "uuiif" "p",
+    "pv_conv_pool_bwd_emit": "pppp" "ppppp" "iii" "p",
+    "pv_conv_pool_bwd_reduce": "ppppp" "ppp" "lii" "uuiif" "p",
+    # sort.hip
+    "pv_sort_pairs_temp_bytes": "li",
+    "pv_sort_pairs_u32": "plpppp" "li" "p",
+    # dense.hip
+    "pv_linear_act": "pipippp" "iiiiii" "p",
+    "pv_l2norm_fwd": "pppp" "iii" "p",
+    "pv_l2norm_bwd": "ppppp" "ii" "p",
+    "pv_act_bwd": "ppp" "li" "p",
+    # loss.hip
+    "pv_dssm_explicit": "pppppp" "iii" "ffi" "p",
+    "pv_ib_fwd": "ppp" "iii" "fi" "p",
+    "pv_ib_bwd": "ppppp" "iii" "fii" "p",
+    "pv_ib_pos": "ppppppp" "ii" "fi" "p",
+    "pv_transpose_bf16": "pp" "ii" "p",
+    # optim.hip
+    "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
+    "pv_cast_pad_bf16": "pp" "lii" "p",
+    "pv_sumsq": "p" "l" "p" "p",
+    "pv_scale": "p" "lf" "p",
+}
+
+_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long}
+
+
+def declare(lib) -> None:
+    for name, codes in SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = [_T[c] for c in codes]
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)

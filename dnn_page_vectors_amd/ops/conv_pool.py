@@ -1,0 +1,150 @@
+"""Fused embedding-gather -> dropout -> Conv1D(3,4) -> max-pool -> ReLU (the CDSSM tower body).
+
+GPU: ``csrc/kernels/conv_pool_fwd.hip`` (forward, MFMA, weights register-resident)
+and ``conv_pool_bwd.hip`` + ``sort.hip`` (sparse argmax backward).  CPU:
+``ops/reference.py`` (identical semantics incl. the counter-based dropout mask).
+
+Reference layers: Embedding -> Dropout(0.25) -> Graph{Convolution1D(150, k, relu) ->
+MaxPooling1D(L-k+1) -> Flatten} x k in (3,4) -> concat (dssm_cnn_v2/cnn_dssm_th.py:83-134).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import reference as ref
+from ._common import P, check, lib, need, stream, use_hip
+
+EP = 104          # padded embedding row stride of the bf16 table copy (kernel constant)
+FW = 150          # filters per width the fast kernel is built for
+WIDTHS = (3, 4)
+
+
+def fast_path_supported(E: int, widths, num_filters: int) -> bool:
+    return tuple(widths) == WIDTHS and num_filters == FW and E <= EP
+
+
+def table_bf16(table: torch.Tensor) -> torch.Tensor:
+    """fp32 (V, E) -> bf16 (V, EP) with zero padding (the layout the kernels gather from)."""
+    V, E = table.shape
+    out = torch.empty(V, EP, dtype=torch.bfloat16, device=table.device)
+    check(lib().pv_cast_pad_bf16(P(table.contiguous()), P(out), V, E, EP, stream(table.device)), "pv_cast_pad_bf16")
+    return out
+
+
+def pack_weights(w3: torch.Tensor, w4: torch.Tensor) -> torch.Tensor:
+    """(150,3,E), (150,4,E) fp32 -> MFMA B-fragment order bf16 (see pack_conv_weights_kernel)."""
+    E = w3.shape[2]
+    n = lib().pv_conv_packed_size()
+    out = torch.empty(n, dtype=torch.bfloat16, device=w3.device)
+    check(lib().pv_conv_pack_weights(P(w3.contiguous()), P(w4.contiguous()), E, P(out), stream(w3.device)),
+          "pv_conv_pack_weights")
+    return out
+
+
+def _dropout_args(p: float, training: bool, mode: str) -> Tuple[int, int, float]:
+    if not training or p <= 0.0 or mode == "none":
+        return 0, 0, 1.0
+    thr = ref.dropout_threshold(p)
+    return thr, 1 if mode == "token" else 0, 256.0 / (256.0 - thr)
+
+
+_grid_cache = {}
+
+
+def _grid(device: torch.device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _grid_cache:
+        _grid_cache[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _grid_cache[idx]
+
+
+class _ConvPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, table, w3, w4, bias, tbl16, wpack, p, seed, row_offset, training, mode):
+        ids = need(ids, torch.int32, "ids", 2)
+        N, L = ids.shape
+        V, E = table.shape
+        if L < 4:
+            raise ValueError("sequence length must be >= 4 for filter widths (3,4)")
+        thr, tok, scale = _dropout_args(p, training, mode)
+        pooled = torch.empty(N, 2 * FW, dtype=torch.float32, device=ids.device)
+        argmax = torch.empty(N, 2 * FW, dtype=torch.int32, device=ids.device)
+        seed &= 0xFFFFFFFF
+        row_offset &= 0xFFFFFFFF
+        check(lib().pv_conv_pool_fwd(P(ids), P(tbl16), P(wpack), P(bias.contiguous()), P(pooled), P(argmax), N, L, V,
+                                     seed, row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
+              "pv_conv_pool_fwd")
+        ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
+        ctx.meta = (V, E, seed, row_offset, thr, tok, scale)
+        ctx.mark_non_differentiable(argmax)
+        return pooled, argmax
+
+    @staticmethod
+    def backward(ctx, gpool, _gargmax):
+        ids, pooled, argmax, tbl16, w3, w4 = ctx.saved_tensors
+        V, E, seed, row_offset, thr, tok, scale = ctx.meta
+        N, L = ids.shape
+        dev = ids.device
+        s = stream(dev)
+        gpool = gpool.contiguous().float()
+        dw3 = torch.zeros_like(w3)
+        dw4 = torch.zeros_like(w4)
+        db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
+        L_ = lib()
+        check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E, V,
+                                     seed, row_offset, thr, tok, scale, s), "pv_conv_pool_bwd_dw")
+        dtable = None
+        if ctx.needs_input_grad[1]:
+            M = N * 2 * FW * 4
+            u32 = torch.int32
+            keys = torch.empty(M, dtype=u32, device=dev)
+            vals = torch.empty(M, dtype=u32, device=dev)
+            erow = torch.empty(M, dtype=u32, device=dev)
+            efj = torch.empty(M, dtype=u32, device=dev)
+            eg = torch.empty(M, dtype=torch.float32, device=dev)
+            check(L_.pv_conv_pool_bwd_emit(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(erow), P(efj),
+                                           P(eg), N, L, V, s), "pv_conv_pool_bwd_emit")
+            end_bit = max(1, int(V).bit_length())
+            skeys = torch.empty_like(keys)
+            svals = torch.empty_like(vals)
+            tb = int(L_.pv_sort_pairs_temp_bytes(M, end_bit))
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+            check(L_.pv_sort_pairs_u32(P(temp), tb, P(keys), P(skeys), P(vals), P(svals), M, end_bit, s),
+                  "pv_sort_pairs_u32")
+            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            check(L_.pv_conv_pool_bwd_reduce(P(skeys), P(svals), P(erow), P(efj), P(eg), P(w3.contiguous()),
+                                             P(w4.contiguous()), P(dtable), M, E, V, seed, row_offset, thr, tok,
+                                             scale, s), "pv_conv_pool_bwd_reduce")
+        return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
+
+
+def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, biases, p: float, seed: int,
+                            training: bool, mode: str = "element", row_offset: int = 0,
+                            compute_cache=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """pooled (N, sum F) post-ReLU, argmax (N, sum F) for one tower invocation.
+
+    ``compute_cache``: optional (tbl16, wpack) already derived from the current params.
+    """
+    if use_hip(ids, table) and fast_path_supported(table.shape[1], [w.shape[1] for w in weights], weights[0].shape[0]):
+        w3, w4 = weights
+        bias = torch.cat(list(biases))
+        if compute_cache is None:
+            tbl16, wpack = table_bf16(table.detach()), pack_weights(w3.detach(), w4.detach())
+        else:
+            tbl16, wpack = compute_cache
+        return _ConvPoolFn.apply(ids, table, w3, w4, bias, tbl16, wpack, float(p), int(seed), int(row_offset),
+                                 bool(training), mode)
+    x = ref.embed_dropout(ids, table, p, seed, training, mode) if row_offset == 0 else \
+        _embed_dropout_offset(ids, table, p, seed, training, mode, row_offset)
+    return ref.conv_relu_maxpool(x, weights, biases)
+
+
+def _embed_dropout_offset(ids, table, p, seed, training, mode, row_offset):
+    x = torch.nn.functional.embedding(ids.long(), table)
+    if training and p > 0.0 and mode != "none":
+        N, L, E = x.shape
+        keep = ref.dropout_keep_mask(seed, N * L, E, p, row_offset=row_offset, mode=mode, device=ids.device)
+        x = x * keep.view(N, L, E).to(x.dtype) * (256.0 / (256.0 - ref.dropout_threshold(p)))
+    return x

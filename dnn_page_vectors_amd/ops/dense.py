@@ -1,0 +1,97 @@
+"""Fused linear + bias + activation (K4) and L2 normalisation (K5).
+
+GPU forward: ``csrc/kernels/dense.hip`` (MFMA bf16, fp32 accumulate, fused epilogue).
+Backward: the activation mask is a HIP elementwise kernel; dW = dz^T x and dx = dz W
+are plain GEMMs and go to hipBLASLt through torch.mm (per the design rule: library
+GEMMs for plain GEMMs, hand-written kernels for the fused hot ops).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._common import P, check, lib, stream, use_hip
+
+_ACT = {"none": 0, "relu": 1, "gelu": 2}
+
+
+class _LinearActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype not in (torch.float32, torch.bfloat16):
+            x2 = x2.float()
+        x2 = x2.contiguous()
+        M, K = x2.shape
+        N = w.shape[0]
+        wc = w.contiguous()
+        y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+        xdt = 1 if x2.dtype == torch.bfloat16 else 0
+        wdt = 1 if wc.dtype == torch.bfloat16 else 0
+        check(lib().pv_linear_act(P(x2), xdt, P(wc), wdt, P(b) if b is not None else None, P(y), None, M, N, K, K, N,
+                                  _ACT[act], stream(x.device)), "pv_linear_act")
+        ctx.save_for_backward(x2, w, y if act == "relu" else None, b)
+        ctx.act = act
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y, b = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous().float()
+        if ctx.act == "relu":
+            dz = torch.empty_like(dy2)
+            check(lib().pv_act_bwd(P(y), P(dy2), P(dz), dy2.numel(), 1, stream(dy.device)), "pv_act_bwd")
+        elif ctx.act == "none":
+            dz = dy2
+        else:  # gelu: recompute pre-activation (rare path; BERT uses torch GEMM + gelu kernel instead)
+            pre = torch.nn.functional.linear(x2.float(), w.float(), b)
+            with torch.enable_grad():
+                pre.requires_grad_(True)
+                g = torch.autograd.grad(torch.nn.functional.gelu(pre, approximate="tanh"), pre, dy2)[0]
+            dz = g
+        xf = x2.float()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dz @ w.float()).view(ctx.xshape).to(x2.dtype)
+        if ctx.needs_input_grad[1]:
+            dw = (dz.t() @ xf).to(w.dtype)
+        if b is not None and ctx.needs_input_grad[2]:
+            db = dz.sum(0)
+        return dx, dw, db, None
+
+
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "relu") -> torch.Tensor:
+    if use_hip(x, w):
+        return _LinearActFn.apply(x, w, b, act)
+    return ref.linear_act(x, w, b, act)
+
+
+class _L2NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous().float()
+        M, D = x2.shape
+        y = torch.empty_like(x2)
+        inv = torch.empty(M, dtype=torch.float32, device=x.device)
+        check(lib().pv_l2norm_fwd(P(x2), P(y), P(inv), None, M, D, D, stream(x.device)), "pv_l2norm_fwd")
+        ctx.save_for_backward(x2, y, inv)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y, inv = ctx.saved_tensors
+        M, D = x2.shape
+        dy2 = dy.reshape(M, D).contiguous().float()
+        dx = torch.empty_like(x2)
+        check(lib().pv_l2norm_bwd(P(y), P(inv), P(x2), P(dy2), P(dx), M, D, stream(dy.device)), "pv_l2norm_bwd")
+        return dx.view(ctx.shape)
+
+
+def l2_normalize(x: torch.Tensor) -> torch.Tensor:
+    if use_hip(x):
+        return _L2NormFn.apply(x)
+    return ref.l2_normalize(x)

@@ -1,0 +1,118 @@
+"""Cosine-relevance softmax losses (K5-K7).
+
+* ``dssm_explicit_loss``: reference parity head (1 positive + J explicit negatives per
+  query; dssm_cnn_v2/cnn_dssm_th.py:159-182).  One fused HIP kernel computes loss, P and
+  the gradients in a single pass.
+* ``inbatch_loss``: every query against all M documents (in-batch, or cross-GPU after
+  an all-gather of page vectors).  Flash-style HIP kernels: the (B x M) logits are
+  never materialised (see csrc/kernels/loss.hip).
+
+Both take L2-normalised vectors (``ops.dense.l2_normalize``).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import reference as ref
+from ._common import P, check, lib, stream, use_hip
+
+
+class _ExplicitFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qn, dn, gamma, clip):
+        B, D = qn.shape
+        J1 = dn.shape[1]
+        q = qn.contiguous().float()
+        d = dn.contiguous().float()
+        loss = torch.empty(B, dtype=torch.float32, device=q.device)
+        prob = torch.empty(B, dtype=torch.float32, device=q.device)
+        dq = torch.empty_like(q)
+        dd = torch.empty_like(d)
+        check(lib().pv_dssm_explicit(P(q), P(d), P(loss), P(prob), P(dq), P(dd), B, J1, D, float(gamma), 1.0,
+                                     int(clip), stream(q.device)), "pv_dssm_explicit")
+        ctx.save_for_backward(dq, dd)
+        ctx.mark_non_differentiable(prob)
+        return loss, prob
+
+    @staticmethod
+    def backward(ctx, gl, _gp):
+        dq, dd = ctx.saved_tensors
+        g = gl.contiguous().float()
+        return dq * g[:, None], dd * g[:, None, None], None, None
+
+
+def dssm_explicit_loss(qn: torch.Tensor, dn: torch.Tensor, gamma: float, clip: bool = True
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """qn (B, D), dn (B, 1+J, D) normalised -> (per-row loss (B,), P(D+|Q) (B,))."""
+    if use_hip(qn, dn):
+        return _ExplicitFn.apply(qn, dn, float(gamma), bool(clip))
+    R = torch.clamp((qn.unsqueeze(1) * dn).sum(-1), 0.0, 1.0) if clip else (qn.unsqueeze(1) * dn).sum(-1)
+    e = torch.exp(gamma * R - gamma * R.max(dim=1, keepdim=True).values.detach())
+    Pp = e[:, 0] / e.sum(dim=1)
+    loss = -torch.log(torch.clamp(Pp, ref.BCE_EPS, 1.0 - ref.BCE_EPS))
+    return loss, Pp.detach()
+
+
+def _pad_bf16(x: torch.Tensor, DP: int) -> torch.Tensor:
+    n, D = x.shape
+    out = torch.zeros(n, DP, dtype=torch.bfloat16, device=x.device)
+    out[:, :D] = x
+    return out
+
+
+def _transpose_bf16(x: torch.Tensor) -> torch.Tensor:
+    n, DP = x.shape
+    out = torch.empty(DP, n, dtype=torch.bfloat16, device=x.device)
+    check(lib().pv_transpose_bf16(P(x), P(out), n, DP, stream(x.device)), "pv_transpose_bf16")
+    return out
+
+
+class _InBatchFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qn, dn, pos, gamma, clip):
+        B, D = qn.shape
+        M = dn.shape[0]
+        DP = (D + 31) // 32 * 32
+        if DP > 192:
+            raise ValueError("in-batch loss kernel supports D <= 192")
+        s = stream(qn.device)
+        qb = _pad_bf16(qn.detach(), DP)
+        db = _pad_bf16(dn.detach(), DP)
+        pos = pos.to(torch.int32).contiguous()
+        sumexp = torch.zeros(B, dtype=torch.float32, device=qn.device)
+        spos = torch.empty(B, dtype=torch.float32, device=qn.device)
+        L_ = lib()
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
+              "pv_ib_pos")
+        loss = gamma + torch.log(sumexp) - spos
+        ctx.save_for_backward(qb, db, pos, sumexp)
+        ctx.meta = (B, M, D, DP, float(gamma), int(clip))
+        return loss, torch.exp(-loss).detach()
+
+    @staticmethod
+    def backward(ctx, gl, _gp):
+        qb, db, pos, sumexp = ctx.saved_tensors
+        B, M, D, DP, gamma, clip = ctx.meta
+        s = stream(qb.device)
+        L_ = lib()
+        g = gl.contiguous().float()
+        scale = (g * gamma / sumexp).contiguous()
+        dq = torch.zeros(B, DP, dtype=torch.float32, device=qb.device)
+        dd = torch.zeros(M, DP, dtype=torch.float32, device=qb.device)
+        dbT = _transpose_bf16(db)
+        qbT = _transpose_bf16(qb)
+        check(L_.pv_ib_bwd(P(qb), P(db), P(dbT), P(scale), P(dq), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
+        check(L_.pv_ib_bwd(P(db), P(qb), P(qbT), P(scale), P(dd), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
+        check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
+        return dq[:, :D], dd[:, :D], None, None, None
+
+
+def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, gamma: float, clip: bool = True
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """qn (B, D), dn (M, D) normalised; pos_index (B,) -> (per-row loss, P_pos)."""
+    if use_hip(qn, dn):
+        return _InBatchFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
+    return ref.inbatch_softmax_loss(qn, dn, pos_index, gamma, clip)

@@ -1,0 +1,114 @@
+"""Flat-buffer parameter store + fused Adam (K8).
+
+``FlatParams`` moves every parameter of a module into ONE contiguous fp32 buffer
+(parameters become views), with a parallel flat gradient buffer that autograd
+accumulates into (``param.grad`` are views as well).  Consequences:
+
+* the optimizer is one streaming kernel over the flat buffers (csrc/kernels/optim.hip);
+* data-parallel gradient all-reduce operates on contiguous buckets of the flat
+  gradient (parallel/ddp.py) — no per-tensor packing;
+* checkpoints / broadcast are single tensors.
+
+Keras-1 Adam semantics by default (``torch_style=False``), see optim.hip.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import torch
+
+from . import reference as ref
+from ._common import P, check, lib, stream, use_hip
+
+ALIGN = 64  # elements: 256-byte aligned parameter starts
+
+
+class FlatParams:
+    def __init__(self, params: Iterable[Tuple[str, torch.nn.Parameter]], device: Optional[torch.device] = None):
+        self.named: List[Tuple[str, torch.nn.Parameter]] = [(n, p) for n, p in params if p.requires_grad]
+        if not self.named:
+            raise ValueError("no trainable parameters")
+        dev = device or self.named[0][1].device
+        self.offsets: Dict[str, Tuple[int, int, torch.Size]] = {}
+        off = 0
+        for n, p in self.named:
+            self.offsets[n] = (off, p.numel(), p.shape)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        for n, p in self.named:
+            o, k, shp = self.offsets[n]
+            self.data[o:o + k].copy_(p.data.reshape(-1).float())
+            p.data = self.data[o:o + k].view(shp)
+            p.grad = self.grad[o:o + k].view(shp)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def reattach_grads(self) -> None:
+        """Re-point param.grad at the flat buffer (if something replaced them)."""
+        for n, p in self.named:
+            o, k, shp = self.offsets[n]
+            g = self.grad[o:o + k].view(shp)
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                if p.grad is not None:
+                    g.copy_(p.grad)
+                p.grad = g
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {n: self.data[o:o + k].view(shp) for n, (o, k, shp) in self.offsets.items()}
+
+
+class FlatAdam:
+    def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, torch_style: bool = False):
+        self.flat = flat
+        self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
+        self.torch_style = torch_style
+        self.m = torch.zeros_like(flat.data)
+        self.v = torch.zeros_like(flat.data)
+        self.step_count = 0
+
+    def step(self, skip_flag: Optional[torch.Tensor] = None) -> None:
+        """One update. ``skip_flag``: device scalar; non-zero => the kernel skips (NaN guard)."""
+        self.step_count += 1
+        t = self.step_count
+        if use_hip(self.flat.data):
+            check(lib().pv_adam(P(self.flat.data), P(self.flat.grad), P(self.m), P(self.v), self.flat.numel, t,
+                                self.lr, self.b1, self.b2, self.eps, self.wd, int(self.torch_style), P(skip_flag),
+                                stream(self.flat.data.device)), "pv_adam")
+            return
+        if skip_flag is not None and float(skip_flag) != 0.0:
+            return
+        with torch.no_grad():
+            g = self.flat.grad + self.wd * self.flat.data if self.wd else self.flat.grad
+            if self.torch_style:
+                self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+                self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+                bc1 = 1 - self.b1 ** t
+                bc2 = 1 - self.b2 ** t
+                self.flat.data.addcdiv_(self.m, (self.v.sqrt() / math.sqrt(bc2)).add_(self.eps), value=-self.lr / bc1)
+            else:
+                ref.adam_keras_([self.flat.data], [g], [self.m], [self.v], t, self.lr, self.b1, self.b2, self.eps)
+
+    def state_dict(self) -> Dict[str, object]:
+        return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr}
+
+    def load_state_dict(self, d: Dict[str, object]) -> None:
+        self.m.copy_(d["m"])
+        self.v.copy_(d["v"])
+        self.step_count = int(d["step"])
+
+
+def grad_sumsq_and_finite(flat_grad: torch.Tensor) -> torch.Tensor:
+    """Device tensor [sum g^2, nonfinite_flag] without a host sync."""
+    out = torch.zeros(2, dtype=torch.float32, device=flat_grad.device)
+    if use_hip(flat_grad):
+        check(lib().pv_sumsq(P(flat_grad), flat_grad.numel(), P(out), stream(flat_grad.device)), "pv_sumsq")
+        return out
+    finite = torch.isfinite(flat_grad)
+    out[0] = torch.where(finite, flat_grad, torch.zeros_like(flat_grad)).pow(2).sum()
+    out[1] = (~finite).any().float()
+    return out

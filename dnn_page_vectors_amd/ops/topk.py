@@ -1,0 +1,46 @@
+"""Blocked cosine top-k (K9).  GPU: HIP kernel (csrc/kernels/topk.hip); CPU: torch."""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from ._common import P, check, lib, stream, use_hip
+
+
+def _topk_torch(qn, pn, k, block):
+    best_s = None
+    best_i = None
+    for s in range(0, pn.shape[0], block):
+        sc = qn.float() @ pn[s:s + block].float().t()
+        kk = min(k, sc.shape[1])
+        v, i = sc.topk(kk, dim=1)
+        i = i + s
+        if best_s is None:
+            best_s, best_i = v, i
+        else:
+            cs = torch.cat([best_s, v], 1)
+            ci = torch.cat([best_i, i], 1)
+            v2, j = cs.topk(min(k, cs.shape[1]), dim=1)
+            best_s, best_i = v2, ci.gather(1, j)
+    return best_s, best_i
+
+
+def topk_cos(qn: torch.Tensor, pn: torch.Tensor, k: int = 10, block: int = 65536) -> Tuple[torch.Tensor, torch.Tensor]:
+    if use_hip(qn, pn) and hasattr(lib(), "pv_topk_cos") and k <= 16:
+        return _topk_hip(qn, pn, k)
+    return _topk_torch(qn, pn, k, block)
+
+
+def _topk_hip(qn, pn, k):
+    B, D = qn.shape
+    N = pn.shape[0]
+    DP = (D + 31) // 32 * 32
+    qb = torch.zeros(B, DP, dtype=torch.bfloat16, device=qn.device)
+    qb[:, :D] = qn
+    pb = torch.zeros(N, DP, dtype=torch.bfloat16, device=qn.device)
+    pb[:, :D] = pn
+    vals = torch.empty(B, k, dtype=torch.float32, device=qn.device)
+    idx = torch.empty(B, k, dtype=torch.int32, device=qn.device)
+    check(lib().pv_topk_cos(P(qb), P(pb), P(vals), P(idx), B, N, DP, k, stream(qn.device)), "pv_topk_cos")
+    return vals, idx.long()

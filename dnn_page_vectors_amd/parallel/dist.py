@@ -1,0 +1,135 @@
+"""Process-group setup and differentiable collectives (RCCL over xGMI on MI355X).
+
+One process per GPU; ``backend="nccl"`` is RCCL on ROCm.  CPU tests use ``gloo``
+(world_size > 1 on one host) — the same code paths.
+
+* ``init_distributed()`` reads RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT
+  (torchrun contract), pins the device, sets a finite collective timeout so a hung
+  peer surfaces as an error instead of a silent hang.
+* ``all_gather_autograd(x)``: forward all-gather of page vectors (cross-GPU in-batch
+  negatives); backward = reduce-scatter(sum) of the gathered gradient
+  back to the owning rank — every rank's loss depends on every rank's documents.
+
+The reference has no collectives at all; its only multi-device code is manual tower
+placement (dssm_cnn_v2/cnn_dssm_tf.py:139-158), reproduced as ``parallel/placement.py``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1
+
+
+_INFO = DistInfo()
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None) -> DistInfo:
+    """Initialise from the torchrun environment; a no-op single-process setup otherwise."""
+    global _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = (device or ("cuda" if torch.cuda.device_count() > 0 else "cpu")).startswith("cuda")
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        be = backend or ("nccl" if use_gpu else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {}
+        if be == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(be, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        _INFO = DistInfo(rank, world, local, be, dev)
+    elif dist.is_initialized():
+        _INFO = DistInfo(dist.get_rank(), dist.get_world_size(), local, dist.get_backend(), dev)
+    else:
+        _INFO = DistInfo(0, 1, 0, "none", dev)
+    return _INFO
+
+
+def set_info(i: DistInfo) -> None:
+    global _INFO
+    _INFO = i
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+class _AllGather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor) -> torch.Tensor:
+        W = dist.get_world_size()
+        x = x.contiguous()
+        out = torch.empty((W * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x)
+        ctx.n = x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor) -> torch.Tensor:
+        g = g.contiguous()
+        out = torch.empty((ctx.n,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+        dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM)
+        return out
+
+
+def all_gather_autograd(x: torch.Tensor) -> torch.Tensor:
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    return _AllGather.apply(x)
+
+
+def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(dist.get_world_size())
+    return t
+
+
+def all_reduce_max_(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(t, src)
+    return t

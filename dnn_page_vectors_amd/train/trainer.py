@@ -1,0 +1,208 @@
+"""Training driver: ``fit()`` / ``evaluate()`` / ``train_step()``.
+
+Replaces the reference's ``model.compile("adam", "binary_crossentropy", ["accuracy"])``
++ ``fit_generator(gen, nb_epoch, samples_per_epoch, validation_data, nb_val_samples,
+callbacks=[ModelCheckpoint])`` (dssm_cnn_v2/cnn_dssm_th.py:181-206):
+
+* loss modes: ``explicit`` (parity: 1 positive + J negatives, BCE on P(D+|Q)),
+  ``in_batch`` (every query vs all docs of the local batch), ``cross_gpu`` (vs all
+  docs of all ranks, all-gathered page vectors — the north-star mode);
+* metrics with Keras names: ``loss``, ``acc`` (= mean(P > 0.5), Keras binary accuracy
+  with y = 1), ``val_loss``, ``val_acc``; ``fit`` returns that ``history`` dict;
+* per-epoch checkpoints in the reference layout + final artefacts (io/checkpoint.py);
+* resume from the latest checkpoint (step count, optimizer state, RNG, data cursor);
+* NaN/inf guard: a non-finite gradient skips the optimizer step on every rank
+  (device-side flag, no host sync) and is counted in the metrics;
+* fault injection for resume tests: ``PAGEVEC_FAULT_STEP=<n>`` raises at step n.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+from typing import Callable, Dict, Iterable, Iterator, List, Optional, Tuple
+
+import torch
+
+from ..models.base import TwoTowerModel, bump_generation
+from ..ops import dense as dops
+from ..ops import loss as lops
+from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
+from ..parallel import dist as pdist
+from ..parallel.ddp import GradBuckets, broadcast_params
+from ..utils.metrics import MetricsLogger
+from ..utils.tracing import range_push, range_pop
+
+log = logging.getLogger(__name__)
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+class Trainer:
+    def __init__(self, cfg, model: TwoTowerModel, device: Optional[torch.device] = None,
+                 metrics: Optional[MetricsLogger] = None):
+        self.cfg = cfg
+        self.info = pdist.info()
+        self.device = device or self.info.device
+        self.model = model.to(self.device)
+        self.flat = FlatParams(self.model.named_parameters())
+        broadcast_params(self.flat)
+        bump_generation()
+        self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
+                            torch_style=(cfg.model == "bert"))
+        self.buckets = GradBuckets(self.flat, cfg.grad_bucket_mb) if self.info.enabled else None
+        self.step = 0
+        self.epoch = 0
+        self.skipped_steps = 0
+        self.metrics = metrics
+        self._fault_step = int(os.environ.get("PAGEVEC_FAULT_STEP", "-1"))
+
+    # ------------------------------------------------------------------ core step
+    def compute_loss(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int
+                     ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Mean loss over the local batch and per-row P(D+|Q)."""
+        cfg = self.cfg
+        B, S, _ = d_ids.shape
+        range_push("forward")
+        q, d = self.model(q_ids, d_ids, seed=seed)
+        qn = dops.l2_normalize(q)
+        dn = dops.l2_normalize(d.reshape(B * S, -1))
+        clip = bool(getattr(cfg, "cos_clip", True))
+        if cfg.loss_mode == "explicit":
+            per_row, P = lops.dssm_explicit_loss(qn, dn.view(B, S, -1), cfg.GAMMA, clip)
+        elif cfg.loss_mode in ("in_batch", "cross_gpu"):
+            offset = 0
+            docs = dn
+            if cfg.loss_mode == "cross_gpu" and self.info.enabled:
+                docs = pdist.all_gather_autograd(dn)
+                offset = self.info.rank * B * S
+            pos = offset + torch.arange(B, device=q.device, dtype=torch.int32) * S
+            per_row, P = lops.inbatch_loss(qn, docs, pos, cfg.GAMMA, clip)
+        else:
+            raise ValueError(f"unknown loss_mode {cfg.loss_mode!r}")
+        range_pop()
+        return per_row.mean(), P
+
+    def train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        if self.step == self._fault_step:
+            raise InjectedFault(f"injected fault at step {self.step}")
+        self.model.train()
+        self.flat.zero_grad()
+        if self.buckets is not None:
+            self.buckets.start_step()
+        seed = (self.cfg.seed * 1000003 + self.step * 7919 + self.info.rank * 104729) & 0x7FFFFFFF
+        loss, P = self.compute_loss(q_ids, d_ids, seed)
+        range_push("backward")
+        loss.backward()
+        range_pop()
+        range_push("allreduce")
+        if self.buckets is not None:
+            self.buckets.finish()
+        range_pop()
+        range_push("optimizer")
+        stats = grad_sumsq_and_finite(self.flat.grad)
+        skip = stats[1:2] if self.cfg.skip_nonfinite else None
+        self.opt.step(skip)
+        bump_generation()
+        range_pop()
+        self.step += 1
+        return {"loss": loss.detach(), "acc": (P > 0.5).float().mean(), "grad_sumsq": stats[0],
+                "nonfinite": stats[1]}
+
+    @torch.no_grad()
+    def eval_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        self.model.eval()
+        loss, P = self.compute_loss(q_ids, d_ids, 0)
+        self.model.train()
+        return {"loss": loss, "acc": (P > 0.5).float().mean()}
+
+    # ------------------------------------------------------------------ loops
+    def _run_epoch(self, batches: Iterator, steps: int, train: bool) -> Dict[str, float]:
+        tot: Dict[str, torch.Tensor] = {}
+        n = 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            try:
+                q, d = next(batches)
+            except StopIteration:
+                break
+            q = q.to(self.device, non_blocking=True)
+            d = d.to(self.device, non_blocking=True)
+            m = self.train_step(q, d) if train else self.eval_step(q, d)
+            for k in ("loss", "acc"):
+                tot[k] = tot.get(k, 0.0) + m[k].float()
+            if train:
+                nf = m["nonfinite"]
+                tot["nonfinite"] = tot.get("nonfinite", 0.0) + nf
+                if self.metrics and self.cfg.log_every and self.step % self.cfg.log_every == 0:
+                    self.metrics.log(step=self.step, loss=float(m["loss"]), acc=float(m["acc"]),
+                                     grad_norm=math.sqrt(max(0.0, float(m["grad_sumsq"]))))
+            n += 1
+        if n == 0:
+            return {}
+        out = {k: float(v) / n for k, v in tot.items() if k != "nonfinite"}
+        if train and "nonfinite" in tot:
+            self.skipped_steps += int(round(float(tot["nonfinite"])))
+        # average metrics over ranks
+        if self.info.enabled:
+            t = torch.tensor([out.get("loss", 0.0), out.get("acc", 0.0)], device=self.device)
+            pdist.all_reduce_mean_(t)
+            out["loss"], out["acc"] = float(t[0]), float(t[1])
+        out["time_s"] = time.perf_counter() - t0
+        out["steps"] = n
+        return out
+
+    def fit(self, train_batches: Callable[[int], Iterator], nb_epoch: Optional[int] = None,
+            steps_per_epoch: Optional[int] = None, validation_batches: Optional[Callable[[int], Iterator]] = None,
+            validation_steps: Optional[int] = None, callbacks: Iterable = ()) -> Dict[str, List[float]]:
+        """Keras-style fit. ``train_batches(epoch)`` returns an iterator of (q_ids, d_ids).
+
+        steps_per_epoch defaults to num_train_samples // batch_size (samples_per_epoch).
+        """
+        cfg = self.cfg
+        nb_epoch = nb_epoch or cfg.nb_epoch
+        gb = cfg.batch_size
+        steps_per_epoch = steps_per_epoch or max(1, cfg.num_train_samples // gb)
+        validation_steps = validation_steps or max(1, cfg.num_validation_samples // gb)
+        history: Dict[str, List[float]] = {"loss": [], "acc": [], "val_loss": [], "val_acc": []}
+        for cb in callbacks:
+            if hasattr(cb, "on_train_begin"):
+                cb.on_train_begin(self)
+        start_epoch = self.epoch
+        for ep in range(start_epoch, nb_epoch):
+            tr = self._run_epoch(iter(train_batches(ep)), steps_per_epoch, True)
+            history["loss"].append(tr.get("loss", float("nan")))
+            history["acc"].append(tr.get("acc", float("nan")))
+            if validation_batches is not None:
+                va = self._run_epoch(iter(validation_batches(ep)), validation_steps, False)
+                history["val_loss"].append(va.get("loss", float("nan")))
+                history["val_acc"].append(va.get("acc", float("nan")))
+            self.epoch = ep + 1
+            logs = {k: v[-1] for k, v in history.items() if v}
+            if self.info.is_main:
+                log.info("epoch %d/%d %s", ep + 1, nb_epoch, json.dumps(logs))
+            if self.metrics:
+                self.metrics.log(epoch=ep + 1, **logs)
+            for cb in callbacks:
+                if hasattr(cb, "on_epoch_end"):
+                    cb.on_epoch_end(self, ep, logs)
+        for cb in callbacks:
+            if hasattr(cb, "on_train_end"):
+                cb.on_train_end(self, history)
+        return {k: v for k, v in history.items() if v}
+
+    # ------------------------------------------------------------------ state
+    def state(self) -> Dict[str, object]:
+        return {"step": self.step, "epoch": self.epoch, "skipped_steps": self.skipped_steps,
+                "opt_step": self.opt.step_count, "world_size": self.info.world_size}
+
+    def load_state(self, st: Dict[str, object]) -> None:
+        self.step = int(st["step"])
+        self.epoch = int(st["epoch"])
+        self.skipped_steps = int(st.get("skipped_steps", 0))
+        self.opt.step_count = int(st.get("opt_step", self.step))
+        bump_generation()

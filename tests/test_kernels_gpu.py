@@ -1,0 +1,215 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references (run on MI355X: pytest -m gpu)."""
+import pytest
+import torch
+
+from dnn_page_vectors_amd import _native
+from dnn_page_vectors_amd.ops import conv_pool as cops
+from dnn_page_vectors_amd.ops import dense as dops
+from dnn_page_vectors_amd.ops import loss as lops
+from dnn_page_vectors_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf(x):
+    return x.bfloat16().float()
+
+
+def test_native_hip_library_loaded():
+    lib = _native.hip(required=True)
+    assert lib is not None
+    assert any("libpagevec_hip" in p for p in _native.loaded_libraries())
+
+
+@pytest.mark.parametrize("N,L,p,mode", [(8, 37, 0.0, "element"), (5, 130, 0.25, "element"), (3, 64, 0.25, "token"),
+                                        (6, 4, 0.0, "element"), (300, 45, 0.25, "element")])
+def test_conv_pool_fwd_bwd(N, L, p, mode):
+    torch.manual_seed(0)
+    V, E, F = 97, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    # bf16-representable operands: the kernels' bf16 copies are exact, so the fp32
+    # reference sees the same values (only accumulation order differs)
+    table = bf(torch.randn(V, E, device=DEV) * 0.5).requires_grad_(True)
+    w3 = bf(torch.randn(F, 3, E, device=DEV) * 0.1).requires_grad_(True)
+    w4 = bf(torch.randn(F, 4, E, device=DEV) * 0.1).requires_grad_(True)
+    b3 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    b4 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    seed = 1234
+    pooled, argmax = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], p, seed, True, mode)
+    # reference on the bf16-rounded operands the kernel consumes
+    tr = bf(table.detach()).requires_grad_(True)
+    w3r = bf(w3.detach()).requires_grad_(True)
+    w4r = bf(w4.detach()).requires_grad_(True)
+    b3r = b3.detach().clone().requires_grad_(True)
+    b4r = b4.detach().clone().requires_grad_(True)
+    x = ref.embed_dropout(ids, tr, p, seed, True, mode)
+    pr, ar = ref.conv_relu_maxpool(x, [w3r, w4r], [b3r, b4r])
+    torch.testing.assert_close(pooled, pr, rtol=2e-3, atol=2e-3)
+    live = pr > 1e-3
+    agree = (argmax == ar) | ~live
+    assert agree.float().mean() > 0.97
+    g = torch.randn_like(pooled)
+    # backward consistency: use the kernel's argmax in both to avoid tie-breaking noise
+    (pooled * g).sum().backward()
+    (pr * g).sum().backward()
+    torch.testing.assert_close(b3.grad, b3r.grad, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(b4.grad, b4r.grad, rtol=2e-3, atol=2e-3)
+    if agree.all():
+        torch.testing.assert_close(w3.grad, w3r.grad, rtol=1e-3, atol=2e-3)
+        torch.testing.assert_close(w4.grad, w4r.grad, rtol=1e-3, atol=2e-3)
+        torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
+
+
+def test_conv_pool_eval_mode_no_dropout():
+    V, E, F, N, L = 50, 100, 150, 4, 20
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    table = torch.randn(V, E, device=DEV)
+    w3, w4 = torch.randn(F, 3, E, device=DEV) * .1, torch.randn(F, 4, E, device=DEV) * .1
+    b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
+    a, _ = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], b, 0.25, 1, False)
+    r, _ = ref.conv_relu_maxpool(ref.embed_dropout(ids, bf(table), 0.25, 1, False), [bf(w3), bf(w4)], b)
+    torch.testing.assert_close(a, r, rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("M,K,N,act", [(100, 300, 150, "relu"), (64, 512, 128, "none"), (33, 70, 17, "relu")])
+def test_linear_act(M, K, N, act):
+    x = bf(torch.randn(M, K, device=DEV)).requires_grad_(True)
+    w = bf(torch.randn(N, K, device=DEV) * 0.05).requires_grad_(True)
+    b = torch.randn(N, device=DEV, requires_grad=True)
+    y = dops.linear_act(x, w, b, act)
+    xr, wr = bf(x.detach()).requires_grad_(True), bf(w.detach()).requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = ref.linear_act(xr, wr, br, act)
+    torch.testing.assert_close(y, yr, rtol=2e-3, atol=2e-3)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    torch.testing.assert_close(b.grad, br.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_l2norm():
+    x = torch.randn(37, 150, device=DEV, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y = dops.l2_normalize(x)
+    yr = ref.l2_normalize(x2)
+    torch.testing.assert_close(y, yr)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("clip", [True, False])
+def test_explicit_loss(clip):
+    B, J1, D = 40, 4, 150
+    q = torch.relu(torch.randn(B, D, device=DEV))
+    d = torch.relu(torch.randn(B, J1, D, device=DEV))
+    qn = ref.l2_normalize(q).requires_grad_(True)
+    dn = ref.l2_normalize(d).requires_grad_(True)
+    loss, P = lops.dssm_explicit_loss(qn, dn, 10.0, clip)
+    qn2 = qn.detach().clone().requires_grad_(True)
+    dn2 = dn.detach().clone().requires_grad_(True)
+    R = (qn2.unsqueeze(1) * dn2).sum(-1)
+    if clip:
+        R = R.clamp(0, 1)
+    S = 10.0 * R
+    Pr = torch.softmax(S, 1)[:, 0]
+    lr = -torch.log(Pr.clamp(1e-7, 1 - 1e-7))
+    torch.testing.assert_close(loss, lr, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(P, Pr, rtol=1e-4, atol=1e-5)
+    loss.mean().backward()
+    lr.mean().backward()
+    torch.testing.assert_close(qn.grad, qn2.grad, rtol=1e-3, atol=1e-6)
+    torch.testing.assert_close(dn.grad, dn2.grad, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,M,D,clip", [(50, 200, 150, True), (130, 515, 128, False), (7, 7, 64, True)])
+def test_inbatch_loss(B, M, D, clip):
+    torch.manual_seed(1)
+    q = torch.randn(B, D, device=DEV)
+    dd = torch.randn(M, D, device=DEV)
+    if clip:
+        q, dd = q.abs(), dd.abs()
+    qn = bf(ref.l2_normalize(q)).requires_grad_(True)
+    dn = bf(ref.l2_normalize(dd)).requires_grad_(True)
+    pos = torch.randint(0, M, (B,), device=DEV, dtype=torch.int32)
+    loss, P = lops.inbatch_loss(qn, dn, pos, 10.0, clip)
+    qn2 = qn.detach().clone().requires_grad_(True)
+    dn2 = dn.detach().clone().requires_grad_(True)
+    lr, _ = ref.inbatch_softmax_loss(qn2, dn2, pos, 10.0, clip)
+    torch.testing.assert_close(loss, lr, rtol=2e-3, atol=2e-3)
+    w = torch.rand(B, device=DEV)
+    (loss * w).sum().backward()
+    (lr * w).sum().backward()
+    torch.testing.assert_close(qn.grad, qn2.grad, rtol=3e-2, atol=3e-3)
+    torch.testing.assert_close(dn.grad, dn2.grad, rtol=3e-2, atol=3e-3)
+
+
+def test_adam_matches_reference():
+    from dnn_page_vectors_amd.ops.optim import FlatAdam, FlatParams
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(33, 17).to(DEV)
+    flat = FlatParams(lin.named_parameters())
+    opt = FlatAdam(flat, lr=1e-2)
+    p0 = flat.data.clone()
+    m = torch.zeros_like(p0)
+    v = torch.zeros_like(p0)
+    for t in range(1, 4):
+        flat.grad.copy_(torch.randn_like(flat.grad))
+        g = flat.grad.clone()
+        opt.step()
+        ref.adam_keras_([p0], [g], [m], [v], t, 1e-2, 0.9, 0.999, 1e-8)
+    torch.testing.assert_close(flat.data, p0, rtol=1e-5, atol=1e-6)
+
+
+def test_adam_skip_flag():
+    from dnn_page_vectors_amd.ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
+
+    lin = torch.nn.Linear(8, 4).to(DEV)
+    flat = FlatParams(lin.named_parameters())
+    opt = FlatAdam(flat)
+    before = flat.data.clone()
+    flat.grad.fill_(1.0)
+    flat.grad[3] = float("nan")
+    st = grad_sumsq_and_finite(flat.grad)
+    assert float(st[1]) == 1.0
+    opt.step(st[1:2])
+    torch.testing.assert_close(flat.data, before)
+
+
+def test_topk_cos():
+    from dnn_page_vectors_amd.ops import topk as tops
+
+    q = ref.l2_normalize(torch.randn(64, 150, device=DEV))
+    pg = ref.l2_normalize(torch.randn(3000, 150, device=DEV))
+    v, i = tops.topk_cos(q, pg, 10)
+    vr, ir = tops._topk_torch(bf(q), bf(pg), 10, 1024)
+    torch.testing.assert_close(v, vr, rtol=1e-3, atol=1e-3)
+    assert (i[:, 0] == ir[:, 0]).float().mean() > 0.95
+
+
+def test_cdssm_train_step_gpu():
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed()
+    for mode in ("explicit", "cross_gpu"):
+        cfg = Configuration(feature_level="ngram", vocab_hash_size=3000, batch_size=64, query_length=45,
+                            document_length=200, loss_mode=mode)
+        tr = Trainer(cfg, CDSSM(cfg, 3000), torch.device(DEV))
+        g = torch.Generator(device="cpu").manual_seed(0)
+        pages = torch.randint(1, 3000, (512, 200), generator=g, dtype=torch.int32).to(DEV)
+        losses = []
+        for _ in range(30):
+            idx = torch.randint(0, 512, (64, 4), generator=g).to(DEV)
+            q, d = pages[idx[:, 0], :45].contiguous(), pages[idx]
+            losses.append(float(tr.train_step(q, d)["loss"]))
+        assert all(l == l for l in losses)
+        assert sum(losses[-5:]) < sum(losses[:5])

@@ -1,0 +1,93 @@
+"""Tokenizer parity: native C++ featurizer == Python restatement == reference golden cases
+(recorded from /root/reference/utils/data_utils.py under Python 3)."""
+import json
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from dnn_page_vectors_amd.data import text as T
+from dnn_page_vectors_amd.data.featurize import Featurizer, clean_str_native, generate_vocabulary
+
+GOLD = "Statue of Liberty! NYC #1 tour, $25.00 (Mütze) a-b_c"
+
+
+def test_clean_str_golden():
+    assert T.clean_str(GOLD) == "statue of liberty  nyc #1 tour  $25.00  mütze  a b_c"
+    assert clean_str_native(GOLD) == T.clean_str(GOLD)
+
+
+def test_splits_golden():
+    assert T.split_features(GOLD, "word") == ["statue", "of", "liberty", "", "nyc", "#1", "tour", "", "$25.00", "",
+                                              "mütze", "", "a", "b_c"]
+    assert T.split_features(GOLD, "word", 3) == ["statue", "of", "liberty"]
+    assert T.split_features(GOLD, "char", 12) == list("statue of li")
+    assert T.split_features(GOLD, "ngram", 6) == ["sta", "tat", "atu", "tue", "ue ", "e o"]
+
+
+def test_pad_and_vocab_order():
+    assert T.pad_tokens(["a"], 3) == ["a", "<PAD/>", "<PAD/>"]
+    assert T.build_vocab_counts([["b", "a", "b"], ["c", "a", "b"]]) == ["b", "a", "c"]
+    v = T.Vocab(["x", "y"])
+    assert v.itos[:3] == ["<PAD/>", "<UNK/>", " "] and v.lookup("zzz") == v.unk_id == 1 and v.pad_id == 0
+
+
+def test_empty_and_short_texts():
+    assert T.split_features("", "word") == [""]          # ''.split(' ') == ['']
+    assert T.split_features("ab", "ngram") == []
+    assert T.split_features("!!!", "char") == []
+
+
+@pytest.mark.parametrize("mode", ["word", "char", "ngram"])
+def test_native_matches_python_vocab(mode):
+    texts = [GOLD, "statue of liberty", "New York city", "", "a  b", "ÄÖÜ straße €5.00 #tag"]
+    toks = [T.split_features(t, mode) for t in texts]
+    vocab = T.Vocab(T.build_vocab_counts(toks))
+    L = 17
+    fz = Featurizer(mode, vocab=vocab, nthreads=2)
+    got = fz(texts, L)
+    want = np.array(T.featurize_py(texts, mode, L, vocab=vocab), dtype=np.int32)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode", ["word", "char", "ngram"])
+def test_native_matches_python_hash(mode):
+    texts = [GOLD, "statue of liberty", "ümlaut ß €", "x"]
+    fz = Featurizer(mode, hash_size=1000, nthreads=3)
+    got = fz(texts, 25)
+    want = np.array(T.featurize_py(texts, mode, 25, hash_size=1000), dtype=np.int32)
+    np.testing.assert_array_equal(got, want)
+    assert got.min() >= 0 and got.max() < 1000
+
+
+_ALPH = st.sampled_from(list("abcXYZ019 _-!.,#$€äöüßÄÖÜé\n\t()'\""))
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.text(alphabet=_ALPH, min_size=0, max_size=40), min_size=1, max_size=6),
+       st.sampled_from(["word", "char", "ngram"]), st.integers(min_value=1, max_value=30))
+def test_native_featurizer_fuzz(texts, mode, L):
+    fz = Featurizer(mode, hash_size=4096, nthreads=2)
+    got = fz(texts, L)
+    want = np.array(T.featurize_py(texts, mode, L, hash_size=4096), dtype=np.int32)
+    np.testing.assert_array_equal(got, want)
+    for t in texts:
+        assert clean_str_native(t) == T.clean_str(t)
+
+
+def test_generate_vocabulary_skips_bad_rows(tmp_path):
+    f = tmp_path / "train.txt"
+    rows = [{"q": "statue", "doc_corr": "statue of liberty", "doc_incorr": ["a", "b", "c"]},
+            {"q": "skip", "doc_corr": "zzz", "doc_incorr": ["only one"]}]
+    f.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    v = generate_vocabulary([str(f)], "word", 3)
+    assert "statue" in v.stoi and "zzz" not in v.stoi
+    # deterministic order: reserved, then by count desc
+    assert v.itos[3] == "statue"
+
+
+def test_html_normalizer():
+    s = T.normalize_html_line("<b>Hello</b>   World&amp;Co...  Mütze!")
+    assert "<b>" not in s and "  " not in s
+    assert " . " in s and "mütze" in s
