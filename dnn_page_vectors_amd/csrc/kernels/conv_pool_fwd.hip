@@ -12,9 +12,12 @@
 //    16-byte-aligned ds_read_b128 at byte 208*t + 64*s + 16*(lane>>4).  Both widths
 //    share the A fragments of steps 0..9; k=4 adds steps 10..12.
 //  * All 2 x 150 filters (padded to 2 x 160 = 20 tiles of 16 columns) live in
-//    REGISTERS for the whole persistent workgroup: 4 waves (one per SIMD) own
-//    {3 k3 + 2 k4} or {2 k3 + 3 k4} tiles => 56/59 MFMAs per 16-row block per wave
-//    (97.5% balance).  Weights are loaded once per workgroup, not per sample.
+//    REGISTERS for the whole persistent workgroup.  8 waves, two per SIMD (waves w and
+//    w+4 share a SIMD under the dispatcher's cyclic wave->SIMD order): every SIMD owns
+//    {3 k3 + 2 k4} or {2 k3 + 3 k4} tiles => 56/59 MFMAs per 16-row block (97.5%
+//    balance), split over its two waves so each wave holds <= 144 weight VGPRs — no
+//    AGPR spills/copies — and one wave's max/argmax VALU epilogue overlaps its partner's
+//    MFMAs.  Weights are loaded once per workgroup, not per sample.
 //  * Conv activations never leave registers: each lane keeps a running max and the
 //    argmax row for its 4 accumulator rows; the cross-lane reduction happens once per
 //    sample.  ReLU(max + bias) == max(ReLU(conv + bias)) because ReLU is monotone.
@@ -26,6 +29,7 @@
 //    MFMA phase, write LDS after the barrier) and token ids two chunks ahead, so the
 //    id->row dependent loads never sit on the critical path.
 #include "common.h"
+#include <stdlib.h>
 
 namespace pv {
 namespace convpool {
@@ -37,9 +41,9 @@ constexpr int S3 = 10;             // K-steps of 32 for k=3 (K = 312 -> 320)
 constexpr int S4 = 13;             // K-steps of 32 for k=4 (K = 416)
 constexpr int NT = 10;             // 16-column tiles per width (150 -> 160 filters)
 constexpr int FW = 150;            // real filters per width
-constexpr int R = 64;              // window rows per chunk
+constexpr int R = 112;             // window rows per chunk (7 blocks; 3 staged pieces per thread)
 constexpr int CROWS = R + 3;       // LDS rows per chunk
-constexpr int NTHREADS = 256;
+constexpr int NTHREADS = 512;
 constexpr int PPT = (CROWS * PIECES + NTHREADS - 1) / NTHREADS;  // pieces per thread (4)
 constexpr int IDS_PT = (CROWS + NTHREADS - 1) / NTHREADS;        // ids per thread (1)
 
@@ -55,6 +59,7 @@ struct Params {
   int thr;                     // dropout byte threshold (0 = off)
   int token_mode;              // 1: one keep decision per row
   float scale;                 // 1/(1-p)
+  int dbg;                     // diagnostic ablations (0 in production): 1 no gather, 2 max-only epilogue, 4 no dropout hash
 };
 
 // fragment base index of tile T in wpack (tiles 0..9 k3 with S3 steps, 10..19 k4 with S4)
@@ -91,7 +96,7 @@ __device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u
     int q = threadIdx.x + i * NTHREADS;
     int r = q / PIECES, pc = q - r * PIECES;
     int tok = (q < CROWS * PIECES) ? ids_lds[r] : -1;
-    if (tok >= 0 && tok < p.V) {
+    if ((p.dbg & 1) == 0 && tok >= 0 && tok < p.V) {
       v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)tok * EP + pc * 8);
     } else {
       v[i] = u32x4{0u, 0u, 0u, 0u};
@@ -115,7 +120,7 @@ __device__ __forceinline__ void store_rows(const Params& p, const Cursor& cu, ch
     if (q < CROWS * PIECES) {
       int r = q / PIECES, pc = q - r * PIECES;
       u32x4 x = v[i];
-      if (p.thr > 0) {
+      if (p.thr > 0 && (p.dbg & 4) == 0) {
         unsigned row = p.row_offset + (unsigned)(cu.n * p.L + cu.c * R + r);
         unsigned hr = dropout_row_hash(p.seed, row);
         if (p.token_mode) {
@@ -138,8 +143,9 @@ template <int N3, int N4>
 __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base, char* xl, int* ids_lds) {
   const int lane = threadIdx.x & 63;
   // ---- weights for this wave's tiles: resident for the whole workgroup lifetime
-  bf16x8 w3[N3][S3];
-  bf16x8 w4[N4][S4];
+  constexpr int A3 = N3 > 0 ? N3 : 1, A4 = N4 > 0 ? N4 : 1;  // array extents (loops use N3/N4)
+  bf16x8 w3[A3][S3];
+  bf16x8 w4[A4][S4];
 #pragma unroll
   for (int i = 0; i < N3; ++i)
 #pragma unroll
@@ -170,8 +176,8 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
   load_ids(p, nxt, tok);
 
   const int nw3 = p.L - 2, nw4 = p.L - 3;  // valid windows per width
-  f32x4 m3[N3], m4[N4];
-  int a3[N3][4], a4[N4][4];
+  f32x4 m3[A3], m4[A4];
+  int a3[A3][4], a4[A4][4];
   auto reset_state = [&]() {
 #pragma unroll
     for (int i = 0; i < N3; ++i) {
@@ -208,17 +214,18 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
     for (int blk = 0; blk < R / 16; ++blk) {
       const int t0 = tc + blk * 16;
       if (t0 >= nw3) break;
-      f32x4 c3[N3], c4[N4];
+      f32x4 c3[A3], c4[A4];
 #pragma unroll
       for (int i = 0; i < N3; ++i) c3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       const char* abase = xl + (blk * 16 + rsub) * ROWB + kq * 16;
+      constexpr int NS = N4 > 0 ? S4 : S3;
       bf16x8 anext = *reinterpret_cast<const bf16x8*>(abase);
 #pragma unroll
-      for (int s = 0; s < S4; ++s) {
+      for (int s = 0; s < NS; ++s) {
         bf16x8 a = anext;  // software-pipelined A fragment (one K-step ahead)
-        if (s + 1 < S4) anext = *reinterpret_cast<const bf16x8*>(abase + (s + 1) * 64);
+        if (s + 1 < NS) anext = *reinterpret_cast<const bf16x8*>(abase + (s + 1) * 64);
         if (s < S3) {
 #pragma unroll
           for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
@@ -228,24 +235,50 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       }
       // running max / argmax; rows of this lane: t0 + 4*kq + r
       const int rowb = t0 + 4 * kq;
-      const bool full = (t0 + 16 <= nw4);
+      if (p.dbg & 2) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rowb + r;
-        const bool v3 = full || row < nw3, v4 = full || row < nw4;
+        for (int i = 0; i < N3; ++i) m3[i] = __builtin_elementwise_max(m3[i], c3[i]);
 #pragma unroll
-        for (int i = 0; i < N3; ++i) {
-          float x = c3[i][r];
-          bool gt = v3 && x > m3[i][r];
-          m3[i][r] = gt ? x : m3[i][r];
-          a3[i][r] = gt ? row : a3[i][r];
+        for (int i = 0; i < N4; ++i) m4[i] = __builtin_elementwise_max(m4[i], c4[i]);
+        continue;
+      }
+      if (t0 + 16 <= nw4) {  // every row valid for both widths (all but the last block)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rowb + r;
+#pragma unroll
+          for (int i = 0; i < N3; ++i) {
+            const float x = c3[i][r];
+            const bool gt = x > m3[i][r];
+            m3[i][r] = gt ? x : m3[i][r];
+            a3[i][r] = gt ? row : a3[i][r];
+          }
+#pragma unroll
+          for (int i = 0; i < N4; ++i) {
+            const float x = c4[i][r];
+            const bool gt = x > m4[i][r];
+            m4[i][r] = gt ? x : m4[i][r];
+            a4[i][r] = gt ? row : a4[i][r];
+          }
         }
+      } else {
 #pragma unroll
-        for (int i = 0; i < N4; ++i) {
-          float x = c4[i][r];
-          bool gt = v4 && x > m4[i][r];
-          m4[i][r] = gt ? x : m4[i][r];
-          a4[i][r] = gt ? row : a4[i][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = rowb + r;
+#pragma unroll
+          for (int i = 0; i < N3; ++i) {
+            const float x = c3[i][r];
+            const bool gt = row < nw3 && x > m3[i][r];
+            m3[i][r] = gt ? x : m3[i][r];
+            a3[i][r] = gt ? row : a3[i][r];
+          }
+#pragma unroll
+          for (int i = 0; i < N4; ++i) {
+            const float x = c4[i][r];
+            const bool gt = row < nw4 && x > m4[i][r];
+            m4[i][r] = gt ? x : m4[i][r];
+            a4[i][r] = gt ? row : a4[i][r];
+          }
         }
       }
     }
@@ -289,15 +322,22 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
   }
 }
 
-__global__ __launch_bounds__(NTHREADS, 1) void conv_pool_fwd_kernel(Params p) {
+__global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[CROWS * ROWB + 2 * CROWS * 4 + 16];
   char* xl = smem;
   int* ids_lds = reinterpret_cast<int*>(smem + CROWS * ROWB);
+  // SIMD s hosts waves s and s+4: per SIMD {3 k3, 2 k4} (56 MFMA/block) or {2 k3, 3 k4} (59)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave == 0) run_wave<3, 2>(p, 0, 0, xl, ids_lds);
-  else if (wave == 1) run_wave<3, 2>(p, 3, 2, xl, ids_lds);
-  else if (wave == 2) run_wave<2, 3>(p, 6, 4, xl, ids_lds);
-  else run_wave<2, 3>(p, 8, 7, xl, ids_lds);
+  switch (wave) {
+    case 0: run_wave<3, 0>(p, 0, 0, xl, ids_lds); break;  // k3 0-2        (30 MFMA / block)
+    case 4: run_wave<0, 2>(p, 0, 0, xl, ids_lds); break;  // k4 0-1        (26)
+    case 1: run_wave<3, 0>(p, 3, 0, xl, ids_lds); break;  // k3 3-5        (30)
+    case 5: run_wave<0, 2>(p, 0, 2, xl, ids_lds); break;  // k4 2-3        (26)
+    case 2: run_wave<0, 2>(p, 0, 4, xl, ids_lds); break;  // k4 4-5        (26)
+    case 6: run_wave<2, 1>(p, 6, 6, xl, ids_lds); break;  // k3 6-7, k4 6  (33)
+    case 3: run_wave<0, 2>(p, 0, 7, xl, ids_lds); break;  // k4 7-8        (26)
+    default: run_wave<2, 1>(p, 8, 9, xl, ids_lds); break; // k3 8-9, k4 9  (33)
+  }
 }
 
 }  // namespace convpool
@@ -349,8 +389,9 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
                             int thr, int token_mode, float scale, int grid, void* stream) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
+  static int dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
   Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
-           seed, row_offset, thr, token_mode, scale};
+           seed, row_offset, thr, token_mode, scale, dbg};
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
   hipLaunchKernelGGL(conv_pool_fwd_kernel, dim3(grid), dim3(NTHREADS), 0, (hipStream_t)stream, p);
