@@ -59,8 +59,11 @@ struct Params {
   int thr;                     // dropout byte threshold (0 = off)
   int token_mode;              // 1: one keep decision per row
   float scale;                 // 1/(1-p)
-  int dbg;                     // diagnostic ablations (0 in production): 1 no gather, 2 max-only epilogue, 4 no dropout hash
 };
+
+// Diagnostic ablations are COMPILE-TIME (template DBG; production instantiation DBG = 0
+// carries no branches): 1 no gather, 2 max-only epilogue, 4 no dropout hash,
+// 8 no A-fragment LDS reads (tools/conv_micro.py times them interleaved in one process).
 
 // fragment base index of tile T in wpack (tiles 0..9 k3 with S3 steps, 10..19 k4 with S4)
 __device__ __forceinline__ int tile_base(int T) {
@@ -90,13 +93,14 @@ __device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int 
 
 // Issue the 16-byte table loads for this thread's pieces of chunk (n,c).
 // tok_of_row(r) reads another thread's id through LDS scratch (ids_lds).
+template <int DBG>
 __device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u32x4 (&v)[PPT]) {
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
     int q = threadIdx.x + i * NTHREADS;
     int r = q / PIECES, pc = q - r * PIECES;
     int tok = (q < CROWS * PIECES) ? ids_lds[r] : -1;
-    if ((p.dbg & 1) == 0 && tok >= 0 && tok < p.V) {
+    if ((DBG & 1) == 0 && tok >= 0 && tok < p.V) {
       v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)tok * EP + pc * 8);
     } else {
       v[i] = u32x4{0u, 0u, 0u, 0u};
@@ -113,16 +117,18 @@ __device__ __forceinline__ unsigned keep_bits_mask(unsigned h, int thr) {
 }
 
 // Apply dropout to the staged pieces and write them into the LDS chunk buffer.
-__device__ __forceinline__ void store_rows(const Params& p, const Cursor& cu, char* xl, u32x4 (&v)[PPT]) {
+// hrow[r] holds the per-row hash of this chunk (computed once per row when its token id
+// was loaded), so each 16-byte piece costs only its two group hashes.
+template <int DBG>
+__device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsigned* hrow, u32x4 (&v)[PPT]) {
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
     int q = threadIdx.x + i * NTHREADS;
     if (q < CROWS * PIECES) {
       int r = q / PIECES, pc = q - r * PIECES;
       u32x4 x = v[i];
-      if (p.thr > 0 && (p.dbg & 4) == 0) {
-        unsigned row = p.row_offset + (unsigned)(cu.n * p.L + cu.c * R + r);
-        unsigned hr = dropout_row_hash(p.seed, row);
+      if ((DBG & 4) == 0 && p.thr > 0) {
+        const unsigned hr = hrow[r];
         if (p.token_mode) {
           unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
           x = x & u32x4{m, m, m, m};
@@ -139,7 +145,13 @@ __device__ __forceinline__ void store_rows(const Params& p, const Cursor& cu, ch
   }
 }
 
-template <int N3, int N4>
+// per-row dropout hash of chunk (n,c) row r (0 when dropout is off)
+__device__ __forceinline__ unsigned row_hash(const Params& p, const Cursor& cu, int r) {
+  if (p.thr <= 0) return 0u;
+  return dropout_row_hash(p.seed, p.row_offset + (unsigned)(cu.n * p.L + cu.c * R + r));
+}
+
+template <int N3, int N4, int PF, int DBG>
 __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base, char* xl, int* ids_lds) {
   const int lane = threadIdx.x & 63;
   // ---- weights for this wave's tiles: resident for the whole workgroup lifetime
@@ -163,17 +175,25 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
   advance(nxt2);
 
   int tok[IDS_PT];
+  unsigned hrw[IDS_PT];
   u32x4 stage[PPT];
-  // prologue: ids of chunk 0 -> LDS, rows of chunk 0 -> regs, ids of chunk 1 -> regs
+  unsigned* hs = reinterpret_cast<unsigned*>(ids_lds + 2 * CROWS);  // 2 x CROWS row hashes
+  int par = 0;
+  // prologue: ids + row hashes of chunk 0 -> LDS, rows of chunk 0 -> regs, ids of chunk 1 -> regs
   load_ids(p, cur, tok);
 #pragma unroll
   for (int i = 0; i < IDS_PT; ++i) {
     int r = threadIdx.x + i * NTHREADS;
-    if (r < CROWS) ids_lds[r] = tok[i];
+    if (r < CROWS) {
+      ids_lds[r] = tok[i];
+      hs[CROWS + r] = row_hash(p, cur, r);
+    }
   }
   __syncthreads();
-  load_rows(p, ids_lds, stage);
+  load_rows<DBG>(p, ids_lds, stage);
   load_ids(p, nxt, tok);
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, nxt, threadIdx.x + i * NTHREADS);
 
   const int nw3 = p.L - 2, nw4 = p.L - 3;  // valid windows per width
   f32x4 m3[A3], m4[A4];
@@ -197,18 +217,24 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
 
   while (cur.n < p.N) {
     __syncthreads();  // previous chunk's LDS reads are complete
-    store_rows(p, cur, xl, stage);
+    store_rows<DBG>(p, xl, hs + (par ^ 1) * CROWS, stage);
 #pragma unroll
     for (int i = 0; i < IDS_PT; ++i) {
       int r = threadIdx.x + i * NTHREADS;
-      if (r < CROWS) ids_lds[CROWS + r] = tok[i];  // ids of `nxt` into the second id slot
+      if (r < CROWS) {
+        ids_lds[CROWS + r] = tok[i];     // ids of `nxt` (consumed by load_rows below)
+        hs[par * CROWS + r] = hrw[i];    // row hashes of `nxt` (consumed by the next store_rows)
+      }
     }
     __syncthreads();
-    // prefetch: rows of nxt (ids already in LDS slot 2), ids of nxt2
-    load_rows(p, ids_lds + CROWS, stage);
+    // prefetch: rows of nxt (ids already in LDS slot 2), ids + row hashes of nxt2
+    load_rows<DBG>(p, ids_lds + CROWS, stage);
     load_ids(p, nxt2, tok);
+#pragma unroll
+    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, nxt2, threadIdx.x + i * NTHREADS);
+    par ^= 1;
 
-    // ---- MFMA phase over the 4 row blocks of this chunk
+    // ---- MFMA phase over the row blocks of this chunk
     const int tc = cur.c * R;
 #pragma unroll 1
     for (int blk = 0; blk < R / 16; ++blk) {
@@ -221,11 +247,17 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       const char* abase = xl + (blk * 16 + rsub) * ROWB + kq * 16;
       constexpr int NS = N4 > 0 ? S4 : S3;
-      bf16x8 anext = *reinterpret_cast<const bf16x8*>(abase);
+      // A fragments software-pipelined PF K-steps ahead (ds_read_b128 latency vs 2-3 MFMAs per step)
+      constexpr bool noread = (DBG & 8) != 0;
+      bf16x8 ab[PF];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) ab[u] = *reinterpret_cast<const bf16x8*>(abase + u * 64);
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        bf16x8 a = anext;  // software-pipelined A fragment (one K-step ahead)
-        if (s + 1 < NS) anext = *reinterpret_cast<const bf16x8*>(abase + (s + 1) * 64);
+        bf16x8 a = ab[0];
+#pragma unroll
+        for (int u = 0; u + 1 < PF; ++u) ab[u] = ab[u + 1];
+        if (s + PF < NS && !noread) ab[PF - 1] = *reinterpret_cast<const bf16x8*>(abase + (s + PF) * 64);
         if (s < S3) {
 #pragma unroll
           for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
@@ -235,7 +267,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       }
       // running max / argmax; rows of this lane: t0 + 4*kq + r
       const int rowb = t0 + 4 * kq;
-      if (p.dbg & 2) {
+      if constexpr ((DBG & 2) != 0) {
 #pragma unroll
         for (int i = 0; i < N3; ++i) m3[i] = __builtin_elementwise_max(m3[i], c3[i]);
 #pragma unroll
@@ -322,21 +354,22 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
   }
 }
 
+template <int PF, int DBG>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd_kernel(Params p) {
-  __shared__ __attribute__((aligned(16))) char smem[CROWS * ROWB + 2 * CROWS * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[CROWS * ROWB + 4 * CROWS * 4 + 16];
   char* xl = smem;
   int* ids_lds = reinterpret_cast<int*>(smem + CROWS * ROWB);
   // SIMD s hosts waves s and s+4: per SIMD {3 k3, 2 k4} (56 MFMA/block) or {2 k3, 3 k4} (59)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   switch (wave) {
-    case 0: run_wave<3, 0>(p, 0, 0, xl, ids_lds); break;  // k3 0-2        (30 MFMA / block)
-    case 4: run_wave<0, 2>(p, 0, 0, xl, ids_lds); break;  // k4 0-1        (26)
-    case 1: run_wave<3, 0>(p, 3, 0, xl, ids_lds); break;  // k3 3-5        (30)
-    case 5: run_wave<0, 2>(p, 0, 2, xl, ids_lds); break;  // k4 2-3        (26)
-    case 2: run_wave<0, 2>(p, 0, 4, xl, ids_lds); break;  // k4 4-5        (26)
-    case 6: run_wave<2, 1>(p, 6, 6, xl, ids_lds); break;  // k3 6-7, k4 6  (33)
-    case 3: run_wave<0, 2>(p, 0, 7, xl, ids_lds); break;  // k4 7-8        (26)
-    default: run_wave<2, 1>(p, 8, 9, xl, ids_lds); break; // k3 8-9, k4 9  (33)
+    case 0: run_wave<3, 0, PF, DBG>(p, 0, 0, xl, ids_lds); break;  // k3 0-2        (30 MFMA / block)
+    case 4: run_wave<0, 2, PF, DBG>(p, 0, 0, xl, ids_lds); break;  // k4 0-1        (26)
+    case 1: run_wave<3, 0, PF, DBG>(p, 3, 0, xl, ids_lds); break;  // k3 3-5        (30)
+    case 5: run_wave<0, 2, PF, DBG>(p, 0, 2, xl, ids_lds); break;  // k4 2-3        (26)
+    case 2: run_wave<0, 2, PF, DBG>(p, 0, 4, xl, ids_lds); break;  // k4 4-5        (26)
+    case 6: run_wave<2, 1, PF, DBG>(p, 6, 6, xl, ids_lds); break;  // k3 6-7, k4 6  (33)
+    case 3: run_wave<0, 2, PF, DBG>(p, 0, 7, xl, ids_lds); break;  // k4 7-8        (26)
+    default: run_wave<2, 1, PF, DBG>(p, 8, 9, xl, ids_lds); break; // k3 8-9, k4 9  (33)
   }
 }
 
@@ -384,17 +417,33 @@ PV_API int pv_conv_packed_size() {
   return (NT * S3 + NT * S4) * 64 * 8;  // bf16 elements
 }
 
+// Diagnostic ablation switch (tools/conv_micro.py): 0 in production.
+static int g_conv_dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
+PV_API void pv_conv_set_dbg(int d) { g_conv_dbg = d; }
+
 PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack, const float* bias,
                             float* pooled, int* argmax, int N, int L, int V, unsigned seed, unsigned row_offset,
                             int thr, int token_mode, float scale, int grid, void* stream) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
-  static int dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
+  const int dbg = g_conv_dbg;
   Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
-           seed, row_offset, thr, token_mode, scale, dbg};
+           seed, row_offset, thr, token_mode, scale};
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
-  hipLaunchKernelGGL(conv_pool_fwd_kernel, dim3(grid), dim3(NTHREADS), 0, (hipStream_t)stream, p);
+  hipStream_t st = (hipStream_t)stream;
+#define PV_CONV_LAUNCH(PFV, DV) \
+  hipLaunchKernelGGL((conv_pool_fwd_kernel<PFV, DV>), dim3(grid), dim3(NTHREADS), 0, st, p)
+  switch (dbg) {
+    case 0: PV_CONV_LAUNCH(2, 0); break;   // production
+    case 16: PV_CONV_LAUNCH(1, 0); break;  // A prefetch depth 1
+    case 2: PV_CONV_LAUNCH(2, 2); break;
+    case 4: PV_CONV_LAUNCH(2, 4); break;
+    case 7: PV_CONV_LAUNCH(2, 7); break;
+    case 15: PV_CONV_LAUNCH(2, 15); break;
+    default: return -3;
+  }
+#undef PV_CONV_LAUNCH
   PV_LAUNCH_CHECK();
   return 0;
 }

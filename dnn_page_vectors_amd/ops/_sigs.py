@@ -11,6 +11,7 @@ SIGS = {
     # conv_pool_fwd.hip
     "pv_conv_pack_weights": "ppipp",
     "pv_conv_packed_size": "",
+    "pv_conv_set_dbg": "i",
     "pv_conv_pool_fwd": "pppppp" "iii" "uu" "ii" "f" "i" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "uuiif" "p",
