@@ -203,10 +203,13 @@ __global__ __launch_bounds__(256) void conv_bwd_emit_kernel(const float* gpool, 
 // ---- dTable: reduce over sorted entries ----------------------------------------------
 // One wave per chunk of 64 sorted entries.  The entry metadata is loaded lane-parallel
 // (lane i <- entry b+i: key, f/j, g, row hash) so the per-entry loop has no dependent
-// global loads: it broadcasts the entry with v_readlane (uniform loop index), fetches the
-// two W values of this lane's columns (e = lane, lane+64; W is L2-resident) four entries
-// ahead, applies the regenerated dropout bit and sums in registers.  A token's run that
-// crosses a chunk boundary is closed with one row of fp32 atomics per chunk.
+// global loads: entries are broadcast with v_readlane (uniform loop index) and lane l owns
+// the contiguous columns e = l, l+64 (coalesced W loads and row atomics).
+// Dropout bits: an entry needs ceil(E/4) group hashes; per PAIR of entries each lane of
+// half h computes the group hash (lane&31) of entry j0+h (one mix32 for two entries),
+// and the lanes fetch their groups' hashes with ds_bpermute — instead of every lane
+// hashing both of its columns for every entry.  W values are fetched for 8 entries
+// before they are used (W is L2-resident).
 __global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __restrict__ skeys,
                                                               const unsigned* __restrict__ svals,
                                                               const unsigned* __restrict__ erow,
@@ -231,29 +234,46 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __
       if (thr > 0) hr = dropout_row_hash(seed, row_offset + erow[idx]);
     }
   }
-  // number of live entries in this chunk (keys are sorted: sentinels are at the end)
   const unsigned long long live = __ballot(key < (unsigned)V);
-  const int n = __popcll(live);
+  const int n = __popcll(live);  // sorted: live entries are a prefix of the chunk
   if (n == 0) return;
   const int c0 = lane, c1 = lane + 64;
   const bool h0 = c0 < E, h1 = c1 < E;
+  // bpermute byte addresses of the lanes holding my two groups' hashes (per half)
+  const int src0 = (c0 >> 2) * 4, src1 = ((c1 >> 2) & 31) * 4 + (c1 >= 128 ? 0 : 0);
+  const int sh0 = 8 * (c0 & 3), sh1 = 8 * (c1 & 3);
   unsigned cur = __builtin_amdgcn_readfirstlane(key);
   float s0 = 0.f, s1 = 0.f;
-  auto wrow = [&](unsigned f_j) -> const float* {
-    const int f = (int)(f_j >> 2), j = (int)(f_j & 3);
-    return f < FW ? (w3 + ((size_t)f * 3 + j) * E) : (w4 + ((size_t)(f - FW) * 4 + j) * E);
-  };
-  for (int j0 = 0; j0 < n; j0 += 4) {
-    float wv0[4], wv1[4];
+  for (int j0 = 0; j0 < n; j0 += 8) {
+    float wv0[8], wv1[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int jj = min(j0 + u, n - 1);
-      const float* w = wrow((unsigned)__builtin_amdgcn_readlane((int)fj, jj));
+      const unsigned f_j = (unsigned)__builtin_amdgcn_readlane((int)fj, jj);
+      const int f = (int)(f_j >> 2), j = (int)(f_j & 3);
+      const float* w = f < FW ? (w3 + ((size_t)f * 3 + j) * E) : (w4 + ((size_t)(f - FW) * 4 + j) * E);
       wv0[u] = h0 ? w[c0] : 0.f;
       wv1[u] = h1 ? w[c1] : 0.f;
     }
+    unsigned hv[8];
+    if (thr > 0 && !token_mode) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; u += 2) {
+        const int ja = min(j0 + u, n - 1), jb = min(j0 + u + 1, n - 1);
+        const unsigned ha = (unsigned)__builtin_amdgcn_readlane((int)hr, ja);
+        const unsigned hb = (unsigned)__builtin_amdgcn_readlane((int)hr, jb);
+        const unsigned gh = dropout_group_hash(lane < 32 ? ha : hb, (unsigned)(lane & 31));
+        // entry A's groups live in lanes 0..31, entry B's in lanes 32..63
+        const unsigned a0 = (unsigned)__builtin_amdgcn_ds_bpermute(src0, (int)gh);
+        const unsigned a1 = (unsigned)__builtin_amdgcn_ds_bpermute(src1, (int)gh);
+        const unsigned b0 = (unsigned)__builtin_amdgcn_ds_bpermute(src0 + 128, (int)gh);
+        const unsigned b1 = (unsigned)__builtin_amdgcn_ds_bpermute(src1 + 128, (int)gh);
+        hv[u] = (((a0 >> sh0) & 0xFF) << 8) | ((a1 >> sh1) & 0xFF);
+        hv[u + 1] = (((b0 >> sh0) & 0xFF) << 8) | ((b1 >> sh1) & 0xFF);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
       const int jj = j0 + u;
       if (jj >= n) break;
       const unsigned k = (unsigned)__builtin_amdgcn_readlane((int)key, jj);
@@ -266,9 +286,15 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __
       const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), jj));
       float v0 = gj * wv0[u], v1 = gj * wv1[u];
       if (thr > 0) {
-        const unsigned hj = (unsigned)__builtin_amdgcn_readlane((int)hr, jj);
-        if ((int)mask_byte(hj, c0, token_mode) < thr) v0 = 0.f;
-        if ((int)mask_byte(hj, c1, token_mode) < thr) v1 = 0.f;
+        unsigned m0, m1;
+        if (token_mode) {
+          m0 = m1 = (unsigned)__builtin_amdgcn_readlane((int)hr, jj) & 0xFF;
+        } else {
+          m0 = hv[u] >> 8;
+          m1 = hv[u] & 0xFF;
+        }
+        if ((int)m0 < thr) v0 = 0.f;
+        if ((int)m1 < thr) v1 = 0.f;
       }
       s0 += v0;
       s1 += v1;
