@@ -1,0 +1,208 @@
+"""Command line: ``python -m dnn_page_vectors_amd {setup,train,encode,eval,bench}``.
+
+The reference has no CLI — each script runs at module level with hard-coded settings
+(SURVEY §5.6).  Every subcommand here takes ``--preset``, ``--config file.yaml`` and
+``--set key=value`` overrides of the Configuration fields (config.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+from typing import List, Optional
+
+log = logging.getLogger("pagevec")
+
+
+def _config(a):
+    from .config import Configuration, preset_config
+
+    if a.config:
+        cfg = Configuration.from_yaml(a.config)
+    elif a.preset:
+        cfg = preset_config(a.preset)
+    else:
+        cfg = Configuration()
+    if a.set:
+        cfg = cfg.override(a.set)
+    return cfg
+
+
+def _common(p):
+    p.add_argument("--preset", default=None)
+    p.add_argument("--config", default=None)
+    p.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
+
+
+def cmd_setup(a) -> int:
+    from .experiment import SetupExperiment
+
+    cfg = _config(a)
+    exp = SetupExperiment(cfg)
+    exp.create_workspace()
+    if a.input:
+        exp.import_dataset(a.input, link=a.link)
+    if os.path.exists(cfg.input_dataset):
+        nt, nv = exp.split_dataset_file()
+        log.info("split: %d train / %d validation rows", nt, nv)
+        if cfg.vocab_hash_size <= 1:
+            v = exp.build_vocabulary()
+            log.info("vocabulary: %d tokens", len(v))
+    cfg.save_json(os.path.join(cfg.data_path, "config.json"))
+    print(json.dumps({"data_path": cfg.data_path}))
+    return 0
+
+
+def _featurizer(cfg):
+    from .data.featurize import Featurizer
+
+    if cfg.vocab_hash_size > 1:
+        return Featurizer(cfg.feature_level, hash_size=cfg.vocab_hash_size)
+    from .io.vocab import load_vocab
+
+    return Featurizer(cfg.feature_level, vocab=load_vocab(cfg))
+
+
+def cmd_train(a) -> int:
+    import torch
+
+    from .data.dataset import JsonlPairDataset, PairLoader, SyntheticLoader
+    from .data.synthetic import SyntheticPairs, spec_from_config
+    from .io import checkpoint as ck
+    from .models import build_model
+    from .ops._common import set_backend
+    from .parallel import dist as pdist
+    from .train.trainer import Trainer
+    from .utils.metrics import MetricsLogger
+
+    cfg = _config(a)
+    info = pdist.init_distributed()
+    if cfg.backend != "auto":
+        set_backend(cfg.backend)
+    torch.manual_seed(cfg.seed)
+    if a.synthetic:
+        V = cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000
+        gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=a.synthetic_pages), info.device,
+                             seed=cfg.seed + info.rank)
+        steps = max(1, cfg.num_train_samples // (cfg.batch_size * info.world_size))
+        train_loader = SyntheticLoader(gen, cfg.batch_size, steps)
+        val_loader = SyntheticLoader(gen, cfg.batch_size, max(1, cfg.num_validation_samples // cfg.batch_size))
+    else:
+        fz = _featurizer(cfg)
+        V = fz.num_ids
+        tr = JsonlPairDataset(cfg.model_training_data, fz, cfg.query_length, cfg.document_length,
+                              cfg.num_negative_examples)
+        va = JsonlPairDataset(cfg.model_validation_data, fz, cfg.query_length, cfg.document_length,
+                              cfg.num_negative_examples)
+        train_loader = PairLoader(tr, cfg.batch_size, shuffle=a.shuffle, seed=cfg.seed, rank=info.rank,
+                                  world_size=info.world_size, prefetch=cfg.prefetch, device=info.device)
+        val_loader = PairLoader(va, cfg.batch_size, rank=info.rank, world_size=info.world_size,
+                                device=info.device)
+        steps = min(train_loader.num_batches(), max(1, cfg.num_train_samples // (cfg.batch_size * info.world_size)))
+    model = build_model(cfg, V)
+    if cfg.feature_level == "word" and cfg.vocab_hash_size <= 1 and os.path.exists(cfg.word_vectors_file):
+        from .io.vectors import cached_word_vectors, init_embedding_
+        from .io.vocab import load_vocab
+
+        W = cached_word_vectors(cfg, load_vocab(cfg))
+        for t in [model.query_tower, *model.doc_towers]:
+            init_embedding_(t.embedding, W)
+    metrics = MetricsLogger(os.path.join(cfg.trained_model_dir, "metrics.jsonl"), enabled=info.is_main)
+    trainer = Trainer(cfg, model, info.device, metrics)
+    if a.resume and ck.resume(trainer, cfg.trained_model_dir):
+        log.info("resumed at epoch %d step %d", trainer.epoch, trainer.step)
+    hist = trainer.fit(lambda ep: train_loader.epoch_iter(ep), steps_per_epoch=steps,
+                       validation_batches=lambda ep: val_loader.epoch_iter(0),
+                       callbacks=[ck.ModelCheckpoint(cfg.trained_model_dir)])
+    ck.save_final(trainer, cfg.trained_model_dir)
+    if info.is_main:
+        print(json.dumps({"history": hist, "model_dir": cfg.trained_model_dir}))
+    pdist.destroy()
+    return 0
+
+
+def cmd_encode(a) -> int:
+    import numpy as np
+    import torch
+
+    from .io import checkpoint as ck
+    from .models import build_model
+
+    cfg = _config(a)
+    dev = torch.device("cuda" if torch.cuda.device_count() > 0 else "cpu")
+    fz = _featurizer(cfg)
+    model = build_model(cfg, fz.num_ids).to(dev)
+    ck.load_weights(model, a.weights or os.path.join(cfg.trained_model_dir, ck.FINAL_WEIGHTS))
+    with open(a.input, encoding="utf-8") as f:
+        texts = [l.rstrip("\n") for l in f]
+    L = cfg.query_length if a.tower == "query" else cfg.document_length
+    ids = torch.from_numpy(fz(texts, L)).to(dev)
+    vec = model.encode(ids, a.tower).float().cpu().numpy()
+    np.save(a.output, vec)
+    print(json.dumps({"vectors": a.output, "shape": list(vec.shape)}))
+    return 0
+
+
+def cmd_eval(a) -> int:
+    import torch
+
+    from .data.synthetic import SyntheticPairs, spec_from_config
+    from .eval.retrieval import recall_table
+    from .io import checkpoint as ck
+    from .models import build_model
+
+    cfg = _config(a)
+    dev = torch.device("cuda" if torch.cuda.device_count() > 0 else "cpu")
+    V = cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000
+    model = build_model(cfg, V).to(dev)
+    if a.weights:
+        ck.load_weights(model, a.weights)
+    gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=1024), dev, seed=cfg.seed)
+    q, p = gen.eval_set(a.pages)
+    r = recall_table(model.encode(q, "query"), model.encode(p, "doc"), torch.arange(a.pages, device=dev))
+    print(json.dumps(r))
+    return 0
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    from .log import setup_logging
+
+    setup_logging()
+    ap = argparse.ArgumentParser(prog="dnn_page_vectors_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("setup", help="create the workspace, import + split the dataset, build the vocab")
+    _common(p)
+    p.add_argument("--input", default=None, help="local JSONL dataset to import")
+    p.add_argument("--link", action="store_true")
+    p.set_defaults(fn=cmd_setup)
+    p = sub.add_parser("train")
+    _common(p)
+    p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--synthetic-pages", type=int, default=65536)
+    p.add_argument("--shuffle", action="store_true")
+    p.add_argument("--resume", action="store_true")
+    p.set_defaults(fn=cmd_train)
+    p = sub.add_parser("encode")
+    _common(p)
+    p.add_argument("--input", required=True)
+    p.add_argument("--output", required=True)
+    p.add_argument("--tower", default="doc", choices=["doc", "query"])
+    p.add_argument("--weights", default=None)
+    p.set_defaults(fn=cmd_encode)
+    p = sub.add_parser("eval")
+    _common(p)
+    p.add_argument("--weights", default=None)
+    p.add_argument("--pages", type=int, default=2048)
+    p.set_defaults(fn=cmd_eval)
+    p = sub.add_parser("bench", help="run bench.py (headline benchmark)")
+    p.add_argument("rest", nargs=argparse.REMAINDER)
+    p.set_defaults(fn=lambda a: __import__("subprocess").call([sys.executable, os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")] + a.rest))
+    a = ap.parse_args(argv)
+    return int(a.fn(a) or 0)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

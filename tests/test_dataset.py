@@ -1,0 +1,69 @@
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from dnn_page_vectors_amd.data import text as T
+from dnn_page_vectors_amd.data.dataset import JsonlPairDataset, PairLoader
+from dnn_page_vectors_amd.data.featurize import Featurizer
+
+
+def _write(tmp_path, n=37, bad_every=5):
+    rows = []
+    for i in range(n):
+        negs = [f"neg {i} a", f"neg {i} b ü", f"neg {i} c"] if (i % bad_every) != bad_every - 1 else [f"only {i}"]
+        rows.append({"q": f"Query {i}!", "doc_corr": f"Page about {i}, \"quoted\" \\ backslash é",
+                     "doc_incorr": negs, "extra": {"nested": [1, 2, {"x": "y"}]}})
+    p = tmp_path / "data.jsonl"
+    p.write_text("\n".join(json.dumps(r) for r in rows) + "\n\n")
+    return str(p), rows
+
+
+def test_native_dataset_reads_and_skips(tmp_path):
+    path, rows = _write(tmp_path)
+    fz = Featurizer("char", hash_size=997)
+    ds = JsonlPairDataset(path, fz, 12, 30, 3)
+    good = [r for r in rows if len(r["doc_incorr"]) == 3]
+    assert len(ds) == len(good) and ds.skipped == len(rows) - len(good)
+    q, d = ds.batch(np.arange(len(ds)))
+    assert q.shape == (len(good), 12) and d.shape == (len(good), 4, 30)
+    for i, r in enumerate(good):
+        np.testing.assert_array_equal(q[i], T.featurize_py([r["q"]], "char", 12, hash_size=997)[0])
+        texts = [r["doc_corr"]] + r["doc_incorr"]
+        np.testing.assert_array_equal(d[i], np.array(T.featurize_py(texts, "char", 30, hash_size=997)))
+    assert ds.texts(0)[1] == good[0]["doc_corr"]
+
+
+def test_loader_sequential_shuffle_shard_resume(tmp_path):
+    path, rows = _write(tmp_path, n=64, bad_every=1000)
+    fz = Featurizer("word", hash_size=101)
+    ds = JsonlPairDataset(path, fz, 5, 9, 3)
+    seq = [q for q, _ in PairLoader(ds, 8).epoch_iter()]
+    assert len(seq) == 8
+    ref_q, _ = ds.batch(np.arange(8))
+    assert torch.equal(seq[0], torch.from_numpy(ref_q))
+    sh = PairLoader(ds, 8, shuffle=True, seed=3)
+    a = [q for q, _ in sh.epoch_iter(0)]
+    b = [q for q, _ in PairLoader(ds, 8, shuffle=True, seed=3).epoch_iter(0)]
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    assert not all(torch.equal(x, y) for x, y in zip(a, seq))
+    # rank shards are disjoint halves
+    r0 = torch.cat([q for q, _ in PairLoader(ds, 8, rank=0, world_size=2).epoch_iter()])
+    r1 = torch.cat([q for q, _ in PairLoader(ds, 8, rank=1, world_size=2).epoch_iter()])
+    assert r0.shape[0] == r1.shape[0] == 32 and not torch.equal(r0, r1)
+    # resume mid-epoch
+    ld = PairLoader(ds, 8, shuffle=True, seed=3)
+    it = ld.epoch_iter(0)
+    first = [next(it) for _ in range(3)]
+    st = ld.state()
+    it.close()
+    ld2 = PairLoader(ds, 8, shuffle=True, seed=3)
+    ld2.load_state(st)
+    rest = [q for q, _ in ld2.epoch_iter()]
+    assert len(rest) == 5 and torch.equal(rest[0], a[3])
+
+
+def test_dataset_missing_file(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        JsonlPairDataset(str(tmp_path / "nope.jsonl"), Featurizer("char", hash_size=10), 4, 4, 3)

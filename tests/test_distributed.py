@@ -1,0 +1,115 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2) — the fake cluster of SURVEY §4.2.
+
+* all_gather_autograd: summed gradients of every rank's loss w.r.t. its local page
+  vectors equal the single-process gradient of the summed loss (backward = reduce-scatter).
+* DP training (bucketed all-reduce): 2 ranks x B/2 == 1 process x B after 3 steps, for
+  the explicit-negative and the cross-GPU in-batch loss.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+
+
+def _gather_worker(rank, world, port, q):
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.parallel import dist as pdist
+
+    pdist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    X = torch.randn(world * 3, 5)
+    local = X[rank * 3:(rank + 1) * 3].clone().requires_grad_(True)
+    g = pdist.all_gather_autograd(local)
+    w = torch.arange(g.numel(), dtype=torch.float32).view_as(g) * (rank + 1)
+    (g * w).sum().backward()
+    q.put((rank, local.grad.clone()))
+    pdist.destroy()
+
+
+def test_all_gather_autograd_gloo():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=120) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    base = torch.arange(world * 3 * 5, dtype=torch.float32).view(world * 3, 5)
+    full = base * 1 + base * 2  # sum over ranks of d(sum(g*w_r))/dg
+    for r in range(world):
+        torch.testing.assert_close(res[r], full[r * 3:(r + 1) * 3])
+
+
+def _cfg(mode, B):
+    from dnn_page_vectors_amd.config import Configuration
+
+    return Configuration(feature_level="ngram", vocab_hash_size=150, query_length=8, document_length=16,
+                         batch_size=B, embedding_dim=12, hidden_dims=16, dropout_prob=(0.0, 0.5), loss_mode=mode,
+                         grad_bucket_mb=0.05)
+
+
+def _data(B):
+    g = torch.Generator().manual_seed(42)
+    out = []
+    for _ in range(3):
+        q = torch.randint(1, 150, (B, 8), generator=g, dtype=torch.int32)
+        d = torch.randint(1, 150, (B, 4, 16), generator=g, dtype=torch.int32)
+        out.append((q, d))
+    return out
+
+
+def _dp_worker(rank, world, port, mode, q):
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed(device="cpu")
+    B = 8
+    cfg = _cfg(mode, B // world)
+    tr = Trainer(cfg, CDSSM(cfg, 150))
+    assert len(tr.buckets.buckets) > 1  # several buckets, launched from grad hooks
+    for qa, da in _data(B):
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+        tr.train_step(qa[sl], da[sl])
+    q.put((rank, tr.flat.data.clone()))
+    pdist.destroy()
+
+
+@pytest.mark.parametrize("mode", ["explicit", "cross_gpu"])
+def test_data_parallel_matches_single_process(mode):
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dp_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=300) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    # single process reference (cross_gpu with one rank == in-batch over the whole batch)
+    pdist.set_info(pdist.DistInfo())
+    cfg = _cfg("in_batch" if mode == "cross_gpu" else mode, 8)
+    tr = Trainer(cfg, CDSSM(cfg, 150))
+    for qa, da in _data(8):
+        tr.train_step(qa, da)
+    torch.testing.assert_close(res[0], res[1], rtol=0, atol=0)
+    torch.testing.assert_close(res[0], tr.flat.data, rtol=1e-4, atol=3e-5)  # Adam amplifies summation-order noise
