@@ -83,6 +83,7 @@ class Configuration:
 
     # MLP tower (config 1 / 3): trigram bag -> dense stack
     mlp_dims: Tuple[int, ...] = (512, 512, 128)
+    mlp_act: str = "tanh"                 # DSSM hidden activation (tanh | relu)
     # BERT dual encoder (config 4)
     bert_layers: int = 12
     bert_hidden: int = 768
@@ -279,8 +280,8 @@ def preset_config(name: str) -> Configuration:
         # Tiny 3-layer DSSM, 1k tri-gram hash, batch 32 on CPU
         return Configuration(model="mlp", feature_level="ngram", vocab_hash_size=1024,
                              embedding_dim=300, mlp_dims=(300, 300, 128), batch_size=32,
-                             query_length=45, document_length=256, nb_epoch=1,
-                             num_train_samples=1024, num_validation_samples=256)
+                             query_length=45, document_length=256, nb_epoch=1, loss_mode="in_batch",
+                             cos_clip=False, lr=3e-3, J=0, num_train_samples=1024, num_validation_samples=256)
     if name in ("cdssm_ngram_bf16", "config2"):
         # CDSSM 1D-conv 300d, 30k hashed tri-grams, bf16, batch 4096 on 1 MI355X
         return Configuration(model="cdssm", feature_level="ngram", vocab_hash_size=30000,
@@ -289,7 +290,7 @@ def preset_config(name: str) -> Configuration:
         # Two-tower MLP 512-512-128, cross-GPU in-batch negatives via all-gather
         return Configuration(model="mlp", feature_level="ngram", vocab_hash_size=30000,
                              embedding_dim=512, mlp_dims=(512, 512, 128), batch_size=4096,
-                             dtype="bf16", loss_mode="cross_gpu", J=0)
+                             dtype="bf16", loss_mode="cross_gpu", J=0, cos_clip=False, lr=3e-3)
     if name in ("bert_dp8", "config4"):
         return Configuration(model="bert", feature_level="word", vocab_hash_size=30522,
                              query_length=32, document_length=256, batch_size=64,

@@ -16,7 +16,7 @@ namespace dense {
 constexpr int BM = 64, BN = 64, BK = 32;
 constexpr int LDA = BK + 8;  // bf16 elements per LDS row (80 B: 16-B aligned, staggers banks)
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3 };
 
 __device__ __forceinline__ float act_fn(float x, int act) {
   if (act == ACT_RELU) return x > 0.f ? x : 0.f;
@@ -25,6 +25,7 @@ __device__ __forceinline__ float act_fn(float x, int act) {
     float u = k0 * (x + k1 * x * x * x);
     return 0.5f * x * (1.f + tanhf(u));
   }
+  if (act == ACT_TANH) return tanhf(x);
   return x;
 }
 
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
   for (int d = lane; d < D; d += 64) dx[(size_t)row * D + d] = clamped ? gr[d] * inv : (gr[d] - yr[d] * s) * inv;
 }
 
-// dz = dy * act'(y) (in place allowed); relu: y > 0 ; none: 1
+// dz = dy * act'(y) (in place allowed); relu: y > 0 ; tanh: 1 - y^2 ; none: 1
 __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy, float* __restrict__ dz,
                                long n, int act) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -156,6 +157,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restr
   for (; i < n; i += stride) {
     float g = dy[i];
     if (act == ACT_RELU) g = y[i] > 0.f ? g : 0.f;
+    else if (act == ACT_TANH) g = g * (1.f - y[i] * y[i]);
     dz[i] = g;
   }
 }

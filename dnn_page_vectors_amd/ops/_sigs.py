@@ -31,6 +31,13 @@ SIGS = {
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_transpose_bf16": "pp" "ii" "p",
+    # embedding.hip
+    "pv_trigram_hash": "ppp" "iiii" "p",
+    "pv_embedding_bag": "pppp" "iiiiii" "p",
+    "pv_bag_counts": "ppp" "iiiii" "p",
+    # topk.hip
+    "pv_topk_splits": "ii",
+    "pv_topk_cos": "pppppp" "iiiii" "p",
     # optim.hip
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",

@@ -14,7 +14,7 @@ import torch
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
-_ACT = {"none": 0, "relu": 1, "gelu": 2}
+_ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 
 
 class _LinearActFn(torch.autograd.Function):
@@ -32,7 +32,7 @@ class _LinearActFn(torch.autograd.Function):
         wdt = 1 if wc.dtype == torch.bfloat16 else 0
         check(lib().pv_linear_act(P(x2), xdt, P(wc), wdt, P(b) if b is not None else None, P(y), None, M, N, K, K, N,
                                   _ACT[act], stream(x.device)), "pv_linear_act")
-        ctx.save_for_backward(x2, w, y if act == "relu" else None, b)
+        ctx.save_for_backward(x2, w, y if act in ("relu", "tanh") else None, b)
         ctx.act = act
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], N)
@@ -41,9 +41,9 @@ class _LinearActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, y, b = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous().float()
-        if ctx.act == "relu":
+        if ctx.act in ("relu", "tanh"):
             dz = torch.empty_like(dy2)
-            check(lib().pv_act_bwd(P(y), P(dy2), P(dz), dy2.numel(), 1, stream(dy.device)), "pv_act_bwd")
+            check(lib().pv_act_bwd(P(y), P(dy2), P(dz), dy2.numel(), _ACT[ctx.act], stream(dy.device)), "pv_act_bwd")
         elif ctx.act == "none":
             dz = dy2
         else:  # gelu: recompute pre-activation (rare path; BERT uses torch GEMM + gelu kernel instead)

@@ -106,6 +106,8 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act:
         return torch.relu(y)
     if act == "gelu":
         return F.gelu(y, approximate="tanh")
+    if act == "tanh":
+        return torch.tanh(y)
     if act == "none":
         return y
     raise ValueError(act)

@@ -42,5 +42,9 @@ def _topk_hip(qn, pn, k):
     pb[:, :D] = pn
     vals = torch.empty(B, k, dtype=torch.float32, device=qn.device)
     idx = torch.empty(B, k, dtype=torch.int32, device=qn.device)
-    check(lib().pv_topk_cos(P(qb), P(pb), P(vals), P(idx), B, N, DP, k, stream(qn.device)), "pv_topk_cos")
+    ns = int(lib().pv_topk_splits(B, N))
+    pv = torch.full((B, ns, 4, 16), float("-inf"), dtype=torch.float32, device=qn.device)
+    pi = torch.full((B, ns, 4, 16), -1, dtype=torch.int32, device=qn.device)
+    check(lib().pv_topk_cos(P(qb), P(pb), P(vals), P(idx), P(pv), P(pi), B, N, DP, k, ns, stream(qn.device)),
+          "pv_topk_cos")
     return vals, idx.long()

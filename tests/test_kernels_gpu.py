@@ -213,3 +213,68 @@ def test_cdssm_train_step_gpu():
             losses.append(float(tr.train_step(q, d)["loss"]))
         assert all(l == l for l in losses)
         assert sum(losses[-5:]) < sum(losses[:5])
+
+
+@pytest.mark.parametrize("plan,L,E", [("gather", 45, 512), ("counts", 300, 512), ("gather", 20, 64), ("counts", 20, 72)])
+def test_embedding_bag(plan, L, E):
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    V, N = 1000, 33
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    ids[:, L // 2:] = 0
+    W = bf(torch.randn(V, E, device=DEV)).requires_grad_(True)
+    Wr = W.detach().clone().requires_grad_(True)
+    out = eops.embedding_bag(ids, W, pad=0, mean=True, plan=plan)
+    cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
+    outr = ref.embedding_bag_sum(ids, Wr, 0) / cnt
+    torch.testing.assert_close(out, outr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    (outr * g).sum().backward()
+    torch.testing.assert_close(W.grad, Wr.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_trigram_hash_device():
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    texts = [b"statue of liberty", b"ab", b"new york city tour"]
+    Lmax = 24
+    buf = torch.zeros(len(texts), Lmax, dtype=torch.uint8)
+    for i, t in enumerate(texts):
+        buf[i, :len(t)] = torch.tensor(list(t), dtype=torch.uint8)
+    lens = torch.tensor([len(t) for t in texts], dtype=torch.int32)
+    got = eops.trigram_hash(buf.to(DEV), lens.to(DEV), 20, 30000).cpu()
+    want = ref.fnv1a_trigram_ids(buf, lens, 20, 30000)
+    assert torch.equal(got, want)
+    from dnn_page_vectors_amd.data import text as T
+
+    host = T.featurize_py([t.decode() for t in texts], "ngram", 20, hash_size=30000)
+    assert got.tolist() == host
+
+
+@pytest.mark.parametrize("B,N,D,k", [(100, 5000, 150, 10), (7, 300, 128, 16), (64, 64, 64, 1)])
+def test_topk_hip_exact(B, N, D, k):
+    from dnn_page_vectors_amd.ops import topk as tops
+
+    torch.manual_seed(2)
+    q = ref.l2_normalize(torch.randn(B, D, device=DEV))
+    pg = ref.l2_normalize(torch.randn(N, D, device=DEV))
+    v, i = tops._topk_hip(q, pg, k)
+    vr, ir = tops._topk_torch(bf(q), bf(pg), k, 100000)
+    torch.testing.assert_close(v, vr, rtol=1e-4, atol=1e-4)
+    assert (i == ir).float().mean() > 0.97
+
+
+def test_mlp_train_step_gpu():
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed()
+    cfg = preset_config("mlp_xgpu").replace(batch_size=256, document_length=400, cos_clip=False)
+    tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device(DEV))
+    data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=2048), DEV)
+    losses = [float(tr.train_step(*data.batch(256))["loss"]) for _ in range(40)]
+    assert losses[-1] < losses[0] - 0.3
