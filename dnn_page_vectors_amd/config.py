@@ -92,6 +92,7 @@ class Configuration:
     bert_vocab: int = 30522
     bert_max_len: int = 512
     bert_out_dim: int = 0                 # 0 => CLS vector (768), else projection
+    bert_dropout: float = 0.1
     # chunked long-page encoder (config 5)
     chunk_len: int = 512
     num_chunks: int = 8
@@ -100,6 +101,7 @@ class Configuration:
     # LSTM legacy tower (old_scripts/lstm.py:125-200)
     lstm_output_size: int = 64
     lstm_dense_units: int = 32
+    lstm_conv: bool = False               # lstm_new.py: Conv1D(64,3)+MaxPool(2) before the LSTM
 
     # ---- training (new) ------------------------------------------------------
     loss_mode: str = "explicit"          # explicit (J negatives, parity) | in_batch | cross_gpu

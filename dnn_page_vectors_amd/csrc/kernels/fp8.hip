@@ -1,0 +1,166 @@
+// FP8 (OCP e4m3) linear layers for the long-page chunked encoder (BASELINE config 5:
+// "Long-page 4k-token chunked encoder, mean-pool, fp8 MFMA on CDNA4").
+//
+// * amax_kernel      : per-tensor max |x| (fp32 atomicMax on the non-negative bit pattern)
+// * quant_fp8_kernel : x -> e4m3 with scale s = 448 / amax (saturating), packed 4 per dword
+//                      by v_cvt_pk_fp8_f32 (gfx950: OCP e4m3fn, not MI300's fnuz)
+// * fp8_linear_kernel: Y[M,N] = act(inv_sx * inv_sw * (X8[M,K] . W8[N,K]^T) + b) with
+//                      v_mfma_f32_16x16x32_fp8_fp8 (2x the bf16 operand density per byte,
+//                      half the staging bytes), fp32 accumulate, fused dequant + bias +
+//                      activation epilogue, fp32 and/or bf16 output.
+// 64x64 block tile, BK = 64 bytes, 4 waves (2x2) of 32x32; K must be a multiple of 16.
+// Training uses fp8 for the forward GEMMs and bf16 hipBLASLt GEMMs for dgrad/wgrad.
+#include "common.h"
+
+namespace pv {
+namespace fp8 {
+
+constexpr int BM = 64, BN = 64, BK = 64;
+constexpr int LDB = BK + 16;  // bytes per LDS row (80: 16-B aligned)
+
+__global__ void amax_kernel(const float* __restrict__ x, long n, float* __restrict__ amax) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float m = 0.f;
+  for (; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(m));
+}
+
+// out: n bytes (n % 4 == 0); scale = 448 / max(amax, tiny)
+__global__ void quant_fp8_kernel(const float* __restrict__ x, const float* __restrict__ amax,
+                                 unsigned* __restrict__ out, long n4) {
+  const float a = fmaxf(*amax, 1e-12f);
+  const float s = 448.f / a;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    unsigned w = 0;
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * s, -448.f), 448.f), fminf(fmaxf(v[1] * s, -448.f), 448.f),
+                                        w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * s, -448.f), 448.f), fminf(fmaxf(v[3] * s, -448.f), 448.f),
+                                        w, true);
+    out[i] = w;
+  }
+}
+
+__device__ __forceinline__ float act_fn(float x, int act) {
+  if (act == 1) return x > 0.f ? x : 0.f;
+  if (act == 3) return tanhf(x);
+  return x;
+}
+
+// X8: (M, K) e4m3 bytes, W8: (N, K) e4m3 bytes. amax_x, amax_w: device scalars.
+__global__ __launch_bounds__(256) void fp8_linear_kernel(const unsigned char* __restrict__ X8,
+                                                         const unsigned char* __restrict__ W8,
+                                                         const float* __restrict__ amax_x,
+                                                         const float* __restrict__ amax_w,
+                                                         const float* __restrict__ bias, float* __restrict__ Y,
+                                                         unsigned short* __restrict__ Ybf, int M, int N, int K,
+                                                         int act) {
+  __shared__ __attribute__((aligned(16))) unsigned char As[BM * LDB];
+  __shared__ __attribute__((aligned(16))) unsigned char Bs[BN * LDB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    {  // 64 rows x 64 bytes per operand: 256 threads x 16 bytes
+      const int r = tid >> 2, c = (tid & 3) * 16;
+      const int gm = m0 + r, gn = n0 + r, gk = k0 + c;
+      u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+      if (gm < M && gk + 16 <= K) a = *reinterpret_cast<const u32x4*>(X8 + (size_t)gm * K + gk);
+      else if (gm < M) {
+        unsigned char t[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t[q] = (gk + q < K) ? X8[(size_t)gm * K + gk + q] : 0;
+        a = *reinterpret_cast<u32x4*>(t);
+      }
+      if (gn < N && gk + 16 <= K) b = *reinterpret_cast<const u32x4*>(W8 + (size_t)gn * K + gk);
+      else if (gn < N) {
+        unsigned char t[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t[q] = (gk + q < K) ? W8[(size_t)gn * K + gk + q] : 0;
+        b = *reinterpret_cast<u32x4*>(t);
+      }
+      *reinterpret_cast<u32x4*>(&As[r * LDB + c]) = a;
+      *reinterpret_cast<u32x4*>(&Bs[r * LDB + c]) = b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      long a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = *reinterpret_cast<const long*>(&As[(wm * 32 + i * 16 + (lane & 15)) * LDB + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b[j] = *reinterpret_cast<const long*>(&Bs[(wn * 32 + j * 16 + (lane & 15)) * LDB + ks * 32 + (lane >> 4) * 8]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const float deq = (fmaxf(*amax_x, 1e-12f) / 448.f) * (fmaxf(*amax_w, 1e-12f) / 448.f);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+      if (col >= N) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        if (row < M) {
+          const float y = act_fn(acc[i][j][r] * deq + bv, act);
+          if (Y) Y[(size_t)row * N + col] = y;
+          if (Ybf) Ybf[(size_t)row * N + col] = f32_to_bf16(y);
+        }
+      }
+    }
+}
+
+}  // namespace fp8
+}  // namespace pv
+
+using namespace pv;
+
+PV_API int pv_amax(const float* x, long n, float* amax, void* stream) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(pv::fp8::amax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, amax);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_quant_fp8(const float* x, const float* amax, void* out, long n, void* stream) {
+  if (n % 4) return -1;
+  long n4 = n / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(pv::fp8::quant_fp8_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, amax,
+                     (unsigned*)out, n4);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_fp8_linear(const void* X8, const void* W8, const float* amax_x, const float* amax_w, const float* bias,
+                         float* Y, void* Ybf, int M, int N, int K, int act, void* stream) {
+  using namespace pv::fp8;
+  if (K % 16) return -1;
+  dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
+  hipLaunchKernelGGL(fp8_linear_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const unsigned char*)X8,
+                     (const unsigned char*)W8, amax_x, amax_w, bias, Y, (unsigned short*)Ybf, M, N, K, act);
+  PV_LAUNCH_CHECK();
+  return 0;
+}

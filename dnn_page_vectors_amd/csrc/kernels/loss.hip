@@ -329,6 +329,39 @@ __global__ __launch_bounds__(256) void ib_pos_kernel(const unsigned short* __res
   }
 }
 
+// Row-materialised variant for wide vectors (D > 192, e.g. BERT's 768) or small M: the
+// (B x M) cosine matrix S comes from a hipBLASLt GEMM; one wave per row computes the
+// log-sum-exp, the loss and the full logit gradient dS = gscale*g*(P - onehot)*clip'
+// in place (the two products dQ = dS.D, dD = dS^T.Q are again library GEMMs).
+__global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, const int* __restrict__ pos,
+                                                      const float* __restrict__ gscale, float* __restrict__ loss,
+                                                      int B, int M, float gamma, int clip) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float* s = S + (size_t)row * M;
+  float sum = 0.f;
+  for (int c = lane; c < M; c += 64) {
+    float r = s[c];
+    if (clip) r = fminf(fmaxf(r, 0.f), 1.f);
+    sum += __expf(gamma * (r - 1.f));
+  }
+  sum = wave_sum(sum);
+  const int p = pos[row];
+  float rp = s[p];
+  if (clip) rp = fminf(fmaxf(rp, 0.f), 1.f);
+  if (lane == 0 && loss) loss[row] = gamma + __logf(sum) - gamma * rp;
+  if (!gscale) return;
+  const float g = gscale[row] * gamma;
+  for (int c = lane; c < M; c += 64) {
+    const float raw = s[c];
+    const bool pass = !clip || (raw >= 0.f && raw <= 1.f);
+    const float r = clip ? fminf(fmaxf(raw, 0.f), 1.f) : raw;
+    const float P = __expf(gamma * (r - 1.f)) / sum;
+    s[c] = pass ? g * (P - (c == p ? 1.f : 0.f)) : 0.f;
+  }
+}
+
 // bf16 transpose (n, DP) -> (DP, n)
 __global__ void transpose_bf16_kernel(const unsigned short* __restrict__ in, unsigned short* __restrict__ out, int n,
                                       int DP) {
@@ -422,6 +455,14 @@ PV_API int pv_ib_pos(const void* X, const void* Y, const int* pos, float* spos, 
   hipLaunchKernelGGL(pv::loss::ib_pos_kernel, dim3((nx + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned short*)X, (const unsigned short*)Y, pos, spos, gscale, dX, dY, nx, DP, gamma,
                      clip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_ib_rows(float* S, const int* pos, const float* gscale, float* loss, int B, int M, float gamma, int clip,
+                      void* stream) {
+  hipLaunchKernelGGL(pv::loss::ib_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, pos, gscale,
+                     loss, B, M, gamma, clip);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -1,0 +1,55 @@
+"""Long-page chunked encoder (BASELINE config 5: "Long-page 4k-token chunked encoder,
+mean-pool, fp8 MFMA on CDNA4").
+
+The reference scales to long pages only by truncation + a global max-pool
+(data_utils.py:29-68, cnn_dssm_th.py:94).  Here a page of up to
+``num_chunks * chunk_len`` (8 x 512 = 4096) hashed trigram ids is cut into chunks,
+every chunk is encoded independently by the DSSM MLP tower (bag-of-trigrams via the
+counts GEMM, then fp8 e4m3 MFMA dense layers), and the page vector is the MEAN of its
+non-empty chunk vectors (empty = all padding; masked out).  Chunks are independent, so
+a page could be split over CUs or GPUs with one all-reduce of partial sums (the
+"context parallel" of this workload) — at 288 GB per MI355X it is not
+needed.  Queries use the same tower type without chunking.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .base import TwoTowerModel
+from .mlp_dssm import MLPTower
+
+
+class ChunkedPageEncoder(TwoTowerModel):
+    def __init__(self, cfg, vocab_size: int):
+        super().__init__(cfg)
+        gen = torch.Generator().manual_seed(int(cfg.seed))
+        act = getattr(cfg, "mlp_act", "tanh")
+        self.vocab_size = vocab_size
+        self.chunk_len = int(cfg.chunk_len)
+        self.num_chunks = int(cfg.num_chunks)
+        self.query_tower = MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)
+        self.doc_towers = nn.ModuleList([MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)])
+
+    @property
+    def out_dim(self) -> int:
+        return self.cfg.mlp_dims[-1]
+
+    def build_cache(self):
+        if not self.query_tower.embedding.is_cuda:
+            return {}
+        return {"query": self.query_tower.build_cache(), "doc0": self.doc_towers[0].build_cache()}
+
+    def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:
+        cache = self.compute_cache()
+        if tower == "query":
+            return self.query_tower(ids, cache.get("query"))
+        N, L = ids.shape
+        C = max(1, -(-L // self.chunk_len))
+        pad = C * self.chunk_len - L
+        if pad:
+            ids = torch.nn.functional.pad(ids, (0, pad))
+        chunks = ids.reshape(N * C, self.chunk_len)
+        v = self.doc_towers[0](chunks, cache.get("doc0")).view(N, C, -1)
+        live = (chunks != 0).any(dim=1).view(N, C, 1).to(v.dtype)
+        return (v * live).sum(1) / live.sum(1).clamp(min=1.0)

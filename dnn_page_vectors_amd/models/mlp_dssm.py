@@ -23,13 +23,15 @@ import torch.nn as nn
 
 from ..ops import dense as dops
 from ..ops import embedding as eops
+from ..ops import fp8 as fops
 from .base import TwoTowerModel
 from .cdssm import glorot_uniform_
 
 
 class MLPTower(nn.Module):
-    def __init__(self, vocab_size: int, dims, act: str, gen: torch.Generator):
+    def __init__(self, vocab_size: int, dims, act: str, gen: torch.Generator, use_fp8: bool = False):
         super().__init__()
+        self.use_fp8 = use_fp8
         d1 = dims[0]
         self.embedding = nn.Parameter(torch.empty(vocab_size, d1))
         lim = math.sqrt(6.0 / (vocab_size + d1)) * math.sqrt(vocab_size / 64.0)  # bag mean of ~64 tokens
@@ -46,14 +48,30 @@ class MLPTower(nn.Module):
             self.bs.append(nn.Parameter(torch.zeros(b)))
         self.act = act
 
+    def build_cache(self):
+        c = {"emb16": self.embedding.detach().to(torch.bfloat16).contiguous()}
+        if self.use_fp8:
+            c["w8"] = [fops.quantize(w.detach()) for w in self.ws]
+        return c
+
     def forward(self, ids: torch.Tensor, cache=None) -> torch.Tensor:
         if ids.dtype != torch.int32:
             ids = ids.to(torch.int32)
-        h = eops.embedding_bag(ids, self.embedding, cache, pad=0, mean=True)
+        cache = cache or {}
+        h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True)
+        return self.dense_stack(h, cache)
+
+    def dense_stack(self, h: torch.Tensor, cache=None) -> torch.Tensor:
+        cache = cache or {}
         h = _bias_act(h, self.b1, self.act)
         n = len(self.ws)
+        w8 = cache.get("w8")
         for i, (w, b) in enumerate(zip(self.ws, self.bs)):
-            h = dops.linear_act(h, w, b, self.act if i < n - 1 else "none")
+            a = self.act if i < n - 1 else "none"
+            if self.use_fp8:
+                h = fops.fp8_linear(h, w, b, a, w8[i] if w8 is not None else None)
+            else:
+                h = dops.linear_act(h, w, b, a)
         return h
 
 
@@ -82,8 +100,8 @@ class MLPDSSM(TwoTowerModel):
     def build_cache(self):
         c = {}
         if self.query_tower.embedding.is_cuda:
-            c["query"] = self.query_tower.embedding.detach().to(torch.bfloat16).contiguous()
-            c["doc0"] = self.doc_towers[0].embedding.detach().to(torch.bfloat16).contiguous()
+            c["query"] = self.query_tower.build_cache()
+            c["doc0"] = self.doc_towers[0].build_cache()
         return c
 
     def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:

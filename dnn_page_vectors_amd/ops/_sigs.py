@@ -31,6 +31,7 @@ SIGS = {
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_transpose_bf16": "pp" "ii" "p",
+    "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
     "pv_embedding_bag": "pppp" "iiiiii" "p",
@@ -38,6 +39,17 @@ SIGS = {
     # topk.hip
     "pv_topk_splits": "ii",
     "pv_topk_cos": "pppppp" "iiiii" "p",
+    # transformer.hip
+    "pv_add_layernorm_fwd": "pppppppp" "iif" "p",
+    "pv_layernorm_bwd": "pppppppp" "ii" "p",
+    "pv_bias_gelu_fwd": "ppp" "li" "p",
+    "pv_bias_gelu_bwd": "ppppp" "ii" "p",
+    "pv_softmax_fwd": "pp" "liif" "p",
+    "pv_softmax_bwd": "pp" "lif" "p",
+    # fp8.hip
+    "pv_amax": "plpp",
+    "pv_quant_fp8": "ppp" "l" "p",
+    "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",

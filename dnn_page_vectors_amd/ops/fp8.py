@@ -1,0 +1,76 @@
+"""FP8 (OCP e4m3) linear layer: quantise -> fp8 MFMA GEMM -> dequant + bias + act.
+
+Forward GEMMs run on ``v_mfma_f32_16x16x32_fp8_fp8`` (csrc/kernels/fp8.hip) with
+per-tensor current scaling (amax of this step's activation; weights re-quantised once
+per optimizer step through the model's compute cache).  Backward uses bf16 GEMMs
+(hipBLASLt) on the unquantised tensors — the usual fp8-forward / bf16-backward recipe.
+CPU: emulated with torch.float8_e4m3fn round-trips (same scaling rule).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._common import P, check, lib, stream, use_hip
+
+FP8_MAX = 448.0
+_ACT = {"none": 0, "relu": 1, "tanh": 3}
+
+
+def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 tensor -> (uint8 e4m3 bytes, amax device scalar)."""
+    x = x.contiguous().float()
+    amax = torch.zeros(1, dtype=torch.float32, device=x.device)
+    n = x.numel()
+    check(lib().pv_amax(P(x), n, P(amax), stream(x.device)), "pv_amax")
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    if n % 4:
+        raise ValueError("fp8 quantisation needs numel % 4 == 0")
+    check(lib().pv_quant_fp8(P(x), P(amax), P(q), n, stream(x.device)), "pv_quant_fp8")
+    return q, amax
+
+
+def _emulate(x: torch.Tensor) -> torch.Tensor:
+    a = x.abs().max().clamp(min=1e-12)
+    s = FP8_MAX / a
+    return (x * s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float() / s
+
+
+class _FP8LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, wq):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous().float()
+        M, K = x2.shape
+        N = w.shape[0]
+        xq, ax = quantize(x2)
+        w8, aw = wq if wq is not None else quantize(w.detach())
+        y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+        check(lib().pv_fp8_linear(P(xq), P(w8), P(ax), P(aw), P(b) if b is not None else None, P(y), None, M, N, K,
+                                  _ACT[act], stream(x.device)), "pv_fp8_linear")
+        ctx.save_for_backward(x2, w, y, b)
+        ctx.act, ctx.xshape = act, x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y, b = ctx.saved_tensors
+        dz = dy.reshape(-1, dy.shape[-1]).float()
+        if ctx.act == "relu":
+            dz = dz * (y > 0)
+        elif ctx.act == "tanh":
+            dz = dz * (1 - y * y)
+        dzb = dz.to(torch.bfloat16)
+        dx = (dzb @ w.detach().to(torch.bfloat16)).float().view(ctx.xshape)
+        dw = (dzb.t() @ x2.to(torch.bfloat16)).float()
+        db = dz.sum(0) if b is not None else None
+        return dx, dw, db, None, None
+
+
+def fp8_linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "none",
+               wq: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """y = act(x @ w^T + b) with e4m3 operands and fp32 accumulation."""
+    if use_hip(x, w):
+        return _FP8LinearFn.apply(x, w, b, act, wq)
+    y = torch.nn.functional.linear(_emulate(x.float()), _emulate(w.float()), b)
+    return {"none": y, "relu": torch.relu(y), "tanh": torch.tanh(y)}[act]

@@ -110,9 +110,38 @@ class _InBatchFn(torch.autograd.Function):
         return dq[:, :D], dd[:, :D], None, None, None
 
 
+class _InBatchRowsFn(torch.autograd.Function):
+    """Wide vectors (D > 192): S by hipBLASLt GEMM, loss/gradient by the ib_rows HIP kernel."""
+
+    @staticmethod
+    def forward(ctx, qn, dn, pos, gamma, clip):
+        B, M = qn.shape[0], dn.shape[0]
+        qb, db = qn.detach().to(torch.bfloat16), dn.detach().to(torch.bfloat16)
+        S = (qb @ db.t()).float().contiguous()
+        pos = pos.to(torch.int32).contiguous()
+        loss = torch.empty(B, dtype=torch.float32, device=qn.device)
+        check(lib().pv_ib_rows(P(S), P(pos), None, P(loss), B, M, float(gamma), int(clip), stream(qn.device)),
+              "pv_ib_rows")
+        ctx.save_for_backward(qb, db, pos, S)
+        ctx.meta = (float(gamma), int(clip))
+        return loss, torch.exp(-loss).detach()
+
+    @staticmethod
+    def backward(ctx, gl, _gp):
+        qb, db, pos, S = ctx.saved_tensors
+        gamma, clip = ctx.meta
+        B, M = S.shape
+        g = gl.contiguous().float()
+        check(lib().pv_ib_rows(P(S), P(pos), P(g), None, B, M, gamma, clip, stream(S.device)), "pv_ib_rows")
+        dS = S.to(torch.bfloat16)
+        return (dS @ db).float(), (dS.t() @ qb).float(), None, None, None
+
+
 def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, gamma: float, clip: bool = True
                  ) -> Tuple[torch.Tensor, torch.Tensor]:
     """qn (B, D), dn (M, D) normalised; pos_index (B,) -> (per-row loss, P_pos)."""
     if use_hip(qn, dn):
+        if qn.shape[1] > 192:
+            return _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
         return _InBatchFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
     return ref.inbatch_softmax_loss(qn, dn, pos_index, gamma, clip)

@@ -278,3 +278,106 @@ def test_mlp_train_step_gpu():
     data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=2048), DEV)
     losses = [float(tr.train_step(*data.batch(256))["loss"]) for _ in range(40)]
     assert losses[-1] < losses[0] - 0.3
+
+
+def test_add_layernorm_and_bias_gelu():
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    M, D = 70, 768
+    x = torch.randn(M, D, device=DEV).bfloat16().requires_grad_(True)
+    r = torch.randn(M, D, device=DEV).bfloat16().requires_grad_(True)
+    g = (1 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    y = tops.add_layernorm(x, r, g, b)
+    xr, rr = x.detach().float().requires_grad_(True), r.detach().float().requires_grad_(True)
+    gr, br = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr + rr, (D,), gr, br, 1e-12)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    dy = torch.randn(M, D, device=DEV)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    torch.testing.assert_close(g.grad, gr.grad, rtol=3e-2, atol=1e-1)
+    torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=1e-1)
+    u = torch.randn(M, 3072, device=DEV).bfloat16().requires_grad_(True)
+    bb = torch.randn(3072, device=DEV).requires_grad_(True)
+    o = tops.bias_gelu(u, bb)
+    ur, bbr = u.detach().float().requires_grad_(True), bb.detach().clone().requires_grad_(True)
+    orf = torch.nn.functional.gelu(ur + bbr, approximate="tanh")
+    torch.testing.assert_close(o.float(), orf, rtol=2e-2, atol=2e-2)
+    do = torch.randn_like(orf)
+    (o.float() * do).sum().backward()
+    (orf * do).sum().backward()
+    torch.testing.assert_close(bb.grad, bbr.grad, rtol=3e-2, atol=2e-1)
+
+
+def test_masked_attention():
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    B, H, L, d = 3, 4, 37, 64
+    q, k, v = (torch.randn(B, H, L, d, device=DEV).bfloat16().requires_grad_(True) for _ in range(3))
+    mask = torch.ones(B, L, dtype=torch.int32, device=DEV)
+    mask[1, 20:] = 0
+    o = tops.attention(q, k, v, mask)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    s = (qr @ kr.transpose(-1, -2)) / 8.0
+    s = s.masked_fill(~mask.bool()[:, None, None, :], float("-inf"))
+    orf = torch.softmax(s, -1) @ vr
+    torch.testing.assert_close(o.float(), orf, rtol=3e-2, atol=3e-2)
+    do = torch.randn_like(orf)
+    (o.float() * do).sum().backward()
+    (orf * do).sum().backward()
+    torch.testing.assert_close(q.grad.float(), qr.grad, rtol=5e-2, atol=5e-2)
+    torch.testing.assert_close(v.grad.float(), vr.grad, rtol=5e-2, atol=5e-2)
+
+
+def test_fp8_linear():
+    from dnn_page_vectors_amd.ops import fp8 as fops
+
+    torch.manual_seed(3)
+    x = torch.randn(100, 512, device=DEV, requires_grad=True)
+    w = (torch.randn(256, 512, device=DEV) * 0.05).requires_grad_(True)
+    b = torch.randn(256, device=DEV, requires_grad=True)
+    y = fops.fp8_linear(x, w, b, "tanh")
+    yr = torch.tanh(torch.nn.functional.linear(fops._emulate(x.detach()), fops._emulate(w.detach()), b.detach()))
+    torch.testing.assert_close(y, yr, rtol=1e-3, atol=1e-3)  # identical e4m3 rounding, fp32 accumulate
+    exact = torch.tanh(torch.nn.functional.linear(x.detach(), w.detach(), b.detach()))
+    assert float((y - exact).detach().abs().mean()) < 0.05  # e4m3 rounding noise only
+    y.sum().backward()
+    assert x.grad is not None and w.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("preset", ["bert_dp8", "longpage_fp8"])
+def test_big_model_train_steps_gpu(preset):
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed()
+    cfg = preset_config(preset)
+    if preset == "bert_dp8":
+        cfg = cfg.replace(bert_layers=2, batch_size=16, document_length=128)
+    else:
+        cfg = cfg.replace(batch_size=64, document_length=2048)
+    tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device(DEV))
+    data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=256), DEV)
+    losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(6)]
+    assert all(l == l for l in losses)
+
+
+def test_inbatch_loss_wide_rows_path():
+    torch.manual_seed(4)
+    B, M, D = 40, 160, 768
+    qn = bf(ref.l2_normalize(torch.randn(B, D, device=DEV))).requires_grad_(True)
+    dn = bf(ref.l2_normalize(torch.randn(M, D, device=DEV))).requires_grad_(True)
+    pos = torch.arange(B, device=DEV, dtype=torch.int32) * 4
+    loss, _ = lops.inbatch_loss(qn, dn, pos, 10.0, False)
+    q2, d2 = qn.detach().clone().requires_grad_(True), dn.detach().clone().requires_grad_(True)
+    lr, _ = ref.inbatch_softmax_loss(q2, d2, pos, 10.0, False)
+    torch.testing.assert_close(loss, lr, rtol=2e-3, atol=2e-3)
+    loss.mean().backward()
+    lr.mean().backward()
+    torch.testing.assert_close(qn.grad, q2.grad, rtol=3e-2, atol=3e-3)
+    torch.testing.assert_close(dn.grad, d2.grad, rtol=3e-2, atol=3e-3)
