@@ -27,6 +27,14 @@ import time
 import torch
 
 
+MODEL_DESC = {
+    "cdssm": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
+    "mlp": "Two-tower MLP 512-512-128, 30k hashed tri-grams, Lq=45, Ld=2000, in-batch/cross-GPU negatives",
+    "bert": "BERT-base dual encoder (12L/768H/12A, shared), Lq=32, Ld=256, cross-GPU negatives",
+    "chunked": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, MLP 512-512-128 fp8 e4m3, mean-pool",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,8 +46,45 @@ def parse():
                     help="torch = eager PyTorch-ROCm implementation of the same model (baseline stand-in)")
     ap.add_argument("--recall", type=int, default=2048, help="held-out pairs for Recall@10 (0 = skip)")
     ap.add_argument("--pool", type=int, default=4, help="pre-featurized batches kept in HBM")
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--eager-compare", type=int, default=1,
+                    help="also time the eager PyTorch-ROCm implementation of the same model (batch 512, "
+                         "single GPU only) and report the speedup")
+    ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked"],
+                    help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5")
     return ap.parse_args()
+
+
+def _eager_pairs_per_s(cfg, V, dev, batch=512, steps=3, warmup=2):
+    """Same model/loss/optimizer through plain PyTorch-ROCm ops (F.embedding, F.conv1d via
+    MIOpen, autograd, torch matmul) — BASELINE.md's stand-in for the reference, which
+    cannot run here (Python 2 + Keras 1 + Theano)."""
+    try:
+        from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+        from dnn_page_vectors_amd.models import build_model
+        from dnn_page_vectors_amd.ops._common import get_backend, set_backend
+        from dnn_page_vectors_amd.train.trainer import Trainer
+
+        prev = get_backend()
+        set_backend("torch")
+        try:
+            c = cfg.replace(batch_size=batch)
+            tr = Trainer(c, build_model(c, V), dev)
+            gen = SyntheticPairs(spec_from_config(c, V, num_pages=2048), dev, seed=7)
+            b = gen.batch(batch)
+            for _ in range(warmup):
+                tr.train_step(*b)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                tr.train_step(*b)
+            torch.cuda.synchronize()
+            return batch * steps / (time.perf_counter() - t0)
+        finally:
+            set_backend(prev)
+            torch.cuda.empty_cache()
+    except Exception as e:  # the comparison is informational only
+        print(f"eager comparison skipped: {e}", file=sys.stderr)
+        return None
 
 
 def main():
@@ -47,7 +92,8 @@ def main():
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
     from dnn_page_vectors_amd.eval.retrieval import recall_at_k
-    from dnn_page_vectors_amd.models.cdssm import CDSSM, cdssm_flops_per_sample
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.models.cdssm import cdssm_flops_per_sample
     from dnn_page_vectors_amd.ops._common import set_backend
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
@@ -55,10 +101,14 @@ def main():
     info = pdist.init_distributed()
     if a.backend == "torch":
         set_backend("torch")
-    cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=a.batch, loss_mode=a.loss)
+    preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "chunked": "longpage_fp8"}[a.model]
+    cfg = preset_config(preset)
+    batch = a.batch if a.model == "cdssm" or a.batch != 4096 else cfg.batch_size
+    cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model == "cdssm" else cfg.loss_mode)
+    a.batch = batch
     V = cfg.vocab_hash_size
     dev = info.device
-    model = CDSSM(cfg, V)
+    model = build_model(cfg, V)
     trainer = Trainer(cfg, model, dev)
 
     spec = spec_from_config(cfg, V, num_pages=16384)
@@ -95,12 +145,17 @@ def main():
         recall = recall_at_k(qv, pv, torch.arange(a.recall, device=dev), k=10)
 
     W = info.world_size
+    eager = None
+    if a.eager_compare and W == 1 and a.backend == "hip" and a.model == "cdssm":
+        eager = _eager_pairs_per_s(cfg, V, dev)
+
     pairs = a.batch * W * a.steps
     value = pairs / dt
-    flops = 3.0 * cdssm_flops_per_sample(cfg) * a.batch * W * a.steps / dt  # fwd + ~2x bwd (dense-equivalent)
+    flops = (3.0 * cdssm_flops_per_sample(cfg) * a.batch * W * a.steps / dt) if a.model == "cdssm" else 0.0
     if info.is_main:
         out = {
-            "metric": "pairs/sec (whole node) + Recall@10, DSSM-300d",
+            "metric": "pairs/sec (whole node) + Recall@10, DSSM-300d" if a.model == "cdssm"
+                      else f"pairs/sec (whole node), {a.model}",
             "value": round(value, 1),
             "unit": "pairs/s",
             "n_gpus": W,
@@ -112,13 +167,17 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (device-resident pre-featurized Zipf trigram-id pages; random-init weights)",
-            "config": {"model": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
+            "config": {"model": MODEL_DESC[a.model],
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend},
             "recall_at_10": None if recall is None else round(recall, 4),
             "final_loss": round(final_loss, 4),
             "dense_equiv_tflops": round(flops / 1e12, 1),
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
         }
+        if eager:
+            out["eager_pytorch_pairs_per_s"] = round(eager, 1)
+            out["speedup_vs_eager_pytorch"] = round(value / eager, 1)
         print(json.dumps(out), flush=True)
     pdist.destroy()
 
