@@ -61,7 +61,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
     else:
         dev = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # PAGEVEC_DIST_BACKEND=gloo rehearses several ranks on one GPU (RCCL refuses duplicate devices)
+        be = backend or os.environ.get("PAGEVEC_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {}
