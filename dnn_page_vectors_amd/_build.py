@@ -90,6 +90,11 @@ def _compile_all(srcs: List[str], compiler: str, flags: List[str], incdir: str, 
     if todo:
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             list(ex.map(one, todo))
+    keep = set(objs)
+    for f in os.listdir(OBJ):  # drop objects of older source versions
+        p = os.path.join(OBJ, f)
+        if f.startswith(tag + "_") and f.endswith(".o") and p not in keep:
+            os.remove(p)
     return objs
 
 

@@ -19,16 +19,16 @@ __device__ __forceinline__ float bf16_to_f32(unsigned short h) {
   return __uint_as_float(((unsigned)h) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (NaN stays NaN via the quiet bit).
+// Round-to-nearest-even f32 -> bf16: gfx950's v_cvt_pk_bf16_f32 (one instruction per pair).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+
 __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){lo, hi}, bf16x2v));
 }
 
 // lowbias32 finaliser — the counter-based RNG shared with ops/reference.py.

@@ -12,10 +12,10 @@
 //       ib_fwd      : per (query block, doc split) partial sum_j exp(S_ij - g)  -> atomics
 //                     (no running max needed: clip bounds S to [0, g] (or [-g, g]), so
 //                     exp(S - g) <= 1 and the sum cannot overflow)
-//       ib_bwd<ROW> : recompute the S tile, G = gscale*g*P*clip'  (bf16, via LDS),
-//                     then dQ += G.Dn  (ROW=true, rows=queries)  or
-//                          dD += G^T.Qn (ROW=false, rows=docs) with MFMA; partial
-//                     results of each split are added with fp32 atomics.
+//       ib_bwd<ROW> : recompute the S tile, G = gscale*g*P*clip' (bf16, in registers),
+//                     then dQ = G.Dn  (ROW=true, rows=queries)  or
+//                          dD = G^T.Qn (ROW=false, rows=docs) with MFMA; per-split
+//                     partials are summed by ib_split_reduce.
 //       ib_pos      : the positive logit (same bf16 inputs) and the one-hot term of
 //                     the gradient, -gscale*g*clip' * {d_pos, q}.
 #include "common.h"
@@ -110,194 +110,244 @@ constexpr int TQ = 128;   // rows per block (4 waves x 32)
 constexpr int TD = 64;    // columns per tile
 constexpr int PADK = 8;   // LDS row padding (bf16 elements)
 
-// S tile for one wave: rows r0..r0+31 (2 subtiles), cols 0..63 of the LDS tile (4 subtiles).
-// a: row fragments [2][KS] (registers); ytile: [TD][DP+PADK] bf16 in LDS.
+// ---- swapped orientation, G never leaves registers ---------------------------
+// The S tile is computed transposed, S^T = Yt . X^T (A = 16 staged rows of Y from LDS,
+// B = 16 register-resident rows of X), so each lane owns ONE X row (lane & 15) and four
+// consecutive Y rows 4g..4g+3 of each 16-row subtile.  Two such subtiles, converted to
+// bf16, are exactly the B operand of the next product  out^T[feat][x] += Y^T[feat][y] .
+// G^T[y][x]  with the k (= y) order permuted as j -> 16*(j>>2) + 4g + (j&3); the matching
+// A operand (Y^T) is read from the SAME row-major LDS image with ds_read_b64_tr_b16
+// (a transposed LDS read), so neither a transposed copy of Y nor a G round trip through
+// LDS is needed.  Y tiles are double-buffered (register prefetch of tile t+1 during the
+// MFMAs of tile t, one barrier per tile).  LDS row stride DP+16 elements puts the 8 rows
+// of a transposed read on disjoint 8-bank groups.
+typedef short v4s __attribute__((ext_vector_type(4)));
+
 template <int KS>
-__device__ __forceinline__ void s_tile(const bf16x8 (&a)[2][KS], const unsigned short* ytile, int ldy,
-                                       f32x4 (&acc)[2][4]) {
+struct IbTile {
+  static constexpr int DP = KS * 32, LDY = DP + 16, CH = DP / 8;
+  static constexpr int NLD = (TD * CH + 255) / 256;  // 16-byte chunks per thread per tile
+};
+
+template <int KS>
+__device__ __forceinline__ void ib_load(const unsigned short* __restrict__ Y, int c0, int c_end, u32x4 (&v)[IbTile<KS>::NLD]) {
+  using T = IbTile<KS>;
+#pragma unroll
+  for (int u = 0; u < T::NLD; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    const int r = q / T::CH, cc = (q % T::CH) * 8;
+    v[u] = (q < TD * T::CH && c0 + r < c_end) ? *reinterpret_cast<const u32x4*>(Y + (size_t)(c0 + r) * T::DP + cc)
+                                              : u32x4{0, 0, 0, 0};
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void ib_store(unsigned short* yt, const u32x4 (&v)[IbTile<KS>::NLD]) {
+  using T = IbTile<KS>;
+#pragma unroll
+  for (int u = 0; u < T::NLD; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    if (q < TD * T::CH) *reinterpret_cast<u32x4*>(yt + (q / T::CH) * T::LDY + (q % T::CH) * 8) = v[u];
+  }
+}
+
+// acc[c][i][r] = X[row i*16 + (lane&15)] . Y[tile row c*16 + 4g + r]
+template <int KS>
+__device__ __forceinline__ void st_tile(const bf16x8 (&xb)[2][KS], const unsigned short* yt, f32x4 (&acc)[4][2]) {
+  using T = IbTile<KS>;
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      bf16x8 b = *reinterpret_cast<const bf16x8*>(ytile + (c * 16 + (lane & 15)) * ldy + s * 32 + (lane >> 4) * 8);
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(yt + (c * 16 + (lane & 15)) * T::LDY + s * 32 + (lane >> 4) * 8);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b, acc[i][c], 0, 0, 0);
+      for (int i = 0; i < 2; ++i) acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[i][s], acc[c][i], 0, 0, 0);
     }
+}
+
+template <int KS>
+__device__ __forceinline__ void load_xb(const unsigned short* __restrict__ X, int r0, int nx, bf16x8 (&xb)[2][KS]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = r0 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      xb[i][s] = r < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)r * KS * 32 + s * 32 + (lane >> 4) * 8)
+                        : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 }
 
 template <int KS>
-__global__ __launch_bounds__(256) void ib_fwd_kernel(const unsigned short* __restrict__ X,  // (nx, DP) queries
-                                                     const unsigned short* __restrict__ Y,  // (ny, DP) docs
-                                                     float* __restrict__ sumexp, int nx, int ny, int per_split,
-                                                     float gamma, int clip) {
-  constexpr int DP = KS * 32, LDY = DP + PADK;
-  __shared__ __attribute__((aligned(16))) unsigned short yt[TD * LDY];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __restrict__ X,
+                                                         const unsigned short* __restrict__ Y,
+                                                         float* __restrict__ sumexp, int nx, int ny, int per_split,
+                                                         float gamma, int clip) {
+  using T = IbTile<KS>;
+  __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int r0 = blockIdx.x * TQ + wave * 32;
   const int c_begin = blockIdx.y * per_split, c_end = min(ny, c_begin + per_split);
-  bf16x8 a[2][KS];
+  bf16x8 xb[2][KS];
+  load_xb<KS>(X, r0, nx, xb);
+  u32x4 st[T::NLD];
+  ib_load<KS>(Y, c_begin, c_end, st);
+  ib_store<KS>(yt[0], st);
+  __syncthreads();
+  float rs[2] = {0.f, 0.f};
+  const float gl = gamma * 1.4426950408889634f;
+  int buf = 0;
+  for (int c0 = c_begin; c0 < c_end; c0 += TD, buf ^= 1) {
+    const bool more = c0 + TD < c_end;
+    if (more) ib_load<KS>(Y, c0 + TD, c_end, st);
+    const bool full = c0 + TD <= c_end;
+    f32x4 acc[4][2];
+    st_tile<KS>(xb, yt[buf], acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool yv = full || c0 + c * 16 + 4 * g + r < c_end;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float v = acc[c][i][r];
+          if (clip) v = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+          rs[i] += yv ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, gl, -gl)) : 0.f;
+        }
+      }
+    if (more) ib_store<KS>(yt[buf ^ 1], st);
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    int r = r0 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      a[i][s] = r < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)r * DP + s * 32 + (lane >> 4) * 8)
-                       : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    float v = rs[i];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const int r = r0 + i * 16 + (lane & 15);
+    if (g == 0 && r < nx) atomicAdd(&sumexp[r], v);
   }
-  float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  for (int c0 = c_begin; c0 < c_end; c0 += TD) {
-    __syncthreads();
-    for (int q = threadIdx.x; q < TD * (DP / 8); q += 256) {
-      int r = q / (DP / 8), cc = (q % (DP / 8)) * 8;
-      u32x4 v = (c0 + r < c_end) ? *reinterpret_cast<const u32x4*>(Y + (size_t)(c0 + r) * DP + cc) : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<u32x4*>(yt + r * LDY + cc) = v;
-    }
-    __syncthreads();
-    f32x4 acc[2][4];
-    s_tile<KS>(a, yt, LDY, acc);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bool cv = c0 + c * 16 + (lane & 15) < c_end;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float r = acc[i][c][k];
-          if (clip) r = fminf(fmaxf(r, 0.f), 1.f);
-          rs[i][k] += cv ? __expf(gamma * (r - 1.f)) : 0.f;
-        }
-    }
-  }
-  // reduce over the 16 column lanes (xor 1,2,4,8), lanes with (lane&15)==0 write rows 4*(lane>>4)+k
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float v = rs[i][k];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      int r = r0 + i * 16 + 4 * (lane >> 4) + k;
-      if ((lane & 15) == 0 && r < nx) atomicAdd(&sumexp[r], v);
-    }
 }
 
-// ROW = true : rows = queries (X=Qn), cols = docs (Y=Dn), out = dQ, scale per row
-// ROW = false: rows = docs (X=Dn),    cols = queries (Y=Qn), out = dD, scale per col
-// scale[i] = gscale_i * gamma / sumexp_i (per query). G = scale * exp(g*(clip(R)-1)) * clip'(R)
+// ROW = true : X = queries, Y = docs,    out = dQ, scale indexed by X row
+// ROW = false: X = docs,    Y = queries, out = dD, scale indexed by Y row
+// Each split writes its partial product with plain stores into out (a single split) or
+// into its slice of the workspace ws[split][nx][DP]; ib_split_reduce sums the slices
+// (fp32 atomics from 16-32 splits cost ~4x more than the extra write + read).
 template <int KS, bool ROW>
-__global__ __launch_bounds__(256) void ib_bwd_kernel(const unsigned short* __restrict__ X,   // (nx, DP)
-                                                     const unsigned short* __restrict__ Y,   // (ny, DP)
-                                                     const unsigned short* __restrict__ YT,  // (DP, ny)
-                                                     const float* __restrict__ scale, float* __restrict__ out,
-                                                     int nx, int ny, int per_split, float gamma, int clip) {
-  constexpr int DP = KS * 32, LDY = DP + PADK, LDT = TD + PADK, NC = DP / 16;
-  __shared__ __attribute__((aligned(16))) unsigned short yt[TD * LDY];     // [col][feat]
-  __shared__ __attribute__((aligned(16))) unsigned short ytt[DP * LDT];    // [feat][col]
-  __shared__ __attribute__((aligned(16))) unsigned short gt[4][32 * LDT];  // per-wave G tile [row][col]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __restrict__ X,
+                                                         const unsigned short* __restrict__ Y,
+                                                         const float* __restrict__ scale, float* __restrict__ out,
+                                                         float* __restrict__ ws, int nx, int ny, int per_split,
+                                                         float gamma, int clip) {
+  using T = IbTile<KS>;
+  constexpr int NC = T::DP / 16;
+  __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
+  __shared__ float ysc[2][TD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int r0 = blockIdx.x * TQ + wave * 32;
   const int c_begin = blockIdx.y * per_split, c_end = min(ny, c_begin + per_split);
-  bf16x8 a[2][KS];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int r = r0 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-      a[i][s] = r < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)r * DP + s * 32 + (lane >> 4) * 8)
-                       : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  float rsc[2][4];
+  const float gl = gamma * 1.4426950408889634f;
+  bf16x8 xb[2][KS];
+  load_xb<KS>(X, r0, nx, xb);
+  float rsc[2] = {0.f, 0.f};
   if (ROW) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int r = r0 + i * 16 + 4 * (lane >> 4) + k;
-        rsc[i][k] = r < nx ? scale[r] : 0.f;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int r = r0 + i * 16 + (lane & 15);
+      rsc[i] = r < nx ? scale[r] : 0.f;
+    }
   }
-  f32x4 o[2][NC];
+  f32x4 o[NC][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int n = 0; n < NC; ++n)
 #pragma unroll
-    for (int n = 0; n < NC; ++n) o[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  unsigned short* gw = gt[wave];
-
-  for (int c0 = c_begin; c0 < c_end; c0 += TD) {
-    __syncthreads();
-    for (int q = threadIdx.x; q < TD * (DP / 8); q += 256) {
-      int r = q / (DP / 8), cc = (q % (DP / 8)) * 8;
-      u32x4 v = (c0 + r < c_end) ? *reinterpret_cast<const u32x4*>(Y + (size_t)(c0 + r) * DP + cc) : u32x4{0, 0, 0, 0};
-      *reinterpret_cast<u32x4*>(yt + r * LDY + cc) = v;
+    for (int i = 0; i < 2; ++i) o[n][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 st[T::NLD];
+  float scv = 0.f;
+  ib_load<KS>(Y, c_begin, c_end, st);
+  if (!ROW && threadIdx.x < TD) scv = c_begin + (int)threadIdx.x < c_end ? scale[c_begin + threadIdx.x] : 0.f;
+  ib_store<KS>(yt[0], st);
+  if (!ROW && threadIdx.x < TD) ysc[0][threadIdx.x] = scv;
+  __syncthreads();
+  // transposed-read lane address: row (4g + (lane&15)/4), column 4*((lane&15)&3) within the block
+  const int trow = 4 * g + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
+  int buf = 0;
+  for (int c0 = c_begin; c0 < c_end; c0 += TD, buf ^= 1) {
+    const bool more = c0 + TD < c_end;
+    if (more) {
+      ib_load<KS>(Y, c0 + TD, c_end, st);
+      if (!ROW && threadIdx.x < TD) scv = c0 + TD + (int)threadIdx.x < c_end ? scale[c0 + TD + threadIdx.x] : 0.f;
     }
-    for (int q = threadIdx.x; q < DP * (TD / 8); q += 256) {
-      int f = q / (TD / 8), cc = (q % (TD / 8)) * 8;
-      u32x4 v = u32x4{0, 0, 0, 0};
-      if (c0 + cc + 8 <= c_end && (ny & 7) == 0) v = *reinterpret_cast<const u32x4*>(YT + (size_t)f * ny + c0 + cc);
-      else {
-        unsigned short tmp[8];
+    const unsigned short* yb = yt[buf];
+    f32x4 acc[4][2];
+    st_tile<KS>(xb, yb, acc);
+    // G^T in registers -> bf16 B fragments gb[s2][i] (s2: 32-row k-step of the tile);
+    // exp(g*(v-1)) = exp2(v*gl - gl) with gl = g*log2(e)
+    const bool full = c0 + TD <= c_end;
+    u32x4 gp[2][2];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) tmp[t] = (c0 + cc + t < c_end) ? YT[(size_t)f * ny + c0 + cc + t] : 0;
-        v = *reinterpret_cast<u32x4*>(tmp);
-      }
-      *reinterpret_cast<u32x4*>(ytt + f * LDT + cc) = v;
-    }
-    __syncthreads();
-    f32x4 acc[2][4];
-    s_tile<KS>(a, yt, LDY, acc);
-    // G tile -> LDS (bf16), row-major [32 rows][64 cols]
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int col = c0 + c * 16 + (lane & 15);
-      const bool cv = col < c_end;
-      const float csc = (!ROW && cv) ? scale[col] : 0.f;
+      for (int i = 0; i < 2; ++i) {
+        float gv[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float r = acc[i][c][k];
-          bool pass = !clip || (r >= 0.f && r <= 1.f);
-          float rc = clip ? fminf(fmaxf(r, 0.f), 1.f) : r;
-          float sc = ROW ? rsc[i][k] : csc;
-          float g = (cv && pass) ? sc * __expf(gamma * (rc - 1.f)) : 0.f;
-          gw[(i * 16 + 4 * (lane >> 4) + k) * LDT + c * 16 + (lane & 15)] = f32_to_bf16(g);
+        for (int r = 0; r < 4; ++r) {
+          const int yr = c * 16 + 4 * g + r;
+          const float v = acc[c][i][r];
+          const float vc = clip ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
+          const bool ok = (!clip || vc == v) && (full || c0 + yr < c_end);
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(vc, gl, -gl));
+          gv[r] = ok ? (ROW ? rsc[i] : ysc[buf][yr]) * e : 0.f;
         }
-    }
-    // o[rows][feat] += G[rows][cols] . Y[cols][feat]  (A from gw, B from ytt)
+        gp[c >> 1][i][(c & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
+        gp[c >> 1][i][(c & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
+      }
+    // out^T[feat][x] += Y^T[feat][y] . G^T[y][x]
 #pragma unroll
-    for (int s = 0; s < TD / 32; ++s) {
-      bf16x8 ga[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        ga[i] = *reinterpret_cast<const bf16x8*>(gw + (i * 16 + (lane & 15)) * LDT + s * 32 + (lane >> 4) * 8);
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int n = 0; n < NC; ++n) {
-        bf16x8 b = *reinterpret_cast<const bf16x8*>(ytt + (n * 16 + (lane & 15)) * LDT + s * 32 + (lane >> 4) * 8);
+        typedef __attribute__((address_space(3))) v4s lds_v4s;
+        const unsigned short* p0 = yb + (s2 * 32 + trow) * T::LDY + n * 16 + tcol;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0 + 16 * T::LDY));
+        const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int i = 0; i < 2; ++i) o[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[i], b, o[i][n], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+          o[n][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, gp[s2][i]), o[n][i], 0, 0, 0);
       }
+    if (more) {
+      ib_store<KS>(yt[buf ^ 1], st);
+      if (!ROW && threadIdx.x < TD) ysc[buf ^ 1][threadIdx.x] = scv;
     }
+    __syncthreads();
   }
+  // o[n][i][r] = out[x = r0 + i*16 + (lane&15)][feat = n*16 + 4g + r]
+  float* dst = gridDim.y == 1 ? out : ws + (size_t)blockIdx.y * nx * T::DP;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int x = r0 + i * 16 + (lane & 15);
+    if (x >= nx) continue;
+    float* orow = dst + (size_t)x * T::DP;
 #pragma unroll
-    for (int n = 0; n < NC; ++n)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int r = r0 + i * 16 + 4 * (lane >> 4) + k;
-        int f = n * 16 + (lane & 15);
-        float v = o[i][n][k];
-        if (r < nx && v != 0.f) atomicAdd(&out[(size_t)r * DP + f], v);
-      }
+    for (int n = 0; n < NC; ++n) *reinterpret_cast<f32x4*>(orow + n * 16 + 4 * g) = o[n][i];
+  }
+}
+
+// out[i] = sum_s ws[s][i], n4 = nx*DP/4
+__global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                              long n4, int ns) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 a = reinterpret_cast<const f32x4*>(ws)[i];
+    for (int sp = 1; sp < ns; ++sp) a += reinterpret_cast<const f32x4*>(ws)[(size_t)sp * n4 + i];
+    reinterpret_cast<f32x4*>(out)[i] = a;
+  }
 }
 
 // Positive logit + one-hot gradient term; one wave per query row.
@@ -362,23 +412,6 @@ __global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, con
   }
 }
 
-// bf16 transpose (n, DP) -> (DP, n)
-__global__ void transpose_bf16_kernel(const unsigned short* __restrict__ in, unsigned short* __restrict__ out, int n,
-                                      int DP) {
-  __shared__ unsigned short t[32][33];
-  int bx = blockIdx.x * 32, by = blockIdx.y * 32;
-  int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
-  for (int k = ty; k < 32; k += 8) {
-    int r = bx + k, c = by + tx;
-    t[k][tx] = (r < n && c < DP) ? in[(size_t)r * DP + c] : 0;
-  }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    int c = by + k, r = bx + tx;
-    if (c < DP && r < n) out[(size_t)c * n + r] = t[tx][k];
-  }
-}
-
 }  // namespace loss
 }  // namespace pv
 
@@ -414,9 +447,9 @@ static int ib_splits(int nx, int ny, int per_min) {
   }
 
 PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, int nx, int ny, int DP, float gamma, int clip,
-                     void* stream) {
+                      void* stream) {
   using namespace pv::loss;
-  if (DP % 32) return -2;
+  if (DP % 32 || DP > 192) return -2;
   int ns = ib_splits(nx, ny, 256);
   int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
   ns = (ny + per - 1) / per;
@@ -428,25 +461,49 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, int nx, int ny
   return 0;
 }
 
-PV_API int pv_ib_bwd(const void* X, const void* Y, const void* YT, const float* scale, float* out, int nx, int ny,
-                     int DP, float gamma, int clip, int row_scale, void* stream) {
+static int ib2_splits(int nx, int ny) {
+  // 2 resident workgroups per CU (242 VGPRs): 512 fill the chip; keep >= 16 tiles per split
+  const int rb = (nx + pv::loss::TQ - 1) / pv::loss::TQ;
+  int ns = (512 + rb - 1) / rb;
+  const int maxs = (ny + 16 * pv::loss::TD - 1) / (16 * pv::loss::TD);
+  if (ns > maxs) ns = maxs;
+  return ns < 1 ? 1 : ns;
+}
+
+// floats of workspace pv_ib_bwd needs for (nx, ny, DP) (0 = writes out directly)
+PV_API long pv_ib_bwd_ws(int nx, int ny, int DP) {
+  const int ns = ib2_splits(nx, ny);
+  return ns > 1 ? (long)ns * nx * DP : 0;
+}
+
+// out (nx, DP) fp32 is fully written (no zeroing needed).
+PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* out, float* ws, int nx, int ny, int DP,
+                      float gamma, int clip, int row_scale, void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
-  int ns = ib_splits(nx, ny, 256);
+  int ns = ib2_splits(nx, ny);
   int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
   ns = (ny + per - 1) / per;
+  if (ns > 1 && !ws) return -3;
   dim3 grid((nx + TQ - 1) / TQ, ns);
   hipStream_t s = (hipStream_t)stream;
   if (row_scale) {
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true>), grid, dim3(256), 0, s, (const unsigned short*)X,
-                                            (const unsigned short*)Y, (const unsigned short*)YT, scale, out, nx, ny,
-                                            per, gamma, clip));
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true>), grid, dim3(256), 0, s,
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx,
+                                            ny, per, gamma, clip));
   } else {
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, false>), grid, dim3(256), 0, s,
-                                            (const unsigned short*)X, (const unsigned short*)Y,
-                                            (const unsigned short*)YT, scale, out, nx, ny, per, gamma, clip));
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx,
+                                            ny, per, gamma, clip));
   }
   PV_LAUNCH_CHECK();
+  if (ns > 1) {
+    const long n4 = (long)nx * DP / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(ib_split_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, out, n4, ns);
+    PV_LAUNCH_CHECK();
+  }
   return 0;
 }
 
@@ -463,14 +520,6 @@ PV_API int pv_ib_rows(float* S, const int* pos, const float* gscale, float* loss
                       void* stream) {
   hipLaunchKernelGGL(pv::loss::ib_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, pos, gscale,
                      loss, B, M, gamma, clip);
-  PV_LAUNCH_CHECK();
-  return 0;
-}
-
-PV_API int pv_transpose_bf16(const void* in, void* out, int n, int DP, void* stream) {
-  dim3 grid((n + 31) / 32, (DP + 31) / 32);
-  hipLaunchKernelGGL(pv::loss::transpose_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const unsigned short*)in, (unsigned short*)out, n, DP);
   PV_LAUNCH_CHECK();
   return 0;
 }

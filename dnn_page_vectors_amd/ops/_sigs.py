@@ -29,8 +29,8 @@ SIGS = {
     "pv_dssm_explicit": "pppppp" "iii" "ffi" "p",
     "pv_ib_fwd": "ppp" "iii" "fi" "p",
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
+    "pv_ib_bwd_ws": "iii",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
-    "pv_transpose_bf16": "pp" "ii" "p",
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
@@ -57,7 +57,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long}
+_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long}
 
 
 def declare(lib) -> None:

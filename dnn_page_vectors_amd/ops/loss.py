@@ -62,13 +62,6 @@ def _pad_bf16(x: torch.Tensor, DP: int) -> torch.Tensor:
     return out
 
 
-def _transpose_bf16(x: torch.Tensor) -> torch.Tensor:
-    n, DP = x.shape
-    out = torch.empty(DP, n, dtype=torch.bfloat16, device=x.device)
-    check(lib().pv_transpose_bf16(P(x), P(out), n, DP, stream(x.device)), "pv_transpose_bf16")
-    return out
-
-
 class _InBatchFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qn, dn, pos, gamma, clip):
@@ -100,12 +93,12 @@ class _InBatchFn(torch.autograd.Function):
         L_ = lib()
         g = gl.contiguous().float()
         scale = (g * gamma / sumexp).contiguous()
-        dq = torch.zeros(B, DP, dtype=torch.float32, device=qb.device)
-        dd = torch.zeros(M, DP, dtype=torch.float32, device=qb.device)
-        dbT = _transpose_bf16(db)
-        qbT = _transpose_bf16(qb)
-        check(L_.pv_ib_bwd(P(qb), P(db), P(dbT), P(scale), P(dq), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
-        check(L_.pv_ib_bwd(P(db), P(qb), P(qbT), P(scale), P(dd), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
+        dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
+        dd = torch.empty(M, DP, dtype=torch.float32, device=qb.device)
+        ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
+                         dtype=torch.float32, device=qb.device)
+        check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
+        check(L_.pv_ib_bwd(P(db), P(qb), P(scale), P(dd), P(ws), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
         return dq[:, :D], dd[:, :D], None, None, None
 
