@@ -3,9 +3,13 @@
 * ``dssm_explicit_loss``: reference parity head (1 positive + J explicit negatives per
   query; dssm_cnn_v2/cnn_dssm_th.py:159-182).  One fused HIP kernel computes loss, P and
   the gradients in a single pass.
-* ``inbatch_loss``: every query against all M documents (in-batch, or cross-GPU after
-  an all-gather of page vectors).  Flash-style HIP kernels: the (B x M) logits are
-  never materialised (see csrc/kernels/loss.hip).
+* ``inbatch_loss``: every query against all M documents of the local batch.
+  Flash-style HIP kernels: the (B x M) logits are never materialised (see
+  csrc/kernels/loss.hip).
+* ``cross_gpu_loss``: every query against the documents of ALL ranks.  The page
+  vectors are all-gathered already in the kernels' bf16 padded layout (half the xGMI
+  bytes of fp32); in backward the reduce-scatter of dD (RCCL, async) runs while the
+  dQ kernel computes, and the positive-pair term is applied to the local slice after.
 
 Both take L2-normalised vectors (``ops.dense.l2_normalize``).
 """
@@ -14,6 +18,7 @@ from __future__ import annotations
 from typing import Tuple
 
 import torch
+import torch.distributed as dist
 
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
@@ -128,6 +133,69 @@ class _InBatchRowsFn(torch.autograd.Function):
         check(lib().pv_ib_rows(P(S), P(pos), P(g), None, B, M, gamma, clip, stream(S.device)), "pv_ib_rows")
         dS = S.to(torch.bfloat16)
         return (dS @ db).float(), (dS.t() @ qb).float(), None, None, None
+
+
+class _CrossGpuFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qn, dn, pos_local, gamma, clip, group):
+        W = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        B, D = qn.shape
+        n = dn.shape[0]
+        M = n * W
+        DP = (D + 31) // 32 * 32
+        s = stream(qn.device)
+        qb = _pad_bf16(qn.detach(), DP)
+        dbl = _pad_bf16(dn.detach(), DP)
+        db = torch.empty(M, DP, dtype=torch.bfloat16, device=qn.device)
+        dist.all_gather_into_tensor(db, dbl, group=group)
+        pos_local = pos_local.to(torch.int32).contiguous()
+        pos = (pos_local + rank * n).contiguous()
+        sumexp = torch.zeros(B, dtype=torch.float32, device=qn.device)
+        spos = torch.empty(B, dtype=torch.float32, device=qn.device)
+        L_ = lib()
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
+              "pv_ib_pos")
+        loss = gamma + torch.log(sumexp) - spos
+        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp)
+        ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group)
+        return loss, torch.exp(-loss).detach()
+
+    @staticmethod
+    def backward(ctx, gl, _gp):
+        qb, db, dbl, pos_local, sumexp = ctx.saved_tensors
+        B, M, n, D, DP, gamma, clip, group = ctx.meta
+        s = stream(qb.device)
+        L_ = lib()
+        g = gl.contiguous().float()
+        scale = (g * gamma / sumexp).contiguous()
+        dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
+        dd_full = torch.empty(M, DP, dtype=torch.float32, device=qb.device)
+        ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
+                         dtype=torch.float32, device=qb.device)
+        check(L_.pv_ib_bwd(P(db), P(qb), P(scale), P(dd_full), P(ws), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
+        dd = torch.empty(n, DP, dtype=torch.float32, device=qb.device)
+        work = dist.reduce_scatter_tensor(dd, dd_full, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
+        work.wait()
+        check(L_.pv_ib_pos(P(qb), P(dbl), P(pos_local), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s),
+              "pv_ib_pos(bwd)")
+        return dq[:, :D], dd[:, :D], None, None, None, None
+
+
+def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, gamma: float, clip: bool = True,
+                   group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """qn (B, D) and the LOCAL page vectors dn (n, D), normalised; pos_local (B,) indexes dn.
+    Every query is scored against the pages of all ranks (rank r's pages at rows r*n...)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return inbatch_loss(qn, dn, pos_local, gamma, clip)
+    if use_hip(qn, dn) and qn.shape[1] <= 192:
+        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group)
+    from ..parallel.dist import all_gather_autograd
+    docs = all_gather_autograd(dn)
+    pos = pos_local + dist.get_rank(group) * dn.shape[0]
+    return inbatch_loss(qn, docs, pos, gamma, clip)
 
 
 def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, gamma: float, clip: bool = True

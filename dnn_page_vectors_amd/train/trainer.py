@@ -75,13 +75,11 @@ class Trainer:
         if cfg.loss_mode == "explicit":
             per_row, P = lops.dssm_explicit_loss(qn, dn.view(B, S, -1), cfg.GAMMA, clip)
         elif cfg.loss_mode in ("in_batch", "cross_gpu"):
-            offset = 0
-            docs = dn
+            pos = torch.arange(B, device=q.device, dtype=torch.int32) * S
             if cfg.loss_mode == "cross_gpu" and self.info.enabled:
-                docs = pdist.all_gather_autograd(dn)
-                offset = self.info.rank * B * S
-            pos = offset + torch.arange(B, device=q.device, dtype=torch.int32) * S
-            per_row, P = lops.inbatch_loss(qn, docs, pos, cfg.GAMMA, clip)
+                per_row, P = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip)
+            else:
+                per_row, P = lops.inbatch_loss(qn, dn, pos, cfg.GAMMA, clip)
         else:
             raise ValueError(f"unknown loss_mode {cfg.loss_mode!r}")
         range_pop()

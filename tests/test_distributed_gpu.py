@@ -1,0 +1,85 @@
+"""Cross-GPU loss on the GPU path: 2 ranks sharing cuda:0 over gloo (RCCL refuses two ranks
+on one device; the collectives' call pattern is identical).  Each rank's loss rows and
+gradients of its LOCAL query / page vectors must equal the single-process in-batch loss
+over the concatenated batch (fp32 oracle; and, tightly, the single-process HIP path), i.e. the bf16 all-gather, the async
+reduce-scatter of dD and the local positive-pair term are wired correctly.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
+    try:
+        from dnn_page_vectors_amd.ops import loss as L
+        from dnn_page_vectors_amd.ops import reference as ref
+        from dnn_page_vectors_amd.parallel import dist as pdist
+
+        info = pdist.init_distributed()
+        dev = info.device
+        B, S, D = 96, 4, 150
+        n = B * S
+        g = torch.Generator(device=dev).manual_seed(0)
+        qa = torch.nn.functional.normalize(torch.randn(world * B, D, device=dev, generator=g), dim=1)
+        da = torch.nn.functional.normalize(torch.randn(world * n, D, device=dev, generator=g), dim=1)
+        da[::S] = torch.nn.functional.normalize(qa + 0.3 * da[::S], dim=1)
+        qa, da = qa.bfloat16().float(), da.bfloat16().float()
+        pos_local = torch.arange(B, device=dev, dtype=torch.int32) * S
+        ql = qa[rank * B:(rank + 1) * B].clone().requires_grad_(True)
+        dl = da[rank * n:(rank + 1) * n].clone().requires_grad_(True)
+        loss, _ = L.cross_gpu_loss(ql, dl, pos_local, 10.0, True)
+        (loss * (1.0 + 0.5 * rank)).sum().backward()
+        # oracle: all queries vs all pages in one process, rank-weighted like above
+        qf = qa.clone().requires_grad_(True)
+        dfull = da.clone().requires_grad_(True)
+        pos_all = torch.arange(world * B, device=dev) * S
+        lf, _ = ref.inbatch_softmax_loss(qf, dfull, pos_all, 10.0, True)
+        wts = torch.repeat_interleave(1.0 + 0.5 * torch.arange(world, device=dev), B)
+        (lf * wts).sum().backward()
+        # same kernels, one process, whole batch: must agree up to fp32 summation order
+        qh = qa.clone().requires_grad_(True)
+        dh = da.clone().requires_grad_(True)
+        lh, _ = L.inbatch_loss(qh, dh, pos_all.int(), 10.0, True)
+        (lh * wts).sum().backward()
+        sl, sd = slice(rank * B, (rank + 1) * B), slice(rank * n, (rank + 1) * n)
+
+        def rel(a, b):
+            return float((a - b).abs().max() / b.abs().max())
+
+        q.put((rank, (float((loss.detach() - lf.detach()[sl]).abs().max()),
+                      rel(ql.grad, qf.grad[sl]), rel(dl.grad, dfull.grad[sd]),
+                      rel(ql.grad, qh.grad[sl]), rel(dl.grad, dh.grad[sd]))))
+        pdist.destroy()
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, repr(e)))
+
+
+def test_cross_gpu_loss_two_ranks_one_gpu():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=300) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+        e_loss, e_q, e_d, h_q, h_d = res[r]
+        assert e_loss < 1e-4, res
+        assert e_q < 5e-2 and e_d < 5e-2, res  # bf16 G vs fp32 oracle
+        assert h_q < 1e-4 and h_d < 1e-4, res  # vs the single-process HIP path
