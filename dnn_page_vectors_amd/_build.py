@@ -25,6 +25,7 @@ LIB = os.path.join(PKG, "lib")
 OBJ = os.path.join(PKG, "lib", "obj")
 
 HIP_LIB = os.path.join(LIB, "libpagevec_hip.so")
+HIP_DEBUG_LIB = os.path.join(LIB, "libpagevec_hip_debug.so")  # PV_CHECK preconditions compiled in
 RT_LIB = os.path.join(LIB, "libpagevec_rt.so")
 
 ARCH = os.environ.get("PAGEVEC_ARCH", "gfx950")
@@ -118,16 +119,18 @@ def build_runtime(verbose: bool = False, jobs: int = 4) -> str:
     return RT_LIB
 
 
-def build_hip(verbose: bool = False, jobs: int = 4) -> str:
+def build_hip(verbose: bool = False, jobs: int = 4, debug: bool = False) -> str:
+    """Release kernels -> libpagevec_hip.so; debug=True -> libpagevec_hip_debug.so with the
+    PV_CHECK precondition flags (out-of-range ids / keys, LDS indices) compiled in."""
     if not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     srcs = _sources(os.path.join(CSRC, "kernels"), ".hip")
-    flags = list(HIP_FLAGS)
-    if os.environ.get("PAGEVEC_DEBUG_KERNELS"):
-        flags += ["-DPAGEVEC_DEBUG=1"]
-    objs = _compile_all(srcs, HIPCC, flags, os.path.join(CSRC, "kernels"), "hip", jobs, verbose)
-    _link(objs, HIP_LIB, [HIPCC, f"--offload-arch={ARCH}", "-fPIC"], verbose)
-    return HIP_LIB
+    flags = list(HIP_FLAGS) + (["-DPAGEVEC_DEBUG=1"] if debug else [])
+    out = HIP_DEBUG_LIB if debug else HIP_LIB
+    objs = _compile_all(srcs, HIPCC, flags, os.path.join(CSRC, "kernels"), "hipdbg" if debug else "hip", jobs,
+                        verbose)
+    _link(objs, out, [HIPCC, f"--offload-arch={ARCH}", "-fPIC"], verbose)
+    return out
 
 
 def build_all(verbose: bool = False, jobs: int = 0) -> None:
@@ -145,6 +148,7 @@ def main(argv: Sequence[str] = ()) -> None:
     ap.add_argument("--hip", action="store_true")
     ap.add_argument("--rt", action="store_true")
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="also build libpagevec_hip_debug.so")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     a = ap.parse_args(list(argv) or sys.argv[1:])
@@ -157,6 +161,8 @@ def main(argv: Sequence[str] = ()) -> None:
         build_hip(a.verbose, jobs)
     elif a.rt:
         build_runtime(a.verbose, jobs)
+    if a.debug:
+        build_hip(a.verbose, jobs, debug=True)
 
 
 if __name__ == "__main__":

@@ -28,6 +28,10 @@ _lock = threading.Lock()
 _rt: Optional[ctypes.CDLL] = None
 _hip: Optional[ctypes.CDLL] = None
 _hip_err: Optional[str] = None
+_hip_debug: Optional[ctypes.CDLL] = None
+_use_debug = os.environ.get("PAGEVEC_DEBUG_KERNELS", "0") == "1"
+DEBUG_UNITS = ("convfwd", "convbwd", "embed")
+DEBUG_BITS = {0: "id out of range", 1: "LDS index out of range", 2: "shape precondition", 3: "sort key out of range"}
 
 
 class NativeUnavailable(RuntimeError):
@@ -91,9 +95,53 @@ def gpu_present() -> bool:
         return False
 
 
+def use_debug_kernels(on: bool = True) -> None:
+    """Route all ops to libpagevec_hip_debug.so (PV_CHECK preconditions compiled in)."""
+    global _use_debug
+    _use_debug = bool(on)
+
+
+def hip_debug() -> ctypes.CDLL:
+    global _hip_debug
+    with _lock:
+        if _hip_debug is None:
+            import torch  # noqa: F401
+
+            if _autobuild():
+                _build.build_hip(debug=True)
+            if not os.path.exists(_build.HIP_DEBUG_LIB):
+                raise NativeUnavailable(f"{_build.HIP_DEBUG_LIB} missing; run python -m dnn_page_vectors_amd._build "
+                                        "--debug")
+            lib = ctypes.CDLL(_build.HIP_DEBUG_LIB)
+            from .ops import _sigs
+
+            _sigs.declare(lib)
+            for u in DEBUG_UNITS:
+                fn = getattr(lib, f"pv_debug_{u}")
+                fn.argtypes = [ctypes.c_int]
+                fn.restype = ctypes.c_uint
+            _hip_debug = lib
+    return _hip_debug
+
+
+def debug_status(reset: bool = True) -> dict:
+    """{unit: [violated preconditions]} recorded by the debug kernels since the last reset
+    (call after a device synchronize)."""
+    lib = hip_debug()
+    out = {}
+    for u in DEBUG_UNITS:
+        v = int(getattr(lib, f"pv_debug_{u}")(int(reset)))
+        bits = [DEBUG_BITS.get(b, f"bit{b}") for b in range(32) if v >> b & 1]
+        if bits:
+            out[u] = bits
+    return out
+
+
 def hip(required: bool = True) -> Optional[ctypes.CDLL]:
     """The HIP kernel library. Raises when ``required`` and it cannot be loaded."""
     global _hip, _hip_err
+    if _use_debug:
+        return hip_debug()
     if _hip is not None:
         return _hip
     with _lock:

@@ -72,6 +72,37 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 }  // namespace pv
 
+// ---- debug build (python -m dnn_page_vectors_amd._build --debug -> libpagevec_hip_debug.so)
+// PV_CHECK(cond, bit) records a violated precondition (out-of-range id, LDS index
+// outside its tile, ...) in a per-file device flag instead of faulting; the host reads
+// and clears it with pv_debug_<file>(reset) (dnn_page_vectors_amd._native.debug_status).
+// The release library compiles every check away.
+enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3 };
+#ifdef PAGEVEC_DEBUG
+#define PV_DEBUG_FLAG static __device__ unsigned pv_dbg_flag_ = 0;
+#define PV_CHECK(cond, bit)                                      \
+  do {                                                           \
+    if (!(cond)) atomicOr(&pv_dbg_flag_, 1u << (bit));           \
+  } while (0)
+#define PV_DEBUG_EXPORT(tu)                                                   \
+  PV_API unsigned pv_debug_##tu(int reset) {                                 \
+    unsigned v = 0;                                                           \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(pv_dbg_flag_), 4) != hipSuccess) \
+      return 0xFFFFFFFFu;                                                     \
+    if (reset) {                                                              \
+      unsigned z = 0;                                                         \
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(pv_dbg_flag_), &z, 4);               \
+    }                                                                         \
+    return v;                                                                 \
+  }
+#else
+#define PV_DEBUG_FLAG
+#define PV_CHECK(cond, bit) \
+  do {                      \
+  } while (0)
+#define PV_DEBUG_EXPORT(tu)
+#endif
+
 #define PV_LAUNCH_CHECK() \
   do {                    \
     hipError_t e__ = hipGetLastError(); \

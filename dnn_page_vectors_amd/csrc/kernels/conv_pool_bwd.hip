@@ -23,6 +23,7 @@
 
 namespace pv {
 namespace convbwd {
+PV_DEBUG_FLAG
 
 constexpr int EP = 104;
 constexpr int FW = 150;
@@ -192,7 +193,9 @@ __global__ __launch_bounds__(256) void conv_bwd_emit_kernel(const float* gpool, 
     const long s = pair * 4 + j;
     const int t = a + j;
     const bool ok = live && j < K && t < L;
-    keys[s] = ok ? (unsigned)ids[(size_t)n * L + t] : (unsigned)V;
+    const int v = ok ? ids[(size_t)n * L + t] : V;
+    PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
+    keys[s] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;  // invalid ids: zero rows, as in fwd
     vals[s] = (unsigned)s;
     erow[s] = (unsigned)(n * L + t);
     efj[s] = (unsigned)((f << 2) | j);
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __
   float g = 0.f;
   if (i < M) {
     key = skeys[i];
+    PV_CHECK(key <= (unsigned)V, PV_ERR_KEY);
     if (key < (unsigned)V) {
       const unsigned idx = svals[i];
       fj = efj[idx];
@@ -304,6 +308,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __
   if (h1) atomicAdd(&dtable[(size_t)cur * E + c1], s1);
 }
 
+PV_DEBUG_EXPORT(convbwd)
 }  // namespace convbwd
 }  // namespace pv
 

@@ -33,6 +33,7 @@
 
 namespace pv {
 namespace convpool {
+PV_DEBUG_FLAG
 
 constexpr int EP = 104;            // padded embedding stride (elements)
 constexpr int ROWB = EP * 2;       // bytes per LDS row (208 = 13 * 16)
@@ -88,6 +89,7 @@ __device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int 
     int r = threadIdx.x + i * NTHREADS;
     int t = cu.c * R + r;
     tok[i] = (cu.n < p.N && r < CROWS && t < p.L) ? p.ids[(size_t)cu.n * p.L + t] : -1;
+    PV_CHECK(tok[i] < p.V && (tok[i] >= 0 || !(cu.n < p.N && r < CROWS && t < p.L)), PV_ERR_ID);
   }
 }
 
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd_kernel(Params p) {
   }
 }
 
+PV_DEBUG_EXPORT(convfwd)
 }  // namespace convpool
 }  // namespace pv
 

@@ -16,6 +16,7 @@
 
 namespace pv {
 namespace embed {
+PV_DEBUG_FLAG
 
 __global__ void trigram_hash_kernel(const unsigned char* __restrict__ text, const int* __restrict__ lens,
                                     int* __restrict__ out, int N, int Lmax, int L, int V) {
@@ -54,6 +55,7 @@ __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restric
   for (int t0 = 0; t0 < L; t0 += 64) {
     const int tl = t0 + lane;
     const int myid = tl < L ? row[tl] : pad;
+    PV_CHECK(myid == pad || (myid >= 0 && myid < V), PV_ERR_ID);
     unsigned long long m = __ballot(myid != pad && myid >= 0 && myid < V);
     cnt += __popcll(m);
     while (m) {
@@ -118,6 +120,7 @@ __global__ void bag_counts_kernel(const int* __restrict__ ids, unsigned short* _
   int local = 0;
   for (int t = threadIdx.x; t < L; t += blockDim.x) {
     const int v = row[t];
+    PV_CHECK(v == pad || (v >= 0 && v < V), PV_ERR_ID);
     if (v != pad && v >= 0 && v < V) {
       ++local;
       // bf16 +1.0 on a 16-bit cell: CAS on the containing 32-bit word
@@ -144,6 +147,7 @@ __global__ void bag_counts_kernel(const int* __restrict__ ids, unsigned short* _
   }
 }
 
+PV_DEBUG_EXPORT(embed)
 }  // namespace embed
 }  // namespace pv
 

@@ -9,7 +9,8 @@
 //
 // (2) in-batch / cross-GPU mode (new): every query is scored against all M gathered
 //     documents, S = g*clip(Qn.Dn^T) (B x M) with bf16 MFMA, never materialised:
-//       ib_fwd      : per (query block, doc split) partial sum_j exp(S_ij - g)  -> atomics
+//       ib_fwd      : per (query block, doc split) partial sum_j exp(S_ij - g), summed
+//                     over the splits in a fixed order (ib_rowsum: no atomics)
 //                     (no running max needed: clip bounds S to [0, g] (or [-g, g]), so
 //                     exp(S - g) <= 1 and the sum cannot overflow)
 //       ib_bwd<ROW> : recompute the S tile, G = gscale*g*P*clip' (bf16, in registers),
@@ -186,7 +187,7 @@ __device__ __forceinline__ void load_xb(const unsigned short* __restrict__ X, in
 template <int KS>
 __global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Y,
-                                                         float* __restrict__ sumexp, int nx, int ny, int per_split,
+                                                         float* __restrict__ part, int nx, int ny, int per_split,
                                                          float gamma, int clip) {
   using T = IbTile<KS>;
   __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
@@ -229,8 +230,17 @@ __global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
     const int r = r0 + i * 16 + (lane & 15);
-    if (g == 0 && r < nx) atomicAdd(&sumexp[r], v);
+    if (g == 0 && r < nx) part[(size_t)blockIdx.y * nx + r] = v;  // summed in split order by ib_rowsum
   }
+}
+
+// sumexp[r] = sum_s part[s][r] in a fixed order (the forward loss is bit-reproducible)
+__global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restrict__ out, int nx, int ns) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nx) return;
+  float a = 0.f;
+  for (int s = 0; s < ns; ++s) a += part[(size_t)s * nx + r];
+  out[r] = a;
 }
 
 // ROW = true : X = queries, Y = docs,    out = dQ, scale indexed by X row
@@ -446,17 +456,30 @@ static int ib_splits(int nx, int ny, int per_min) {
     default: return -1;                  \
   }
 
-PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, int nx, int ny, int DP, float gamma, int clip,
-                      void* stream) {
+static int ib_fwd_splits(int nx, int ny) {
+  int ns = ib_splits(nx, ny, 256);
+  const int per = ((ny + ns - 1) / ns + pv::loss::TD - 1) / pv::loss::TD * pv::loss::TD;
+  return (ny + per - 1) / per;
+}
+
+// floats of workspace pv_ib_fwd needs
+PV_API long pv_ib_fwd_ws(int nx, int ny, int DP) {
+  (void)DP;
+  return (long)ib_fwd_splits(nx, ny) * nx;
+}
+
+PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int nx, int ny, int DP, float gamma,
+                     int clip, void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
-  int ns = ib_splits(nx, ny, 256);
-  int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
-  ns = (ny + per - 1) / per;
+  const int ns = ib_fwd_splits(nx, ny);
+  const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
   dim3 grid((nx + TQ - 1) / TQ, ns);
   IB_DISPATCH(DP / 32, hipLaunchKernelGGL(ib_fwd_kernel<KS>, grid, dim3(256), 0, (hipStream_t)stream,
-                                          (const unsigned short*)X, (const unsigned short*)Y, sumexp, nx, ny, per,
+                                          (const unsigned short*)X, (const unsigned short*)Y, ws, nx, ny, per,
                                           gamma, clip));
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, sumexp, nx, ns);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -27,7 +27,8 @@ SIGS = {
     "pv_act_bwd": "ppp" "li" "p",
     # loss.hip
     "pv_dssm_explicit": "pppppp" "iii" "ffi" "p",
-    "pv_ib_fwd": "ppp" "iii" "fi" "p",
+    "pv_ib_fwd": "pppp" "iii" "fi" "p",
+    "pv_ib_fwd_ws": "iii",
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
     "pv_ib_bwd_ws": "iii",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
@@ -57,7 +58,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long}
+_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long}
 
 
 def declare(lib) -> None:

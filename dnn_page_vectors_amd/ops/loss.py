@@ -79,10 +79,11 @@ class _InBatchFn(torch.autograd.Function):
         qb = _pad_bf16(qn.detach(), DP)
         db = _pad_bf16(dn.detach(), DP)
         pos = pos.to(torch.int32).contiguous()
-        sumexp = torch.zeros(B, dtype=torch.float32, device=qn.device)
+        sumexp = torch.empty(B, dtype=torch.float32, device=qn.device)
         spos = torch.empty(B, dtype=torch.float32, device=qn.device)
         L_ = lib()
-        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qn.device)
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
               "pv_ib_pos")
         loss = gamma + torch.log(sumexp) - spos
@@ -151,10 +152,11 @@ class _CrossGpuFn(torch.autograd.Function):
         dist.all_gather_into_tensor(db, dbl, group=group)
         pos_local = pos_local.to(torch.int32).contiguous()
         pos = (pos_local + rank * n).contiguous()
-        sumexp = torch.zeros(B, dtype=torch.float32, device=qn.device)
+        sumexp = torch.empty(B, dtype=torch.float32, device=qn.device)
         spos = torch.empty(B, dtype=torch.float32, device=qn.device)
         L_ = lib()
-        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qn.device)
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
               "pv_ib_pos")
         loss = gamma + torch.log(sumexp) - spos

@@ -22,12 +22,14 @@ from ..ops.optim import FlatParams
 
 
 class GradBuckets:
-    def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True):
+    def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg"):
+        """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients)."""
         self.flat = flat
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
+        self.sum_only = reduce == "sum"
         self.avg_op = None
-        if self.world > 1:
+        if self.world > 1 and not self.sum_only:
             self.avg_op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         self.buckets: List[List[int]] = []  # [lo, hi, n_params]
@@ -89,7 +91,7 @@ class GradBuckets:
                 self._launch(bi)
         for bi, h in enumerate(self.handles):
             h.wait()
-            if self.avg_op is None:
+            if self.avg_op is None and not self.sum_only:
                 lo, hi, _ = self.buckets[bi]
                 self.flat.grad[lo:hi].div_(self.world)
         self.handles = [None] * len(self.buckets)

@@ -31,6 +31,7 @@ from ..ops import dense as dops
 from ..ops import loss as lops
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
+from ..parallel import placement
 from ..parallel.ddp import GradBuckets, broadcast_params
 from ..utils.metrics import MetricsLogger
 from ..utils.tracing import range_push, range_pop
@@ -54,7 +55,13 @@ class Trainer:
         bump_generation()
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
                             torch_style=(cfg.model == "bert"))
-        self.buckets = GradBuckets(self.flat, cfg.grad_bucket_mb) if self.info.enabled else None
+        self.placement = getattr(cfg, "placement", "dp")
+        if self.placement not in ("dp", "tower"):
+            raise ValueError(f"unknown placement {self.placement!r}")
+        if self.placement == "tower" and cfg.loss_mode != "explicit":
+            raise ValueError("tower placement splits the explicit J-negative slots; use loss_mode=explicit")
+        self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg")
+                        if self.info.enabled else None)
         self.step = 0
         self.epoch = 0
         self.skipped_steps = 0
@@ -62,13 +69,20 @@ class Trainer:
         self._fault_step = int(os.environ.get("PAGEVEC_FAULT_STEP", "-1"))
 
     # ------------------------------------------------------------------ core step
+    def _base_seed(self) -> int:
+        return (self.cfg.seed * 1000003 + self.step * 7919) & 0x7FFFFFFF
+
     def compute_loss(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int
                      ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Mean loss over the local batch and per-row P(D+|Q)."""
         cfg = self.cfg
         B, S, _ = d_ids.shape
         range_push("forward")
-        q, d = self.model(q_ids, d_ids, seed=seed)
+        tower = self.placement == "tower" and self.info.enabled
+        if tower:  # every rank: same query/head seed; doc slots on their owning ranks
+            q, d = placement.placed_forward(self.model, q_ids, d_ids, self._base_seed())
+        else:
+            q, d = self.model(q_ids, d_ids, seed=seed)
         qn = dops.l2_normalize(q)
         dn = dops.l2_normalize(d.reshape(B * S, -1))
         clip = bool(getattr(cfg, "cos_clip", True))
@@ -83,7 +97,10 @@ class Trainer:
         else:
             raise ValueError(f"unknown loss_mode {cfg.loss_mode!r}")
         range_pop()
-        return per_row.mean(), P
+        loss = per_row.mean()
+        if tower:  # W identical heads: back-propagate 1/W of each, gradients are SUM-reduced
+            loss = placement.scale_grad(loss, 1.0 / self.info.world_size)
+        return loss, P
 
     def train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
         if self.step == self._fault_step:
@@ -92,7 +109,7 @@ class Trainer:
         self.flat.zero_grad()
         if self.buckets is not None:
             self.buckets.start_step()
-        seed = (self.cfg.seed * 1000003 + self.step * 7919 + self.info.rank * 104729) & 0x7FFFFFFF
+        seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
         loss, P = self.compute_loss(q_ids, d_ids, seed)
         range_push("backward")
         loss.backward()

@@ -113,3 +113,43 @@ def test_data_parallel_matches_single_process(mode):
         tr.train_step(qa, da)
     torch.testing.assert_close(res[0], res[1], rtol=0, atol=0)
     torch.testing.assert_close(res[0], tr.flat.data, rtol=1e-4, atol=3e-5)  # Adam amplifies summation-order noise
+
+
+def _placement_worker(rank, world, port, q):
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed(device="cpu")
+    cfg = _cfg("explicit", 8).replace(placement="tower")
+    tr = Trainer(cfg, CDSSM(cfg, 150))
+    losses = []
+    for qa, da in _data(8):  # every rank sees the whole batch; the 4 doc slots are split 2 + 2
+        losses.append(float(tr.train_step(qa, da)["loss"]))
+    q.put((rank, (tr.flat.data.clone(), losses)))
+    pdist.destroy()
+
+
+def test_tower_placement_matches_single_process():
+    """P9 (cnn_dssm_tf.py:139-158): doc slots on different ranks == one process (no dropout)."""
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_placement_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=300) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    pdist.set_info(pdist.DistInfo())
+    cfg = _cfg("explicit", 8)
+    tr = Trainer(cfg, CDSSM(cfg, 150))
+    losses = [float(tr.train_step(qa, da)["loss"]) for qa, da in _data(8)]
+    assert res[0][1] == res[1][1]  # identical head on every rank
+    for a, b in zip(res[0][1], losses):
+        assert abs(a - b) < 1e-5
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
+    torch.testing.assert_close(res[0][0], tr.flat.data, rtol=1e-4, atol=3e-5)

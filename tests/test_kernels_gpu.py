@@ -381,3 +381,41 @@ def test_inbatch_loss_wide_rows_path():
     lr.mean().backward()
     torch.testing.assert_close(qn.grad, q2.grad, rtol=3e-2, atol=3e-3)
     torch.testing.assert_close(dn.grad, d2.grad, rtol=3e-2, atol=3e-3)
+
+
+def test_debug_kernels_flag_bad_ids_without_faulting():
+    """libpagevec_hip_debug.so: out-of-range ids are recorded, not faulted on,
+    and contribute zero rows exactly like the release kernels."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    V, E, F, N, L = 64, 100, 150, 6, 40
+    torch.manual_seed(3)
+    table = bf(torch.randn(V, E, device=DEV)).requires_grad_(True)
+    ws = [bf(torch.randn(F, k, E, device=DEV) * 0.1).requires_grad_(True) for k in (3, 4)]
+    bs = [torch.zeros(F, device=DEV, requires_grad=True) for _ in range(2)]
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    _native.use_debug_kernels(True)
+    try:
+        _native.debug_status(reset=True)
+        out, _ = cops.conv_relu_maxpool_fused(ids, table, ws, bs, 0.0, 1, True)
+        out.sum().backward()
+        torch.cuda.synchronize()
+        assert _native.debug_status() == {}
+        assert any("libpagevec_hip_debug" in p for p in _native.loaded_libraries())
+        bad = ids.clone()
+        bad[1, 5] = V + 7
+        bad[2, 0] = -3
+        table.grad = None
+        out_b, _ = cops.conv_relu_maxpool_fused(bad, table, ws, bs, 0.0, 1, True)
+        out_b.sum().backward()
+        eops.embedding_bag(bad, table.detach(), pad=0)
+        torch.cuda.synchronize()
+        st = _native.debug_status()
+        assert "id out of range" in st.get("convfwd", []), st
+        assert "id out of range" in st.get("embed", []), st
+        ref_tab = torch.cat([table.detach(), torch.zeros(1, E, device=DEV)])  # invalid -> zero row
+        x = ref_tab[torch.where((bad >= 0) & (bad < V), bad.long(), torch.full_like(bad.long(), V))]
+        pr, _ = ref.conv_relu_maxpool(x, [w.detach() for w in ws], [b.detach() for b in bs])
+        torch.testing.assert_close(out_b, pr, rtol=2e-3, atol=2e-3)
+    finally:
+        _native.use_debug_kernels(False)

@@ -32,3 +32,14 @@ def test_hip_library_builds_for_gfx950():
     with open(path, "rb") as f:
         blob = f.read()
     assert b"gfx950" in blob
+
+
+def test_debug_kernel_library_builds_with_checks():
+    """the PV_CHECK build exists and exports its per-file flag readers."""
+    path = _build.build_hip(debug=True)
+    with open(path, "rb") as f:
+        blob = f.read()
+    for unit in ("convfwd", "convbwd", "embed"):
+        assert f"pv_debug_{unit}".encode() in blob
+    with open(_build.HIP_LIB, "rb") as f:
+        assert b"pv_debug_convfwd" not in f.read()  # compiled out of the release library
