@@ -162,6 +162,10 @@ def cmd_eval(a) -> int:
     gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=1024), dev, seed=cfg.seed)
     q, p = gen.eval_set(a.pages)
     r = recall_table(model.encode(q, "query"), model.encode(p, "doc"), torch.arange(a.pages, device=dev))
+    if a.metrics:
+        from .utils.metrics import MetricsLogger
+
+        MetricsLogger(a.metrics).log(eval="synthetic_retrieval", pages=a.pages, weights=a.weights, **r)
     print(json.dumps(r))
     return 0
 
@@ -195,6 +199,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     _common(p)
     p.add_argument("--weights", default=None)
     p.add_argument("--pages", type=int, default=2048)
+    p.add_argument("--metrics", default=None, help="append the eval record to this metrics JSONL")
     p.set_defaults(fn=cmd_eval)
     p = sub.add_parser("bench", help="run bench.py (headline benchmark)")
     p.add_argument("rest", nargs=argparse.REMAINDER)

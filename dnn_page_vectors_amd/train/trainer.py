@@ -33,7 +33,7 @@ from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
 from ..parallel import placement
 from ..parallel.ddp import GradBuckets, broadcast_params
-from ..utils.metrics import MetricsLogger
+from ..utils.metrics import MetricsLogger, hbm_used_gb
 from ..utils.tracing import range_push, range_pop
 
 log = logging.getLogger(__name__)
@@ -41,6 +41,38 @@ log = logging.getLogger(__name__)
 
 class InjectedFault(RuntimeError):
     pass
+
+
+class PhaseTimer:
+    """Step-time breakdown (forward / backward / allreduce / optimizer) for the metrics
+    JSONL.  GPU: HIP events, read only when the record is written, so
+    the timed steps run without host syncs; CPU: wall clock."""
+
+    PHASES = ("forward", "backward", "allreduce", "optimizer")
+
+    def __init__(self, device: torch.device):
+        self.gpu = device.type == "cuda"
+        self.marks = []
+
+    def mark(self) -> None:
+        if self.gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.marks.append(e)
+        else:
+            self.marks.append(time.perf_counter())
+
+    def result_ms(self) -> Dict[str, float]:
+        if len(self.marks) != len(self.PHASES) + 1:
+            return {}
+        if self.gpu:
+            self.marks[-1].synchronize()
+            d = [self.marks[i].elapsed_time(self.marks[i + 1]) for i in range(len(self.PHASES))]
+        else:
+            d = [1e3 * (self.marks[i + 1] - self.marks[i]) for i in range(len(self.PHASES))]
+        out = {f"{p}_ms": round(v, 3) for p, v in zip(self.PHASES, d)}
+        out["step_ms"] = round(sum(d), 3)
+        return out
 
 
 class Trainer:
@@ -67,6 +99,7 @@ class Trainer:
         self.skipped_steps = 0
         self.metrics = metrics
         self._fault_step = int(os.environ.get("PAGEVEC_FAULT_STEP", "-1"))
+        self._timer: Optional[PhaseTimer] = None
 
     # ------------------------------------------------------------------ core step
     def _base_seed(self) -> int:
@@ -106,24 +139,38 @@ class Trainer:
         if self.step == self._fault_step:
             raise InjectedFault(f"injected fault at step {self.step}")
         self.model.train()
+        le = self.cfg.log_every
+        timer = PhaseTimer(self.device) if (self.metrics and self.metrics.enabled and le and
+                                            (self.step + 1) % le == 0) else None
+        if timer:
+            timer.mark()
         self.flat.zero_grad()
         if self.buckets is not None:
             self.buckets.start_step()
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
         loss, P = self.compute_loss(q_ids, d_ids, seed)
+        if timer:
+            timer.mark()
         range_push("backward")
         loss.backward()
         range_pop()
+        if timer:
+            timer.mark()
         range_push("allreduce")
         if self.buckets is not None:
             self.buckets.finish()
         range_pop()
+        if timer:
+            timer.mark()
         range_push("optimizer")
         stats = grad_sumsq_and_finite(self.flat.grad)
         skip = stats[1:2] if self.cfg.skip_nonfinite else None
         self.opt.step(skip)
         bump_generation()
         range_pop()
+        if timer:
+            timer.mark()
+            self._timer = timer
         self.step += 1
         return {"loss": loss.detach(), "acc": (P > 0.5).float().mean(), "grad_sumsq": stats[0],
                 "nonfinite": stats[1]}
@@ -154,8 +201,14 @@ class Trainer:
                 nf = m["nonfinite"]
                 tot["nonfinite"] = tot.get("nonfinite", 0.0) + nf
                 if self.metrics and self.cfg.log_every and self.step % self.cfg.log_every == 0:
-                    self.metrics.log(step=self.step, loss=float(m["loss"]), acc=float(m["acc"]),
-                                     grad_norm=math.sqrt(max(0.0, float(m["grad_sumsq"]))))
+                    rec = dict(step=self.step, loss=float(m["loss"]), acc=float(m["acc"]),
+                               grad_norm=math.sqrt(max(0.0, float(m["grad_sumsq"]))), hbm_gb=round(hbm_used_gb(), 3))
+                    if self._timer is not None:
+                        rec.update(self._timer.result_ms())
+                        if rec.get("step_ms"):
+                            rec["pairs_per_s"] = round(q.shape[0] * self.info.world_size * 1e3 / rec["step_ms"], 1)
+                        self._timer = None
+                    self.metrics.log(**rec)
             n += 1
         if n == 0:
             return {}

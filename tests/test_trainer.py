@@ -89,3 +89,18 @@ def test_nonfinite_gradient_skips_step(tmp_path):
     torch.testing.assert_close(tr.flat.data, before, rtol=0, atol=0)
     m = tr.train_step(q, d)
     assert float(m["nonfinite"]) == 0.0 and not torch.equal(tr.flat.data, before)
+
+
+def test_metrics_jsonl_has_step_breakdown(tmp_path):
+    from dnn_page_vectors_amd.utils.metrics import MetricsLogger
+
+    cfg = _cfg(tmp_path, log_every=2, nb_epoch=1)
+    ml = MetricsLogger(str(tmp_path / "m.jsonl"))
+    tr = Trainer(cfg, CDSSM(cfg, 200), metrics=ml)
+    tr.fit(_batches(3))
+    recs = [r for r in ml.read() if "step" in r]  # per-step records (epoch summaries have no "step")
+    assert [r["step"] for r in recs] == [2, 4]
+    for r in recs:
+        for k in ("forward_ms", "backward_ms", "allreduce_ms", "optimizer_ms", "step_ms", "pairs_per_s", "hbm_gb"):
+            assert k in r, r
+        assert abs(r["step_ms"] - (r["forward_ms"] + r["backward_ms"] + r["allreduce_ms"] + r["optimizer_ms"])) < 0.01
