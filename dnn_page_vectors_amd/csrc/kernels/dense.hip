@@ -4,17 +4,17 @@
 // RTH/RTF magnitude sqrt(max(sum x^2, float32 tiny)) (cnn_dssm_th.py:66-75).
 //
 // linear_act: Y[M,N] = act(X[M,K] . W[N,K]^T + b) with fp32 (or bf16) X/W converted to
-// bf16 while staging into LDS, v_mfma_f32_16x16x32_bf16, fp32 accumulate, fused
-// bias/activation epilogue, optional bf16 copy of Y.  64x64 block tile, BK=32,
-// 4 waves in 2x2, each wave a 32x32 sub-tile (2x2 MFMA tiles).  Used for the CDSSM
-// dense head (300->150), the MLP tower (512-512-128) and BERT projections.
+// bf16 while staging into LDS (16-byte vector loads), v_mfma_f32_16x16x32_bf16, fp32
+// accumulate, fused bias/activation epilogue, optional bf16 copy of Y.  64x64 block
+// tile, BK=64 double-buffered, 4 waves in 2x2, each wave a 32x32 sub-tile.  Used for
+// the CDSSM dense head (300->150) and the MLP tower (512-512-128).
 #include "common.h"
 
 namespace pv {
 namespace dense {
 
-constexpr int BM = 64, BN = 64, BK = 32;
-constexpr int LDA = BK + 8;  // bf16 elements per LDS row (80 B: 16-B aligned, staggers banks)
+constexpr int BM = 64, BN = 64, BK = 64;
+constexpr int LDA = BK + 8;  // bf16 elements per LDS row (144 B: 16-B aligned, staggers banks)
 
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3 };
 
@@ -29,80 +29,133 @@ __device__ __forceinline__ float act_fn(float x, int act) {
   return x;
 }
 
-template <typename TX>
-__device__ __forceinline__ float ldf(const TX* p, size_t i);
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, size_t i);
 template <>
 __device__ __forceinline__ float ldf<float>(const float* p, size_t i) { return p[i]; }
 template <>
 __device__ __forceinline__ float ldf<unsigned short>(const unsigned short* p, size_t i) { return bf16_to_f32(p[i]); }
 
+// 16 consecutive elements of row `row` starting at column k as bf16 (two 16-byte words);
+// vector loads when the run is in bounds and aligned, element loads at the edges.
+template <typename T>
+__device__ __forceinline__ void load16(const T* __restrict__ P, int rows, int cols, int ld, int row, int k,
+                                       bool vec_ok, u32x4 (&out)[2]) {
+  if (row < rows && k + 16 <= cols && vec_ok) {
+    const T* q = P + (size_t)row * ld + k;
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 v0 = reinterpret_cast<const f32x4*>(q)[2 * h];
+        const f32x4 v1 = reinterpret_cast<const f32x4*>(q)[2 * h + 1];
+        out[h] = u32x4{pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                       pack_bf16x2(v1[2], v1[3])};
+      }
+    } else {
+      out[0] = reinterpret_cast<const u32x4*>(q)[0];
+      out[1] = reinterpret_cast<const u32x4*>(q)[1];
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = k + 8 * h + 2 * e;
+        const float x0 = (row < rows && c < cols) ? ldf<T>(P, (size_t)row * ld + c) : 0.f;
+        const float x1 = (row < rows && c + 1 < cols) ? ldf<T>(P, (size_t)row * ld + c + 1) : 0.f;
+        w[e] = pack_bf16x2(x0, x1);
+      }
+      out[h] = u32x4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+
+// Y^T tile = W . X^T: A operand = W rows (n), B operand = X rows (m), so the C layout
+// puts one m per lane and 4 CONSECUTIVE n per lane -> 16-byte fp32 / 8-byte bf16 stores.
+// BK = 64 (2 MFMA k-steps per tile, 8 MFMAs per wave), tile t+1 is fetched into
+// registers while tile t's MFMAs run and written to the other LDS buffer (1 barrier/tile).
 template <typename TX, typename TW>
 __global__ __launch_bounds__(256) void linear_act_kernel(const TX* __restrict__ X, const TW* __restrict__ W,
                                                          const float* __restrict__ bias, float* __restrict__ Y,
                                                          unsigned short* __restrict__ Ybf, int M, int N, int K,
                                                          int ldx, int ldy, int act) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[BM * LDA];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[BN * LDA];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM * LDA];  // X rows (m)
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN * LDA];  // W rows (n)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  f32x4 acc[2][2];
+  const bool xvec = (ldx % (16 / (int)sizeof(TX))) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  const bool wvec = (K % (16 / (int)sizeof(TW))) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0;
+  const int sr = tid >> 2, sc = (tid & 3) * 16;  // staging: row, first column of 16
+  f32x4 acc[2][2];  // [n-subtile][m-subtile]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // stage A (BM x BK) and B (BN x BK) as bf16: 64 rows x 4 segments of 8 per operand
-    {
-      const int r = tid >> 2, c = (tid & 3) * 8;
-      unsigned pa[4], pb[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gk = k0 + c + 2 * q;
-        const int gm = m0 + r, gn = n0 + r;
-        float x0 = (gm < M && gk < K) ? ldf<TX>(X, (size_t)gm * ldx + gk) : 0.f;
-        float x1 = (gm < M && gk + 1 < K) ? ldf<TX>(X, (size_t)gm * ldx + gk + 1) : 0.f;
-        float w0 = (gn < N && gk < K) ? ldf<TW>(W, (size_t)gn * K + gk) : 0.f;
-        float w1 = (gn < N && gk + 1 < K) ? ldf<TW>(W, (size_t)gn * K + gk + 1) : 0.f;
-        pa[q] = pack_bf16x2(x0, x1);
-        pb[q] = pack_bf16x2(w0, w1);
-      }
-      *reinterpret_cast<u32x4*>(&As[r * LDA + c]) = u32x4{pa[0], pa[1], pa[2], pa[3]};
-      *reinterpret_cast<u32x4*>(&Bs[r * LDA + c]) = u32x4{pb[0], pb[1], pb[2], pb[3]};
+  u32x4 ra[2], rb[2];
+  load16<TX>(X, M, K, ldx, m0 + sr, sc, xvec, ra);
+  load16<TW>(W, N, K, K, n0 + sr, sc, wvec, rb);
+  *reinterpret_cast<u32x4*>(&As[0][sr * LDA + sc]) = ra[0];
+  *reinterpret_cast<u32x4*>(&As[0][sr * LDA + sc + 8]) = ra[1];
+  *reinterpret_cast<u32x4*>(&Bs[0][sr * LDA + sc]) = rb[0];
+  *reinterpret_cast<u32x4*>(&Bs[0][sr * LDA + sc + 8]) = rb[1];
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += BK, buf ^= 1) {
+    const bool more = k0 + BK < K;
+    if (more) {
+      load16<TX>(X, M, K, ldx, m0 + sr, k0 + BK + sc, xvec, ra);
+      load16<TW>(W, N, K, K, n0 + sr, k0 + BK + sc, wvec, rb);
     }
-    __syncthreads();
-    bf16x8 a[2], b[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * 32 + i * 16 + (lane & 15)) * LDA + (lane >> 4) * 8]);
+    for (int s2 = 0; s2 < BK / 32; ++s2) {
+      bf16x8 a[2], b[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      b[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wn * 32 + j * 16 + (lane & 15)) * LDA + (lane >> 4) * 8]);
+      for (int i = 0; i < 2; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&Bs[buf][(wn * 32 + i * 16 + (lane & 15)) * LDA + s2 * 32 + g * 8]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&As[buf][(wm * 32 + j * 16 + (lane & 15)) * LDA + s2 * 32 + g * 8]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      *reinterpret_cast<u32x4*>(&As[buf ^ 1][sr * LDA + sc]) = ra[0];
+      *reinterpret_cast<u32x4*>(&As[buf ^ 1][sr * LDA + sc + 8]) = ra[1];
+      *reinterpret_cast<u32x4*>(&Bs[buf ^ 1][sr * LDA + sc]) = rb[0];
+      *reinterpret_cast<u32x4*>(&Bs[buf ^ 1][sr * LDA + sc + 8]) = rb[1];
+    }
     __syncthreads();
   }
-  // epilogue: row = m0 + wm*32 + i*16 + 4*(lane>>4) + r ; col = n0 + wn*32 + j*16 + (lane&15)
+  // acc[i][j][r] = Y[m = m0 + wm*32 + j*16 + (lane&15)][n = n0 + wn*32 + i*16 + 4g + r]
+  const bool yvec = (ldy & 3) == 0;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + wm * 32 + j * 16 + (lane & 15);
+    if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn * 32 + j * 16 + (lane & 15);
-      if (col >= N) continue;
-      const float bv = bias ? bias[col] : 0.f;
+    for (int i = 0; i < 2; ++i) {
+      const int n = n0 + wn * 32 + i * 16 + 4 * g;
+      if (n >= N) continue;
+      float y[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
-        if (row < M) {
-          float y = act_fn(acc[i][j][r] + bv, act);
-          if (Y) Y[(size_t)row * ldy + col] = y;
-          if (Ybf) Ybf[(size_t)row * ldy + col] = f32_to_bf16(y);
-        }
+      for (int r = 0; r < 4; ++r) y[r] = act_fn(acc[i][j][r] + ((bias && n + r < N) ? bias[n + r] : 0.f), act);
+      if (yvec && n + 4 <= N) {
+        if (Y) *reinterpret_cast<f32x4*>(Y + (size_t)m * ldy + n) = f32x4{y[0], y[1], y[2], y[3]};
+        if (Ybf) *reinterpret_cast<uint2*>(Ybf + (size_t)m * ldy + n) = uint2{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) {
+            if (Y) Y[(size_t)m * ldy + n + r] = y[r];
+            if (Ybf) Ybf[(size_t)m * ldy + n + r] = f32_to_bf16(y[r]);
+          }
       }
     }
+  }
 }
 
 // Row-wise L2 normalisation: y = x / sqrt(max(|x|^2, tiny)); one wave per row.

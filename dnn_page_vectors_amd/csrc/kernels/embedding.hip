@@ -147,6 +147,45 @@ __global__ void bag_counts_kernel(const int* __restrict__ ids, unsigned short* _
   }
 }
 
+// LDS-histogram variant (V <= HIST_MAX): one workgroup per bag counts its tokens with
+// LDS atomics (no CAS loops on global bf16 cells, no contention between bags), then
+// writes the WHOLE bf16 row (zeros included) with 8-byte stores — the caller does not
+// have to clear the (N, ldc) matrix.
+constexpr int HIST_MAX = 38912;  // 152 KB of u32 counters
+__global__ __launch_bounds__(1024) void bag_counts_lds_kernel(const int* __restrict__ ids,
+                                                              unsigned short* __restrict__ counts,
+                                                              float* __restrict__ lens, int N, int L, int V, int ldc,
+                                                              int pad) {
+  extern __shared__ unsigned hist[];
+  __shared__ int part[16];
+  const int n = blockIdx.x;
+  for (int c = threadIdx.x; c < ldc; c += blockDim.x) hist[c] = 0u;
+  __syncthreads();
+  const int* row = ids + (size_t)n * L;
+  int local = 0;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    const int v = row[t];
+    PV_CHECK(v == pad || (v >= 0 && v < V), PV_ERR_ID);
+    if (v != pad && v >= 0 && v < V) {
+      ++local;
+      atomicAdd(&hist[v], 1u);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
+  __syncthreads();
+  uint2* crow = reinterpret_cast<uint2*>(counts + (size_t)n * ldc);
+  for (int c4 = threadIdx.x; c4 < ldc / 4; c4 += blockDim.x) {
+    const unsigned* h = hist + 4 * c4;
+    crow[c4] = uint2{pack_bf16x2((float)h[0], (float)h[1]), pack_bf16x2((float)h[2], (float)h[3])};
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    lens[n] = (float)s;
+  }
+}
+
 PV_DEBUG_EXPORT(embed)
 }  // namespace embed
 }  // namespace pv
@@ -171,9 +210,27 @@ PV_API int pv_embedding_bag(const int* ids, const void* W, float* out, float* le
   return 0;
 }
 
+// counts (N, ldc) bf16.  ldc <= HIST_MAX and ldc % 4 == 0: the LDS path writes every
+// element (no zeroing needed); otherwise the caller's zeroed matrix is accumulated into
+// (zeroed must be 1).
 PV_API int pv_bag_counts(const int* ids, void* counts, float* lens, int N, int L, int V, int ldc, int pad,
-                         void* stream) {
+                         int zeroed, void* stream) {
   if (ldc < V || (ldc & 1)) return -1;
+  if (ldc <= pv::embed::HIST_MAX && (ldc & 3) == 0) {
+    static bool attr = false;
+    if (!attr) {  // > 64 KB of dynamic LDS (gfx950: 160 KB per CU)
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&pv::embed::bag_counts_lds_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pv::embed::HIST_MAX * (int)sizeof(unsigned)) != hipSuccess)
+        return -3;
+      attr = true;
+    }
+    hipLaunchKernelGGL(pv::embed::bag_counts_lds_kernel, dim3(N), dim3(1024), ldc * sizeof(unsigned),
+                       (hipStream_t)stream, ids, (unsigned short*)counts, lens, N, L, V, ldc, pad);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
+  if (!zeroed) return -2;
   hipLaunchKernelGGL(pv::embed::bag_counts_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, ids,
                      (unsigned short*)counts, lens, N, L, V, ldc, pad);
   PV_LAUNCH_CHECK();

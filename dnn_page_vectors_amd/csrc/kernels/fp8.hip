@@ -18,13 +18,26 @@ namespace fp8 {
 constexpr int BM = 64, BN = 64, BK = 64;
 constexpr int LDB = BK + 16;  // bytes per LDS row (80: 16-B aligned)
 
-__global__ void amax_kernel(const float* __restrict__ x, long n, float* __restrict__ amax) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// grid-stride 16-byte loads, wave then block reduction, ONE atomic per block (a few
+// hundred blocks: contention-free, unlike per-wave atomics on one address)
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long n, float* __restrict__ amax,
+                                                   int aligned) {
+  __shared__ float sh[4];
+  const long n4 = aligned ? n / 4 : 0;
   const long stride = (long)gridDim.x * blockDim.x;
   float m = 0.f;
-  for (; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+    atomicMax(reinterpret_cast<unsigned*>(amax), __float_as_uint(m));
+  }
 }
 
 // out: n bytes (n % 4 == 0); scale = 448 / max(amax, tiny)
@@ -134,10 +147,12 @@ __global__ __launch_bounds__(256) void fp8_linear_kernel(const unsigned char* __
 using namespace pv;
 
 PV_API int pv_amax(const float* x, long n, float* amax, void* stream) {
-  long blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  const int aligned = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  long blocks = ((aligned ? n / 4 : n) + 255) / 256;
+  if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(pv::fp8::amax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, amax);
+  hipLaunchKernelGGL(pv::fp8::amax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, amax,
+                     aligned);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -11,6 +11,8 @@
 //   * softmax_fwd/bwd   : scale + key-padding mask + row softmax of the attention scores
 //                         (bf16, one wave per row, vectorised 16-byte loads)
 // One 256-thread block handles one row for D in {768, 3072}; rows are independent.
+#include <algorithm>
+
 #include "common.h"
 
 namespace pv {
@@ -133,6 +135,79 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const unsigned short
   }
 }
 
+// Wave-per-row LayerNorm backward for D = 256 * VPT: each lane holds VPT 4-element
+// vectors of dy and x_hat in registers (one read of each), the two row means are wave
+// reductions (no barriers), and dgamma/dbeta accumulate in registers over the rows this
+// wave owns; the 4 waves of a block combine through LDS and issue one atomic per column.
+template <int VPT>
+__global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned short* __restrict__ dy,
+                                                                 const unsigned short* __restrict__ hsum,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 unsigned short* __restrict__ dx,
+                                                                 float* __restrict__ dgamma,
+                                                                 float* __restrict__ dbeta, int M) {
+  constexpr int D = 256 * VPT;
+  __shared__ float red[2][4][D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gm[VPT][4], ga[VPT][4], gb[VPT][4];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const f32x4 g4 = *reinterpret_cast<const f32x4*>(gamma + (i * 64 + lane) * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      gm[i][k] = g4[k];
+      ga[i][k] = 0.f;
+      gb[i][k] = 0.f;
+    }
+  }
+  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[VPT][4], xh[VPT][4];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const size_t o = (size_t)row * D + (i * 64 + lane) * 4;
+      const uint2 gv = *reinterpret_cast<const uint2*>(dy + o);
+      const uint2 hv = *reinterpret_cast<const uint2*>(hsum + o);
+      const unsigned gw[2] = {gv.x, gv.y}, hw[2] = {hv.x, hv.y};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        g[i][k] = __uint_as_float((k & 1) ? (gw[k >> 1] & 0xFFFF0000u) : (gw[k >> 1] << 16));
+        xh[i][k] = (__uint_as_float((k & 1) ? (hw[k >> 1] & 0xFFFF0000u) : (hw[k >> 1] << 16)) - mu) * rs;
+        const float gg = g[i][k] * gm[i][k];
+        a += gg;
+        b += gg * xh[i][k];
+        ga[i][k] += g[i][k] * xh[i][k];
+        gb[i][k] += g[i][k];
+      }
+    }
+    a = wave_sum(a) * (1.f / D);
+    b = wave_sum(b) * (1.f / D);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      float o4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o4[k] = rs * (g[i][k] * gm[i][k] - a - xh[i][k] * b);
+      *reinterpret_cast<uint2*>(dx + (size_t)row * D + (i * 64 + lane) * 4) =
+          uint2{pack_bf16x2(o4[0], o4[1]), pack_bf16x2(o4[2], o4[3])};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[0][wave][(i * 64 + lane) * 4 + k] = ga[i][k];
+      red[1][wave][(i * 64 + lane) * 4 + k] = gb[i][k];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    atomicAdd(&dgamma[c], red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    atomicAdd(&dbeta[c], red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+  }
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
   return 0.5f * x * (1.f + tanhf(u));
@@ -143,6 +218,84 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x2 * x);
   const float t = tanhf(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x2);
+}
+
+// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp instead of libm tanhf
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f / (__expf(2.f * u) + 1.f);
+}
+
+__device__ __forceinline__ float gelu_tanh_grad_fast(float x) {
+  const float x2 = x * x;
+  const float t = fast_tanh(0.7978845608028654f * (x + 0.044715f * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x2);
+}
+
+// Vectorised bias-GELU backward: a thread owns 8 consecutive columns (16-byte loads and
+// stores) for RPB rows; its bias-gradient partial goes to part[blockIdx.y][col] and
+// colsum_kernel adds the partials in a fixed order (no atomics, deterministic).
+// grid = (ceil(D/8/256), ceil(M/RPB)).
+__global__ __launch_bounds__(256) void bias_gelu_bwd_vec_kernel(const unsigned short* __restrict__ x,
+                                                                const float* __restrict__ b,
+                                                                const unsigned short* __restrict__ dy,
+                                                                unsigned short* __restrict__ dx,
+                                                                float* __restrict__ part, int M, int D, int rpb) {
+  const int c8 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c8 >= D) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  float bc[8], acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    bc[k] = b[c8 + k];
+    acc[k] = 0.f;
+  }
+  for (int row = r0; row < r1; ++row) {
+    const size_t o = (size_t)row * D + c8;
+    const u32x4 xv = *reinterpret_cast<const u32x4*>(x + o);
+    const u32x4 gv = *reinterpret_cast<const u32x4*>(dy + o);
+    u32x4 out;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float x0 = __uint_as_float(xv[w] << 16) + bc[2 * w];
+      const float x1 = __uint_as_float(xv[w] & 0xFFFF0000u) + bc[2 * w + 1];
+      const float g0 = __uint_as_float(gv[w] << 16) * gelu_tanh_grad_fast(x0);
+      const float g1 = __uint_as_float(gv[w] & 0xFFFF0000u) * gelu_tanh_grad_fast(x1);
+      acc[2 * w] += g0;
+      acc[2 * w + 1] += g1;
+      out[w] = pack_bf16x2(g0, g1);
+    }
+    *reinterpret_cast<u32x4*>(dx + o) = out;
+  }
+  float* pr = part + (size_t)blockIdx.y * D + c8;
+  *reinterpret_cast<f32x4*>(pr) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<f32x4*>(pr + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+}
+
+// Column sums in a fixed order, two stages: colsum_part (grid (ceil(D/64), S)) reduces
+// a 1/S slice of the rows of 64 columns with 4 row lanes + LDS into part2[S][D];
+// colsum_final adds the S partials.
+constexpr int kColSplits = 32;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ part, float* __restrict__ part2,
+                                                          int R, int D) {
+  __shared__ float sh[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int per = (R + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
+  float a = 0.f;
+  if (c < D)
+    for (int r = r0 + ty; r < r1; r += 4) a += part[(size_t)r * D + c];
+  sh[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < D) part2[(size_t)blockIdx.y * D + c] = sh[0][tx] + sh[1][tx] + sh[2][tx] + sh[3][tx];
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part2, float* __restrict__ out, int S, int D) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += part2[(size_t)s * D + c];
+  out[c] = a;
 }
 
 // x: (M, D) bf16 pre-activation (without bias); y = gelu(x + b)
@@ -207,6 +360,56 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(unsigned short* __rest
   }
 }
 
+// Register-resident variant for L = 256 * NV4 / 4 ... : lane holds NV4 4-element vectors of
+// its row (8-byte loads), the row is read and written exactly once.
+template <int NV4>
+__global__ __launch_bounds__(256) void softmax_fwd_reg_kernel(unsigned short* __restrict__ S,
+                                                              const int* __restrict__ mask, long R, int L,
+                                                              int rows_per_item, float scale) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= R) return;
+  unsigned short* s = S + row * L;
+  const int* mk = mask ? mask + (row / rows_per_item) * L : nullptr;
+  float v[NV4][4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < L) {
+      const uint2 a = *reinterpret_cast<const uint2*>(s + c);
+      const int4 m4 = mk ? *reinterpret_cast<const int4*>(mk + c) : int4{1, 1, 1, 1};
+      v[i][0] = m4.x ? __uint_as_float(a.x << 16) * scale : -INFINITY;
+      v[i][1] = m4.y ? __uint_as_float(a.x & 0xFFFF0000u) * scale : -INFINITY;
+      v[i][2] = m4.z ? __uint_as_float(a.y << 16) * scale : -INFINITY;
+      v[i][3] = m4.w ? __uint_as_float(a.y & 0xFFFF0000u) * scale : -INFINITY;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[i][k] = -INFINITY;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mx = fmaxf(mx, v[i][k]);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[i][k] = v[i][k] == -INFINITY ? 0.f : __expf(v[i][k] - mx);
+      sum += v[i][k];
+    }
+  sum = wave_sum(sum);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+  for (int i = 0; i < NV4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < L)
+      *reinterpret_cast<uint2*>(s + c) =
+          uint2{pack_bf16x2(v[i][0] * inv, v[i][1] * inv), pack_bf16x2(v[i][2] * inv, v[i][3] * inv)};
+  }
+}
+
 // dS = scale * P * (dP - sum(dP * P)) written into dP
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(const unsigned short* __restrict__ P,
                                                           unsigned short* __restrict__ dP, long R, int L, float scale) {
@@ -221,6 +424,49 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const unsigned short* 
   for (int c = lane; c < L; c += 64) {
     const float pv = bf16_to_f32(p[c]);
     d[c] = f32_to_bf16(scale * pv * (bf16_to_f32(d[c]) - dot));
+  }
+}
+
+template <int NV4>
+__global__ __launch_bounds__(256) void softmax_bwd_reg_kernel(const unsigned short* __restrict__ P,
+                                                              unsigned short* __restrict__ dP, long R, int L,
+                                                              float scale) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const unsigned short* p = P + row * L;
+  unsigned short* d = dP + row * L;
+  float pv[NV4][4], dv[NV4][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    uint2 a = {0u, 0u}, b = {0u, 0u};
+    if (c < L) {
+      a = *reinterpret_cast<const uint2*>(p + c);
+      b = *reinterpret_cast<const uint2*>(d + c);
+    }
+    pv[i][0] = __uint_as_float(a.x << 16);
+    pv[i][1] = __uint_as_float(a.x & 0xFFFF0000u);
+    pv[i][2] = __uint_as_float(a.y << 16);
+    pv[i][3] = __uint_as_float(a.y & 0xFFFF0000u);
+    dv[i][0] = __uint_as_float(b.x << 16);
+    dv[i][1] = __uint_as_float(b.x & 0xFFFF0000u);
+    dv[i][2] = __uint_as_float(b.y << 16);
+    dv[i][3] = __uint_as_float(b.y & 0xFFFF0000u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dot += pv[i][k] * dv[i][k];
+  }
+  dot = wave_sum(dot);
+#pragma unroll
+  for (int i = 0; i < NV4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < L) {
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = scale * pv[i][k] * (dv[i][k] - dot);
+      *reinterpret_cast<uint2*>(d + c) = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+    }
   }
 }
 
@@ -241,6 +487,21 @@ PV_API int pv_add_layernorm_fwd(const void* x, const void* r, const float* gamma
 
 PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma, const float* mean, const float* rstd,
                             void* dx, float* dgamma, float* dbeta, int M, int D, void* stream) {
+  const unsigned blocks = (unsigned)std::min(512, std::max(1, (M + 3) / 4));
+#define PV_LN_ROWS(VPT)                                                                                          \
+  hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,   \
+                     (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd, (unsigned short*)dx, \
+                     dgamma, dbeta, M);                                                                           \
+  PV_LAUNCH_CHECK();                                                                                             \
+  return 0;
+  switch (D) {
+    case 256: { PV_LN_ROWS(1) }
+    case 512: { PV_LN_ROWS(2) }
+    case 768: { PV_LN_ROWS(3) }
+    case 1024: { PV_LN_ROWS(4) }
+    default: break;
+  }
+#undef PV_LN_ROWS
   const int rpb = 32;
   hipLaunchKernelGGL(pv::tfm::layernorm_bwd_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 2 * D * sizeof(float),
                      (hipStream_t)stream, (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,
@@ -259,8 +520,31 @@ PV_API int pv_bias_gelu_fwd(const void* x, const float* b, void* y, long n, int 
   return 0;
 }
 
-PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void* dx, float* db, int M, int D,
-                            void* stream) {
+static constexpr int kGeluRpb = 16;
+
+// floats of workspace pv_bias_gelu_bwd needs (vector path)
+PV_API long pv_bias_gelu_bwd_ws(int M, int D) {
+  return (long)((M + kGeluRpb - 1) / kGeluRpb + pv::tfm::kColSplits) * D;
+}
+
+// db is overwritten on the vector path (D % 8 == 0, ws != null), accumulated otherwise.
+PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void* dx, float* db, float* ws, int M,
+                            int D, void* stream) {
+  if (D % 8 == 0 && ws) {
+    const int rpb = kGeluRpb, R = (M + rpb - 1) / rpb;
+    dim3 grid((D / 8 + 255) / 256, R);
+    hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_vec_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, ws, M, D, rpb);
+    PV_LAUNCH_CHECK();
+    float* ws2 = ws + (size_t)R * D;
+    hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0,
+                       (hipStream_t)stream, ws, ws2, R, D);
+    PV_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pv::tfm::colsum_final_kernel, dim3((D + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws2, db,
+                       pv::tfm::kColSplits, D);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   const int rpb = 64;
   hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, db, M, D, rpb);
@@ -269,6 +553,17 @@ PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void*
 }
 
 PV_API int pv_softmax_fwd(void* S, const int* mask, long R, int L, int rows_per_item, float scale, void* stream) {
+  const dim3 grid((unsigned)((R + 3) / 4));
+  if (L % 4 == 0 && L <= 512) {
+    if (L <= 256)
+      hipLaunchKernelGGL(pv::tfm::softmax_fwd_reg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (unsigned short*)S, mask, R, L, rows_per_item, scale);
+    else
+      hipLaunchKernelGGL(pv::tfm::softmax_fwd_reg_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (unsigned short*)S, mask, R, L, rows_per_item, scale);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   hipLaunchKernelGGL(pv::tfm::softmax_fwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      (unsigned short*)S, mask, R, L, rows_per_item, scale);
   PV_LAUNCH_CHECK();
@@ -276,6 +571,17 @@ PV_API int pv_softmax_fwd(void* S, const int* mask, long R, int L, int rows_per_
 }
 
 PV_API int pv_softmax_bwd(const void* P, void* dP, long R, int L, float scale, void* stream) {
+  if (L % 4 == 0 && L <= 512) {
+    const dim3 grid((unsigned)((R + 3) / 4));
+    if (L <= 256)
+      hipLaunchKernelGGL(pv::tfm::softmax_bwd_reg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)P, (unsigned short*)dP, R, L, scale);
+    else
+      hipLaunchKernelGGL(pv::tfm::softmax_bwd_reg_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)P, (unsigned short*)dP, R, L, scale);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   hipLaunchKernelGGL(pv::tfm::softmax_bwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned short*)P, (unsigned short*)dP, R, L, scale);
   PV_LAUNCH_CHECK();

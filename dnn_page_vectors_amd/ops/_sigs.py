@@ -36,7 +36,7 @@ SIGS = {
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
     "pv_embedding_bag": "pppp" "iiiiii" "p",
-    "pv_bag_counts": "ppp" "iiiii" "p",
+    "pv_bag_counts": "ppp" "iiiiii" "p",
     # topk.hip
     "pv_topk_splits": "ii",
     "pv_topk_cos": "pppppp" "iiiii" "p",
@@ -44,7 +44,8 @@ SIGS = {
     "pv_add_layernorm_fwd": "pppppppp" "iif" "p",
     "pv_layernorm_bwd": "pppppppp" "ii" "p",
     "pv_bias_gelu_fwd": "ppp" "li" "p",
-    "pv_bias_gelu_bwd": "ppppp" "ii" "p",
+    "pv_bias_gelu_bwd": "pppppp" "ii" "p",
+    "pv_bias_gelu_bwd_ws": "ii",
     "pv_softmax_fwd": "pp" "liif" "p",
     "pv_softmax_bwd": "pp" "lif" "p",
     # fp8.hip
@@ -58,7 +59,8 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long}
+_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+            "pv_bias_gelu_bwd_ws": ctypes.c_long}
 
 
 def declare(lib) -> None:

@@ -22,12 +22,17 @@ from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
 
+_HIST_MAX = 38912  # csrc/kernels/embedding.hip HIST_MAX
+
+
 def _counts(ids: torch.Tensor, V: int, pad: int):
     N, L = ids.shape
     ldc = (V + 63) // 64 * 64
-    C = torch.zeros(N, ldc, dtype=torch.bfloat16, device=ids.device)
+    small = ldc <= _HIST_MAX  # LDS-histogram kernel writes every element itself (ldc % 64 == 0)
+    C = (torch.empty if small else torch.zeros)(N, ldc, dtype=torch.bfloat16, device=ids.device)
     lens = torch.empty(N, dtype=torch.float32, device=ids.device)
-    check(lib().pv_bag_counts(P(ids), P(C), P(lens), N, L, V, ldc, pad, stream(ids.device)), "pv_bag_counts")
+    check(lib().pv_bag_counts(P(ids), P(C), P(lens), N, L, V, ldc, pad, int(not small), stream(ids.device)),
+          "pv_bag_counts")
     return C, lens
 
 

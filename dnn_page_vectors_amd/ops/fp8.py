@@ -21,6 +21,8 @@ _ACT = {"none": 0, "relu": 1, "tanh": 3}
 def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """fp32 tensor -> (uint8 e4m3 bytes, amax device scalar)."""
     x = x.contiguous().float()
+    if x.data_ptr() % 16:  # the quantiser reads 16-byte vectors
+        x = x.clone()
     amax = torch.zeros(1, dtype=torch.float32, device=x.device)
     n = x.numel()
     check(lib().pv_amax(P(x), n, P(amax), stream(x.device)), "pv_amax")

@@ -72,7 +72,9 @@ class _BiasGeluFn(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(x)
         db = torch.zeros_like(b)
-        check(lib().pv_bias_gelu_bwd(P(x), P(b), P(dy), P(dx), P(db), M, D, stream(x.device)), "pv_bias_gelu_bwd")
+        L_ = lib()
+        ws = torch.empty(L_.pv_bias_gelu_bwd_ws(M, D), dtype=torch.float32, device=x.device) if D % 8 == 0 else None
+        check(L_.pv_bias_gelu_bwd(P(x), P(b), P(dy), P(dx), P(db), P(ws), M, D, stream(x.device)), "pv_bias_gelu_bwd")
         return dx, db
 
 
