@@ -13,12 +13,13 @@
 // (same function as the forward staging), never stored.
 //
 // dTable without 17M x 400-byte float atomics:
-//   emit   : one thread per (n, f) writes up to k small entries
-//            {key = token id, row = n*L + a + j, fj = f<<2|j, g} (sentinel key = V);
-//   sort   : stable radix sort of (key, entry index) (sort.hip);
-//   reduce : each wave walks a fixed chunk of sorted entries, recomputes the
-//            contribution s*g*W[f,j,:]*m on the fly (W is L2-resident) and sums it
-//            in registers per token; one row-atomic per (chunk, token) boundary.
+//   emit   : one thread per (n, f) writes its 4 slot keys (token id, sentinel V when
+//            dead) + slot ids, and one {g*scale, argmax} record per pair;
+//   sort   : stable radix sort of (key, slot id) (sort.hip);
+//   reduce : each wave walks 64 sorted entries, 4 at a time (one per 16-lane group),
+//            recomputes the contribution s*g*W[f,j,:]*m on the fly (bf16 W rows are
+//            L2-resident) and sums it in registers per token; one row-atomic per
+//            (chunk, token) boundary.
 #include "common.h"
 
 namespace pv {
@@ -175,12 +176,14 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
                  token_mode, scale);
 }
 
-// ---- dTable: emit ------------------------------------------------------------------
-// 4 slots per (n,f) pair; slot j >= k or dead (ReLU / g == 0 / t >= L) gets key = V.
-__global__ __launch_bounds__(256) void conv_bwd_emit_kernel(const float* gpool, const float* pooled,
-                                                            const int* argmax, const int* ids, unsigned* keys,
-                                                            unsigned* vals, unsigned* erow, unsigned* efj, float* eg,
-                                                            int N, int L, int V) {
+// ---- dTable emit (compact): keys + slot values + one 8-byte record per (n,f) pair -------
+// Everything the reduce needs per entry follows from the slot s = 4*(n*2FW + f) + j and
+// rec[s >> 2] = {g * scale, argmax}: ONE 8-byte gather per sorted entry instead of three
+// 4-byte gathers from 4x larger per-slot arrays (the sorted order scatters them).
+__global__ __launch_bounds__(256) void conv_bwd_emit2_kernel(const float* gpool, const float* pooled,
+                                                             const int* argmax, const int* ids, unsigned* keys,
+                                                             unsigned* vals, int2* rec, int N, int L, int V,
+                                                             float scale) {
   const long pair = (long)blockIdx.x * 256 + threadIdx.x;
   if (pair >= (long)N * 2 * FW) return;
   const int n = (int)(pair / (2 * FW)), f = (int)(pair % (2 * FW));
@@ -188,124 +191,145 @@ __global__ __launch_bounds__(256) void conv_bwd_emit_kernel(const float* gpool, 
   const float g = gpool[pair];
   const bool live = pooled[pair] > 0.f && g != 0.f;
   const int a = argmax[pair];
+  rec[pair] = int2{__float_as_int(g * scale), a};
+  unsigned k4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const long s = pair * 4 + j;
     const int t = a + j;
     const bool ok = live && j < K && t < L;
     const int v = ok ? ids[(size_t)n * L + t] : V;
     PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
-    keys[s] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;  // invalid ids: zero rows, as in fwd
-    vals[s] = (unsigned)s;
-    erow[s] = (unsigned)(n * L + t);
-    efj[s] = (unsigned)((f << 2) | j);
-    eg[s] = g;
+    k4[j] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;
   }
+  reinterpret_cast<u32x4*>(keys)[pair] = u32x4{k4[0], k4[1], k4[2], k4[3]};
+  const unsigned s0 = (unsigned)(pair * 4);
+  reinterpret_cast<u32x4*>(vals)[pair] = u32x4{s0, s0 + 1, s0 + 2, s0 + 3};
 }
 
-// ---- dTable: reduce over sorted entries ----------------------------------------------
-// One wave per chunk of 64 sorted entries.  The entry metadata is loaded lane-parallel
-// (lane i <- entry b+i: key, f/j, g, row hash) so the per-entry loop has no dependent
-// global loads: entries are broadcast with v_readlane (uniform loop index) and lane l owns
-// the contiguous columns e = l, l+64 (coalesced W loads and row atomics).
-// Dropout bits: an entry needs ceil(E/4) group hashes; per PAIR of entries each lane of
-// half h computes the group hash (lane&31) of entry j0+h (one mix32 for two entries),
-// and the lanes fetch their groups' hashes with ds_bpermute — instead of every lane
-// hashing both of its columns for every entry.  W values are fetched for 8 entries
-// before they are used (W is L2-resident).
-__global__ __launch_bounds__(256) void conv_bwd_reduce_kernel(const unsigned* __restrict__ skeys,
-                                                              const unsigned* __restrict__ svals,
-                                                              const unsigned* __restrict__ erow,
-                                                              const unsigned* __restrict__ efj,
-                                                              const float* __restrict__ eg, const float* __restrict__ w3,
-                                                              const float* __restrict__ w4, float* __restrict__ dtable,
-                                                              long M, int E, int V, unsigned seed, unsigned row_offset,
-                                                              int thr, int token_mode, float scale) {
-  const int lane = threadIdx.x & 63;
-  const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+// ---- dTable reduce, 4 entries per wave-instruction ------------------------------------
+// A 16-lane group owns one sorted entry per round (4 entries per round per wave); lane p
+// of the group owns columns 8p..8p+7 of the 104-wide padded row: one 16-byte load of the
+// bf16 weight row W[f][j] (layout [2*FW][4][EP], zero padded), the two dropout group
+// hashes of those 8 columns, 8 FMAs into its accumulator.  Entries are sorted by key, so
+// a round's keys are ascending across the groups: the common round (all 4 keys equal the
+// current run's key) just accumulates; a round with a key change flushes the finished
+// run — the 4 groups' partials meet in a wave-private LDS slab (write 104 floats per
+// group, read back lane-linear) and lane l adds columns l, l+64 to dTable with two
+// 256-byte-shaped atomic instructions.
+constexpr int RPIECES = EP / 8;  // 13 pieces of 8 columns
+__device__ __forceinline__ void reduce4_flush(float* slab, const float (&acc)[8], int g, int p, int lane, int E,
+                                              unsigned key, float* __restrict__ dtable) {
+  if (p < RPIECES) {
+    *reinterpret_cast<f32x4*>(slab + g * EP + 8 * p) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    *reinterpret_cast<f32x4*>(slab + g * EP + 8 * p + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's slab writes are done
+  const int c0 = lane, c1 = lane + 64;
+  if (c0 < E) {
+    const float v = slab[c0] + slab[EP + c0] + slab[2 * EP + c0] + slab[3 * EP + c0];
+    atomicAdd(&dtable[(size_t)key * E + c0], v);
+  }
+  if (c1 < E) {
+    const float v = slab[c1] + slab[EP + c1] + slab[2 * EP + c1] + slab[3 * EP + c1];
+    atomicAdd(&dtable[(size_t)key * E + c1], v);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // slab reads done before the next flush overwrites it
+}
+
+__global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* __restrict__ skeys,
+                                                               const unsigned* __restrict__ svals,
+                                                               const int2* __restrict__ rec,
+                                                               const unsigned short* __restrict__ wrow,
+                                                               float* __restrict__ dtable, long M, int L, int E,
+                                                               int V, unsigned seed, unsigned row_offset, int thr,
+                                                               int token_mode) {
+  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, p = lane & 15;
+  float* slab = slabs[wave];
+  const long chunk = (long)blockIdx.x * 4 + wave;
   const long b = chunk * 64;
   if (b >= M) return;
   const long i = b + lane;
   unsigned key = (unsigned)V, fj = 0, hr = 0;
-  float g = 0.f;
+  float gg = 0.f;
   if (i < M) {
     key = skeys[i];
     PV_CHECK(key <= (unsigned)V, PV_ERR_KEY);
     if (key < (unsigned)V) {
-      const unsigned idx = svals[i];
-      fj = efj[idx];
-      g = eg[idx] * scale;
-      if (thr > 0) hr = dropout_row_hash(seed, row_offset + erow[idx]);
+      const unsigned sl = svals[i];
+      const unsigned pair = sl >> 2, j = sl & 3;
+      const unsigned nn = pair / (2 * FW), f = pair - nn * (2 * FW);
+      const int2 rc = rec[pair];
+      fj = (f << 2) | j;
+      gg = __int_as_float(rc.x);
+      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)rc.y + j);
     }
   }
-  const unsigned long long live = __ballot(key < (unsigned)V);
-  const int n = __popcll(live);  // sorted: live entries are a prefix of the chunk
+  const int n = __popcll(__ballot(key < (unsigned)V));  // live entries are a prefix (sorted)
   if (n == 0) return;
-  const int c0 = lane, c1 = lane + 64;
-  const bool h0 = c0 < E, h1 = c1 < E;
-  // bpermute byte addresses of the lanes holding my two groups' hashes (per half)
-  const int src0 = (c0 >> 2) * 4, src1 = ((c1 >> 2) & 31) * 4 + (c1 >= 128 ? 0 : 0);
-  const int sh0 = 8 * (c0 & 3), sh1 = 8 * (c1 & 3);
   unsigned cur = __builtin_amdgcn_readfirstlane(key);
-  float s0 = 0.f, s1 = 0.f;
-  for (int j0 = 0; j0 < n; j0 += 8) {
-    float wv0[8], wv1[8];
+  float acc[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int jj = min(j0 + u, n - 1);
-      const unsigned f_j = (unsigned)__builtin_amdgcn_readlane((int)fj, jj);
-      const int f = (int)(f_j >> 2), j = (int)(f_j & 3);
-      const float* w = f < FW ? (w3 + ((size_t)f * 3 + j) * E) : (w4 + ((size_t)(f - FW) * 4 + j) * E);
-      wv0[u] = h0 ? w[c0] : 0.f;
-      wv1[u] = h1 ? w[c1] : 0.f;
-    }
-    unsigned hv[8];
-    if (thr > 0 && !token_mode) {
-#pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        const int ja = min(j0 + u, n - 1), jb = min(j0 + u + 1, n - 1);
-        const unsigned ha = (unsigned)__builtin_amdgcn_readlane((int)hr, ja);
-        const unsigned hb = (unsigned)__builtin_amdgcn_readlane((int)hr, jb);
-        const unsigned gh = dropout_group_hash(lane < 32 ? ha : hb, (unsigned)(lane & 31));
-        // entry A's groups live in lanes 0..31, entry B's in lanes 32..63
-        const unsigned a0 = (unsigned)__builtin_amdgcn_ds_bpermute(src0, (int)gh);
-        const unsigned a1 = (unsigned)__builtin_amdgcn_ds_bpermute(src1, (int)gh);
-        const unsigned b0 = (unsigned)__builtin_amdgcn_ds_bpermute(src0 + 128, (int)gh);
-        const unsigned b1 = (unsigned)__builtin_amdgcn_ds_bpermute(src1 + 128, (int)gh);
-        hv[u] = (((a0 >> sh0) & 0xFF) << 8) | ((a1 >> sh1) & 0xFF);
-        hv[u + 1] = (((b0 >> sh0) & 0xFF) << 8) | ((b1 >> sh1) & 0xFF);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int jj = j0 + u;
-      if (jj >= n) break;
-      const unsigned k = (unsigned)__builtin_amdgcn_readlane((int)key, jj);
-      if (k != cur) {
-        if (h0) atomicAdd(&dtable[(size_t)cur * E + c0], s0);
-        if (h1) atomicAdd(&dtable[(size_t)cur * E + c1], s1);
-        s0 = s1 = 0.f;
-        cur = k;
-      }
-      const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), jj));
-      float v0 = gj * wv0[u], v1 = gj * wv1[u];
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const bool act = p < RPIECES;
+  for (int r0 = 0; r0 < n; r0 += 4) {
+    const int e = r0 + g;                 // this group's entry (lane index in the wave)
+    const bool valid = e < n;
+    const int src = (valid ? e : r0) * 4;
+    unsigned kg = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
+    const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
+    float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
+    const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
+    if (!valid) ge = 0.f;
+    // contribution of this group's entry to columns 8p..8p+7
+    float v[8];
+    {
+      u32x4 w = u32x4{0u, 0u, 0u, 0u};
+      if (act) w = *reinterpret_cast<const u32x4*>(wrow + (size_t)f_j * EP + 8 * p);
+      unsigned hm0 = 0xFFFFFFFFu, hm1 = 0xFFFFFFFFu;  // one byte per column (>= thr keeps)
       if (thr > 0) {
-        unsigned m0, m1;
         if (token_mode) {
-          m0 = m1 = (unsigned)__builtin_amdgcn_readlane((int)hr, jj) & 0xFF;
+          hm0 = hm1 = (he & 0xFFu) * 0x01010101u;
         } else {
-          m0 = hv[u] >> 8;
-          m1 = hv[u] & 0xFF;
+          hm0 = dropout_group_hash(he, (unsigned)(2 * p));
+          hm1 = dropout_group_hash(he, (unsigned)(2 * p + 1));
         }
-        if ((int)m0 < thr) v0 = 0.f;
-        if ((int)m1 < thr) v1 = 0.f;
       }
-      s0 += v0;
-      s1 += v1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
+        const unsigned hb = ((k < 4 ? hm0 : hm1) >> (8 * (k & 3))) & 0xFFu;
+        v[k] = (thr > 0 && (int)hb < thr) ? 0.f : ge * __uint_as_float(wk);
+      }
+    }
+    // keys of the 4 groups (ascending); invalid groups join the current run with v = 0
+    if (!valid) kg = cur;
+    const unsigned k0 = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
+    const unsigned k3 = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
+    if (k0 == cur && k3 == cur) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      continue;
+    }
+    // boundary round: runs end inside it
+    bool done = false;
+    for (int it = 0; it < 5; ++it) {
+      const bool mine = !done && kg == cur;
+      if (mine) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        done = true;
+      }
+      const unsigned long long left = __ballot(!done);
+      if (left == 0) break;
+      reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+      cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
     }
   }
-  if (h0) atomicAdd(&dtable[(size_t)cur * E + c0], s0);
-  if (h1) atomicAdd(&dtable[(size_t)cur * E + c1], s1);
+  reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
 }
 
 PV_DEBUG_EXPORT(convbwd)
@@ -330,28 +354,29 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   return 0;
 }
 
-// Entries: M = N*2*FW*4 slots.
-PV_API int pv_conv_pool_bwd_emit(const float* gpool, const float* pooled, const int* argmax, const int* ids,
-                                 unsigned* keys, unsigned* vals, unsigned* erow, unsigned* efj, float* eg, int N,
-                                 int L, int V, void* stream) {
+// keys/vals: M = N*2*FW*4 slots; rec: N*2*FW records {g*scale, argmax}.
+PV_API int pv_conv_pool_bwd_emit2(const float* gpool, const float* pooled, const int* argmax, const int* ids,
+                                  unsigned* keys, unsigned* vals, void* rec, int N, int L, int V, float scale,
+                                  void* stream) {
   using namespace pv::convbwd;
-  long pairs = (long)N * 2 * FW;
-  hipLaunchKernelGGL(conv_bwd_emit_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     gpool, pooled, argmax, ids, keys, vals, erow, efj, eg, N, L, V);
+  const long pairs = (long)N * 2 * FW;
+  hipLaunchKernelGGL(conv_bwd_emit2_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale);
   PV_LAUNCH_CHECK();
   return 0;
 }
 
-PV_API int pv_conv_pool_bwd_reduce(const unsigned* skeys, const unsigned* svals, const unsigned* erow,
-                                   const unsigned* efj, const float* eg, const float* w3, const float* w4,
-                                   float* dtable, long M, int E, int V, unsigned seed, unsigned row_offset, int thr,
-                                   int token_mode, float scale, void* stream) {
+// wrow: bf16 [2*FW][4][EP] weight rows (zero padded); requires E <= EP.
+PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                    float* dtable, long M, int L, int E, int V, unsigned seed, unsigned row_offset,
+                                    int thr, int token_mode, void* stream) {
   using namespace pv::convbwd;
-  if (E > 128) return -1;
-  long chunks = (M + 63) / 64;
-  hipLaunchKernelGGL(conv_bwd_reduce_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, skeys, svals, erow, efj, eg, w3, w4, dtable, M, E, V, seed, row_offset,
-                     thr, token_mode, scale);
+  if (E > EP) return -1;
+  const long chunks = (M + 63) / 64;
+  hipLaunchKernelGGL(conv_bwd_reduce4_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, L, E, V, seed,
+                     row_offset, thr, token_mode);
   PV_LAUNCH_CHECK();
   return 0;
 }
+

@@ -15,8 +15,8 @@ SIGS = {
     "pv_conv_pool_fwd": "pppppp" "iii" "uu" "ii" "f" "i" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "uuiif" "p",
-    "pv_conv_pool_bwd_emit": "pppp" "ppppp" "iii" "p",
-    "pv_conv_pool_bwd_reduce": "ppppp" "ppp" "lii" "uuiif" "p",
+    "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "uuii" "p",
+    "pv_conv_pool_bwd_emit2": "ppppppp" "iii" "f" "p",
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",
     "pv_sort_pairs_u32": "plpppp" "li" "p",

@@ -101,11 +101,9 @@ class _ConvPoolFn(torch.autograd.Function):
             u32 = torch.int32
             keys = torch.empty(M, dtype=u32, device=dev)
             vals = torch.empty(M, dtype=u32, device=dev)
-            erow = torch.empty(M, dtype=u32, device=dev)
-            efj = torch.empty(M, dtype=u32, device=dev)
-            eg = torch.empty(M, dtype=torch.float32, device=dev)
-            check(L_.pv_conv_pool_bwd_emit(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(erow), P(efj),
-                                           P(eg), N, L, V, s), "pv_conv_pool_bwd_emit")
+            rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
+            check(L_.pv_conv_pool_bwd_emit2(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
+                                            scale, s), "pv_conv_pool_bwd_emit2")
             end_bit = max(1, int(V).bit_length())
             skeys = torch.empty_like(keys)
             svals = torch.empty_like(vals)
@@ -114,9 +112,12 @@ class _ConvPoolFn(torch.autograd.Function):
             check(L_.pv_sort_pairs_u32(P(temp), tb, P(keys), P(skeys), P(vals), P(svals), M, end_bit, s),
                   "pv_sort_pairs_u32")
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
-            check(L_.pv_conv_pool_bwd_reduce(P(skeys), P(svals), P(erow), P(efj), P(eg), P(w3.contiguous()),
-                                             P(w4.contiguous()), P(dtable), M, E, V, seed, row_offset, thr, tok,
-                                             scale, s), "pv_conv_pool_bwd_reduce")
+            # bf16 weight rows [2*FW][4][EP] (the operands the forward MFMAs used)
+            wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)
+            wrow[:FW, :3, :E] = w3.detach()
+            wrow[FW:, :, :E] = w4.detach()
+            check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
+                                              row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
         return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
 
 
