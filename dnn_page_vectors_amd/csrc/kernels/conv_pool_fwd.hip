@@ -66,6 +66,19 @@ struct Params {
 // carries no branches): 1 no gather, 2 max-only epilogue, 4 no dropout hash,
 // 8 no A-fragment LDS reads (tools/conv_micro.py times them interleaved in one process).
 
+// Conflict-free A-fragment reads.  ds_read_b128 is serviced in 4 lane groups
+// {0-3,12-15,20-27} {4-11,16-19,28-31} {32-35,44-47,52-59} {36-43,48-51,60-63}; with the
+// fixed 208-byte row stride (13 quads) lane (row i, k-chunk c) hits quad 13*w(i) + c (mod
+// 16).  Mapping the MFMA A rows 4..11 to the EVEN windows and rows 0..3, 12..15 to the ODD
+// windows, and letting lane group kq read k-chunk {0,2,1,3}[kq] of each 32-wide step, puts
+// the 16 lanes of every group on 16 distinct quads (the natural order is 2-way on most
+// groups: measured SQ_LDS_BANK_CONFLICT ~3.6 cycles per read).  The packed weights use the
+// same k-chunk order; the epilogue maps accumulator row i back to window w(i).
+__device__ __forceinline__ int win_of_row(int i) {
+  return (i >= 4 && i < 12) ? 2 * (i - 4) : (i < 4 ? 2 * i + 1 : 2 * (i - 12) + 9);
+}
+__device__ __forceinline__ int chunk_of_kq(int kq) { return kq == 1 ? 2 : (kq == 2 ? 1 : kq); }
+
 // fragment base index of tile T in wpack (tiles 0..9 k3 with S3 steps, 10..19 k4 with S4)
 __device__ __forceinline__ int tile_base(int T) {
   return T < NT ? T * S3 : NT * S3 + (T - NT) * S4;
@@ -247,7 +260,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       for (int i = 0; i < N3; ++i) c3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const char* abase = xl + (blk * 16 + rsub) * ROWB + kq * 16;
+      const char* abase = xl + (blk * 16 + win_of_row(rsub)) * ROWB + chunk_of_kq(kq) * 16;
       constexpr int NS = N4 > 0 ? S4 : S3;
       // A fragments software-pipelined PF K-steps ahead (ds_read_b128 latency vs 2-3 MFMAs per step)
       constexpr bool noread = (DBG & 8) != 0;
@@ -267,8 +280,8 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
 #pragma unroll
         for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
       }
-      // running max / argmax; rows of this lane: t0 + 4*kq + r
-      const int rowb = t0 + 4 * kq;
+      // running max / argmax; accumulator row 4*kq + r is window t0 + win_of_row(4*kq + r)
+      const int rowb = t0;
       if constexpr ((DBG & 2) != 0) {
 #pragma unroll
         for (int i = 0; i < N3; ++i) m3[i] = __builtin_elementwise_max(m3[i], c3[i]);
@@ -279,7 +292,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       if (t0 + 16 <= nw4) {  // every row valid for both widths (all but the last block)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = rowb + r;
+          const int row = rowb + win_of_row(4 * kq + r);
 #pragma unroll
           for (int i = 0; i < N3; ++i) {
             const float x = c3[i][r];
@@ -298,7 +311,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = rowb + r;
+          const int row = rowb + win_of_row(4 * kq + r);
 #pragma unroll
           for (int i = 0; i < N3; ++i) {
             const float x = c3[i][r];
@@ -375,6 +388,246 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd_kernel(Params p) {
   }
 }
 
+// ---- v2 schedule: double-buffered chunk tiles + tag-encoded argmax -----------------
+// * Two LDS chunk buffers: a wave stores chunk i+1's staged rows into the idle buffer
+//   right after ITS OWN MFMA phase on chunk i (no wait for slower waves), then ONE
+//   barrier per chunk (v1: store between two barriers).
+// * Running max with the argmax in the low TAGB mantissa bits: value bits & ~mask |
+//   block index (uniform SGPR) -> v_and_or + v_max per accumulator (v1: v_cmp + two
+//   v_cndmask), and no argmax registers.  The pooled value loses the low TAGB mantissa
+//   bits (relative change < 2^-(23-TAGB)); ties within that are broken by block order.
+constexpr int TAGB = 10;                      // <= 1024 blocks of 16 windows (L <= 16386)
+constexpr unsigned TAGM = (1u << TAGB) - 1u;
+
+__device__ __forceinline__ float tagged(float x, unsigned blk) {
+  return __uint_as_float((__float_as_uint(x) & ~TAGM) | blk);
+}
+
+// m = max(m, tag(x)): the tag is plain C++ (v_and/v_or, whose MFMA-result read hazards the
+// compiler resolves); only the max is inline asm — fmaxf in IEEE mode would canonicalise
+// BOTH operands (two extra v_max x,x per accumulator), and both operands here come from
+// ordinary VALU ops, so the asm needs no MFMA hazard handling.
+__device__ __forceinline__ float max_tagged(float m, float x, unsigned keep, unsigned btag) {
+  const float t = __uint_as_float((__float_as_uint(x) & keep) | btag);
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(m), "v"(t));
+  return r;
+}
+
+template <int N3, int N4, int PF, int DBG>
+__device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4base, char* xl0, int* ids_lds) {
+  const int lane = threadIdx.x & 63;
+  constexpr int A3 = N3 > 0 ? N3 : 1, A4 = N4 > 0 ? N4 : 1;
+  bf16x8 w3[A3][S3];
+  bf16x8 w4[A4][S4];
+#pragma unroll
+  for (int i = 0; i < N3; ++i)
+#pragma unroll
+    for (int s = 0; s < S3; ++s) w3[i][s] = p.wpack[(tile_base(t3base + i) + s) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < N4; ++i)
+#pragma unroll
+    for (int s = 0; s < S4; ++s) w4[i][s] = p.wpack[(tile_base(NT + t4base + i) + s) * 64 + lane];
+
+  const int nchunks = (p.L - 3 + 1 + R - 1) / R;
+  // chunk cursors: cur (MFMA), c1 (staged in regs / stored this iteration), c2 (ids in LDS), c3 (ids in regs)
+  Cursor cur{(int)blockIdx.x, 0, nchunks};
+  Cursor c1 = cur;
+  advance(c1);
+  Cursor c2 = c1;
+  advance(c2);
+  Cursor c3 = c2;
+  advance(c3);
+  unsigned* hs = reinterpret_cast<unsigned*>(ids_lds + 2 * CROWS);  // 2 x CROWS row hashes
+  int tok[IDS_PT];
+  unsigned hrw[IDS_PT];
+  u32x4 stage[PPT];
+  // prologue: chunk 0 -> xl[0]; chunk 1 rows -> regs; chunk 2 ids + hashes -> LDS slot 0; chunk 3 ids -> regs
+  load_ids(p, cur, tok);
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) {
+    const int r = threadIdx.x + i * NTHREADS;
+    if (r < CROWS) {
+      ids_lds[r] = tok[i];
+      hs[r] = row_hash(p, cur, r);
+    }
+  }
+  __syncthreads();
+  load_rows<DBG>(p, ids_lds, stage);
+  store_rows<DBG>(p, xl0, hs, stage);
+  load_ids(p, c1, tok);
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) {
+    const int r = threadIdx.x + i * NTHREADS;
+    if (r < CROWS) {
+      ids_lds[CROWS + r] = tok[i];
+      hs[CROWS + r] = row_hash(p, c1, r);
+    }
+  }
+  load_ids(p, c2, tok);
+#pragma unroll
+  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, c2, threadIdx.x + i * NTHREADS);
+  __syncthreads();
+  load_rows<DBG>(p, ids_lds + CROWS, stage);  // rows of c1
+  // slot bookkeeping: ids/hashes of chunk c live in slot (c parity); the stage regs hold c1
+  int par = 0;  // parity of `cur` (xl buffer and id/hash slot of cur)
+  const int nw3 = p.L - 2, nw4 = p.L - 3;
+  f32x4 m3[A3], m4[A4];
+  auto reset_state = [&]() {
+#pragma unroll
+    for (int i = 0; i < N3; ++i) m3[i] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int i = 0; i < N4; ++i) m4[i] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  };
+  reset_state();
+  const int rsub = lane & 15, kq = lane >> 4;
+  const unsigned keep = ~TAGM;
+
+  while (cur.n < p.N) {
+    const char* xl = xl0 + par * (CROWS * ROWB);
+    const int tc = cur.c * R;
+    // A fragments are prefetched PF K-steps ahead ACROSS blocks: the last steps of block b
+    // already fetch block b+1's first fragments (the block loop is not unrolled, so the
+    // compiler cannot pipeline it by itself)
+    const char* abase0 = xl + win_of_row(rsub) * ROWB + chunk_of_kq(kq) * 16;
+    bf16x8 ab[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) ab[u] = *reinterpret_cast<const bf16x8*>(abase0 + u * 64);
+#pragma unroll 1
+    for (int blk = 0; blk < R / 16; ++blk) {
+      const int t0 = tc + blk * 16;
+      if (t0 >= nw3) break;
+      const unsigned btag = (unsigned)(t0 >> 4);
+      f32x4 c3[A3], c4[A4];
+#pragma unroll
+      for (int i = 0; i < N3; ++i) c3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* abase = abase0 + blk * 16 * ROWB;
+      const char* anext = blk + 1 < R / 16 ? abase + 16 * ROWB : abase;
+      constexpr int NS = N4 > 0 ? S4 : S3;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        bf16x8 a = ab[0];
+#pragma unroll
+        for (int u = 0; u + 1 < PF; ++u) ab[u] = ab[u + 1];
+        if constexpr ((DBG & 8) == 0) {
+          if (s + PF < NS) ab[PF - 1] = *reinterpret_cast<const bf16x8*>(abase + (s + PF) * 64);
+          else ab[PF - 1] = *reinterpret_cast<const bf16x8*>(anext + (s + PF - NS) * 64);
+        }
+        if (s < S3) {
+#pragma unroll
+          for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
+      }
+      if constexpr ((DBG & 2) != 0) {
+#pragma unroll
+        for (int i = 0; i < N3; ++i) m3[i] += c3[i];
+#pragma unroll
+        for (int i = 0; i < N4; ++i) m4[i] += c4[i];
+        continue;
+      }
+      if (t0 + 16 <= nw4) {
+#pragma unroll
+        for (int i = 0; i < N3; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
+#pragma unroll
+        for (int i = 0; i < N4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = t0 + win_of_row(4 * kq + r);
+#pragma unroll
+          for (int i = 0; i < N3; ++i)
+            if (row < nw3) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
+#pragma unroll
+          for (int i = 0; i < N4; ++i)
+            if (row < nw4) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+        }
+      }
+    }
+    // sample epilogue: decode (value, window) per register, reduce over regs and lane groups
+    if (cur.c == cur.nchunks - 1) {
+      auto finish = [&](f32x4& m, int colbase) {
+        float bv = -INFINITY;
+        int bi = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const unsigned u = __float_as_uint(m[r]);
+          const float v = m[r] == -INFINITY ? -INFINITY : __uint_as_float(u & ~TAGM);
+          const int row = (int)(u & TAGM) * 16 + win_of_row(4 * kq + r);
+          const bool take = v > bv || (v == bv && row < bi) || r == 0;
+          bv = take ? v : bv;
+          bi = take ? row : bi;
+        }
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+          const float ov = __shfl_xor(bv, o, 64);
+          const int oi = __shfl_xor(bi, o, 64);
+          const bool take = ov > bv || (ov == bv && oi < bi);
+          bv = take ? ov : bv;
+          bi = take ? oi : bi;
+        }
+        const int col = colbase + rsub;
+        if (kq == 0 && (col % 160) < FW) {
+          const int f = (col / 160) * FW + (col % 160);
+          const float y = bv * p.scale + p.bias[f];
+          p.pooled[(size_t)cur.n * (2 * FW) + f] = y > 0.f ? y : 0.f;
+          p.argmax[(size_t)cur.n * (2 * FW) + f] = bi;
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < N3; ++i) finish(m3[i], (t3base + i) * 16);
+#pragma unroll
+      for (int i = 0; i < N4; ++i) finish(m4[i], 160 + (t4base + i) * 16);
+      reset_state();
+    }
+    // stage chunk c1 into the idle buffer (its hashes are in slot par^1), publish c2's ids/hashes
+    store_rows<DBG>(p, xl0 + (par ^ 1) * (CROWS * ROWB), hs + (par ^ 1) * CROWS, stage);
+#pragma unroll
+    for (int i = 0; i < IDS_PT; ++i) {
+      const int r = threadIdx.x + i * NTHREADS;
+      if (r < CROWS) {
+        ids_lds[par * CROWS + r] = tok[i];  // c2 has the parity of cur
+        hs[par * CROWS + r] = hrw[i];
+      }
+    }
+    if constexpr ((DBG & 64) == 0) __syncthreads();
+    load_rows<DBG>(p, ids_lds + par * CROWS, stage);  // rows of c2
+    load_ids(p, c3, tok);
+#pragma unroll
+    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, c3, threadIdx.x + i * NTHREADS);
+    cur = c1;
+    c1 = c2;
+    c2 = c3;
+    advance(c3);
+    par ^= 1;
+  }
+}
+
+template <int PF, int DBG>
+__global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd2_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  switch (wave) {
+    case 0: run_wave2<3, 0, PF, DBG>(p, 0, 0, xl, ids_lds); break;
+    case 4: run_wave2<0, 2, PF, DBG>(p, 0, 0, xl, ids_lds); break;
+    case 1: run_wave2<3, 0, PF, DBG>(p, 3, 0, xl, ids_lds); break;
+    case 5: run_wave2<0, 2, PF, DBG>(p, 0, 2, xl, ids_lds); break;
+    case 2: run_wave2<0, 2, PF, DBG>(p, 0, 4, xl, ids_lds); break;
+    case 6: run_wave2<2, 1, PF, DBG>(p, 6, 6, xl, ids_lds); break;
+    case 3: run_wave2<0, 2, PF, DBG>(p, 0, 7, xl, ids_lds); break;
+    default: run_wave2<2, 1, PF, DBG>(p, 8, 9, xl, ids_lds); break;
+  }
+}
+
 PV_DEBUG_EXPORT(convfwd)
 }  // namespace convpool
 }  // namespace pv
@@ -396,7 +649,7 @@ __global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E
   bf16x8 v;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    int kk = s * 32 + (lane >> 4) * 8 + j;  // window element
+    int kk = s * 32 + chunk_of_kq(lane >> 4) * 8 + j;  // window element (k-chunk order of the A reads)
     int jj = kk / EP, e = kk % EP;
     float x = 0.f;
     if (col < FW && jj < k && e < E) x = w[((size_t)col * k + jj) * E + e];
@@ -429,6 +682,7 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
                             int thr, int token_mode, float scale, int grid, void* stream) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
+  if ((L - 2 + 15) / 16 > 1024) return -2;  // tagged argmax: block index must fit TAGB bits
   const int dbg = g_conv_dbg;
   Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
            seed, row_offset, thr, token_mode, scale};
@@ -438,12 +692,22 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #define PV_CONV_LAUNCH(PFV, DV) \
   hipLaunchKernelGGL((conv_pool_fwd_kernel<PFV, DV>), dim3(grid), dim3(NTHREADS), 0, st, p)
   switch (dbg) {
-    case 0: PV_CONV_LAUNCH(2, 0); break;   // production
+    case 0:  // production: v2 schedule (double-buffered chunks, tag-encoded argmax)
+      hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0>), dim3(grid), dim3(NTHREADS), 0, st, p);
+      break;
+    case 128: PV_CONV_LAUNCH(2, 0); break;  // v1 schedule (two barriers per chunk, cmp/select argmax)
     case 16: PV_CONV_LAUNCH(1, 0); break;  // A prefetch depth 1
     case 2: PV_CONV_LAUNCH(2, 2); break;
     case 4: PV_CONV_LAUNCH(2, 4); break;
     case 7: PV_CONV_LAUNCH(2, 7); break;
     case 15: PV_CONV_LAUNCH(2, 15); break;
+    case 32:  // v2 schedule (double buffer + tagged argmax)
+      hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0>), dim3(grid), dim3(NTHREADS), 0, st, p);
+      break;
+#define PV_CONV2_ABL(D) \
+    case 32 + D: hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, D>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    PV_CONV2_ABL(1) PV_CONV2_ABL(2) PV_CONV2_ABL(4) PV_CONV2_ABL(8) PV_CONV2_ABL(64) PV_CONV2_ABL(15)
+#undef PV_CONV2_ABL
     default: return -3;
   }
 #undef PV_CONV_LAUNCH
