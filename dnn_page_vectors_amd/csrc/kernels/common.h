@@ -50,6 +50,61 @@ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g
   return mix32(hrow + g * 0x9E3779B9u);
 }
 
+// Byte k of the result is 0xFF iff byte k of the group hash is >= thr (element 4g+k kept).
+// thr = 64 / 128 / 192 (p = 0.25 — the reference's rate — / 0.5 / 0.75) is a function of the
+// top two bits of each byte: 4 bit ops instead of 4 compares + selects.
+__device__ __forceinline__ unsigned keep_bytes(unsigned h, int thr) {
+  unsigned b;
+  if (thr == 64) {
+    b = ((h | (h << 1)) >> 7) & 0x01010101u;
+  } else if (thr == 128) {
+    b = (h >> 7) & 0x01010101u;
+  } else if (thr == 192) {
+    b = ((h & (h << 1)) >> 7) & 0x01010101u;
+  } else {
+    b = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b |= ((int)((h >> (8 * k)) & 0xFFu) >= thr ? 1u : 0u) << (8 * k);
+  }
+  return b * 0xFFu;
+}
+
+// AND-mask for the bf16 pair (elements 2j, 2j+1) of a packed dword, from keep_bytes (v_perm_b32).
+__device__ __forceinline__ unsigned keep_pair(unsigned kb, int j) {
+  return __builtin_amdgcn_perm(0u, kb, j ? 0x03030202u : 0x01010000u);
+}
+
+// Element-dropout AND-masks for the 8 bf16 columns 8q..8q+7 (one 16-byte piece) of a row
+// with row hash hrow (ops/reference.py dropout_keep_mask is the specification):
+//  * thr % 16 == 0 (p = k/16, incl. the reference's 0.25): ONE group hash per piece, nibble
+//    k decides column 8q+k (kept iff nibble >= thr/16);
+//  * otherwise two byte-wise group hashes (groups 2q, 2q+1, byte k decides column 4g+k).
+__device__ __forceinline__ u32x4 keep_piece(unsigned hrow, int q, int thr) {
+  if ((thr & 15) == 0) {
+    const unsigned h = dropout_group_hash(hrow, (unsigned)q);
+    const int t = thr >> 4;
+    unsigned b;  // bit 0 of nibble k = keep column k
+    if (t == 4) {
+      b = ((h | (h >> 1)) >> 2) & 0x11111111u;
+    } else if (t == 8) {
+      b = (h >> 3) & 0x11111111u;
+    } else if (t == 12) {
+      b = ((h & (h >> 1)) >> 2) & 0x11111111u;
+    } else {
+      b = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b |= (((h >> (4 * k)) & 0xFu) >= (unsigned)t ? 1u : 0u) << (4 * k);
+    }
+    const unsigned lo = (b & 0x01010101u) * 0xFFu;         // byte j: column 2j (even nibbles)
+    const unsigned hi = ((b >> 4) & 0x01010101u) * 0xFFu;  // byte j: column 2j+1
+    return u32x4{__builtin_amdgcn_perm(hi, lo, 0x04040000u), __builtin_amdgcn_perm(hi, lo, 0x05050101u),
+                 __builtin_amdgcn_perm(hi, lo, 0x06060202u), __builtin_amdgcn_perm(hi, lo, 0x07070303u)};
+  }
+  const unsigned k0 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q)), thr);
+  const unsigned k1 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q + 1)), thr);
+  return u32x4{keep_pair(k0, 0), keep_pair(k0, 1), keep_pair(k1, 0), keep_pair(k1, 1)};
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

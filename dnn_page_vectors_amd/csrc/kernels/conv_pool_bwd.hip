@@ -102,10 +102,20 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
           const int t = jj[i] == 0 ? tj[0] : jj[i] == 1 ? tj[1] : jj[i] == 2 ? tj[2] : tj[3];
           const bool ok = gv[i] && t >= 0 && t < V;
           raw[u][i] = ok ? *reinterpret_cast<const uint2*>(table + (size_t)t * EP + ee[i]) : uint2{0u, 0u};
-          unsigned h = 0xFFFFFFFFu;
+          unsigned h = 0xFFFFFFFFu;  // keep bytes of columns ee..ee+3 (ops/reference.py dropout_keep_mask)
           if (thr > 0) {
             const unsigned hr = dropout_row_hash(seed, row_offset + (unsigned)(nn * L + a_ + jj[i]));
-            h = token_mode ? (hr & 0xFF) * 0x01010101u : dropout_group_hash(hr, (unsigned)(ee[i] >> 2));
+            if (token_mode) {
+              h = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+            } else if ((thr & 15) == 0) {  // nibble decisions, one hash per 8 columns
+              const unsigned x = dropout_group_hash(hr, (unsigned)(ee[i] >> 3)) >> (16 * ((ee[i] >> 2) & 1));
+              unsigned b = 0u;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) b |= (((x >> (4 * k)) & 0xFu) >= (unsigned)(thr >> 4) ? 1u : 0u) << (8 * k);
+              h = b * 0xFFu;
+            } else {
+              h = keep_bytes(dropout_group_hash(hr, (unsigned)(ee[i] >> 2)), thr);
+            }
           }
           hh[u][i] = h;
         }
@@ -116,16 +126,13 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), sl[u]));
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const unsigned h = hh[u][i];
-          const uint2 r = raw[u][i];
-          float x0 = __uint_as_float(r.x << 16), x1 = __uint_as_float(r.x & 0xFFFF0000u);
-          float x2 = __uint_as_float(r.y << 16), x3 = __uint_as_float(r.y & 0xFFFF0000u);
+          uint2 r = raw[u][i];
           if (thr > 0) {
-            x0 = ((int)(h & 0xFF) >= thr) ? x0 : 0.f;
-            x1 = ((int)((h >> 8) & 0xFF) >= thr) ? x1 : 0.f;
-            x2 = ((int)((h >> 16) & 0xFF) >= thr) ? x2 : 0.f;
-            x3 = ((int)(h >> 24) >= thr) ? x3 : 0.f;
+            r.x &= keep_pair(hh[u][i], 0);
+            r.y &= keep_pair(hh[u][i], 1);
           }
+          const float x0 = __uint_as_float(r.x << 16), x1 = __uint_as_float(r.x & 0xFFFF0000u);
+          const float x2 = __uint_as_float(r.y << 16), x3 = __uint_as_float(r.y & 0xFFFF0000u);
           acc[i][0] += gj * x0;
           acc[i][1] += gj * x1;
           acc[i][2] += gj * x2;
@@ -287,20 +294,18 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
     {
       u32x4 w = u32x4{0u, 0u, 0u, 0u};
       if (act) w = *reinterpret_cast<const u32x4*>(wrow + (size_t)f_j * EP + 8 * p);
-      unsigned hm0 = 0xFFFFFFFFu, hm1 = 0xFFFFFFFFu;  // one byte per column (>= thr keeps)
-      if (thr > 0) {
+      if (thr > 0) {  // zero the dropped columns of the weight row (bf16 pairs)
         if (token_mode) {
-          hm0 = hm1 = (he & 0xFFu) * 0x01010101u;
+          const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+          w &= u32x4{k, k, k, k};
         } else {
-          hm0 = dropout_group_hash(he, (unsigned)(2 * p));
-          hm1 = dropout_group_hash(he, (unsigned)(2 * p + 1));
+          w &= keep_piece(he, p, thr);
         }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
-        const unsigned hb = ((k < 4 ? hm0 : hm1) >> (8 * (k & 3))) & 0xFFu;
-        v[k] = (thr > 0 && (int)hb < thr) ? 0.f : ge * __uint_as_float(wk);
+        v[k] = ge * __uint_as_float(wk);
       }
     }
     // keys of the 4 groups (ascending); invalid groups join the current run with v = 0

@@ -123,14 +123,6 @@ __device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u
   }
 }
 
-__device__ __forceinline__ unsigned keep_bits_mask(unsigned h, int thr) {
-  // 2 bf16 lanes per dword: returns AND-mask for the dword pair (bytes b0,b1 of h)
-  unsigned m = 0;
-  if ((int)(h & 0xFF) >= thr) m |= 0x0000FFFFu;
-  if ((int)((h >> 8) & 0xFF) >= thr) m |= 0xFFFF0000u;
-  return m;
-}
-
 // Apply dropout to the staged pieces and write them into the LDS chunk buffer.
 // hrow[r] holds the per-row hash of this chunk (computed once per row when its token id
 // was loaded), so each 16-byte piece costs only its two group hashes.
@@ -148,11 +140,7 @@ __device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsi
           unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
           x = x & u32x4{m, m, m, m};
         } else {
-          unsigned h0 = dropout_group_hash(hr, 2 * pc), h1 = dropout_group_hash(hr, 2 * pc + 1);
-          x.x &= keep_bits_mask(h0, p.thr);
-          x.y &= keep_bits_mask(h0 >> 16, p.thr);
-          x.z &= keep_bits_mask(h1, p.thr);
-          x.w &= keep_bits_mask(h1 >> 16, p.thr);
+          x &= keep_piece(hr, pc, p.thr);
         }
       }
       *reinterpret_cast<u32x4*>(xl + r * ROWB + pc * 16) = x;

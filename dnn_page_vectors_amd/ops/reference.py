@@ -44,7 +44,10 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
                       mode: str = "element", device=None) -> torch.Tensor:
     """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r``.
 
-    element: h_row = mix(seed ^ mix(row)); byte b of mix(h_row + g*0x9E3779B9) decides column 4g+b.
+    element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25):
+             h_row = mix(seed ^ mix(row)); nibble b of mix(h_row + g*0x9E3779B9) decides column
+             8g+b (kept iff nibble >= thr/16) — one hash per 8 columns;
+    element, other thr: byte b of mix(h_row + g*0x9E3779B9) decides column 4g+b (>= thr);
     token:   one decision per row: byte 0 of h_row.
     """
     thr = dropout_threshold(p)
@@ -53,6 +56,13 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     if mode == "token":
         b = h_row & 0xFF
         return (b >= thr).unsqueeze(1).expand(n_rows, width)
+    if thr % 16 == 0:
+        ng = (width + 7) // 8
+        g = torch.arange(ng, dtype=torch.int64, device=device)
+        h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
+        shifts = torch.arange(0, 32, 4, dtype=torch.int64, device=device)
+        nib = (h.unsqueeze(2) >> shifts) & 0xF  # (n, ng, 8)
+        return nib.reshape(n_rows, ng * 8)[:, :width] >= thr // 16
     ng = (width + 3) // 4
     g = torch.arange(ng, dtype=torch.int64, device=device)
     h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
