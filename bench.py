@@ -151,7 +151,15 @@ def main():
 
     pairs = a.batch * W * a.steps
     value = pairs / dt
-    flops = (3.0 * cdssm_flops_per_sample(cfg) * a.batch * W * a.steps / dt) if a.model == "cdssm" else 0.0
+    if a.model == "cdssm":
+        per_pair = 3.0 * cdssm_flops_per_sample(cfg)
+    elif a.model == "bert":
+        from dnn_page_vectors_amd.models.bert_dual import bert_flops_per_token
+        per_pair = 3.0 * (cfg.query_length * bert_flops_per_token(cfg, cfg.query_length) +
+                          (1 + cfg.J) * cfg.document_length * bert_flops_per_token(cfg, cfg.document_length))
+    else:
+        per_pair = 0.0
+    flops = per_pair * a.batch * W * a.steps / dt
     if info.is_main:
         out = {
             "metric": "pairs/sec (whole node) + Recall@10, DSSM-300d" if a.model == "cdssm"

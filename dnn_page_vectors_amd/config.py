@@ -296,7 +296,7 @@ def preset_config(name: str) -> Configuration:
                              dtype="bf16", loss_mode="cross_gpu", J=0, cos_clip=False, lr=3e-3)
     if name in ("bert_dp8", "config4"):
         return Configuration(model="bert", feature_level="word", vocab_hash_size=30522,
-                             query_length=32, document_length=256, batch_size=64,
+                             query_length=32, document_length=256, batch_size=256,
                              dtype="bf16", loss_mode="cross_gpu", J=0, lr=2e-5)
     if name in ("longpage_fp8", "config5"):
         return Configuration(model="chunked", feature_level="ngram", vocab_hash_size=30000,

@@ -1,0 +1,456 @@
+// Fused multi-head attention for the BERT dual encoder (BASELINE config 4), head dim 64,
+// key-padding mask, straight from / into the PACKED projection layouts:
+//   qkv  (N, L, 3, H, 64) bf16   (the QKV GEMM output, no permute/contiguous copies)
+//   out  (N, L, H, 64)    bf16   (= (N, L, H*64), the input of the output projection)
+//   dqkv (N, L, 3, H, 64) bf16   (the backward writes dQ, dK, dV into their slots — no cat)
+//
+// Every product uses the swapped orientation of loss.hip: scores are computed TRANSPOSED
+// (A = the 16 key rows staged in LDS, B = the 16 query rows held in registers), so one
+// lane owns one query column and 4 keys of each 16-key subtile.  The softmax statistics
+// are then lane-local (+ two xor shuffles across the 4 lane groups), and the bf16 P^T
+// registers are directly the B operand of O^T += V^T . P^T, whose A operand (V^T) comes
+// from the row-major V tile through ds_read_b64_tr_b16 (k order j -> 16*(j>>2)+4g+(j&3)).
+//
+//   attn_fwd      : online softmax over 64-key blocks (exp2 domain), O and the per-row
+//                   log-sum-exp (for the backward)
+//   attn_bwd_prep : D = rowsum(dO * O)
+//   attn_bwd_dkdv : one workgroup per 64-key block, loops over query blocks; dV = P^T dO,
+//                   dK = dS^T Q with P recomputed from the saved log-sum-exp
+//   attn_bwd_dq   : one workgroup per 64-query block, loops over key blocks; dQ = dS K
+// No atomics: every output element is owned by exactly one workgroup.
+#include "common.h"
+
+namespace pv {
+namespace attn {
+
+constexpr int HD = 64;         // head dim
+constexpr int TB = 64;         // rows per staged tile (keys or queries)
+constexpr int LDT = HD + 8;    // LDS row stride (elements): 144 B, 16-B aligned
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// Stage rows [r0, r0+64) of one head slot (slot 0/1/2 of qkv, or the dO / O layout with
+// stride ld) into an LDS tile [64][LDT]; rows >= L are zero.  256 threads x 2 x 16 B.
+__device__ __forceinline__ void load_tile(const unsigned short* __restrict__ base, size_t ld, int r0, int L,
+                                          u32x4 (&v)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    const int r = q >> 3, c = (q & 7) * 8;
+    v[u] = (r0 + r < L) ? *reinterpret_cast<const u32x4*>(base + (size_t)(r0 + r) * ld + c) : u32x4{0, 0, 0, 0};
+  }
+}
+
+__device__ __forceinline__ void store_tile(unsigned short* t, const u32x4 (&v)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    *reinterpret_cast<u32x4*>(t + (q >> 3) * LDT + (q & 7) * 8) = v[u];
+  }
+}
+
+// fragment of 16 rows (r0 + lane&15) x 8 columns (8g + 32s) from a row-major tile
+__device__ __forceinline__ bf16x8 row_frag(const unsigned short* t, int r0, int s) {
+  const int lane = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(t + (r0 + (lane & 15)) * LDT + s * 32 + (lane >> 4) * 8);
+}
+
+// transposed fragment: A[col = c0 + lane&15][k = rows permuted] from a row-major tile [row][col]:
+// rows 32*s2 + 4g + q (q = 0..3) and +16, columns c0 .. c0+15
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned short* t, int s2, int c0) {
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const unsigned short* p = t + (s2 * 32 + 4 * g + ((lane & 15) >> 2)) * LDT + c0 + 4 * (lane & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + 16 * LDT));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// 16 rows (row0 + lane&15) x 64 d of a global row-major matrix as two B/A fragments (d-steps)
+__device__ __forceinline__ void glob_frag(const unsigned short* __restrict__ base, size_t ld, int row, int L,
+                                          bf16x8 (&f)[2]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    f[s] = row < L ? *reinterpret_cast<const bf16x8*>(base + (size_t)row * ld + s * 32 + (lane >> 4) * 8)
+                   : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+}
+
+// 4 C-layout accumulators (16 rows each, rows 4g+r) -> bf16 B fragments of 2 k-steps of 32
+__device__ __forceinline__ void pack_b(const f32x4 (&x)[4], bf16x8 (&b)[2]) {
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    u32x4 w;
+    w[0] = pack_bf16x2(x[2 * s2][0], x[2 * s2][1]);
+    w[1] = pack_bf16x2(x[2 * s2][2], x[2 * s2][3]);
+    w[2] = pack_bf16x2(x[2 * s2 + 1][0], x[2 * s2 + 1][1]);
+    w[3] = pack_bf16x2(x[2 * s2 + 1][2], x[2 * s2 + 1][3]);
+    b[s2] = __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+// ---------------------------------------------------------------------------- forward
+// grid (ceil(L/64), H, N), 256 threads; wave w owns queries q0 + 16w .. +15
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const unsigned short* __restrict__ qkv,
+                                                          const int* __restrict__ mask,
+                                                          unsigned short* __restrict__ out, float* __restrict__ lse,
+                                                          int L, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short kt[2][TB * LDT];
+  __shared__ __attribute__((aligned(16))) unsigned short vt[2][TB * LDT];
+  __shared__ float mk[2][TB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int n = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TB + wave * 16;
+  const size_t ld = (size_t)3 * H * HD;
+  const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
+  const unsigned short* K = Q + (size_t)H * HD;
+  const unsigned short* V = Q + (size_t)2 * H * HD;
+  const int* mrow = mask ? mask + (size_t)n * L : nullptr;
+  const float sl = scale * LOG2E;
+  bf16x8 qb[2];
+  glob_frag(Q, ld, q0 + (lane & 15), L, qb);
+  f32x4 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  u32x4 sk[2], sv[2];
+  float smk = 0.f;
+  load_tile(K, ld, 0, L, sk);
+  load_tile(V, ld, 0, L, sv);
+  if (threadIdx.x < TB) smk = (threadIdx.x < L && (!mrow || mrow[threadIdx.x])) ? 1.f : 0.f;
+  store_tile(kt[0], sk);
+  store_tile(vt[0], sv);
+  if (threadIdx.x < TB) mk[0][threadIdx.x] = smk;
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < L; k0 += TB, buf ^= 1) {
+    const bool more = k0 + TB < L;
+    if (more) {
+      load_tile(K, ld, k0 + TB, L, sk);
+      load_tile(V, ld, k0 + TB, L, sv);
+      if (threadIdx.x < TB) {
+        const int kk = k0 + TB + threadIdx.x;
+        smk = (kk < L && (!mrow || mrow[kk])) ? 1.f : 0.f;
+      }
+    }
+    // S^T (keys x queries), 4 key subtiles
+    f32x4 s[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) s[c] = MFMA(row_frag(kt[buf], c * 16, st), qb[st], s[c]);
+    }
+    float bm = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float keep = mk[buf][c * 16 + 4 * g + r];
+        s[c][r] = keep != 0.f ? s[c][r] * sl : -INFINITY;
+        bm = fmaxf(bm, s[c][r]);
+      }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= corr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= corr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = s[c][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[c][r] - mn);
+        s[c][r] = pv;
+        l += pv;
+      }
+    bf16x8 pb[2];
+    pack_b(s, pb);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = MFMA(tr_frag(vt[buf], s2, i * 16), pb[s2], o[i]);
+    if (more) {
+      store_tile(kt[buf ^ 1], sk);
+      store_tile(vt[buf ^ 1], sv);
+      if (threadIdx.x < TB) mk[buf ^ 1][threadIdx.x] = smk;
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const int q = q0 + (lane & 15);
+  if (q < L) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    unsigned short* orow = out + ((size_t)n * L + q) * H * HD + (size_t)h * HD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint2*>(orow + i * 16 + 4 * g) =
+          uint2{pack_bf16x2(o[i][0] * inv, o[i][1] * inv), pack_bf16x2(o[i][2] * inv, o[i][3] * inv)};
+    if (g == 0) lse[((size_t)n * H + h) * L + q] = m + __log2f(l);  // log2 domain, includes scale
+  }
+}
+
+// ---------------------------------------------------------------------------- backward
+// D[n,h,q] = sum_d dO * O ; one wave per (n, q), lanes over heads x 16 pieces
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const unsigned short* __restrict__ dout,
+                                                            const unsigned short* __restrict__ out,
+                                                            float* __restrict__ Dv, int NL, int L, int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // n*L + q
+  const int lane = threadIdx.x & 63;
+  if (row >= NL) return;
+  const int n = row / L, q = row - n * L;
+  const unsigned short* a = dout + (size_t)row * H * HD;
+  const unsigned short* b = out + (size_t)row * H * HD;
+  for (int h = 0; h < H; ++h) {
+    // lane covers one element pair of the head's 64 (32 lanes) -> use all 64 lanes on 2 heads
+    float acc = 0.f;
+    if (lane < 32) {
+      const unsigned x = reinterpret_cast<const unsigned*>(a + h * HD)[lane];
+      const unsigned y = reinterpret_cast<const unsigned*>(b + h * HD)[lane];
+      acc = __uint_as_float(x << 16) * __uint_as_float(y << 16) +
+            __uint_as_float(x & 0xFFFF0000u) * __uint_as_float(y & 0xFFFF0000u);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) Dv[((size_t)n * H + h) * L + q] = acc;
+  }
+}
+
+// grid (ceil(L/64) key blocks, H, N); wave w owns keys k0 + 16w .. +15 (lane column)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned short* __restrict__ qkv,
+                                                               const int* __restrict__ mask,
+                                                               const unsigned short* __restrict__ dout,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ Dv,
+                                                               unsigned short* __restrict__ dqkv, int L, int H,
+                                                               float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short qt[2][TB * LDT];
+  __shared__ __attribute__((aligned(16))) unsigned short dt[2][TB * LDT];
+  __shared__ float sl_[2][TB], sd_[2][TB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int n = blockIdx.z, h = blockIdx.y, kw = blockIdx.x * TB + wave * 16;
+  const size_t ld = (size_t)3 * H * HD, ldo = (size_t)H * HD;
+  const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
+  const unsigned short* K = Q + (size_t)H * HD;
+  const unsigned short* V = Q + (size_t)2 * H * HD;
+  const unsigned short* dO = dout + (size_t)n * L * ldo + (size_t)h * HD;
+  const float* LS = lse + ((size_t)n * H + h) * L;
+  const float* DD = Dv + ((size_t)n * H + h) * L;
+  const int key = kw + (lane & 15);
+  const bool kvalid = key < L && (!mask || mask[(size_t)n * L + key]);
+  const float sl = scale * LOG2E;
+  bf16x8 kb[2], vb[2];
+  glob_frag(K, ld, key, L, kb);
+  glob_frag(V, ld, key, L, vb);
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 sq[2], sdo[2];
+  float slv = 0.f, sdv = 0.f;
+  load_tile(Q, ld, 0, L, sq);
+  load_tile(dO, ldo, 0, L, sdo);
+  if (threadIdx.x < TB) {
+    slv = threadIdx.x < L ? LS[threadIdx.x] : 0.f;
+    sdv = threadIdx.x < L ? DD[threadIdx.x] : 0.f;
+  }
+  store_tile(qt[0], sq);
+  store_tile(dt[0], sdo);
+  if (threadIdx.x < TB) {
+    sl_[0][threadIdx.x] = slv;
+    sd_[0][threadIdx.x] = sdv;
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int q0 = 0; q0 < L; q0 += TB, buf ^= 1) {
+    const bool more = q0 + TB < L;
+    if (more) {
+      load_tile(Q, ld, q0 + TB, L, sq);
+      load_tile(dO, ldo, q0 + TB, L, sdo);
+      if (threadIdx.x < TB) {
+        const int qq = q0 + TB + threadIdx.x;
+        slv = qq < L ? LS[qq] : 0.f;
+        sdv = qq < L ? DD[qq] : 0.f;
+      }
+    }
+    // S (queries x keys) and dP = dO . V^T, 4 query subtiles: rows q = c*16 + 4g + r, col = key
+    f32x4 p[4], dp[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      p[c] = dp[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        p[c] = MFMA(row_frag(qt[buf], c * 16, st), kb[st], p[c]);
+        dp[c] = MFMA(row_frag(dt[buf], c * 16, st), vb[st], dp[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = c * 16 + 4 * g + r;
+        const bool ok = kvalid && q0 + qi < L;
+        const float pv = ok ? __builtin_amdgcn_exp2f(p[c][r] * sl - sl_[buf][qi]) : 0.f;
+        p[c][r] = pv;
+        dp[c][r] = pv * (dp[c][r] - sd_[buf][qi]);  // dS (without the softmax scale)
+      }
+    bf16x8 pb[2], db[2];
+    pack_b(p, pb);
+    pack_b(dp, db);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dv[i] = MFMA(tr_frag(dt[buf], s2, i * 16), pb[s2], dv[i]);
+        dk[i] = MFMA(tr_frag(qt[buf], s2, i * 16), db[s2], dk[i]);
+      }
+    if (more) {
+      store_tile(qt[buf ^ 1], sq);
+      store_tile(dt[buf ^ 1], sdo);
+      if (threadIdx.x < TB) {
+        sl_[buf ^ 1][threadIdx.x] = slv;
+        sd_[buf ^ 1][threadIdx.x] = sdv;
+      }
+    }
+    __syncthreads();
+  }
+  if (key < L) {
+    unsigned short* row = dqkv + ((size_t)n * L + key) * ld + (size_t)h * HD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<uint2*>(row + (size_t)H * HD + i * 16 + 4 * g) =
+          uint2{pack_bf16x2(dk[i][0] * scale, dk[i][1] * scale), pack_bf16x2(dk[i][2] * scale, dk[i][3] * scale)};
+      *reinterpret_cast<uint2*>(row + (size_t)2 * H * HD + i * 16 + 4 * g) =
+          uint2{pack_bf16x2(dv[i][0], dv[i][1]), pack_bf16x2(dv[i][2], dv[i][3])};
+    }
+  }
+}
+
+// grid (ceil(L/64) query blocks, H, N); wave w owns queries q0 + 16w .. +15
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned short* __restrict__ qkv,
+                                                             const int* __restrict__ mask,
+                                                             const unsigned short* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ Dv,
+                                                             unsigned short* __restrict__ dqkv, int L, int H,
+                                                             float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short kt[2][TB * LDT];
+  __shared__ __attribute__((aligned(16))) unsigned short vt[2][TB * LDT];
+  __shared__ float mk[2][TB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int n = blockIdx.z, h = blockIdx.y, q = blockIdx.x * TB + wave * 16 + (lane & 15);
+  const size_t ld = (size_t)3 * H * HD, ldo = (size_t)H * HD;
+  const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
+  const unsigned short* K = Q + (size_t)H * HD;
+  const unsigned short* V = Q + (size_t)2 * H * HD;
+  const unsigned short* dO = dout + (size_t)n * L * ldo + (size_t)h * HD;
+  const int* mrow = mask ? mask + (size_t)n * L : nullptr;
+  const float sl = scale * LOG2E;
+  const float lq = q < L ? lse[((size_t)n * H + h) * L + q] : 0.f;
+  const float dq_ = q < L ? Dv[((size_t)n * H + h) * L + q] : 0.f;
+  bf16x8 qb[2], ob[2];
+  glob_frag(Q, ld, q, L, qb);
+  glob_frag(dO, ldo, q, L, ob);
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 sk[2], sv[2];
+  float smk = 0.f;
+  load_tile(K, ld, 0, L, sk);
+  load_tile(V, ld, 0, L, sv);
+  if (threadIdx.x < TB) smk = (threadIdx.x < L && (!mrow || mrow[threadIdx.x])) ? 1.f : 0.f;
+  store_tile(kt[0], sk);
+  store_tile(vt[0], sv);
+  if (threadIdx.x < TB) mk[0][threadIdx.x] = smk;
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < L; k0 += TB, buf ^= 1) {
+    const bool more = k0 + TB < L;
+    if (more) {
+      load_tile(K, ld, k0 + TB, L, sk);
+      load_tile(V, ld, k0 + TB, L, sv);
+      if (threadIdx.x < TB) {
+        const int kk = k0 + TB + threadIdx.x;
+        smk = (kk < L && (!mrow || mrow[kk])) ? 1.f : 0.f;
+      }
+    }
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s[c] = dp[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        s[c] = MFMA(row_frag(kt[buf], c * 16, st), qb[st], s[c]);
+        dp[c] = MFMA(row_frag(vt[buf], c * 16, st), ob[st], dp[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float keep = mk[buf][c * 16 + 4 * g + r];
+        const float pv = keep != 0.f ? __builtin_amdgcn_exp2f(s[c][r] * sl - lq) : 0.f;
+        s[c][r] = pv * (dp[c][r] - dq_);  // dS^T
+      }
+    bf16x8 db[2];
+    pack_b(s, db);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = MFMA(tr_frag(kt[buf], s2, i * 16), db[s2], acc[i]);
+    if (more) {
+      store_tile(kt[buf ^ 1], sk);
+      store_tile(vt[buf ^ 1], sv);
+      if (threadIdx.x < TB) mk[buf ^ 1][threadIdx.x] = smk;
+    }
+    __syncthreads();
+  }
+  if (q < L) {
+    unsigned short* row = dqkv + ((size_t)n * L + q) * ld + (size_t)h * HD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint2*>(row + i * 16 + 4 * g) =
+          uint2{pack_bf16x2(acc[i][0] * scale, acc[i][1] * scale), pack_bf16x2(acc[i][2] * scale, acc[i][3] * scale)};
+  }
+}
+
+#undef MFMA
+
+}  // namespace attn
+}  // namespace pv
+
+using namespace pv;
+
+// qkv (N, L, 3, H, 64) bf16; mask (N, L) int32 or null; out (N, L, H, 64) bf16; lse (N, H, L) f32
+PV_API int pv_attn_fwd(const void* qkv, const int* mask, void* out, float* lse, int N, int L, int H, float scale,
+                       void* stream) {
+  if (N <= 0 || L <= 0 || H <= 0) return -1;
+  dim3 grid((L + pv::attn::TB - 1) / pv::attn::TB, H, N);
+  hipLaunchKernelGGL(pv::attn::attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const unsigned short*)qkv, mask, (unsigned short*)out, lse, L, H, scale);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// dout, out (N, L, H, 64) bf16; lse (N, H, L); D workspace (N, H, L) f32; dqkv (N, L, 3, H, 64) bf16
+PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const void* dout, const float* lse,
+                       float* D, void* dqkv, int N, int L, int H, float scale, void* stream) {
+  using namespace pv::attn;
+  if (N <= 0 || L <= 0 || H <= 0) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const int NL = N * L;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
+                     (const unsigned short*)out, D, NL, L, H);
+  PV_LAUNCH_CHECK();
+  dim3 grid((L + TB - 1) / TB, H, N);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, s, (const unsigned short*)qkv, mask,
+                     (const unsigned short*)dout, lse, D, (unsigned short*)dqkv, L, H, scale);
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, s, (const unsigned short*)qkv, mask,
+                     (const unsigned short*)dout, lse, D, (unsigned short*)dqkv, L, H, scale);
+  PV_LAUNCH_CHECK();
+  return 0;
+}

@@ -146,8 +146,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
                                                                  const float* __restrict__ mean,
                                                                  const float* __restrict__ rstd,
                                                                  unsigned short* __restrict__ dx,
-                                                                 float* __restrict__ dgamma,
-                                                                 float* __restrict__ dbeta, int M) {
+                                                                 float* __restrict__ part, int M) {
   constexpr int D = 256 * VPT;
   __shared__ float red[2][4][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -202,9 +201,11 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
       red[1][wave][(i * 64 + lane) * 4 + k] = gb[i][k];
     }
   __syncthreads();
+  // per-block partials part[block][0:D] = dgamma, [D:2D] = dbeta (summed by colsum_*)
+  float* pb = part + (size_t)blockIdx.x * 2 * D;
   for (int c = threadIdx.x; c < D; c += 256) {
-    atomicAdd(&dgamma[c], red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
-    atomicAdd(&dbeta[c], red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+    pb[c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    pb[D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
   }
 }
 
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_vec_kernel(const unsigned s
 // colsum_final adds the S partials.
 constexpr int kColSplits = 32;
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ part, float* __restrict__ part2,
-                                                          int R, int D) {
+                                                          int R, int D, int ld) {
   __shared__ float sh[4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
   float a = 0.f;
   if (c < D)
-    for (int r = r0 + ty; r < r1; r += 4) a += part[(size_t)r * D + c];
+    for (int r = r0 + ty; r < r1; r += 4) a += part[(size_t)r * ld + c];
   sh[ty][tx] = a;
   __syncthreads();
   if (ty == 0 && c < D) part2[(size_t)blockIdx.y * D + c] = sh[0][tx] + sh[1][tx] + sh[2][tx] + sh[3][tx];
@@ -485,15 +486,47 @@ PV_API int pv_add_layernorm_fwd(const void* x, const void* r, const float* gamma
   return 0;
 }
 
+static int ln_blocks(int M) { return std::min(512, std::max(1, (M + 3) / 4)); }
+
+static bool ln_rows_ok(int D) { return D == 256 || D == 512 || D == 768 || D == 1024; }
+
+// floats of workspace pv_layernorm_bwd needs (0: the generic kernel accumulates into
+// zeroed dgamma/dbeta with atomics)
+PV_API long pv_layernorm_bwd_ws(int M, int D) {
+  return ln_rows_ok(D) ? (long)ln_blocks(M) * 2 * D + 2L * pv::tfm::kColSplits * D : 0;
+}
+
+// dgamma/dbeta are overwritten on the wave-per-row path (D in {256,512,768,1024}, ws given)
 PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma, const float* mean, const float* rstd,
-                            void* dx, float* dgamma, float* dbeta, int M, int D, void* stream) {
-  const unsigned blocks = (unsigned)std::min(512, std::max(1, (M + 3) / 4));
+                            void* dx, float* dgamma, float* dbeta, float* ws, int M, int D, void* stream) {
+  const int blocks = ln_blocks(M);
+  hipStream_t st = (hipStream_t)stream;
 #define PV_LN_ROWS(VPT)                                                                                          \
-  hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,   \
-                     (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd, (unsigned short*)dx, \
-                     dgamma, dbeta, M);                                                                           \
-  PV_LAUNCH_CHECK();                                                                                             \
-  return 0;
+  {                                                                                                              \
+    hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, st,                  \
+                       (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,                \
+                       (unsigned short*)dx, ws, M);                                                              \
+    PV_LAUNCH_CHECK();                                                                                           \
+    float* ws2 = ws + (size_t)blocks * 2 * D;                                                                    \
+    for (int half = 0; half < 2; ++half) {                                                                       \
+      hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0, st, \
+                         ws + half * D, ws2 + (size_t)half * pv::tfm::kColSplits * D, blocks, D, 2 * D);          \
+      PV_LAUNCH_CHECK();                                                                                         \
+      hipLaunchKernelGGL(pv::tfm::colsum_final_kernel, dim3((D + 255) / 256), dim3(256), 0, st,                  \
+                         ws2 + (size_t)half * pv::tfm::kColSplits * D, half ? dbeta : dgamma, pv::tfm::kColSplits, D); \
+      PV_LAUNCH_CHECK();                                                                                         \
+    }                                                                                                            \
+    return 0;                                                                                                    \
+  }
+  if (ws) {
+    switch (D) {
+      case 256: PV_LN_ROWS(1)
+      case 512: PV_LN_ROWS(2)
+      case 768: PV_LN_ROWS(3)
+      case 1024: PV_LN_ROWS(4)
+      default: break;
+    }
+  }
   switch (D) {
     case 256: { PV_LN_ROWS(1) }
     case 512: { PV_LN_ROWS(2) }
@@ -538,7 +571,7 @@ PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void*
     PV_LAUNCH_CHECK();
     float* ws2 = ws + (size_t)R * D;
     hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0,
-                       (hipStream_t)stream, ws, ws2, R, D);
+                       (hipStream_t)stream, ws, ws2, R, D, D);
     PV_LAUNCH_CHECK();
     hipLaunchKernelGGL(pv::tfm::colsum_final_kernel, dim3((D + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws2, db,
                        pv::tfm::kColSplits, D);

@@ -6,10 +6,12 @@ model plugs a 12-layer / 768-hidden / 12-head Transformer encoder into it (share
 weights for queries and pages by default, ``[CLS]`` pooling, optional projection),
 trained with the same cosine softmax head (in-batch / cross-GPU negatives).
 
-MI355X mapping: every projection and the two attention products are plain bf16 GEMMs
-(hipBLASLt via torch.matmul); residual-add + LayerNorm, bias + GELU and the masked
-softmax are fused HIP row kernels (csrc/kernels/transformer.hip); master weights are
-fp32 in the flat parameter buffer (one bucketed all-reduce stream, ~440 MB/step at
+MI355X mapping: every projection is a bf16 GEMM (hipBLASLt) over a cached bf16 copy of
+the fp32 master weight (refreshed once per optimizer step; fp32 weight gradients);
+attention is one fused HIP kernel pair on the packed QKV layout (csrc/kernels/
+attention.hip: online softmax, no S/P materialisation, no head permutes); residual-add
++ LayerNorm and bias + GELU are fused HIP row kernels (transformer.hip); master weights
+are fp32 in the flat parameter buffer (one bucketed all-reduce stream, ~440 MB/step at
 BERT-base, overlapped with the backward by parallel/ddp.py).
 Token ids come from the hashed word featurizer (no WordPiece vocab is available
 offline); id 0 = [PAD], position 0 of every sequence is treated as [CLS].
@@ -43,16 +45,14 @@ class BertLayer(nn.Module):
 
     def forward(self, x: torch.Tensor, mask: torch.Tensor, dt: torch.dtype, p_drop: float, training: bool):
         N, L, H = x.shape
-        nh = self.heads
-        qkv = F.linear(x, self.wqkv.to(dt), self.bqkv.to(dt))
-        q, k, v = qkv.view(N, L, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
-        a = tops.attention(q, k, v, mask).transpose(1, 2).reshape(N, L, H)
-        o = F.linear(a, self.wo.to(dt), self.bo.to(dt))
+        qkv = tops.linear(x, self.wqkv, self.bqkv)            # (N, L, 3H) packed [slot][head][d]
+        a = tops.fused_attention(qkv, mask, self.heads)       # (N, L, H), no permute copies
+        o = tops.linear(a, self.wo, self.bo)
         if training and p_drop > 0:
             o = F.dropout(o, p_drop, True)
         x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b)
-        f = tops.bias_gelu(F.linear(x, self.w1.to(dt)), self.b1)
-        f2 = F.linear(f, self.w2.to(dt), self.b2.to(dt))
+        f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
+        f2 = tops.linear(f, self.w2, self.b2)
         if training and p_drop > 0:
             f2 = F.dropout(f2, p_drop, True)
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b)

@@ -31,6 +31,8 @@ SIGS = {
     "pv_ib_fwd_ws": "iii",
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
     "pv_ib_bwd_ws": "iii",
+    "pv_attn_fwd": "pppp" "iii" "f" "p",
+    "pv_attn_bwd": "ppppppp" "iii" "f" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
@@ -42,7 +44,8 @@ SIGS = {
     "pv_topk_cos": "pppppp" "iiiii" "p",
     # transformer.hip
     "pv_add_layernorm_fwd": "pppppppp" "iif" "p",
-    "pv_layernorm_bwd": "pppppppp" "ii" "p",
+    "pv_layernorm_bwd_ws": "ii",
+    "pv_layernorm_bwd": "ppppppppp" "ii" "p",
     "pv_bias_gelu_fwd": "ppp" "li" "p",
     "pv_bias_gelu_bwd": "pppppp" "ii" "p",
     "pv_bias_gelu_bwd_ws": "ii",
@@ -60,7 +63,7 @@ SIGS = {
 }
 
 _RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
-            "pv_bias_gelu_bwd_ws": ctypes.c_long}
+            "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 
 def declare(lib) -> None:

@@ -1,5 +1,6 @@
 """Transformer ops for the BERT dual encoder: fused residual-add + LayerNorm, fused
-bias + GELU, masked softmax attention (HIP row kernels around hipBLASLt GEMMs).
+bias + GELU, fused multi-head attention on the packed QKV layout, and a bf16 linear layer
+over cached bf16 weights (HIP kernels around hipBLASLt GEMMs).
 
 CPU: plain torch (the reference semantics).  GPU activations are bf16; LayerNorm
 statistics and parameter gradients are fp32.
@@ -39,10 +40,14 @@ class _AddLNFn(torch.autograd.Function):
         M = h.numel() // D
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(h)
-        dg = torch.zeros_like(gamma)
-        db = torch.zeros_like(gamma)
-        check(lib().pv_layernorm_bwd(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dg), P(db), M, D,
-                                     stream(h.device)), "pv_layernorm_bwd")
+        L_ = lib()
+        nws = int(L_.pv_layernorm_bwd_ws(M, D))
+        alloc = torch.empty if nws > 0 else torch.zeros  # generic kernel accumulates atomically
+        dg = alloc(gamma.shape, dtype=torch.float32, device=h.device)
+        db = alloc(gamma.shape, dtype=torch.float32, device=h.device)
+        ws = torch.empty(nws, dtype=torch.float32, device=h.device) if nws > 0 else None
+        check(L_.pv_layernorm_bwd(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dg), P(db), P(ws), M, D,
+                                  stream(h.device)), "pv_layernorm_bwd")
         return dx, (dx if ctx.has_r else None), dg, db, None
 
 
@@ -71,7 +76,7 @@ class _BiasGeluFn(torch.autograd.Function):
         M = x.numel() // D
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(x)
-        db = torch.zeros_like(b)
+        db = torch.empty_like(b) if D % 8 == 0 else torch.zeros_like(b)  # vector path overwrites db
         L_ = lib()
         ws = torch.empty(L_.pv_bias_gelu_bwd_ws(M, D), dtype=torch.float32, device=x.device) if D % 8 == 0 else None
         check(L_.pv_bias_gelu_bwd(P(x), P(b), P(dy), P(dx), P(db), P(ws), M, D, stream(x.device)), "pv_bias_gelu_bwd")
@@ -104,6 +109,100 @@ class _SoftmaxFn(torch.autograd.Function):
         d = dp.to(torch.bfloat16).contiguous().clone()
         check(lib().pv_softmax_bwd(P(p), P(d), R, L, ctx.scale, stream(p.device)), "pv_softmax_bwd")
         return d, None, None, None
+
+
+class _FusedAttnFn(torch.autograd.Function):
+    """qkv (N, L, 3*H*64) bf16 packed [slot][head][d] -> (N, L, H*64); csrc/kernels/attention.hip."""
+
+    @staticmethod
+    def forward(ctx, qkv, mask, heads, scale):
+        qkv = qkv.to(torch.bfloat16).contiguous()
+        N, L, C = qkv.shape
+        H = heads
+        if C != 3 * H * 64:
+            raise ValueError("fused attention needs head dim 64")
+        out = torch.empty(N, L, H * 64, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
+        check(lib().pv_attn_fwd(P(qkv), P(mask), P(out), P(lse), N, L, H, float(scale), stream(qkv.device)),
+              "pv_attn_fwd")
+        ctx.save_for_backward(qkv, mask, out, lse)
+        ctx.meta = (H, float(scale))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, mask, out, lse = ctx.saved_tensors
+        H, scale = ctx.meta
+        N, L, _ = qkv.shape
+        dout = dout.to(torch.bfloat16).contiguous()
+        D = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
+        dqkv = torch.empty_like(qkv)
+        check(lib().pv_attn_bwd(P(qkv), P(mask), P(out), P(dout), P(lse), P(D), P(dqkv), N, L, H, scale,
+                                stream(qkv.device)), "pv_attn_bwd")
+        return dqkv, None, None, None
+
+
+def fused_attention(qkv: torch.Tensor, mask: Optional[torch.Tensor], heads: int) -> torch.Tensor:
+    """qkv (N, L, 3*H*d) packed projection output -> attention output (N, L, H*d), mask (N, L)."""
+    N, L, C = qkv.shape
+    d = C // (3 * heads)
+    scale = 1.0 / math.sqrt(d)
+    if use_hip(qkv) and d == 64:
+        m = mask.to(torch.int32).contiguous() if mask is not None else None
+        return _FusedAttnFn.apply(qkv, m, heads, scale)
+    q, k, v = qkv.view(N, L, 3, heads, d).permute(2, 0, 3, 1, 4)
+    return attention(q, k, v, mask).transpose(1, 2).reshape(N, L, heads * d)
+
+
+# bf16 copies of fp32 master weights, refreshed once per optimizer step (generation counter
+# of models.base: bump_generation() after every update)
+_W16 = {}
+
+
+def weight_bf16(w: torch.Tensor) -> torch.Tensor:
+    from ..models.base import _GENERATION
+
+    key = id(w)
+    ent = _W16.get(key)
+    if ent is None or ent[0] != _GENERATION[0] or ent[1] is not w or ent[2].shape != w.shape:
+        ent = (_GENERATION[0], w, w.detach().to(torch.bfloat16))
+        _W16[key] = ent
+    return ent[2]
+
+
+class _Linear16Fn(torch.autograd.Function):
+    """y = x @ W^T (+ b) in bf16 on hipBLASLt over a cached bf16 W; fp32 weight/bias grads."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, w16):
+        x = x.to(torch.bfloat16)
+        x2 = x.reshape(-1, x.shape[-1])
+        if b is not None:
+            y = torch.addmm(b.to(torch.bfloat16), x2, w16.t())
+        else:
+            y = x2 @ w16.t()
+        ctx.save_for_backward(x2, w16)
+        ctx.has_b = b is not None
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], w16.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w16 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16)
+        dx = (dy2 @ w16).view(ctx.shape)
+        try:
+            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        except (TypeError, RuntimeError):
+            dw = (dy2.t() @ x2).float()
+        db = dy2.sum(0, dtype=torch.float32) if ctx.has_b else None
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if use_hip(x):
+        return _Linear16Fn.apply(x, w, b, weight_bf16(w))
+    return F.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:

@@ -421,3 +421,32 @@ def test_debug_kernels_flag_bad_ids_without_faulting():
         torch.testing.assert_close(out_b, pr, rtol=2e-3, atol=2e-3)
     finally:
         _native.use_debug_kernels(False)
+
+
+@pytest.mark.parametrize("L", [32, 37, 64, 200, 300])
+def test_fused_attention_packed_qkv(L):
+    """attention.hip (online softmax fwd, dK/dV + dQ bwd) vs an fp32 reference on the same
+    bf16 packed QKV, with key padding."""
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    torch.manual_seed(L)
+    N, H, d = 3, 4, 64
+    qkv = (torch.randn(N, L, 3 * H * d, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    mask = torch.ones(N, L, dtype=torch.int32, device=DEV)
+    mask[1, L // 2:] = 0
+    mask[2, 5:9] = 0
+    o = tops.fused_attention(qkv, mask, H)
+    ref_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref_in.view(N, L, 3, H, d).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / 8.0
+    s = s.masked_fill(~mask.bool()[:, None, None, :], float("-inf"))
+    orf = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(N, L, H * d)
+    torch.testing.assert_close(o.float(), orf, rtol=2e-2, atol=2e-2)
+    do = torch.randn_like(orf)
+    (o.float() * do).sum().backward()
+    (orf * do).sum().backward()
+    g, gr = qkv.grad.float().view(N, L, 3, H * d), ref_in.grad.view(N, L, 3, H * d)
+    for slot in range(3):
+        scale = gr[:, :, slot].abs().max()
+        err = (g[:, :, slot] - gr[:, :, slot]).abs().max() / scale
+        assert err < 3e-2, (slot, float(err))
