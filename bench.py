@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--eager-compare", type=int, default=1,
                     help="also time the eager PyTorch-ROCm implementation of the same model (batch 512, "
                          "single GPU only) and report the speedup")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="capture the training step in a hipGraph after 2 eager steps (single process only)")
     ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5")
     return ap.parse_args()
@@ -109,7 +111,8 @@ def main():
     V = cfg.vocab_hash_size
     dev = info.device
     model = build_model(cfg, V)
-    trainer = Trainer(cfg, model, dev)
+    # the capture happens after 2 eager steps: only inside the untimed warmup
+    trainer = Trainer(cfg, model, dev, graph=bool(a.graph) and a.warmup > Trainer.GRAPH_WARMUP)
 
     spec = spec_from_config(cfg, V, num_pages=16384)
     data = SyntheticPairs(spec, dev, seed=1337 + info.rank)
@@ -182,6 +185,7 @@ def main():
             "final_loss": round(final_loss, 4),
             "dense_equiv_tflops": round(flops / 1e12, 1),
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
+            "hip_graph": bool(trainer.graph_mode),
         }
         if eager:
             out["eager_pytorch_pairs_per_s"] = round(eager, 1)

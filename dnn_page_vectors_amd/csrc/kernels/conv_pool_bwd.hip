@@ -169,9 +169,10 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
 __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, const float* pooled, const int* argmax,
                                                           const int* ids, const unsigned short* table, float* dw3,
                                                           float* dw4, float* db, int N, int L, int E, int V, int nsplit,
-                                                          unsigned seed, unsigned row_offset, int thr,
-                                                          int token_mode, float scale) {
+                                                          unsigned seed, const unsigned* seed_ptr,
+                                                          unsigned row_offset, int thr, int token_mode, float scale) {
   __shared__ float red[4 * 4 * EP];
+  if (seed_ptr) seed += *seed_ptr;  // device seed offset (captured hipGraph steps)
   const int f = blockIdx.x;
   const int per = ((N + nsplit - 1) / nsplit + 255) / 256 * 256;
   const int n0 = blockIdx.y * per, n1 = min(N, n0 + per);
@@ -248,9 +249,10 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
                                                                const int2* __restrict__ rec,
                                                                const unsigned short* __restrict__ wrow,
                                                                float* __restrict__ dtable, long M, int L, int E,
-                                                               int V, unsigned seed, unsigned row_offset, int thr,
-                                                               int token_mode) {
+                                                               int V, unsigned seed, const unsigned* seed_ptr,
+                                                               unsigned row_offset, int thr, int token_mode) {
   __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
+  if (seed_ptr) seed += *seed_ptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, p = lane & 15;
   float* slab = slabs[wave];
@@ -345,16 +347,16 @@ using namespace pv;
 
 PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                                const void* table, float* dw3, float* dw4, float* db, int N, int L, int E, int V,
-                               unsigned seed, unsigned row_offset, int thr, int token_mode, float scale,
-                               void* stream) {
+                               unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                               float scale, void* stream) {
   using namespace pv::convbwd;
   if (E > EP || L < 4) return -1;
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
   hipLaunchKernelGGL(conv_bwd_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, (hipStream_t)stream, gpool, pooled,
-                     argmax, ids, (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, row_offset, thr,
-                     token_mode, scale);
+                     argmax, ids, (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr,
+                     row_offset, thr, token_mode, scale);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -373,14 +375,15 @@ PV_API int pv_conv_pool_bwd_emit2(const float* gpool, const float* pooled, const
 
 // wrow: bf16 [2*FW][4][EP] weight rows (zero padded); requires E <= EP.
 PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
-                                    float* dtable, long M, int L, int E, int V, unsigned seed, unsigned row_offset,
-                                    int thr, int token_mode, void* stream) {
+                                    float* dtable, long M, int L, int E, int V, unsigned seed,
+                                    const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                                    void* stream) {
   using namespace pv::convbwd;
   if (E > EP) return -1;
   const long chunks = (M + 63) / 64;
   hipLaunchKernelGGL(conv_bwd_reduce4_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, L, E, V, seed,
-                     row_offset, thr, token_mode);
+                     seed_ptr, row_offset, thr, token_mode);
   PV_LAUNCH_CHECK();
   return 0;
 }

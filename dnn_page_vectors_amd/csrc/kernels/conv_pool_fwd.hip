@@ -60,6 +60,7 @@ struct Params {
   int thr;                     // dropout byte threshold (0 = off)
   int token_mode;              // 1: one keep decision per row
   float scale;                 // 1/(1-p)
+  const unsigned* seed_ptr;    // optional device seed offset (added to seed; captured hipGraph steps)
 };
 
 // Diagnostic ablations are COMPILE-TIME (template DBG; production instantiation DBG = 0
@@ -359,6 +360,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
 
 template <int PF, int DBG>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
   __shared__ __attribute__((aligned(16))) char smem[CROWS * ROWB + 4 * CROWS * 4 + 16];
   char* xl = smem;
   int* ids_lds = reinterpret_cast<int*>(smem + CROWS * ROWB);
@@ -600,6 +602,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
 
 template <int PF, int DBG>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd2_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
   __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
   char* xl = smem;
   int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
@@ -666,14 +669,15 @@ static int g_conv_dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_D
 PV_API void pv_conv_set_dbg(int d) { g_conv_dbg = d; }
 
 PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack, const float* bias,
-                            float* pooled, int* argmax, int N, int L, int V, unsigned seed, unsigned row_offset,
+                            float* pooled, int* argmax, int N, int L, int V, unsigned seed, const unsigned* seed_ptr,
+                            unsigned row_offset,
                             int thr, int token_mode, float scale, int grid, void* stream) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
   if ((L - 2 + 15) / 16 > 1024) return -2;  // tagged argmax: block index must fit TAGB bits
   const int dbg = g_conv_dbg;
   Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
-           seed, row_offset, thr, token_mode, scale};
+           seed, row_offset, thr, token_mode, scale, seed_ptr};
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
   hipStream_t st = (hipStream_t)stream;

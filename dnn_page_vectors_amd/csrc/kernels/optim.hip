@@ -17,8 +17,19 @@ namespace optim {
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
                                                    float b1, float b2, float eps, float wd, int torch_style,
-                                                   float bc2_sqrt_inv, const float* __restrict__ skip) {
+                                                   float bc2_sqrt_inv, const float* __restrict__ skip,
+                                                   const float* __restrict__ tdev) {
   if (skip && *skip != 0.f) return;  // non-finite guard: skip the whole step
+  if (tdev) {  // step count on the device (hipGraph replays): bias corrections computed here
+    const float t = *tdev, lr = lr_t;
+    const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+    if (torch_style) {
+      lr_t = lr / bc1;
+      bc2_sqrt_inv = rsqrtf(bc2);
+    } else {
+      lr_t = lr * sqrtf(bc2) / bc1;
+    }
+  }
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x);
   const long stride = (long)gridDim.x * blockDim.x;
   const long n4 = n / 4;
@@ -47,6 +58,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     p[i] -= lr_t * m[i] / den;
   }
 }
+
+__global__ void step_inc_kernel(float* t) { *t += 1.f; }
 
 // fp32 (rows, cols) -> bf16 (rows, ldo) with zero padding of columns cols..ldo-1
 __global__ void cast_pad_bf16_kernel(const float* __restrict__ in, unsigned short* __restrict__ out, long rows, int cols,
@@ -103,6 +116,19 @@ static unsigned grid_for(long n, int per_thread) {
   return (unsigned)b;
 }
 
+// Device-counter variant: *tdev += 1, then the update with the bias corrections of step
+// *tdev computed in the kernel — the whole optimizer step is replayable from a hipGraph.
+PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, float* tdev, float lr, float b1,
+                       float b2, float eps, float wd, int torch_style, const float* skip, void* stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  hipLaunchKernelGGL(pv::optim::step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, tdev);
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     lr, b1, b2, eps, wd, torch_style, 1.f, skip, (const float*)tdev);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
 PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int step, float lr, float b1, float b2,
                    float eps, float wd, int torch_style, const float* skip, void* stream) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
@@ -115,7 +141,7 @@ PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int ste
     lr_t = (float)(lr * sqrt(bc2) / bc1);
   }
   hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip);
+                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip, (const float*)nullptr);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -12,10 +12,10 @@ SIGS = {
     "pv_conv_pack_weights": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
-    "pv_conv_pool_fwd": "pppppp" "iii" "uu" "ii" "f" "i" "p",
+    "pv_conv_pool_fwd": "pppppp" "iii" "upu" "ii" "f" "i" "p",
     # conv_pool_bwd.hip
-    "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "uuiif" "p",
-    "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "uuii" "p",
+    "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
+    "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "upuii" "p",
     "pv_conv_pool_bwd_emit2": "ppppppp" "iii" "f" "p",
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",
@@ -56,6 +56,7 @@ SIGS = {
     "pv_quant_fp8": "ppp" "l" "p",
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip
+    "pv_adam_dev": "pppp" "l" "p" "fffff" "i" "p" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
     "pv_sumsq": "p" "l" "p" "p",

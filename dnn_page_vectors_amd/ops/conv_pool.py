@@ -9,7 +9,7 @@ MaxPooling1D(L-k+1) -> Flatten} x k in (3,4) -> concat (dssm_cnn_v2/cnn_dssm_th.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
@@ -52,6 +52,15 @@ def _dropout_args(p: float, training: bool, mode: str) -> Tuple[int, int, float]
 
 _grid_cache = {}
 
+# Device seed offset for captured (hipGraph) training steps: when set, every conv kernel
+# adds *_SEED_DEV to its seed, so one captured graph draws fresh dropout masks per replay.
+_SEED_DEV: Optional[torch.Tensor] = None
+
+
+def set_seed_tensor(t: Optional[torch.Tensor]) -> None:
+    global _SEED_DEV
+    _SEED_DEV = t
+
 
 def _grid(device: torch.device) -> int:
     idx = device.index if device.index is not None else torch.cuda.current_device()
@@ -73,18 +82,19 @@ class _ConvPoolFn(torch.autograd.Function):
         argmax = torch.empty(N, 2 * FW, dtype=torch.int32, device=ids.device)
         seed &= 0xFFFFFFFF
         row_offset &= 0xFFFFFFFF
+        sp = _SEED_DEV
         check(lib().pv_conv_pool_fwd(P(ids), P(tbl16), P(wpack), P(bias.contiguous()), P(pooled), P(argmax), N, L, V,
-                                     seed, row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
+                                     seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
               "pv_conv_pool_fwd")
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
-        ctx.meta = (V, E, seed, row_offset, thr, tok, scale)
+        ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
         return pooled, argmax
 
     @staticmethod
     def backward(ctx, gpool, _gargmax):
         ids, pooled, argmax, tbl16, w3, w4 = ctx.saved_tensors
-        V, E, seed, row_offset, thr, tok, scale = ctx.meta
+        V, E, seed, row_offset, thr, tok, scale, sp = ctx.meta
         N, L = ids.shape
         dev = ids.device
         s = stream(dev)
@@ -94,7 +104,7 @@ class _ConvPoolFn(torch.autograd.Function):
         db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
         L_ = lib()
         check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E, V,
-                                     seed, row_offset, thr, tok, scale, s), "pv_conv_pool_bwd_dw")
+                                     seed, P(sp), row_offset, thr, tok, scale, s), "pv_conv_pool_bwd_dw")
         dtable = None
         if ctx.needs_input_grad[1]:
             M = N * 2 * FW * 4
@@ -117,7 +127,7 @@ class _ConvPoolFn(torch.autograd.Function):
             wrow[:FW, :3, :E] = w3.detach()
             wrow[FW:, :, :E] = w4.detach()
             check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
-                                              row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
+                                              P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
         return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
 
 

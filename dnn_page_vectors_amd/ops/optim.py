@@ -70,15 +70,18 @@ class FlatAdam:
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
         self.step_count = 0
+        # the step count also lives on the device: the HIP update reads (and advances) it,
+        # so a captured training step replays with the right bias corrections
+        self.t_dev = torch.zeros(1, dtype=torch.float32, device=flat.data.device)
 
     def step(self, skip_flag: Optional[torch.Tensor] = None) -> None:
         """One update. ``skip_flag``: device scalar; non-zero => the kernel skips (NaN guard)."""
         self.step_count += 1
         t = self.step_count
         if use_hip(self.flat.data):
-            check(lib().pv_adam(P(self.flat.data), P(self.flat.grad), P(self.m), P(self.v), self.flat.numel, t,
-                                self.lr, self.b1, self.b2, self.eps, self.wd, int(self.torch_style), P(skip_flag),
-                                stream(self.flat.data.device)), "pv_adam")
+            check(lib().pv_adam_dev(P(self.flat.data), P(self.flat.grad), P(self.m), P(self.v), self.flat.numel,
+                                    P(self.t_dev), self.lr, self.b1, self.b2, self.eps, self.wd,
+                                    int(self.torch_style), P(skip_flag), stream(self.flat.data.device)), "pv_adam_dev")
             return
         if skip_flag is not None and float(skip_flag) != 0.0:
             return
@@ -100,6 +103,7 @@ class FlatAdam:
         self.m.copy_(d["m"])
         self.v.copy_(d["v"])
         self.step_count = int(d["step"])
+        self.t_dev.fill_(float(self.step_count))
 
 
 def grad_sumsq_and_finite(flat_grad: torch.Tensor) -> torch.Tensor:

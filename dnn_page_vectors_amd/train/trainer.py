@@ -77,7 +77,7 @@ class PhaseTimer:
 
 class Trainer:
     def __init__(self, cfg, model: TwoTowerModel, device: Optional[torch.device] = None,
-                 metrics: Optional[MetricsLogger] = None):
+                 metrics: Optional[MetricsLogger] = None, graph: bool = False):
         self.cfg = cfg
         self.info = pdist.info()
         self.device = device or self.info.device
@@ -100,6 +100,13 @@ class Trainer:
         self.metrics = metrics
         self._fault_step = int(os.environ.get("PAGEVEC_FAULT_STEP", "-1"))
         self._timer: Optional[PhaseTimer] = None
+        # hipGraph mode (single process on a GPU): after GRAPH_WARMUP eager steps the whole
+        # step (forward, backward, Adam) is captured once and replayed — one launch per step
+        # instead of hundreds (the launch-bound MLP / BERT steps)
+        self.graph_mode = bool(graph) and self.device.type == "cuda" and not self.info.enabled
+        self._graph = None
+        self._graph_key = None
+        self._graph_warm = 0
 
     # ------------------------------------------------------------------ core step
     def _base_seed(self) -> int:
@@ -135,12 +142,57 @@ class Trainer:
             loss = placement.scale_grad(loss, 1.0 / self.info.world_size)
         return loss, P
 
+    GRAPH_WARMUP = 2
+
     def train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
         if self.step == self._fault_step:
             raise InjectedFault(f"injected fault at step {self.step}")
+        if self.graph_mode:
+            key = (tuple(q_ids.shape), tuple(d_ids.shape), q_ids.dtype, d_ids.dtype)
+            if self._graph is not None and key == self._graph_key:
+                return self._replay(q_ids, d_ids)
+            if self._graph_warm >= self.GRAPH_WARMUP and self._graph is None:
+                self._capture(q_ids, d_ids, key)
+                return self._replay(q_ids, d_ids)
+            self._graph_warm += 1
+        return self._eager_step(q_ids, d_ids)
+
+    # ------------------------------------------------------------------ hipGraph
+    def _capture(self, q_ids: torch.Tensor, d_ids: torch.Tensor, key) -> None:
+        from ..ops import conv_pool as cops
+
+        self._gq = q_ids.to(self.device).clone()
+        self._gd = d_ids.to(self.device).clone()
+        self._seed_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize()
+        step0, count0 = self.step, self.opt.step_count
+        g = torch.cuda.CUDAGraph()
+        cops.set_seed_tensor(self._seed_dev)  # conv kernels add the per-replay device seed
+        try:
+            with torch.cuda.graph(g):
+                self._gout = self._eager_step(self._gq, self._gd, seed_override=0, timing=False)
+        finally:
+            cops.set_seed_tensor(None)
+        # the capture only recorded the step: undo its host-side bookkeeping
+        self.step, self.opt.step_count = step0, count0
+        self._graph, self._graph_key = g, key
+
+    def _replay(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        self._gq.copy_(q_ids, non_blocking=True)
+        self._gd.copy_(d_ids, non_blocking=True)
+        seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
+        self._seed_dev.fill_(seed)
+        self._graph.replay()
+        self.opt.step_count += 1
+        bump_generation()
+        self.step += 1
+        return self._gout
+
+    def _eager_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed_override: Optional[int] = None,
+                    timing: bool = True) -> Dict[str, torch.Tensor]:
         self.model.train()
         le = self.cfg.log_every
-        timer = PhaseTimer(self.device) if (self.metrics and self.metrics.enabled and le and
+        timer = PhaseTimer(self.device) if (timing and self.metrics and self.metrics.enabled and le and
                                             (self.step + 1) % le == 0) else None
         if timer:
             timer.mark()
@@ -148,6 +200,8 @@ class Trainer:
         if self.buckets is not None:
             self.buckets.start_step()
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
+        if seed_override is not None:
+            seed = seed_override
         loss, P = self.compute_loss(q_ids, d_ids, seed)
         if timer:
             timer.mark()

@@ -450,3 +450,32 @@ def test_fused_attention_packed_qkv(L):
         scale = gr[:, :, slot].abs().max()
         err = (g[:, :, slot] - gr[:, :, slot]).abs().max() / scale
         assert err < 3e-2, (slot, float(err))
+
+
+@pytest.mark.parametrize("model", ["cdssm", "mlp"])
+def test_hipgraph_step_matches_eager(model):
+    """Trainer(graph=True): the captured + replayed step gives the eager trajectory (no
+    dropout: identical math; replays also keep advancing Adam's device step counter)."""
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    cfg = Configuration(model=model, feature_level="ngram", vocab_hash_size=500, query_length=12,
+                        document_length=64, batch_size=32, embedding_dim=100, dropout_prob=(0.0, 0.5),
+                        loss_mode="in_batch", mlp_dims=(64, 64, 32), hidden_dims=64)
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randint(1, 500, (32, 12), generator=g, dtype=torch.int32).to(DEV),
+             torch.randint(1, 500, (32, 4, 64), generator=g, dtype=torch.int32).to(DEV)) for _ in range(6)]
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = Trainer(cfg, build_model(cfg, 500), torch.device(DEV), graph=graph)
+        losses = [float(tr.train_step(q, d)["loss"]) for q, d in data]
+        runs.append((losses, tr.flat.data.clone(), tr.opt.step_count, tr._graph is not None))
+    (le, pe, ce, _), (lg, pg, cg, captured) = runs
+    assert captured and ce == cg == 6
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (le, lg)
+    torch.testing.assert_close(pg, pe, rtol=1e-3, atol=1e-4)
