@@ -29,17 +29,16 @@ PV_DEBUG_FLAG
 constexpr int EP = 104;
 constexpr int FW = 150;
 
-__device__ __forceinline__ unsigned mask_byte(unsigned hr, int e, int token_mode) {
-  return token_mode ? (hr & 0xFF) : ((dropout_group_hash(hr, (unsigned)(e >> 2)) >> (8 * (e & 3))) & 0xFF);
-}
-
 // ---- dW, db -----------------------------------------------------------------------
 // grid (2*FW, nsplit), block 256 (4 waves).  Each wave takes its samples 64 at a time:
 // lane l loads sample (base+l)'s g / ReLU flag / argmax and the k token ids of its
 // argmax window (independent loads, issued together), then the wave walks the live
-// samples with v_readlane broadcasts.  Lane l owns the 4-element groups q = l, l+64 of
-// the (k x EP) window (EP % 4 == 0, so a group never crosses rows and ONE group hash
-// yields its 4 dropout bytes); table loads for 4 samples are issued before use.
+// samples with v_readlane broadcasts.  Lane l owns the 16-byte piece l of the (k x EP)
+// window (row l / 13, columns 8*(l % 13) .. +7): one 16-byte table load, the dropout mask
+// of the piece from keep_piece (one group hash in the nibble mode), 8 FMAs.  The k row
+// hashes of a sample are computed once by lanes 0..k-1 and fetched with ds_bpermute.
+// Table loads for 4 samples are issued before use.
+constexpr int PIECES_ROW = EP / 8;  // 13
 template <int K>
 __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const float* __restrict__ pooled,
                                           const int* __restrict__ argmax, const int* __restrict__ ids,
@@ -47,19 +46,13 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
                                           float* __restrict__ db, float* red, int L, int E, int V, int fg, int fl,
                                           int n0, int n1, unsigned seed, unsigned row_offset, int thr, int token_mode,
                                           float scale) {
-  constexpr int NG = K * EP / 4;  // groups per window
+  constexpr int NP = K * PIECES_ROW;  // pieces per window (39 / 52)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float gsum = 0.f;
-  int jj[2], ee[2];
-  bool gv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = lane + 64 * i;
-    jj[i] = (q * 4) / EP;
-    ee[i] = (q * 4) % EP;
-    gv[i] = q < NG && ee[i] < E;
-  }
+  const int jj = lane / PIECES_ROW, pc = lane - jj * PIECES_ROW;
+  const bool pv_ = lane < NP && pc * 8 < E;
+  const int jsel = jj < K ? jj : 0;
   for (int base = n0 + wave * 64; base < n1; base += 256) {
     const int n = base + lane;
     float g = 0.f;
@@ -86,8 +79,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         sl[u] = m ? (int)__builtin_ctzll(m) : -1;
         if (m) { m &= m - 1; ++cnt; }
       }
-      uint2 raw[4][2];
-      unsigned hh[4][2];
+      u32x4 raw[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u >= cnt) break;
@@ -97,27 +89,18 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         int tj[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) tj[j] = __builtin_amdgcn_readlane(tok[j], s_);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int t = jj[i] == 0 ? tj[0] : jj[i] == 1 ? tj[1] : jj[i] == 2 ? tj[2] : tj[3];
-          const bool ok = gv[i] && t >= 0 && t < V;
-          raw[u][i] = ok ? *reinterpret_cast<const uint2*>(table + (size_t)t * EP + ee[i]) : uint2{0u, 0u};
-          unsigned h = 0xFFFFFFFFu;  // keep bytes of columns ee..ee+3 (ops/reference.py dropout_keep_mask)
-          if (thr > 0) {
-            const unsigned hr = dropout_row_hash(seed, row_offset + (unsigned)(nn * L + a_ + jj[i]));
-            if (token_mode) {
-              h = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
-            } else if ((thr & 15) == 0) {  // nibble decisions, one hash per 8 columns
-              const unsigned x = dropout_group_hash(hr, (unsigned)(ee[i] >> 3)) >> (16 * ((ee[i] >> 2) & 1));
-              unsigned b = 0u;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) b |= (((x >> (4 * k)) & 0xFu) >= (unsigned)(thr >> 4) ? 1u : 0u) << (8 * k);
-              h = b * 0xFFu;
-            } else {
-              h = keep_bytes(dropout_group_hash(hr, (unsigned)(ee[i] >> 2)), thr);
-            }
+        const int t = jsel == 0 ? tj[0] : jsel == 1 ? tj[1] : jsel == 2 ? tj[2] : tj[3];
+        const bool ok = pv_ && t >= 0 && t < V;
+        raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (size_t)t * EP + pc * 8) : u32x4{0u, 0u, 0u, 0u};
+        if (thr > 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
+          const unsigned hown = lane < K ? dropout_row_hash(seed, row_offset + (unsigned)(nn * L + a_ + lane)) : 0u;
+          const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute(jsel * 4, (int)hown);
+          if (token_mode) {
+            const unsigned k = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+            raw[u] &= u32x4{k, k, k, k};
+          } else {
+            raw[u] &= keep_piece(hr, pc, thr);
           }
-          hh[u][i] = h;
         }
       }
 #pragma unroll
@@ -125,30 +108,17 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         if (u >= cnt) break;
         const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), sl[u]));
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          uint2 r = raw[u][i];
-          if (thr > 0) {
-            r.x &= keep_pair(hh[u][i], 0);
-            r.y &= keep_pair(hh[u][i], 1);
-          }
-          const float x0 = __uint_as_float(r.x << 16), x1 = __uint_as_float(r.x & 0xFFFF0000u);
-          const float x2 = __uint_as_float(r.y << 16), x3 = __uint_as_float(r.y & 0xFFFF0000u);
-          acc[i][0] += gj * x0;
-          acc[i][1] += gj * x1;
-          acc[i][2] += gj * x2;
-          acc[i][3] += gj * x3;
+        for (int w = 0; w < 4; ++w) {
+          acc[2 * w] += gj * __uint_as_float(raw[u][w] << 16);
+          acc[2 * w + 1] += gj * __uint_as_float(raw[u][w] & 0xFFFF0000u);
         }
       }
     }
   }
-  // cross-wave reduction through LDS: red[wave][K*EP]
+  // cross-wave reduction through LDS: red[wave][K*EP], piece l -> elements 8l .. 8l+7
+  if (lane < NP) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = lane + 64 * i;
-    if (q < NG) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) red[wave * (K * EP) + q * 4 + c] = acc[i][c];
-    }
+    for (int c = 0; c < 8; ++c) red[wave * (K * EP) + lane * 8 + c] = acc[c];
   }
   const float gs = wave_sum(gsum);
   __syncthreads();

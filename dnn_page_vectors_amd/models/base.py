@@ -55,19 +55,24 @@ class TwoTowerModel(nn.Module):
             self._cache_gen = _GENERATION[0]
         return self._cache
 
-    def forward(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    def forward(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int = 0, doc_hook=None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
         """q_ids (B, Lq); d_ids (B, S, Ld) with S = 1+J docs per query (positive first).
 
-        Returns raw (unnormalised) q (B, D) and d (B, S, D).
+        Returns raw (unnormalised) q (B, D) and d (B, S, D).  The doc tower runs FIRST and
+        ``doc_hook(d)`` is called before the query tower, so a cross-GPU page gather can be
+        in flight while the query tower computes.
         """
         B, S, Ld = d_ids.shape
         training = self.training
-        q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
         if getattr(self.cfg, "share_doc_tower", True):
             d = self.tower_forward("doc", d_ids.reshape(B * S, Ld), training, seed * 2 + 2).view(B, S, -1)
         else:  # v1: independent towers per document slot (dssm_cnn/cnn_dssm.py:160-164)
             d = torch.stack([self.tower_forward("doc", d_ids[:, s], training, seed * 2 + 2 + 1000 * s, slot=s)
                              for s in range(S)], dim=1)
+        if doc_hook is not None:
+            doc_hook(d)
+        q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
         return q, d
 
     @torch.no_grad()

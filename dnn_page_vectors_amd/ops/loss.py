@@ -15,7 +15,7 @@ Both take L2-normalised vectors (``ops.dense.l2_normalize``).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -136,9 +136,37 @@ class _InBatchRowsFn(torch.autograd.Function):
         return (dS @ db).float(), (dS.t() @ qb).float(), None, None, None
 
 
+class PageGather:
+    """An in-flight all-gather of the local page vectors in the loss kernels' bf16 padded
+    layout, started as soon as the doc tower is done so that RCCL overlaps the query
+    tower's forward; consumed by cross_gpu_loss."""
+
+    def __init__(self, dn: torch.Tensor, group=None):
+        W = dist.get_world_size(group)
+        self.D = dn.shape[1]
+        self.DP = (self.D + 31) // 32 * 32
+        self.dbl = _pad_bf16(dn.detach(), self.DP)
+        self.db = torch.empty(dn.shape[0] * W, self.DP, dtype=torch.bfloat16, device=dn.device)
+        self.work = dist.all_gather_into_tensor(self.db, self.dbl, group=group, async_op=True)
+        self.source = dn
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        return self.dbl, self.db
+
+
+def start_page_gather(dn: torch.Tensor, group=None) -> Optional[PageGather]:
+    """Begin the cross-GPU page-vector gather early (None when it does not apply)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1 or not use_hip(dn) or dn.shape[1] > 192:
+        return None
+    return PageGather(dn, group)
+
+
 class _CrossGpuFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qn, dn, pos_local, gamma, clip, group):
+    def forward(ctx, qn, dn, pos_local, gamma, clip, group, pre):
         W = dist.get_world_size(group)
         rank = dist.get_rank(group)
         B, D = qn.shape
@@ -147,9 +175,12 @@ class _CrossGpuFn(torch.autograd.Function):
         DP = (D + 31) // 32 * 32
         s = stream(qn.device)
         qb = _pad_bf16(qn.detach(), DP)
-        dbl = _pad_bf16(dn.detach(), DP)
-        db = torch.empty(M, DP, dtype=torch.bfloat16, device=qn.device)
-        dist.all_gather_into_tensor(db, dbl, group=group)
+        if pre is not None:
+            dbl, db = pre.wait()
+        else:
+            dbl = _pad_bf16(dn.detach(), DP)
+            db = torch.empty(M, DP, dtype=torch.bfloat16, device=qn.device)
+            dist.all_gather_into_tensor(db, dbl, group=group)
         pos_local = pos_local.to(torch.int32).contiguous()
         pos = (pos_local + rank * n).contiguous()
         sumexp = torch.empty(B, dtype=torch.float32, device=qn.device)
@@ -183,17 +214,20 @@ class _CrossGpuFn(torch.autograd.Function):
         work.wait()
         check(L_.pv_ib_pos(P(qb), P(dbl), P(pos_local), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s),
               "pv_ib_pos(bwd)")
-        return dq[:, :D], dd[:, :D], None, None, None, None
+        return dq[:, :D], dd[:, :D], None, None, None, None, None
 
 
 def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, gamma: float, clip: bool = True,
-                   group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                   group=None, gathered: Optional[PageGather] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """qn (B, D) and the LOCAL page vectors dn (n, D), normalised; pos_local (B,) indexes dn.
-    Every query is scored against the pages of all ranks (rank r's pages at rows r*n...)."""
+    Every query is scored against the pages of all ranks (rank r's pages at rows r*n...).
+    ``gathered``: the PageGather started on ``dn`` right after the doc tower."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return inbatch_loss(qn, dn, pos_local, gamma, clip)
     if use_hip(qn, dn) and qn.shape[1] <= 192:
-        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group)
+        if gathered is not None and gathered.source is not dn:
+            raise ValueError("the prefetched gather belongs to another page tensor")
+        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group, gathered)
     from ..parallel.dist import all_gather_autograd
     docs = all_gather_autograd(dn)
     pos = pos_local + dist.get_rank(group) * dn.shape[0]

@@ -119,19 +119,25 @@ class Trainer:
         B, S, _ = d_ids.shape
         range_push("forward")
         tower = self.placement == "tower" and self.info.enabled
+        pre = {}
         if tower:  # every rank: same query/head seed; doc slots on their owning ranks
             q, d = placement.placed_forward(self.model, q_ids, d_ids, self._base_seed())
+            dn = dops.l2_normalize(d.reshape(B * S, -1))
         else:
-            q, d = self.model(q_ids, d_ids, seed=seed)
+            def doc_hook(d_):  # normalise + start the RCCL page gather before the query tower
+                pre["dn"] = dops.l2_normalize(d_.reshape(B * S, -1))
+                if cfg.loss_mode == "cross_gpu" and self.info.enabled:
+                    pre["gather"] = lops.start_page_gather(pre["dn"])
+            q, d = self.model(q_ids, d_ids, seed=seed, doc_hook=doc_hook)
+            dn = pre["dn"]
         qn = dops.l2_normalize(q)
-        dn = dops.l2_normalize(d.reshape(B * S, -1))
         clip = bool(getattr(cfg, "cos_clip", True))
         if cfg.loss_mode == "explicit":
             per_row, P = lops.dssm_explicit_loss(qn, dn.view(B, S, -1), cfg.GAMMA, clip)
         elif cfg.loss_mode in ("in_batch", "cross_gpu"):
             pos = torch.arange(B, device=q.device, dtype=torch.int32) * S
             if cfg.loss_mode == "cross_gpu" and self.info.enabled:
-                per_row, P = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip)
+                per_row, P = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip, gathered=pre.get("gather"))
             else:
                 per_row, P = lops.inbatch_loss(qn, dn, pos, cfg.GAMMA, clip)
         else:

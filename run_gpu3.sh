@@ -1,7 +1,8 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -q -x -k "hipgraph or adam" > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-for m in cdssm mlp chunked bert; do
-timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 --eager-compare 0 --recall 0 --graph 1 > gpurun_out/g_$m.log 2>&1; rc=$?; echo "$m graph rc=$rc"; tail -1 gpurun_out/g_$m.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 --eager-compare 0 --recall 0 --graph 0 > gpurun_out/e_$m.log 2>&1; rc=$?; echo "$m eager rc=$rc"; tail -1 gpurun_out/e_$m.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
-done
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python tools/conv_micro.py --variants 0 --rounds 3 --bwd > gpurun_out/micro.log 2>&1; rc=$?; cat gpurun_out/micro.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b.log 2>&1; rc=$?; tail -1 gpurun_out/b.log
+export PAGEVEC_DIST_BACKEND=gloo
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --batch 1024 --recall 256 > gpurun_out/bench_2rank.log 2>&1; rc=$?
+echo "2rank rc=$rc"; tail -1 gpurun_out/bench_2rank.log | cut -c1-150
