@@ -132,13 +132,18 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // outside its tile, ...) in a per-file device flag instead of faulting; the host reads
 // and clears it with pv_debug_<file>(reset) (dnn_page_vectors_amd._native.debug_status).
 // The release library compiles every check away.
-enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3 };
+// PV_OK(cond, bit) is the guarding form for data-dependent addresses: in the debug build it
+// records a violation AND evaluates to cond so the caller skips the access; in the release
+// build it is the constant true.
+enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3, PV_ERR_ARGMAX = 4, PV_ERR_SLOT = 5,
+       PV_ERR_POS = 6 };
 #ifdef PAGEVEC_DEBUG
 #define PV_DEBUG_FLAG static __device__ unsigned pv_dbg_flag_ = 0;
 #define PV_CHECK(cond, bit)                                      \
   do {                                                           \
     if (!(cond)) atomicOr(&pv_dbg_flag_, 1u << (bit));           \
   } while (0)
+#define PV_OK(cond, bit) ((cond) ? true : (atomicOr(&pv_dbg_flag_, 1u << (bit)), false))
 #define PV_DEBUG_EXPORT(tu)                                                   \
   PV_API unsigned pv_debug_##tu(int reset) {                                 \
     unsigned v = 0;                                                           \
@@ -155,6 +160,7 @@ enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3 };
 #define PV_CHECK(cond, bit) \
   do {                      \
   } while (0)
+#define PV_OK(cond, bit) true
 #define PV_DEBUG_EXPORT(tu)
 #endif
 

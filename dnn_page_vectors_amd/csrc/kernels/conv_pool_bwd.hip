@@ -62,8 +62,8 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
     if (n < n1) {
       const size_t o = (size_t)n * (2 * FW) + fg;
       g = gpool[o];
-      live = pooled[o] > 0.f && g != 0.f;
       a = argmax[o];
+      live = pooled[o] > 0.f && g != 0.f && PV_OK(a >= 0 && a < L, PV_ERR_ARGMAX);
       if (live) {
 #pragma unroll
         for (int j = 0; j < K; ++j) tok[j] = (a + j < L) ? ids[(size_t)n * L + a + j] : -1;
@@ -167,8 +167,8 @@ __global__ __launch_bounds__(256) void conv_bwd_emit2_kernel(const float* gpool,
   const int n = (int)(pair / (2 * FW)), f = (int)(pair % (2 * FW));
   const int K = f < FW ? 3 : 4;
   const float g = gpool[pair];
-  const bool live = pooled[pair] > 0.f && g != 0.f;
   const int a = argmax[pair];
+  const bool live = pooled[pair] > 0.f && g != 0.f && PV_OK(a >= 0 && a < L, PV_ERR_ARGMAX);
   rec[pair] = int2{__float_as_int(g * scale), a};
   unsigned k4[4];
 #pragma unroll
@@ -235,8 +235,8 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
   if (i < M) {
     key = skeys[i];
     PV_CHECK(key <= (unsigned)V, PV_ERR_KEY);
-    if (key < (unsigned)V) {
-      const unsigned sl = svals[i];
+    const unsigned sl = key < (unsigned)V ? svals[i] : 0u;
+    if (key < (unsigned)V && PV_OK((long)sl < M, PV_ERR_SLOT)) {
       const unsigned pair = sl >> 2, j = sl & 3;
       const unsigned nn = pair / (2 * FW), f = pair - nn * (2 * FW);
       const int2 rc = rec[pair];
@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
   const int n = __popcll(__ballot(key < (unsigned)V));  // live entries are a prefix (sorted)
   if (n == 0) return;
   unsigned cur = __builtin_amdgcn_readfirstlane(key);
+  const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);  // largest live key
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
@@ -280,8 +281,9 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
         v[k] = ge * __uint_as_float(wk);
       }
     }
-    // keys of the 4 groups (ascending); invalid groups join the current run with v = 0
-    if (!valid) kg = cur;
+    // keys of the 4 groups (ascending); groups past the live prefix take the largest live
+    // key (keeps the order ascending, so k0 == k3 == cur still means "all equal") and v = 0
+    if (!valid) kg = klast;
     const unsigned k0 = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
     const unsigned k3 = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
     if (k0 == cur && k3 == cur) {

@@ -566,6 +566,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
         const int col = colbase + rsub;
         if (kq == 0 && (col % 160) < FW) {
           const int f = (col / 160) * FW + (col % 160);
+          PV_CHECK(bi >= 0 && bi < (col < 160 ? nw3 : nw4), PV_ERR_ARGMAX);
           const float y = bv * p.scale + p.bias[f];
           p.pooled[(size_t)cur.n * (2 * FW) + f] = y > 0.f ? y : 0.f;
           p.argmax[(size_t)cur.n * (2 * FW) + f] = bi;

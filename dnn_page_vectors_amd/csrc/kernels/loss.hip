@@ -23,6 +23,7 @@
 
 namespace pv {
 namespace loss {
+PV_DEBUG_FLAG
 
 constexpr float BCE_EPS = 1e-7f;
 
@@ -408,6 +409,7 @@ __global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, con
   }
   sum = wave_sum(sum);
   const int p = pos[row];
+  if (!PV_OK(p >= 0 && p < M, PV_ERR_POS)) return;
   float rp = s[p];
   if (clip) rp = fminf(fmaxf(rp, 0.f), 1.f);
   if (lane == 0 && loss) loss[row] = gamma + __logf(sum) - gamma * rp;
@@ -422,6 +424,7 @@ __global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, con
   }
 }
 
+PV_DEBUG_EXPORT(loss)
 }  // namespace loss
 }  // namespace pv
 

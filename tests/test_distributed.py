@@ -38,7 +38,7 @@ def _gather_worker(rank, world, port, q):
     g = pdist.all_gather_autograd(local)
     w = torch.arange(g.numel(), dtype=torch.float32).view_as(g) * (rank + 1)
     (g * w).sum().backward()
-    q.put((rank, local.grad.clone()))
+    q.put((rank, local.grad.detach().numpy().copy()))
     pdist.destroy()
 
 
@@ -53,7 +53,7 @@ def test_all_gather_autograd_gloo():
     base = torch.arange(world * 3 * 5, dtype=torch.float32).view(world * 3, 5)
     full = base * 1 + base * 2  # sum over ranks of d(sum(g*w_r))/dg
     for r in range(world):
-        torch.testing.assert_close(res[r], full[r * 3:(r + 1) * 3])
+        torch.testing.assert_close(torch.from_numpy(res[r]), full[r * 3:(r + 1) * 3])
 
 
 def _cfg(mode, B):
@@ -88,7 +88,7 @@ def _dp_worker(rank, world, port, mode, q):
     for qa, da in _data(B):
         sl = slice(rank * B // world, (rank + 1) * B // world)
         tr.train_step(qa[sl], da[sl])
-    q.put((rank, tr.flat.data.clone()))
+    q.put((rank, tr.flat.data.detach().numpy().copy()))
     pdist.destroy()
 
 
@@ -103,7 +103,7 @@ def test_data_parallel_matches_single_process(mode):
     q = ctx.Queue()
     ps = [ctx.Process(target=_dp_worker, args=(r, world, port, mode, q)) for r in range(world)]
     [p.start() for p in ps]
-    res = dict(q.get(timeout=300) for _ in ps)
+    res = {r: torch.from_numpy(v) for r, v in (q.get(timeout=300) for _ in ps)}
     [p.join(timeout=60) for p in ps]
     # single process reference (cross_gpu with one rank == in-batch over the whole batch)
     pdist.set_info(pdist.DistInfo())
@@ -127,7 +127,7 @@ def _placement_worker(rank, world, port, q):
     losses = []
     for qa, da in _data(8):  # every rank sees the whole batch; the 4 doc slots are split 2 + 2
         losses.append(float(tr.train_step(qa, da)["loss"]))
-    q.put((rank, (tr.flat.data.clone(), losses)))
+    q.put((rank, (tr.flat.data.detach().numpy().copy(), losses)))
     pdist.destroy()
 
 
@@ -142,7 +142,7 @@ def test_tower_placement_matches_single_process():
     q = ctx.Queue()
     ps = [ctx.Process(target=_placement_worker, args=(r, world, port, q)) for r in range(world)]
     [p.start() for p in ps]
-    res = dict(q.get(timeout=300) for _ in ps)
+    res = {r: (torch.from_numpy(v[0]), v[1]) for r, v in (q.get(timeout=300) for _ in ps)}
     [p.join(timeout=60) for p in ps]
     pdist.set_info(pdist.DistInfo())
     cfg = _cfg("explicit", 8)

@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--loss", default="")
     ap.add_argument("--set", nargs="*", default=[])
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--sync-each", action="store_true", help="synchronize + print after every step (debug)")
+    ap.add_argument("--no-initial-eval", action="store_true")
+    ap.add_argument("--print-each", action="store_true", help="print the step number after each launch (no sync)")
     a = ap.parse_args()
     info = pdist.init_distributed()
     cfg = preset_config(a.preset).replace(batch_size=a.batch)
@@ -43,7 +47,7 @@ def main():
     dev = info.device
     data = SyntheticPairs(spec_from_config(cfg, V, num_pages=65536), dev, seed=11)
     model = build_model(cfg, V)
-    tr = Trainer(cfg, model, dev, graph=True)
+    tr = Trainer(cfg, model, dev, graph=bool(a.graph))
     qe, pe = data.eval_set(a.eval_pages)
     rel = torch.arange(a.eval_pages, device=dev)
     t0 = time.time()
@@ -54,10 +58,20 @@ def main():
                           **{k: round(v, 4) for k, v in r.items()}, "wall_s": round(time.time() - t0, 1)}),
               flush=True)
 
-    evaluate(0, float("nan"))
+    if not a.no_initial_eval:
+        evaluate(0, float("nan"))
     for s in range(1, a.steps + 1):
         q, d = data.batch(a.batch)
         m = tr.train_step(q, d)
+        if a.sync_each:
+            torch.cuda.synchronize()
+            rec = {"step": s, "ok": True, "graph": tr._graph is not None}
+            if os.environ.get("PAGEVEC_DEBUG_KERNELS") == "1":
+                from dnn_page_vectors_amd import _native
+                rec["debug"] = _native.debug_status()
+            print(json.dumps(rec), flush=True)
+        elif a.print_each:
+            print(json.dumps({"launched": s}), flush=True)
         if s % a.eval_every == 0 or s == a.steps:
             evaluate(s, float(m["loss"]))
 
