@@ -9,7 +9,9 @@ batch 4096 (weak scaling), cross-GPU in-batch negatives: every query is scored a
 ALL W * 4096 * (1 + J) page vectors of the step (all-gathered over RCCL).  Synthetic
 data: a device-resident pool of pre-featurized batches (no dataset/network available),
 random-init weights.  Each timed step = forward + backward + gradient all-reduce +
-Adam update.
+Adam update.  After the timed steps the run continues UNTIMED on fresh synthetic batches
+up to --quality-steps optimizer steps (default 1000 for cdssm / mlp) and reports Recall@10
+of that trained model on held-out query/page pairs (`recall_at_10`, `recall_after_steps`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
@@ -49,8 +51,14 @@ def parse():
     ap.add_argument("--eager-compare", type=int, default=1,
                     help="also time the eager PyTorch-ROCm implementation of the same model (batch 512, "
                          "single GPU only) and report the speedup")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="capture the training step in a hipGraph after 2 eager steps (single process only)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the training step in a hipGraph after 2 eager steps (single process only); "
+                         "-1 = auto: on for the launch-bound mlp / chunked / bert steps, off for cdssm (its "
+                         "step is kernel-bound: eager 9.76 vs graph 9.89 ms measured)")
+    ap.add_argument("--quality-steps", type=int, default=-1,
+                    help="after the timed steps, keep training (untimed, fresh synthetic batches, eager) until "
+                         "this many optimizer steps in total, then measure Recall@10 on held-out pairs; "
+                         "-1 = auto (1000 for cdssm / mlp, 0 = none for bert / chunked)")
     ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5")
     return ap.parse_args()
@@ -112,9 +120,16 @@ def main():
     dev = info.device
     model = build_model(cfg, V)
     # the capture happens after 2 eager steps: only inside the untimed warmup
-    trainer = Trainer(cfg, model, dev, graph=bool(a.graph) and a.warmup > Trainer.GRAPH_WARMUP)
+    if a.graph < 0:
+        a.graph = 0 if a.model == "cdssm" else 1
+    if a.quality_steps < 0:
+        a.quality_steps = 1000 if a.model in ("cdssm", "mlp") else 0
+    # pre-built device-resident batches and nothing eager between replays: no per-replay fence
+    trainer = Trainer(cfg, model, dev, graph=bool(a.graph) and a.warmup > Trainer.GRAPH_WARMUP, graph_fence=False)
 
-    spec = spec_from_config(cfg, V, num_pages=16384)
+    # 65536 distinct synthetic pages (the quality phase draws fresh batches from them; a
+    # smaller pool lets the towers memorise training pages instead of generalising)
+    spec = spec_from_config(cfg, V, num_pages=65536)
     data = SyntheticPairs(spec, dev, seed=1337 + info.rank)
     pool = [data.batch(a.batch) for _ in range(max(1, a.pool))]
     torch.cuda.synchronize()
@@ -139,6 +154,14 @@ def main():
     pdist.all_reduce_max_(t)
     dt = float(t[0])
     final_loss = float(m["loss"])
+
+    # quality phase (untimed): continue on fresh batches so Recall@10 reflects a trained model
+    done = a.warmup + a.steps
+    graph_used = trainer._graph is not None
+    trainer.graph_mode = False  # fresh per-step batches run eager (see Trainer graph_fence)
+    for i in range(max(0, a.quality_steps - done)):
+        m = trainer.train_step(*data.batch(a.batch))
+    quality_loss = float(m["loss"])
 
     recall = None
     if a.recall > 0:
@@ -182,10 +205,12 @@ def main():
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend},
             "recall_at_10": None if recall is None else round(recall, 4),
+            "recall_after_steps": max(done, a.quality_steps),
             "final_loss": round(final_loss, 4),
+            "loss_after_quality_steps": round(quality_loss, 4),
             "dense_equiv_tflops": round(flops / 1e12, 1),
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
-            "hip_graph": bool(trainer.graph_mode),
+            "hip_graph": graph_used,
         }
         if eager:
             out["eager_pytorch_pairs_per_s"] = round(eager, 1)

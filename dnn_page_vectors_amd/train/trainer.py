@@ -77,7 +77,7 @@ class PhaseTimer:
 
 class Trainer:
     def __init__(self, cfg, model: TwoTowerModel, device: Optional[torch.device] = None,
-                 metrics: Optional[MetricsLogger] = None, graph: bool = False):
+                 metrics: Optional[MetricsLogger] = None, graph: bool = False, graph_fence: bool = True):
         self.cfg = cfg
         self.info = pdist.info()
         self.device = device or self.info.device
@@ -104,6 +104,14 @@ class Trainer:
         # step (forward, backward, Adam) is captured once and replayed — one launch per step
         # instead of hundreds (the launch-bound MLP / BERT steps)
         self.graph_mode = bool(graph) and self.device.type == "cuda" and not self.info.enabled
+        # graph_fence: device-synchronize after every replay.  Measured on MI355X / ROCm 7.2 /
+        # torch 2.10: replays interleaved with eager allocating work (a fresh synthetic batch
+        # per step) and no device-wide sync hit an illegal-address fault after ~97 replays,
+        # deterministically; with a device sync per replay (or device-resident pre-built
+        # batches, bench.py) 100+ replays ran clean.  The fence costs one host round trip per
+        # step; bench.py turns it off because its batches are pre-built and nothing eager
+        # runs between replays.
+        self.graph_fence = bool(graph_fence)
         self._graph = None
         self._graph_key = None
         self._graph_warm = 0
@@ -189,6 +197,8 @@ class Trainer:
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
         self._seed_dev.fill_(seed)
         self._graph.replay()
+        if self.graph_fence:
+            torch.cuda.synchronize(self.device)
         self.opt.step_count += 1
         bump_generation()
         self.step += 1

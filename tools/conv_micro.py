@@ -63,6 +63,16 @@ def main():
         pooled.backward(torch.ones_like(pooled) * 1e-3)
 
     variants = [int(v) for v in a.variants.split(",")]
+    # schedule variants (>= 256) must reproduce the production kernel bit for bit
+    lib().pv_conv_set_dbg(0)
+    ref_p, ref_a = fwd()
+    for v in variants:
+        if v >= 256:
+            lib().pv_conv_set_dbg(v)
+            pv_, av_ = fwd()
+            print(json.dumps({"variant": v, "pooled_maxdiff": float((pv_ - ref_p).abs().max()),
+                              "argmax_mismatch": int((av_ != ref_a).sum())}))
+    lib().pv_conv_set_dbg(0)
     res = {v: [] for v in variants}
     resb = []
     for r in range(a.rounds):

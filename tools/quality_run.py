@@ -30,9 +30,10 @@ def main():
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--loss", default="")
     ap.add_argument("--set", nargs="*", default=[])
-    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--graph", type=int, default=0, help="hipGraph steps (fenced by a device sync per replay)")
     ap.add_argument("--sync-each", action="store_true", help="synchronize + print after every step (debug)")
     ap.add_argument("--no-initial-eval", action="store_true")
+    ap.add_argument("--pool", type=int, default=0, help="pre-generate this many batches and cycle them (0 = fresh batch per step)")
     ap.add_argument("--print-each", action="store_true", help="print the step number after each launch (no sync)")
     a = ap.parse_args()
     info = pdist.init_distributed()
@@ -54,14 +55,18 @@ def main():
 
     def evaluate(step, loss):
         r = recall_table(model.encode(qe, "query"), model.encode(pe, "doc"), rel, ks=(1, 10, 100))
-        print(json.dumps({"preset": a.preset, "step": step, "pairs_seen": step * a.batch, "loss": round(loss, 4),
-                          **{k: round(v, 4) for k, v in r.items()}, "wall_s": round(time.time() - t0, 1)}),
-              flush=True)
+        rec = {"preset": a.preset, "step": step, "pairs_seen": step * a.batch, "loss": round(loss, 4),
+               **{k: round(v, 4) for k, v in r.items()}, "wall_s": round(time.time() - t0, 1)}
+        if os.environ.get("PAGEVEC_DEBUG_KERNELS") == "1":
+            from dnn_page_vectors_amd import _native
+            rec["debug"] = _native.debug_status()
+        print(json.dumps(rec), flush=True)
 
     if not a.no_initial_eval:
         evaluate(0, float("nan"))
+    pool = [data.batch(a.batch) for _ in range(a.pool)]
     for s in range(1, a.steps + 1):
-        q, d = data.batch(a.batch)
+        q, d = pool[s % a.pool] if pool else data.batch(a.batch)
         m = tr.train_step(q, d)
         if a.sync_each:
             torch.cuda.synchronize()
