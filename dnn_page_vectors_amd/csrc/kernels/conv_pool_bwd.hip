@@ -311,6 +311,129 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
   reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
 }
 
+// ---- dTable reduce, long runs: each wave owns EPW consecutive sorted entries --------------
+// Same per-round arithmetic as reduce4, but a wave walks EPW entries (64 per sub-chunk) and
+// carries its open run (key + register partials) across sub-chunks, so a token whose run
+// spans many sub-chunks is flushed once per wave instead of once per 64 entries: under the
+// Zipf token distribution of real (and synthetic) pages the most frequent rows otherwise
+// take thousands of serialised row-atomics at one L2 channel.  Entry metadata is software-
+// pipelined: keys/slots two sub-chunks ahead, the {g, argmax} record gather one ahead.
+__device__ __forceinline__ void rd_meta(const unsigned* __restrict__ skeys, const unsigned* __restrict__ svals,
+                                        long i, long wend, unsigned V, unsigned& key, unsigned& sl) {
+  key = V;
+  sl = 0u;
+  if (i < wend) {
+    key = skeys[i];
+    PV_CHECK(key <= V, PV_ERR_KEY);
+    if (key < V) sl = svals[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const unsigned* __restrict__ skeys,
+                                                               const unsigned* __restrict__ svals,
+                                                               const int2* __restrict__ rec,
+                                                               const unsigned short* __restrict__ wrow,
+                                                               float* __restrict__ dtable, long M, int EPW, int L,
+                                                               int E, int V, unsigned seed, const unsigned* seed_ptr,
+                                                               unsigned row_offset, int thr, int token_mode) {
+  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
+  if (seed_ptr) seed += *seed_ptr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, p = lane & 15;
+  float* slab = slabs[wave];
+  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
+  if (wbeg >= M) return;
+  const long wend = min(M, wbeg + (long)EPW);
+  const unsigned UV = (unsigned)V;
+  // pipeline: (k0, s0, r0) = current sub-chunk, (k1, s1) = next, (k2, s2) = the one after
+  unsigned k0, s0, k1, s1, k2, s2;
+  rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
+  rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
+  auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
+    return (key < UV && PV_OK((long)sl < M, PV_ERR_SLOT)) ? rec[sl >> 2] : int2{0, 0};
+  };
+  int2 r0 = ld_rec(k0, s0);
+  unsigned cur = UV;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const bool act = p < RPIECES;
+  for (long b = wbeg; b < wend; b += 64) {
+    rd_meta(skeys, svals, b + 128 + lane, wend, UV, k2, s2);
+    const int2 r1 = ld_rec(k1, s1);
+    // this lane's entry of sub-chunk b
+    const unsigned key = k0;
+    unsigned fj = 0, hr = 0;
+    float gg = 0.f;
+    if (key < UV) {
+      const unsigned pair = s0 >> 2, j = s0 & 3;
+      const unsigned nn = pair / (2 * FW), f = pair - nn * (2 * FW);
+      fj = (f << 2) | j;
+      gg = __int_as_float(r0.x);
+      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
+    }
+    const int n = __popcll(__ballot(key < UV));  // live entries are a prefix (sorted)
+    if (n == 0) break;
+    if (cur == UV) cur = __builtin_amdgcn_readfirstlane(key);
+    const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);
+    for (int q0 = 0; q0 < n; q0 += 4) {
+      const int e = q0 + g;
+      const bool valid = e < n;
+      const int src = (valid ? e : q0) * 4;
+      unsigned kg = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
+      const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
+      float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
+      const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
+      if (!valid) ge = 0.f;
+      float v[8];
+      {
+        u32x4 w = u32x4{0u, 0u, 0u, 0u};
+        if (act) w = *reinterpret_cast<const u32x4*>(wrow + (size_t)f_j * EP + 8 * p);
+        if (thr > 0) {
+          if (token_mode) {
+            const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+            w &= u32x4{k, k, k, k};
+          } else {
+            w &= keep_piece(he, p, thr);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
+          v[k] = ge * __uint_as_float(wk);
+        }
+      }
+      if (!valid) kg = klast;
+      const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
+      const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
+      if (ka == cur && kb == cur) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        continue;
+      }
+      bool done = false;
+      for (int it = 0; it < 5; ++it) {
+        const bool mine = !done && kg == cur;
+        if (mine) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += v[k];
+          done = true;
+        }
+        const unsigned long long left = __ballot(!done);
+        if (left == 0) break;
+        reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
+      }
+    }
+    if (n < 64) break;  // the dead (key == V) tail starts inside this sub-chunk
+    k0 = k1; s0 = s1; r0 = r1;
+    k1 = k2; s1 = s2;
+  }
+  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+}
+
 PV_DEBUG_EXPORT(convbwd)
 }  // namespace convbwd
 }  // namespace pv
@@ -346,6 +469,21 @@ PV_API int pv_conv_pool_bwd_emit2(const float* gpool, const float* pooled, const
 }
 
 // wrow: bf16 [2*FW][4][EP] weight rows (zero padded); requires E <= EP.
+// epw: sorted entries per wave (multiple of 64); 0 = the 64-entry reduce4 kernel.
+PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                    float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
+                                    const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                                    void* stream) {
+  using namespace pv::convbwd;
+  if (E > EP || epw < 64 || (epw & 63)) return -1;
+  const long waves = (M + epw - 1) / epw;
+  hipLaunchKernelGGL(conv_bwd_reduce5_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed,
+                     seed_ptr, row_offset, thr, token_mode);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
 PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
                                     float* dtable, long M, int L, int E, int V, unsigned seed,
                                     const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,

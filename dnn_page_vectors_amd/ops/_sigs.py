@@ -16,6 +16,7 @@ SIGS = {
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "upuii" "p",
+    "pv_conv_pool_bwd_reduce5": "ppppp" "liiii" "upuii" "p",
     "pv_conv_pool_bwd_emit2": "ppppppp" "iii" "f" "p",
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",

@@ -9,6 +9,8 @@ MaxPooling1D(L-k+1) -> Flatten} x k in (3,4) -> concat (dssm_cnn_v2/cnn_dssm_th.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -51,6 +53,9 @@ def _dropout_args(p: float, training: bool, mode: str) -> Tuple[int, int, float]
 
 
 _grid_cache = {}
+
+# sorted dTable entries per wave in the reduce (conv_bwd_reduce5_kernel); 0 = 64-entry reduce4
+REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
 
 # Device seed offset for captured (hipGraph) training steps: when set, every conv kernel
 # adds *_SEED_DEV to its seed, so one captured graph draws fresh dropout masks per replay.
@@ -126,8 +131,12 @@ class _ConvPoolFn(torch.autograd.Function):
             wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)
             wrow[:FW, :3, :E] = w3.detach()
             wrow[FW:, :, :E] = w4.detach()
-            check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
-                                              P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
+            if REDUCE_EPW > 0:
+                check(L_.pv_conv_pool_bwd_reduce5(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E,
+                                                  V, seed, P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce5")
+            else:
+                check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
+                                                  P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
         return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
 
 

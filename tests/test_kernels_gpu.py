@@ -61,6 +61,34 @@ def test_conv_pool_fwd_bwd(N, L, p, mode):
         torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("epw", [64, 512, 1024])
+def test_dtable_reduce_long_runs_match_reduce4(epw):
+    """reduce5 (a wave walks epw sorted entries, runs carried across 64-entry sub-chunks)
+    equals the 64-entry reduce4 kernel on Zipf-skewed ids whose hottest rows span many
+    sub-chunks and waves (fp32 atomics: equal up to summation order)."""
+    torch.manual_seed(1)
+    V, E, F, N, L = 500, 100, 150, 64, 300
+    ranks = torch.arange(1, V, dtype=torch.float64)
+    probs = ranks.pow(-1.1)
+    ids = (torch.multinomial(probs / probs.sum(), N * L, replacement=True) + 1).view(N, L).to(torch.int32).to(DEV)
+    table = bf(torch.randn(V, E, device=DEV) * 0.5)
+    w3, w4 = bf(torch.randn(F, 3, E, device=DEV) * 0.1), bf(torch.randn(F, 4, E, device=DEV) * 0.1)
+    b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
+    grads = []
+    saved = cops.REDUCE_EPW
+    try:
+        for e in (0, epw):
+            cops.REDUCE_EPW = e
+            t = table.clone().requires_grad_(True)
+            pooled, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], b, 0.25, 99, True)
+            (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
+            grads.append(t.grad)
+    finally:
+        cops.REDUCE_EPW = saved
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-5)
+    assert grads[0].abs().sum() > 0
+
+
 def test_conv_pool_eval_mode_no_dropout():
     V, E, F, N, L = 50, 100, 150, 4, 20
     ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
