@@ -30,6 +30,7 @@
 //    id->row dependent loads never sit on the critical path.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace pv {
 namespace convpool {
@@ -471,7 +472,12 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
   };
   reset_state();
   const int rsub = lane & 15, kq = lane >> 4;
-  const unsigned keep = ~TAGM;
+  unsigned keep = ~TAGM;
+  if constexpr ((OPT & 4) != 0) {
+    // the tag mask in a VGPR: (x & keep) | btag can then be ONE v_and_or_b32 (VGPR, VGPR, SGPR)
+    // — a literal mask forces v_and + v_or (gfx9 VOP3 has no literal operand)
+    asm("v_mov_b32 %0, 0xfffffc00" : "=v"(keep));
+  }
   // OPT & 2: software-pipelined epilogue — the max/argmax of FULL block b runs inside block
   // b+1's K-step loop (element e at step e mod NS), so its VALU issues in the MFMA shadow
   // instead of as a burst between blocks; the pending block is flushed before the sample
@@ -504,10 +510,11 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
     bf16x8 ab[PF];
 #pragma unroll
     for (int u = 0; u < PF; ++u) ab[u] = *reinterpret_cast<const bf16x8*>(abase0 + u * 64);
-#pragma unroll 1
-    for (int blk = 0; blk < R / 16; ++blk) {
+    // one 16-window block: MFMAs over all K-steps, then the running max/argmax.  FULL blocks
+    // (every window valid for both widths) take the unmasked epilogue.
+    auto block = [&](const int blk, auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
       const int t0 = tc + blk * 16;
-      if (t0 >= nw3) break;
       const unsigned btag = (unsigned)(t0 >> 4);
       f32x4 c3[A3], c4[A4];
 #pragma unroll
@@ -532,31 +539,13 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
         }
 #pragma unroll
         for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
-        if constexpr (PIPE) {
-          if (qpend) {
-#pragma unroll
-            for (int e = s; e < NPEND; e += NS) pend_elem(e);
-          }
-        }
       }
       if constexpr ((DBG & 2) != 0) {
 #pragma unroll
         for (int i = 0; i < N3; ++i) m3[i] += c3[i];
 #pragma unroll
         for (int i = 0; i < N4; ++i) m4[i] += c4[i];
-        continue;
-      }
-      if (PIPE && t0 + 16 <= nw4) {  // defer this full block's epilogue into the next block
-#pragma unroll
-        for (int i = 0; i < N3; ++i) q3[i] = c3[i];
-#pragma unroll
-        for (int i = 0; i < N4; ++i) q4[i] = c4[i];
-        qtag = btag;
-        qpend = true;
-        continue;
-      }
-      flush_pending();
-      if (t0 + 16 <= nw4) {
+      } else if constexpr (FULL) {
 #pragma unroll
         for (int i = 0; i < N3; ++i)
 #pragma unroll
@@ -575,6 +564,92 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
 #pragma unroll
           for (int i = 0; i < N4; ++i)
             if (row < nw4) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+        }
+      }
+    };
+    if constexpr ((OPT & 8) != 0) {
+      // peeled: the full blocks of the chunk in one loop, the (at most 2) partial tail blocks
+      // of the sample in a second one — the hot loop carries no masked-epilogue path
+      const int nvalid = min(R / 16, (nw3 - tc + 15) / 16);
+      const int nfull = nw4 - tc >= 16 ? min(nvalid, (nw4 - tc - 16) / 16 + 1) : 0;
+      int blk = 0;
+#pragma unroll 1
+      for (; blk < nfull; ++blk) block(blk, std::true_type{});
+#pragma unroll 1
+      for (; blk < nvalid; ++blk) block(blk, std::false_type{});
+    } else {
+#pragma unroll 1
+      for (int blk = 0; blk < R / 16; ++blk) {
+        const int t0 = tc + blk * 16;
+        if (t0 >= nw3) break;
+        const unsigned btag = (unsigned)(t0 >> 4);
+        f32x4 c3[A3], c4[A4];
+  #pragma unroll
+        for (int i = 0; i < N3; ++i) c3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int i = 0; i < N4; ++i) c4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* abase = abase0 + blk * 16 * ROWB;
+        const char* anext = blk + 1 < R / 16 ? abase + 16 * ROWB : abase;
+        constexpr int NS = N4 > 0 ? S4 : S3;
+  #pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          bf16x8 a = ab[0];
+  #pragma unroll
+          for (int u = 0; u + 1 < PF; ++u) ab[u] = ab[u + 1];
+          if constexpr ((DBG & 8) == 0) {
+            if (s + PF < NS) ab[PF - 1] = *reinterpret_cast<const bf16x8*>(abase + (s + PF) * 64);
+            else ab[PF - 1] = *reinterpret_cast<const bf16x8*>(anext + (s + PF - NS) * 64);
+          }
+          if (s < S3) {
+  #pragma unroll
+            for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
+          }
+  #pragma unroll
+          for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
+          if constexpr (PIPE) {
+            if (qpend) {
+  #pragma unroll
+              for (int e = s; e < NPEND; e += NS) pend_elem(e);
+            }
+          }
+        }
+        if constexpr ((DBG & 2) != 0) {
+  #pragma unroll
+          for (int i = 0; i < N3; ++i) m3[i] += c3[i];
+  #pragma unroll
+          for (int i = 0; i < N4; ++i) m4[i] += c4[i];
+          continue;
+        }
+        if (PIPE && t0 + 16 <= nw4) {  // defer this full block's epilogue into the next block
+  #pragma unroll
+          for (int i = 0; i < N3; ++i) q3[i] = c3[i];
+  #pragma unroll
+          for (int i = 0; i < N4; ++i) q4[i] = c4[i];
+          qtag = btag;
+          qpend = true;
+          continue;
+        }
+        flush_pending();
+        if (t0 + 16 <= nw4) {
+  #pragma unroll
+          for (int i = 0; i < N3; ++i)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
+  #pragma unroll
+          for (int i = 0; i < N4; ++i)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+        } else {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = t0 + win_of_row(4 * kq + r);
+  #pragma unroll
+            for (int i = 0; i < N3; ++i)
+              if (row < nw3) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
+  #pragma unroll
+            for (int i = 0; i < N4; ++i)
+              if (row < nw4) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+          }
         }
       }
     }
@@ -729,10 +804,13 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #define PV_CONV_LAUNCH(PFV, DV) \
   hipLaunchKernelGGL((conv_pool_fwd_kernel<PFV, DV>), dim3(grid), dim3(NTHREADS), 0, st, p)
   switch (dbg) {
-    case 0:  // production: v2 schedule (double-buffered chunks, tag-encoded argmax) + s_setprio 1
-             // for waves 4-7 (6.04 -> 5.94 ms at the bench shape; the pipelined epilogue, OPT 2,
-             // measured 6.18 ms and is kept only as a variant)
-      hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0, 1>), dim3(grid), dim3(NTHREADS), 0, st, p);
+    case 0:  // production: v2 schedule (double-buffered chunks, tag-encoded argmax) + OPT 13:
+             // s_setprio 1 for waves 4-7, the tag mask in a VGPR (one v_and_or_b32 per element)
+             // and the partial tail blocks peeled out of the hot loop.  Same-process A/B at the
+             // bench shape: OPT 1 6.065 ms, OPT 5 6.008, OPT 9 5.938, OPT 13 5.891 (v2 without
+             // setprio measured 6.04 vs 5.94 with it on another box); the pipelined epilogue
+             // (OPT 2) measured 6.18 ms and is kept only as a variant.
+      hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0, 13>), dim3(grid), dim3(NTHREADS), 0, st, p);
       break;
     case 128: PV_CONV_LAUNCH(2, 0); break;  // v1 schedule (two barriers per chunk, cmp/select argmax)
     case 16: PV_CONV_LAUNCH(1, 0); break;  // A prefetch depth 1
@@ -749,7 +827,7 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #undef PV_CONV2_ABL
 #define PV_CONV2_OPT(O) \
     case 256 + O: hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0, O>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
-    PV_CONV2_OPT(1) PV_CONV2_OPT(2) PV_CONV2_OPT(3)
+    PV_CONV2_OPT(1) PV_CONV2_OPT(2) PV_CONV2_OPT(3) PV_CONV2_OPT(5) PV_CONV2_OPT(9) PV_CONV2_OPT(13)
 #undef PV_CONV2_OPT
     default: return -3;
   }
