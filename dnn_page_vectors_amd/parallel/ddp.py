@@ -8,8 +8,11 @@ complete, so communication of late layers overlaps the backward of early ones.
 
 Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); RCCL spreads a
 ring/tree over several channels, and messages of a few tens of MB keep them busy while
-staying latency-light.  Default 32 MB (the whole CDSSM-ngram gradient, ~25 MB, is one
-bucket; the BERT-base gradient, ~440 MB, is ~14 buckets overlapped with backward).
+staying latency-light.  Default 32 MB (the BERT-base gradient, ~440 MB, is ~14 buckets
+overlapped with backward).  Buckets are also cut where the top-level module changes
+(``query_tower`` | ``doc_towers``): the query tower runs last in forward, so its gradient
+(12.6 MB for CDSSM-ngram) is complete early in backward and its all-reduce overlaps the
+doc tower's backward instead of sharing one 25 MB bucket launched after everything.
 """
 from __future__ import annotations
 
@@ -22,6 +25,8 @@ from ..ops.optim import FlatParams
 
 
 class GradBuckets:
+    MIN_SPLIT_BYTES = 1 << 20  # module-boundary cuts only once the open bucket holds >= 1 MB
+
     def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg"):
         """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients)."""
         self.flat = flat
@@ -35,18 +40,24 @@ class GradBuckets:
         self.buckets: List[List[int]] = []  # [lo, hi, n_params]
         self.param_bucket = {}
         cur_lo = cur_hi = None
+        cur_mod = None
         members: List[str] = []
+        min_split = self.MIN_SPLIT_BYTES // 4
         for name, p in reversed(flat.named):
             o, k, _ = flat.offsets[name]
             end = o + (k + 63) // 64 * 64
+            mod = name.split(".", 1)[0]
             if cur_lo is None:
-                cur_lo, cur_hi, members = o, end, [name]
+                cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
+            elif mod != cur_mod and (cur_hi - cur_lo) >= min_split:
+                self._add(cur_lo, cur_hi, members)
+                cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
             elif (cur_hi - o) <= cap:
                 cur_lo = o
                 members.append(name)
             else:
                 self._add(cur_lo, cur_hi, members)
-                cur_lo, cur_hi, members = o, end, [name]
+                cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
         if cur_lo is not None:
             self._add(cur_lo, cur_hi, members)
         self.pending = [0] * len(self.buckets)
