@@ -155,10 +155,28 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
 }
 
 // ---- dTable emit (compact): keys + slot values + one 8-byte record per (n,f) pair -------
-// Everything the reduce needs per entry follows from the slot s = 4*(n*2FW + f) + j and
-// rec[s >> 2] = {g * scale, argmax}: ONE 8-byte gather per sorted entry instead of three
-// 4-byte gathers from 4x larger per-slot arrays (the sorted order scatters them).
-__global__ __launch_bounds__(256) void conv_bwd_emit2_kernel(const float* gpool, const float* pooled,
+// Slots are numbered per sample without the dead 4th row of the k=3 filters:
+//   sample n owns slots [n*SPS, (n+1)*SPS), SPS = 3*FW + 4*FW = 1050; k=3 filter f (< FW) row j
+//   is slot n*SPS + 3f + j, k=4 filter f row j is n*SPS + 3*FW + 4(f - FW) + j
+// (a 12.5% smaller sort than 4 slots per pair).  Everything the reduce needs per entry
+// follows from the slot and rec[pair] = {g * scale, argmax}: ONE 8-byte gather per sorted
+// entry instead of three 4-byte gathers from per-slot arrays (the sorted order scatters them).
+constexpr int SPS = 7 * FW;
+
+__device__ __forceinline__ void slot_decode(unsigned sl, unsigned& n, unsigned& f, unsigned& j) {
+  n = sl / (unsigned)SPS;
+  const unsigned r = sl - n * (unsigned)SPS;
+  if (r < 3u * FW) {
+    f = r / 3u;
+    j = r - 3u * f;
+  } else {
+    const unsigned q = r - 3u * FW;
+    f = FW + (q >> 2);
+    j = q & 3u;
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool, const float* pooled,
                                                              const int* argmax, const int* ids, unsigned* keys,
                                                              unsigned* vals, int2* rec, int N, int L, int V,
                                                              float scale) {
@@ -170,18 +188,18 @@ __global__ __launch_bounds__(256) void conv_bwd_emit2_kernel(const float* gpool,
   const int a = argmax[pair];
   const bool live = pooled[pair] > 0.f && g != 0.f && PV_OK(a >= 0 && a < L, PV_ERR_ARGMAX);
   rec[pair] = int2{__float_as_int(g * scale), a};
-  unsigned k4[4];
+  const unsigned s0 = (unsigned)n * SPS + (f < FW ? 3u * f : 3u * FW + 4u * (f - FW));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int t = a + j;
-    const bool ok = live && j < K && t < L;
-    const int v = ok ? ids[(size_t)n * L + t] : V;
-    PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
-    k4[j] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;
+    if (j < K) {
+      const int t = a + j;
+      const bool ok = live && t < L;
+      const int v = ok ? ids[(size_t)n * L + t] : V;
+      PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
+      keys[s0 + j] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;
+      vals[s0 + j] = s0 + j;
+    }
   }
-  reinterpret_cast<u32x4*>(keys)[pair] = u32x4{k4[0], k4[1], k4[2], k4[3]};
-  const unsigned s0 = (unsigned)(pair * 4);
-  reinterpret_cast<u32x4*>(vals)[pair] = u32x4{s0, s0 + 1, s0 + 2, s0 + 3};
 }
 
 // ---- dTable reduce, 4 entries per wave-instruction ------------------------------------
@@ -237,9 +255,9 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
     PV_CHECK(key <= (unsigned)V, PV_ERR_KEY);
     const unsigned sl = key < (unsigned)V ? svals[i] : 0u;
     if (key < (unsigned)V && PV_OK((long)sl < M, PV_ERR_SLOT)) {
-      const unsigned pair = sl >> 2, j = sl & 3;
-      const unsigned nn = pair / (2 * FW), f = pair - nn * (2 * FW);
-      const int2 rc = rec[pair];
+      unsigned nn, f, j;
+      slot_decode(sl, nn, f, j);
+      const int2 rc = rec[nn * (2 * FW) + f];
       fj = (f << 2) | j;
       gg = __int_as_float(rc.x);
       if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)rc.y + j);
@@ -350,7 +368,10 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const unsigned* _
   rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
   rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
   auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
-    return (key < UV && PV_OK((long)sl < M, PV_ERR_SLOT)) ? rec[sl >> 2] : int2{0, 0};
+    if (!(key < UV && PV_OK((long)sl < M, PV_ERR_SLOT))) return int2{0, 0};
+    unsigned nn, f, j;
+    slot_decode(sl, nn, f, j);
+    return rec[nn * (2 * FW) + f];
   };
   int2 r0 = ld_rec(k0, s0);
   unsigned cur = UV;
@@ -366,8 +387,8 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const unsigned* _
     unsigned fj = 0, hr = 0;
     float gg = 0.f;
     if (key < UV) {
-      const unsigned pair = s0 >> 2, j = s0 & 3;
-      const unsigned nn = pair / (2 * FW), f = pair - nn * (2 * FW);
+      unsigned nn, f, j;
+      slot_decode(s0, nn, f, j);
       fj = (f << 2) | j;
       gg = __int_as_float(r0.x);
       if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
@@ -456,13 +477,15 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   return 0;
 }
 
-// keys/vals: M = N*2*FW*4 slots; rec: N*2*FW records {g*scale, argmax}.
-PV_API int pv_conv_pool_bwd_emit2(const float* gpool, const float* pooled, const int* argmax, const int* ids,
+// keys/vals: M = N * pv_conv_bwd_slots_per_sample() slots; rec: N*2*FW records {g*scale, argmax}.
+PV_API int pv_conv_bwd_slots_per_sample() { return pv::convbwd::SPS; }
+
+PV_API int pv_conv_pool_bwd_emit3(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                                   unsigned* keys, unsigned* vals, void* rec, int N, int L, int V, float scale,
                                   void* stream) {
   using namespace pv::convbwd;
   const long pairs = (long)N * 2 * FW;
-  hipLaunchKernelGGL(conv_bwd_emit2_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(conv_bwd_emit3_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale);
   PV_LAUNCH_CHECK();
   return 0;

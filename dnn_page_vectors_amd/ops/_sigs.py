@@ -17,7 +17,8 @@ SIGS = {
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "upuii" "p",
     "pv_conv_pool_bwd_reduce5": "ppppp" "liiii" "upuii" "p",
-    "pv_conv_pool_bwd_emit2": "ppppppp" "iii" "f" "p",
+    "pv_conv_pool_bwd_emit3": "ppppppp" "iii" "f" "p",
+    "pv_conv_bwd_slots_per_sample": "",
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",
     "pv_sort_pairs_u32": "plpppp" "li" "p",

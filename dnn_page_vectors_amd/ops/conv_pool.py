@@ -21,6 +21,7 @@ from ._common import P, check, lib, need, stream, use_hip
 EP = 104          # padded embedding row stride of the bf16 table copy (kernel constant)
 FW = 150          # filters per width the fast kernel is built for
 WIDTHS = (3, 4)
+SLOTS_PER_SAMPLE = 7 * FW  # dTable entries per sample: 3 per k=3 filter + 4 per k=4 filter
 
 
 def fast_path_supported(E: int, widths, num_filters: int) -> bool:
@@ -112,13 +113,13 @@ class _ConvPoolFn(torch.autograd.Function):
                                      seed, P(sp), row_offset, thr, tok, scale, s), "pv_conv_pool_bwd_dw")
         dtable = None
         if ctx.needs_input_grad[1]:
-            M = N * 2 * FW * 4
+            M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
             u32 = torch.int32
             keys = torch.empty(M, dtype=u32, device=dev)
             vals = torch.empty(M, dtype=u32, device=dev)
             rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
-            check(L_.pv_conv_pool_bwd_emit2(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
-                                            scale, s), "pv_conv_pool_bwd_emit2")
+            check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
+                                            scale, s), "pv_conv_pool_bwd_emit3")
             end_bit = max(1, int(V).bit_length())
             skeys = torch.empty_like(keys)
             svals = torch.empty_like(vals)

@@ -64,7 +64,7 @@ def main():
     check(L_.pv_conv_pool_fwd(P(ids), P(tbl16), P(wpack), P(bias), P(pooled), P(argmax), N, L, V, 7, None, 0, thr, 0,
                               scale, 256, s), "fwd")
     gpool = torch.randn(N, 2 * FW, generator=g).to(dev) * 1e-3
-    M = N * 2 * FW * 4
+    M = N * cops.SLOTS_PER_SAMPLE
     keys = torch.empty(M, dtype=torch.int32, device=dev)
     vals = torch.empty(M, dtype=torch.int32, device=dev)
     rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)
@@ -78,7 +78,7 @@ def main():
     dw3, dw4, db = torch.zeros_like(w3), torch.zeros_like(w4), torch.zeros(2 * FW, device=dev)
 
     def emit():
-        check(L_.pv_conv_pool_bwd_emit2(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
+        check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
                                         scale, s), "emit")
 
     def sort():
