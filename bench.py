@@ -199,7 +199,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8_e4m3 MFMA (bf16 elsewhere)" if a.model == "chunked" else "bf16",
             "data": "synthetic (device-resident pre-featurized Zipf trigram-id pages; random-init weights)",
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,

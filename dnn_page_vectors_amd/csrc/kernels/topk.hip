@@ -15,16 +15,20 @@ namespace pv {
 namespace topk {
 
 constexpr int K = 16;
-constexpr int TP = 64;  // pages per LDS tile
+constexpr int TP = 64;  // pages per split granule (and per LDS tile up to DP = 256)
 constexpr int PADK = 8;
+
+// Wide vectors (BERT's 768-d CLS, DP > 256) stage 32-page tiles: 32 x 776 bf16 = 49.7 KB LDS.
+template <int KS>
+__device__ constexpr int tile_pages() { return KS <= 8 ? TP : 32; }
 
 template <int KS>
 __global__ __launch_bounds__(256) void topk_partial_kernel(const unsigned short* __restrict__ Q,
                                                            const unsigned short* __restrict__ Pg,
                                                            float* __restrict__ pv, int* __restrict__ pi, int B,
                                                            int N, int per_split, int nsplit) {
-  constexpr int DP = KS * 32, LDP = DP + PADK;
-  __shared__ __attribute__((aligned(16))) unsigned short pt[TP * LDP];
+  constexpr int DP = KS * 32, LDP = DP + PADK, T = tile_pages<KS>();
+  __shared__ __attribute__((aligned(16))) unsigned short pt[T * LDP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = blockIdx.x * 64 + wave * 16 + (lane & 15);
   const int p_begin = blockIdx.y * per_split, p_end = min(N, p_begin + per_split);
@@ -41,9 +45,9 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(const unsigned short*
     vals[i] = -INFINITY;
     idx[i] = -1;
   }
-  for (int p0 = p_begin; p0 < p_end; p0 += TP) {
+  for (int p0 = p_begin; p0 < p_end; p0 += T) {
     __syncthreads();
-    for (int x = threadIdx.x; x < TP * (DP / 8); x += 256) {
+    for (int x = threadIdx.x; x < T * (DP / 8); x += 256) {
       int r = x / (DP / 8), cc = (x % (DP / 8)) * 8;
       u32x4 v = (p0 + r < p_end) ? *reinterpret_cast<const u32x4*>(Pg + (size_t)(p0 + r) * DP + cc)
                                  : u32x4{0, 0, 0, 0};
@@ -51,7 +55,7 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(const unsigned short*
     }
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < TP / 16; ++c) {
+    for (int c = 0; c < T / 16; ++c) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -154,7 +158,7 @@ PV_API int pv_topk_splits(int B, int N) {
 PV_API int pv_topk_cos(const void* Q, const void* Pg, float* vals, int* idx, float* pv, int* pi, int B, int N, int DP,
                        int k, int nsplit, void* stream) {
   using namespace pv::topk;
-  if (k > K || k < 1 || DP % 32 || DP > 256 || nsplit < 1) return -1;
+  if (k > K || k < 1 || DP % 32 || DP > 768 || nsplit < 1) return -1;
   const int qb = (B + 63) / 64;
   const int per = ((N + nsplit - 1) / nsplit + TP - 1) / TP * TP;
   if ((N + per - 1) / per > nsplit) return -1;
@@ -171,6 +175,9 @@ PV_API int pv_topk_cos(const void* Q, const void* Pg, float* vals, int* idx, flo
     case 5: PV_TOPK(5); break;
     case 6: PV_TOPK(6); break;
     case 8: PV_TOPK(8); break;
+    case 12: PV_TOPK(12); break;
+    case 16: PV_TOPK(16); break;
+    case 24: PV_TOPK(24); break;
     default: return -1;
   }
 #undef PV_TOPK

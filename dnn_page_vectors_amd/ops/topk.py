@@ -27,15 +27,19 @@ def _topk_torch(qn, pn, k, block):
 
 
 def topk_cos(qn: torch.Tensor, pn: torch.Tensor, k: int = 10, block: int = 65536) -> Tuple[torch.Tensor, torch.Tensor]:
-    if use_hip(qn, pn) and hasattr(lib(), "pv_topk_cos") and k <= 16:
+    if use_hip(qn, pn) and hasattr(lib(), "pv_topk_cos") and k <= 16 and qn.shape[1] <= 768:
         return _topk_hip(qn, pn, k)
     return _topk_torch(qn, pn, k, block)
+
+
+_KS = (1, 2, 3, 4, 5, 6, 8, 12, 16, 24)
 
 
 def _topk_hip(qn, pn, k):
     B, D = qn.shape
     N = pn.shape[0]
-    DP = (D + 31) // 32 * 32
+    # zero-padded feature width: one of the kernel's compiled 32-multiples (topk.hip)
+    DP = 32 * next(ks for ks in _KS if 32 * ks >= D)
     qb = torch.zeros(B, DP, dtype=torch.bfloat16, device=qn.device)
     qb[:, :D] = qn
     pb = torch.zeros(N, DP, dtype=torch.bfloat16, device=qn.device)

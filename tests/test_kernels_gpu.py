@@ -280,7 +280,8 @@ def test_trigram_hash_device():
     assert got.tolist() == host
 
 
-@pytest.mark.parametrize("B,N,D,k", [(100, 5000, 150, 10), (7, 300, 128, 16), (64, 64, 64, 1)])
+@pytest.mark.parametrize("B,N,D,k", [(100, 5000, 150, 10), (7, 300, 128, 16), (64, 64, 64, 1),
+                                     (300, 3000, 768, 10), (50, 1000, 300, 5)])
 def test_topk_hip_exact(B, N, D, k):
     from dnn_page_vectors_amd.ops import topk as tops
 
@@ -507,3 +508,32 @@ def test_hipgraph_step_matches_eager(model):
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (le, lg)
     torch.testing.assert_close(pg, pe, rtol=1e-3, atol=1e-4)
+
+
+def test_hipgraph_bert_many_unfenced_replays():
+    """BERT (config 4) step in a hipGraph, 40 unfenced replays over pre-built batches (the
+    bench.py pattern): replays track the eager trajectory and never fault (the token
+    embedding's backward is an index_add_ scatter, not torch's sort + unique_by_key)."""
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    cfg = preset_config("bert_dp8").replace(bert_layers=2, batch_size=16, document_length=64, query_length=16,
+                                            bert_dropout=0.0)
+    data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=512), DEV, seed=5)
+    pool = [data.batch(cfg.batch_size) for _ in range(4)]
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device(DEV), graph=graph, graph_fence=False)
+        losses = [tr.train_step(*pool[i % 4])["loss"].clone() for i in range(40)]
+        torch.cuda.synchronize()
+        runs.append(([float(l) for l in losses], tr._graph is not None))
+    (le, _), (lg, captured) = runs
+    assert captured
+    assert all(l == l for l in lg)
+    for a, b in zip(le[:8], lg[:8]):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lg)
