@@ -58,6 +58,18 @@ _grid_cache = {}
 # sorted dTable entries per wave in the reduce (conv_bwd_reduce5_kernel); 0 = 64-entry reduce4
 REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
 
+# dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
+# (both halves are gather/latency-bound and leave CU slots idle when run back to back)
+DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "0") != "0"  # measured: no gain (9.30 vs 9.30 ms)
+_side = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _side:
+        _side[idx] = torch.cuda.Stream(device=idx)
+    return _side[idx]
+
 # Device seed offset for captured (hipGraph) training steps: when set, every conv kernel
 # adds *_SEED_DEV to its seed, so one captured graph draws fresh dropout masks per replay.
 _SEED_DEV: Optional[torch.Tensor] = None
@@ -109,8 +121,17 @@ class _ConvPoolFn(torch.autograd.Function):
         dw4 = torch.zeros_like(w4)
         db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
         L_ = lib()
+        # every buffer the side stream touches is allocated on the main stream above/before
+        # and the main stream joins the side stream before returning: no cross-stream reuse
+        side = _side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] else None
+        if side is not None:
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
+            s_dw = side.cuda_stream
+        else:
+            s_dw = s
         check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E, V,
-                                     seed, P(sp), row_offset, thr, tok, scale, s), "pv_conv_pool_bwd_dw")
+                                     seed, P(sp), row_offset, thr, tok, scale, s_dw), "pv_conv_pool_bwd_dw")
         dtable = None
         if ctx.needs_input_grad[1]:
             M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
@@ -138,6 +159,8 @@ class _ConvPoolFn(torch.autograd.Function):
             else:
                 check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
                                                   P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
+        if side is not None:
+            main.wait_stream(side)
         return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
 
 

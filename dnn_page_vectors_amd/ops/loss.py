@@ -8,8 +8,13 @@
   csrc/kernels/loss.hip).
 * ``cross_gpu_loss``: every query against the documents of ALL ranks.  The page
   vectors are all-gathered already in the kernels' bf16 padded layout (half the xGMI
-  bytes of fp32); in backward the reduce-scatter of dD (RCCL, async) runs while the
-  dQ kernel computes, and the positive-pair term is applied to the local slice after.
+  bytes of fp32), and the bf16 queries are gathered too (async, B*DP*2 bytes per rank).
+  The backward then needs no reduce-scatter: dQ = local queries x all pages, and dD of
+  the LOCAL pages = local pages x all W*B queries with the gathered per-query softmax
+  scales (B floats per rank, gathered while the dQ kernel runs).  At W = 8 that replaces
+  a reduce-scatter of an (M, DP) fp32 partial (~168 MB in, ~147 MB over xGMI per rank at
+  B = 4096, J = 3) by ~2.6 MB of query gather; the FLOPs are the same.  The positive-pair
+  term is applied to the local slice after.
 
 Both take L2-normalised vectors (``ops.dense.l2_normalize``).
 """
@@ -191,27 +196,38 @@ class _CrossGpuFn(torch.autograd.Function):
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
               "pv_ib_pos")
         loss = gamma + torch.log(sumexp) - spos
-        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp)
-        ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group)
+        # the backward scores the LOCAL pages against ALL ranks' queries (dD needs no
+        # cross-rank sum then): gather the bf16 queries now, in flight during the rest of
+        # the forward and the tower's own backward (B*DP*2 bytes per rank)
+        qall = torch.empty(B * W, DP, dtype=torch.bfloat16, device=qn.device)
+        ctx.qwork = dist.all_gather_into_tensor(qall, qb, group=group, async_op=True)
+        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp, qall)
+        ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
         return loss, torch.exp(-loss).detach()
 
     @staticmethod
     def backward(ctx, gl, _gp):
-        qb, db, dbl, pos_local, sumexp = ctx.saved_tensors
-        B, M, n, D, DP, gamma, clip, group = ctx.meta
+        qb, db, dbl, pos_local, sumexp, qall = ctx.saved_tensors
+        B, M, n, D, DP, gamma, clip, group, W = ctx.meta
         s = stream(qb.device)
         L_ = lib()
         g = gl.contiguous().float()
         scale = (g * gamma / sumexp).contiguous()
+        # every rank's per-query softmax scale (B floats each), gathered while dQ runs
+        scale_all = torch.empty(B * W, dtype=torch.float32, device=qb.device)
+        swork = dist.all_gather_into_tensor(scale_all, scale, group=group, async_op=True)
         dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
-        dd_full = torch.empty(M, DP, dtype=torch.float32, device=qb.device)
-        ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
-                         dtype=torch.float32, device=qb.device)
-        check(L_.pv_ib_bwd(P(db), P(qb), P(scale), P(dd_full), P(ws), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
         dd = torch.empty(n, DP, dtype=torch.float32, device=qb.device)
-        work = dist.reduce_scatter_tensor(dd, dd_full, op=dist.ReduceOp.SUM, group=group, async_op=True)
+        ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(n, B * W, DP), 1),
+                         dtype=torch.float32, device=qb.device)
         check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
-        work.wait()
+        ctx.qwork.wait()
+        ctx.qwork = None
+        swork.wait()
+        # dD of the local pages = sum over all W*B queries: no reduce-scatter of an (M, DP)
+        # fp32 partial (W x the bytes of dd) over xGMI
+        check(L_.pv_ib_bwd(P(dbl), P(qall), P(scale_all), P(dd), P(ws), n, B * W, DP, gamma, clip, 0, s),
+              "pv_ib_bwd(dD)")
         check(L_.pv_ib_pos(P(qb), P(dbl), P(pos_local), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s),
               "pv_ib_pos(bwd)")
         return dq[:, :D], dd[:, :D], None, None, None, None, None
