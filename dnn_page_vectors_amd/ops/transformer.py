@@ -170,6 +170,35 @@ def weight_bf16(w: torch.Tensor) -> torch.Tensor:
     return ent[2]
 
 
+def _wgrad_splits(T: int) -> int:
+    """Token-axis split count of the weight-gradient GEMM (a power of two dividing T)."""
+    sk = 1
+    while sk < 16 and T % (2 * sk) == 0 and T // (2 * sk) >= 2048:
+        sk *= 2
+    return sk
+
+
+def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW = dy^T x (bf16 operands, fp32 result) for T >> N, K.
+
+    A single GEMM has only (N/256)(K/256) output tiles (36 for 768 x 3072) for a 65536-long
+    reduction, so hipBLASLt runs it on a fraction of the 256 CUs (285-680 TF/s measured,
+    tools/gemm_micro.py).  Splitting the token axis into up to 16 batched fp32-output GEMMs
+    and summing the partials in fp32 fills the chip: 1.82 -> 1.03 ms per BERT layer at
+    T = 65536 (bmm out_dtype=fp32; same fp32 accumulation, different summation order).
+    """
+    T = dy2.shape[0]
+    sk = _wgrad_splits(T)
+    try:
+        if sk == 1:
+            return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        dy3 = dy2.view(sk, T // sk, dy2.shape[1])
+        x3 = x2.view(sk, T // sk, x2.shape[1])
+        return torch.bmm(dy3.transpose(1, 2), x3, out_dtype=torch.float32).sum(0)
+    except (TypeError, RuntimeError, NotImplementedError):  # no mm/bmm out_dtype (CPU)
+        return (dy2.t().float() @ x2.float())
+
+
 class _Linear16Fn(torch.autograd.Function):
     """y = x @ W^T (+ b) in bf16 on hipBLASLt over a cached bf16 W; fp32 weight/bias grads."""
 
@@ -191,10 +220,7 @@ class _Linear16Fn(torch.autograd.Function):
         x2, w16 = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16)
         dx = (dy2 @ w16).view(ctx.shape)
-        try:
-            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
-        except (TypeError, RuntimeError):
-            dw = (dy2.t() @ x2).float()
+        dw = wgrad_f32(dy2, x2)
         db = dy2.sum(0, dtype=torch.float32) if ctx.has_b else None
         return dx, dw, db, None
 

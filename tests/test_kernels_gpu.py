@@ -537,3 +537,17 @@ def test_hipgraph_bert_many_unfenced_replays():
     assert all(l == l for l in lg)
     for a, b in zip(le[:8], lg[:8]):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lg)
+
+
+@pytest.mark.parametrize("T", [65536, 8192, 1000])
+def test_wgrad_split_k_matches_fp32(T):
+    from dnn_page_vectors_amd.ops import transformer as tf
+
+    torch.manual_seed(7)
+    dy = torch.randn(T, 768, device=DEV).to(torch.bfloat16)
+    x = torch.randn(T, 384, device=DEV).to(torch.bfloat16)
+    got = tf.wgrad_f32(dy, x)
+    want = dy.double().t() @ x.double()
+    assert got.dtype == torch.float32 and got.shape == (768, 384)
+    err = (got.double() - want).abs().max() / want.abs().max()
+    assert err < 1e-5, float(err)
