@@ -140,12 +140,24 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
                                                           const int* ids, const unsigned short* table, float* dw3,
                                                           float* dw4, float* db, int N, int L, int E, int V, int nsplit,
                                                           unsigned seed, const unsigned* seed_ptr,
-                                                          unsigned row_offset, int thr, int token_mode, float scale) {
+                                                          unsigned row_offset, int thr, int token_mode, float scale,
+                                                          int xcd_map) {
   __shared__ float red[4 * 4 * EP];
   if (seed_ptr) seed += *seed_ptr;  // device seed offset (captured hipGraph steps)
-  const int f = blockIdx.x;
+  // XCD-aware work mapping: workgroups are dealt round-robin to the 8 XCDs (each with its
+  // own L2).  The natural (f = blockIdx.x, split = blockIdx.y) order puts filters f, f+1 of
+  // one sample range on different XCDs, so every L2 fetches the same gpool / argmax /
+  // pooled / id lines (rows of 2*FW floats hold all filters of a sample).  Remapped, the
+  // 2*FW filter blocks of a split run on ONE XCD and share those lines in its L2.
+  int f = blockIdx.x, split = blockIdx.y;
+  if (xcd_map && (nsplit & 7) == 0) {
+    const int b = blockIdx.x + gridDim.x * blockIdx.y;
+    const int logical = (b & 7) * (gridDim.x * (nsplit >> 3)) + (b >> 3);
+    f = logical % (int)gridDim.x;
+    split = logical / (int)gridDim.x;
+  }
   const int per = ((N + nsplit - 1) / nsplit + 255) / 256 * 256;
-  const int n0 = blockIdx.y * per, n1 = min(N, n0 + per);
+  const int n0 = split * per, n1 = min(N, n0 + per);
   if (f < FW)
     dw_filter<3>(gpool, pooled, argmax, ids, table, dw3, db, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
                  token_mode, scale);
@@ -470,9 +482,13 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
+  static const int xcd_map = [] {  // PAGEVEC_DW_XCD=0: natural block order (A/B switch)
+    const char* e = getenv("PAGEVEC_DW_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   hipLaunchKernelGGL(conv_bwd_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, (hipStream_t)stream, gpool, pooled,
                      argmax, ids, (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr,
-                     row_offset, thr, token_mode, scale);
+                     row_offset, thr, token_mode, scale, xcd_map);
   PV_LAUNCH_CHECK();
   return 0;
 }
