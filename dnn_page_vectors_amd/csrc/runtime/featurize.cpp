@@ -21,6 +21,7 @@
 #include <cwctype>
 #include <fcntl.h>
 #include <locale.h>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <sys/mman.h>
@@ -111,6 +112,29 @@ inline uint32_t fnv1a(const char* p, size_t n) {
 
 struct Vocab {
   std::unordered_map<std::string, int32_t> map;
+  // char mode: direct code-point -> id table for the BMP (rebuilt after vocabulary edits),
+  // so a character costs one array load instead of a std::string hash + compare
+  std::vector<int32_t> cp_ids;
+  int32_t cp_unk = 0;
+  bool cp_valid = false;
+  std::mutex mu;
+  void add(const char* tok, int32_t id) {
+    std::lock_guard<std::mutex> g(mu);
+    map[std::string(tok)] = id;
+    cp_valid = false;
+  }
+  void build_cp_table(int32_t unk) {
+    std::lock_guard<std::mutex> g(mu);
+    if (cp_valid && cp_unk == unk) return;
+    cp_ids.assign(0x10000, unk);
+    std::vector<uint32_t> cps;
+    for (const auto& kv : map) {
+      decode_utf8(kv.first.data(), kv.first.size(), cps);
+      if (cps.size() == 1 && cps[0] < 0x10000) cp_ids[cps[0]] = kv.second;
+    }
+    cp_unk = unk;
+    cp_valid = true;
+  }
 };
 
 struct Spec {
@@ -128,6 +152,7 @@ struct Scratch {
   std::string utf8;
   std::vector<uint32_t> off;  // byte offset of each code point (+ sentinel)
   std::string key;
+  size_t first = 0;           // index in cps of the first code point after the leading strip
 };
 
 inline int32_t token_id(const Spec& sp, const char* p, size_t n, Scratch& sc) {
@@ -145,6 +170,7 @@ void clean(const char* s, size_t n, Scratch& sc) {
   auto ws = [](uint32_t c) { return c == ' ' || c == '\n'; };
   while (b < e && ws(sc.cps[b])) ++b;
   while (e > b && ws(sc.cps[e - 1])) --e;
+  sc.first = b;
   sc.utf8.clear();
   sc.off.clear();
   for (size_t i = b; i < e; ++i) {
@@ -170,7 +196,13 @@ void featurize_one(const char* s, size_t n, const Spec& sp, int32_t* out, Scratc
   } else if (sp.mode == 1) {  // overlapping 3-grams of code points
     for (size_t i = 0; i + 3 <= ncp && t < sp.length; ++i)
       out[t++] = token_id(sp, u + sc.off[i], sc.off[i + 3] - sc.off[i], sc);
-  } else {  // char
+  } else if (sp.hash_size == 0) {  // char, exact vocabulary: BMP code points by table
+    const int32_t* tab = sp.vocab->cp_ids.data();
+    for (size_t i = 0; i < ncp && t < sp.length; ++i) {
+      const uint32_t c = lower_cp(sc.cps[sc.first + i]);
+      out[t++] = c < 0x10000 ? tab[c] : token_id(sp, u + sc.off[i], sc.off[i + 1] - sc.off[i], sc);
+    }
+  } else {  // char, hashed
     for (size_t i = 0; i < ncp && t < sp.length; ++i)
       out[t++] = token_id(sp, u + sc.off[i], sc.off[i + 1] - sc.off[i], sc);
   }
@@ -364,7 +396,7 @@ extern "C" {
 
 void* pv_vocab_new() { return new Vocab(); }
 void pv_vocab_free(void* v) { delete (Vocab*)v; }
-void pv_vocab_add(void* v, const char* tok, int32_t id) { ((Vocab*)v)->map[std::string(tok)] = id; }
+void pv_vocab_add(void* v, const char* tok, int32_t id) { ((Vocab*)v)->add(tok, id); }
 int64_t pv_vocab_size(void* v) { return (int64_t)((Vocab*)v)->map.size(); }
 
 // texts: n NUL-terminated UTF-8 strings. out: n x length int32.
@@ -373,6 +405,7 @@ int pv_featurize(const char** texts, int n, int mode, int length, void* vocab, i
   if (mode < 0 || mode > 2 || length <= 0) return -1;
   if (hash_size <= 1 && !vocab) return -2;
   Spec sp{mode, length, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
+  if (mode == 2 && sp.hash_size == 0) ((Vocab*)vocab)->build_cp_table(unk_id);
   parallel_for(n, nthreads, [&](int i, Scratch& sc) {
     featurize_one(texts[i], strlen(texts[i]), sp, out + (int64_t)i * length, sc);
   });

@@ -1,4 +1,4 @@
-"""Multi-process data parallelism on CPU (gloo, world_size 2) — the fake cluster of SURVEY §4.2.
+"""Multi-process data parallelism on CPU (gloo, world_size 2 / 4 / 8) — the fake cluster of SURVEY §4.2.
 
 * all_gather_autograd: summed gradients of every rank's loss w.r.t. its local page
   vectors equal the single-process gradient of the summed loss (backward = reduce-scatter).
@@ -42,8 +42,9 @@ def _gather_worker(rank, world, port, q):
     pdist.destroy()
 
 
-def test_all_gather_autograd_gloo():
-    world, port = 2, _port()
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_all_gather_autograd_gloo(world):
+    port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
@@ -51,7 +52,7 @@ def test_all_gather_autograd_gloo():
     res = dict(q.get(timeout=120) for _ in ps)
     [p.join(timeout=60) for p in ps]
     base = torch.arange(world * 3 * 5, dtype=torch.float32).view(world * 3, 5)
-    full = base * 1 + base * 2  # sum over ranks of d(sum(g*w_r))/dg
+    full = base * (world * (world + 1) // 2)  # sum over ranks r of d(sum(g*w_r))/dg, w_r = base*(r+1)
     for r in range(world):
         torch.testing.assert_close(torch.from_numpy(res[r]), full[r * 3:(r + 1) * 3])
 
@@ -92,13 +93,13 @@ def _dp_worker(rank, world, port, mode, q):
     pdist.destroy()
 
 
-@pytest.mark.parametrize("mode", ["explicit", "cross_gpu"])
-def test_data_parallel_matches_single_process(mode):
+@pytest.mark.parametrize("mode,world", [("explicit", 2), ("cross_gpu", 2), ("cross_gpu", 4)])
+def test_data_parallel_matches_single_process(mode, world):
     from dnn_page_vectors_amd.models.cdssm import CDSSM
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
-    world, port = 2, _port()
+    port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_dp_worker, args=(r, world, port, mode, q)) for r in range(world)]
@@ -111,7 +112,8 @@ def test_data_parallel_matches_single_process(mode):
     tr = Trainer(cfg, CDSSM(cfg, 150))
     for qa, da in _data(8):
         tr.train_step(qa, da)
-    torch.testing.assert_close(res[0], res[1], rtol=0, atol=0)
+    for r in range(1, world):
+        torch.testing.assert_close(res[0], res[r], rtol=0, atol=0)
     torch.testing.assert_close(res[0], tr.flat.data, rtol=1e-4, atol=3e-5)  # Adam amplifies summation-order noise
 
 
