@@ -33,6 +33,8 @@ MODEL_DESC = {
     "cdssm": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
     "mlp": "Two-tower MLP 512-512-128, 30k hashed tri-grams, Lq=45, Ld=2000, in-batch/cross-GPU negatives",
     "bert": "BERT-base dual encoder (12L/768H/12A, shared), Lq=32, Ld=256, cross-GPU negatives",
+    "cdssm_char": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), char level (reference default), ~100-symbol "
+                  "vocab, Lq=250, Ld=5000, J=3",
     "chunked": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, MLP 512-512-128 fp8 e4m3, mean-pool",
 }
 
@@ -43,7 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (queries)")
-    ap.add_argument("--loss", default="cross_gpu", choices=["cross_gpu", "explicit", "in_batch"])
+    ap.add_argument("--loss", default=None, choices=["cross_gpu", "explicit", "in_batch"],
+                    help="default: cross_gpu (cdssm headline); explicit J=3 for cdssm_char (reference head)")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"],
                     help="torch = eager PyTorch-ROCm implementation of the same model (baseline stand-in)")
     ap.add_argument("--recall", type=int, default=2048, help="held-out pairs for Recall@10 (0 = skip)")
@@ -59,8 +62,10 @@ def parse():
                     help="after the timed steps, keep training (untimed, fresh synthetic batches, eager) until "
                          "this many optimizer steps in total, then measure Recall@10 on held-out pairs; "
                          "-1 = auto (1000 for cdssm / mlp, 0 = none for bert / chunked)")
-    ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked"],
-                    help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5")
+    ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "cdssm_char"],
+                    help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5; "
+                         "cdssm_char = the reference's default run (char level, 250 / 5000 tokens), per-GPU "
+                         "batch --batch (default 1024 here)")
     return ap.parse_args()
 
 
@@ -111,17 +116,24 @@ def main():
     info = pdist.init_distributed()
     if a.backend == "torch":
         set_backend("torch")
-    preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "chunked": "longpage_fp8"}[a.model]
+    preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "chunked": "longpage_fp8",
+              "cdssm_char": "reference_char"}[a.model]
     cfg = preset_config(preset)
-    batch = a.batch if a.model == "cdssm" or a.batch != 4096 else cfg.batch_size
-    cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model == "cdssm" else cfg.loss_mode)
+    if a.loss is None:
+        a.loss = "explicit" if a.model == "cdssm_char" else "cross_gpu"
+    if a.model == "cdssm_char":  # reference run config (char, 250 / 5000) on the HIP fast path
+        cfg = cfg.replace(dtype="bf16", vocab_hash_size=100)
+        if a.batch == 4096:
+            a.batch = 1024
+    batch = a.batch if a.model in ("cdssm", "cdssm_char") or a.batch != 4096 else cfg.batch_size
+    cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode)
     a.batch = batch
     V = cfg.vocab_hash_size
     dev = info.device
     model = build_model(cfg, V)
     # the capture happens after 2 eager steps: only inside the untimed warmup
     if a.graph < 0:
-        a.graph = 0 if a.model == "cdssm" else 1
+        a.graph = 0 if a.model in ("cdssm", "cdssm_char") else 1
     if a.quality_steps < 0:
         a.quality_steps = 1000 if a.model in ("cdssm", "mlp") else 0
     # pre-built device-resident batches and nothing eager between replays: no per-replay fence
@@ -177,14 +189,19 @@ def main():
 
     pairs = a.batch * W * a.steps
     value = pairs / dt
-    if a.model == "cdssm":
-        per_pair = 3.0 * cdssm_flops_per_sample(cfg)
+    # forward model FLOPs per pair (the CDSSM backward is sparse — gradients reach only the
+    # argmax windows — so a dense "3 x forward" count would overstate the work done)
+    if a.model in ("cdssm", "cdssm_char"):
+        per_pair = cdssm_flops_per_sample(cfg)
+        train_mult = None
     elif a.model == "bert":
         from dnn_page_vectors_amd.models.bert_dual import bert_flops_per_token
-        per_pair = 3.0 * (cfg.query_length * bert_flops_per_token(cfg, cfg.query_length) +
-                          (1 + cfg.J) * cfg.document_length * bert_flops_per_token(cfg, cfg.document_length))
+        per_pair = (cfg.query_length * bert_flops_per_token(cfg, cfg.query_length) +
+                    (1 + cfg.J) * cfg.document_length * bert_flops_per_token(cfg, cfg.document_length))
+        train_mult = 3.0  # dense backward: 2 x forward
     else:
         per_pair = 0.0
+        train_mult = None
     flops = per_pair * a.batch * W * a.steps / dt
     if info.is_main:
         out = {
@@ -208,7 +225,8 @@ def main():
             "recall_after_steps": max(done, a.quality_steps),
             "final_loss": round(final_loss, 4),
             "loss_after_quality_steps": round(quality_loss, 4),
-            "dense_equiv_tflops": round(flops / 1e12, 1),
+            "fwd_model_tflops": round(flops / 1e12, 1),
+            "train_model_tflops": round(flops * train_mult / 1e12, 1) if train_mult else None,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
             "hip_graph": graph_used,
         }

@@ -23,7 +23,8 @@ def test_native_hip_library_loaded():
 
 
 @pytest.mark.parametrize("N,L,p,mode", [(8, 37, 0.0, "element"), (5, 130, 0.25, "element"), (3, 64, 0.25, "token"),
-                                        (6, 4, 0.0, "element"), (300, 45, 0.25, "element")])
+                                        (6, 4, 0.0, "element"), (300, 45, 0.25, "element"),
+                                        (12, 5000, 0.25, "element")])  # char-level page length
 def test_conv_pool_fwd_bwd(N, L, p, mode):
     torch.manual_seed(0)
     V, E, F = 97, 100, 150
