@@ -33,11 +33,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x);
   const long stride = (long)gridDim.x * blockDim.x;
   const long n4 = n / 4;
-  for (long i = i4; i < n4; i += stride) {
-    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
-    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+  auto upd = [&](f32x4& pp, const f32x4& gg, f32x4& mm, f32x4& vv) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gg[k] + wd * pp[k];
@@ -46,6 +42,31 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
       float den = torch_style ? (sqrtf(vv[k]) * bc2_sqrt_inv + eps) : (sqrtf(vv[k]) + eps);
       pp[k] -= lr_t * mm[k] / den;
     }
+  };
+  // two 16-byte groups per thread per trip: 8 independent 16-byte loads in flight per lane
+  // (the update is a pure 28 B/parameter stream; one group per trip left HBM at ~3 TB/s)
+  long i = i4;
+  for (; i + stride < n4; i += 2 * stride) {
+    const long j = i + stride;
+    f32x4 p0 = reinterpret_cast<f32x4*>(p)[i], p1 = reinterpret_cast<f32x4*>(p)[j];
+    f32x4 g0 = reinterpret_cast<const f32x4*>(g)[i], g1 = reinterpret_cast<const f32x4*>(g)[j];
+    f32x4 m0 = reinterpret_cast<f32x4*>(m)[i], m1 = reinterpret_cast<f32x4*>(m)[j];
+    f32x4 v0 = reinterpret_cast<f32x4*>(v)[i], v1 = reinterpret_cast<f32x4*>(v)[j];
+    upd(p0, g0, m0, v0);
+    upd(p1, g1, m1, v1);
+    reinterpret_cast<f32x4*>(p)[i] = p0;
+    reinterpret_cast<f32x4*>(m)[i] = m0;
+    reinterpret_cast<f32x4*>(v)[i] = v0;
+    reinterpret_cast<f32x4*>(p)[j] = p1;
+    reinterpret_cast<f32x4*>(m)[j] = m1;
+    reinterpret_cast<f32x4*>(v)[j] = v1;
+  }
+  for (; i < n4; i += stride) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+    upd(pp, gg, mm, vv);
     reinterpret_cast<f32x4*>(p)[i] = pp;
     reinterpret_cast<f32x4*>(m)[i] = mm;
     reinterpret_cast<f32x4*>(v)[i] = vv;
@@ -74,13 +95,34 @@ __global__ void cast_pad_bf16_kernel(const float* __restrict__ in, unsigned shor
   }
 }
 
-// sum of squares + non-finite flag over a flat buffer (block partials -> atomics)
+// sum of squares + non-finite flag over a flat buffer.  One workgroup per CU-pair at most
+// (<= 512 same-address atomics per call: 4096 of them serialised at one L2 channel cost
+// ~40 us), 16-byte loads with four in flight per lane.
+__device__ __forceinline__ void sq_acc(const f32x4& v, float& s, float& bad) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (!isfinite(v[k])) bad = 1.f;
+    else s += v[k] * v[k];
+  }
+}
+
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ out2) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long stride = (long)gridDim.x * blockDim.x;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
   float s = 0.f, bad = 0.f;
-  for (; i < n; i += stride) {
-    float v = x[i];
+  long i = t;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const f32x4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+    sq_acc(a, s, bad);
+    sq_acc(b, s, bad);
+    sq_acc(c, s, bad);
+    sq_acc(d, s, bad);
+  }
+  for (; i < n4; i += stride) sq_acc(x4[i], s, bad);
+  for (long j = n4 * 4 + t; j < n; j += stride) {
+    const float v = x[j];
     if (!isfinite(v)) bad = 1.f;
     else s += v * v;
   }
@@ -91,9 +133,9 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (lane == 0) { ws[w] = s; wb[w] = bad; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = ws[0] + ws[1] + ws[2] + ws[3];
+    float tot = ws[0] + ws[1] + ws[2] + ws[3];
     float b = fmaxf(fmaxf(wb[0], wb[1]), fmaxf(wb[2], wb[3]));
-    atomicAdd(&out2[0], t);
+    atomicAdd(&out2[0], tot);
     if (b != 0.f) atomicExch(&out2[1], 1.f);
   }
 }
@@ -154,7 +196,9 @@ PV_API int pv_cast_pad_bf16(const float* in, void* out, long rows, int cols, int
 }
 
 PV_API int pv_sumsq(const float* x, long n, float* out2, void* stream) {
-  hipLaunchKernelGGL(pv::optim::sumsq_kernel, dim3(grid_for(n, 8)), dim3(256), 0, (hipStream_t)stream, x, n, out2);
+  unsigned blocks = grid_for(n, 16);
+  if (blocks > 512) blocks = 512;
+  hipLaunchKernelGGL(pv::optim::sumsq_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, out2);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -552,3 +552,30 @@ def test_wgrad_split_k_matches_fp32(T):
     assert got.dtype == torch.float32 and got.shape == (768, 384)
     err = (got.double() - want).abs().max() / want.abs().max()
     assert err < 1e-5, float(err)
+
+
+@pytest.mark.parametrize("n", [3_000_003, 16_777_216])
+def test_adam_and_sumsq_large_flat(n):
+    """Large flat buffers: the unrolled (two 16-byte groups per trip) Adam path and the
+    vectorised sum-of-squares, including the scalar tails."""
+    from dnn_page_vectors_amd.ops._common import P, check, lib, stream
+
+    torch.manual_seed(1)
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.randn(n, device=DEV).abs() * 0.1
+    v = torch.randn(n, device=DEV).abs() * 0.01
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    check(lib().pv_adam(P(p), P(g), P(m), P(v), n, 5, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, stream()), "pv_adam")
+    ref.adam_keras_([pr], [g], [mr], [vr], 5, 1e-3, 0.9, 0.999, 1e-8)
+    torch.testing.assert_close(m, mr, rtol=3e-5, atol=1e-6)  # FMA contraction vs torch's op order
+    torch.testing.assert_close(v, vr, rtol=3e-5, atol=1e-6)
+    torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
+    out = torch.zeros(2, device=DEV)
+    check(lib().pv_sumsq(P(g), n, P(out), stream()), "pv_sumsq")
+    want = float((g.double() ** 2).sum())
+    assert abs(float(out[0]) - want) / want < 1e-4 and float(out[1]) == 0.0
+    g[n // 3] = float("inf")
+    out.zero_()
+    check(lib().pv_sumsq(P(g[1:]), n - 1, P(out), stream()), "pv_sumsq")  # misaligned start
+    assert float(out[1]) == 1.0
