@@ -135,6 +135,99 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const unsigned short
   }
 }
 
+// Dropout keep decisions of columns c..c+3 (c % 4 == 0) of a row, bit k = column c+k kept:
+// the same counter hash as the conv kernels and ops/reference.py::dropout_keep_mask
+// (thr % 16 == 0: nibble b of mix(h_row + g8*phi) decides column 8*g8+b; otherwise byte b of
+// mix(h_row + g4*phi) decides column 4*g4+b).  thr = round(256 p), scale = 256 / (256 - thr).
+__device__ __forceinline__ unsigned keep4(unsigned hrow, int c, int thr) {
+  unsigned bits = 0u;
+  if ((thr & 15) == 0) {
+    const unsigned h = dropout_group_hash(hrow, (unsigned)(c >> 3)) >> (4 * (c & 7));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bits |= (((h >> (4 * k)) & 0xFu) >= (unsigned)(thr >> 4) ? 1u : 0u) << k;
+  } else {
+    const unsigned h = dropout_group_hash(hrow, (unsigned)(c >> 2));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bits |= (((h >> (8 * k)) & 0xFFu) >= (unsigned)thr ? 1u : 0u) << k;
+  }
+  return bits;
+}
+
+// Wave-per-row fused  h = dropout(x) + r;  y = LayerNorm(h) * gamma + beta  for D = 256 * VPT.
+// Lane l owns columns (i*64 + l)*4 .. +3 of every row (coalesced 8-byte accesses), the two
+// row statistics are wave reductions (no LDS, no barriers), and the dropout mask is a
+// counter hash of (seed, row, column) regenerated in the backward — nothing is stored.
+// thr = 0: no dropout (the plain residual add + LayerNorm).
+template <int VPT>
+__global__ __launch_bounds__(256) void add_ln_drop_fwd_kernel(const unsigned short* __restrict__ x,
+                                                              const unsigned short* __restrict__ r,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta,
+                                                              unsigned short* __restrict__ y,
+                                                              unsigned short* __restrict__ h,
+                                                              float* __restrict__ mean_out,
+                                                              float* __restrict__ rstd_out, int M, float eps,
+                                                              int thr, float scale, unsigned seed,
+                                                              const unsigned* __restrict__ seed_ptr) {
+  constexpr int D = 256 * VPT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= M) return;
+  if (seed_ptr) seed += *seed_ptr;
+  const unsigned hrow = thr > 0 ? dropout_row_hash(seed, (unsigned)row) : 0u;
+  float v[VPT][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const size_t o = (size_t)row * D + c;
+    const uint2 a = *reinterpret_cast<const uint2*>(x + o);
+    v[i][0] = __uint_as_float(a.x << 16);
+    v[i][1] = __uint_as_float(a.x & 0xFFFF0000u);
+    v[i][2] = __uint_as_float(a.y << 16);
+    v[i][3] = __uint_as_float(a.y & 0xFFFF0000u);
+    if (thr > 0) {
+      const unsigned kb = keep4(hrow, c, thr);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[i][k] = ((kb >> k) & 1u) ? v[i][k] * scale : 0.f;
+    }
+    if (r) {
+      const uint2 b = *reinterpret_cast<const uint2*>(r + o);
+      v[i][0] += __uint_as_float(b.x << 16);
+      v[i][1] += __uint_as_float(b.x & 0xFFFF0000u);
+      v[i][2] += __uint_as_float(b.y << 16);
+      v[i][3] += __uint_as_float(b.y & 0xFFFF0000u);
+    }
+    // h is stored in bf16 and the backward reads it back: normalise the bf16-rounded sum
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[i][k] = bf16_to_f32(f32_to_bf16(v[i][k]));
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float mu = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q += (v[i][k] - mu) * (v[i][k] - mu);
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    const size_t o = (size_t)row * D + c;
+    const f32x4 g4 = *reinterpret_cast<const f32x4*>(gamma + c);
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(beta + c);
+    float out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = (v[i][k] - mu) * rstd * g4[k] + b4[k];
+    *reinterpret_cast<uint2*>(y + o) = uint2{pack_bf16x2(out[0], out[1]), pack_bf16x2(out[2], out[3])};
+    if (h) *reinterpret_cast<uint2*>(h + o) = uint2{pack_bf16x2(v[i][0], v[i][1]), pack_bf16x2(v[i][2], v[i][3])};
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rstd;
+  }
+}
+
 // Wave-per-row LayerNorm backward for D = 256 * VPT: each lane holds VPT 4-element
 // vectors of dy and x_hat in registers (one read of each), the two row means are wave
 // reductions (no barriers), and dgamma/dbeta accumulate in registers over the rows this
@@ -146,8 +239,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
                                                                  const float* __restrict__ mean,
                                                                  const float* __restrict__ rstd,
                                                                  unsigned short* __restrict__ dx,
-                                                                 float* __restrict__ part, int M) {
+                                                                 float* __restrict__ part, int M,
+                                                                 unsigned short* __restrict__ dxm, int thr,
+                                                                 float scale, unsigned seed,
+                                                                 const unsigned* __restrict__ seed_ptr) {
   constexpr int D = 256 * VPT;
+  if (dxm && seed_ptr) seed += *seed_ptr;
   __shared__ float red[2][4][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float gm[VPT][4], ga[VPT][4], gb[VPT][4];
@@ -191,6 +288,13 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
       for (int k = 0; k < 4; ++k) o4[k] = rs * (g[i][k] * gm[i][k] - a - xh[i][k] * b);
       *reinterpret_cast<uint2*>(dx + (size_t)row * D + (i * 64 + lane) * 4) =
           uint2{pack_bf16x2(o4[0], o4[1]), pack_bf16x2(o4[2], o4[3])};
+      if (dxm) {  // gradient of the dropout branch: dh * keep * scale (mask regenerated)
+        const unsigned kb = keep4(dropout_row_hash(seed, (unsigned)row), (i * 64 + lane) * 4, thr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o4[k] = ((kb >> k) & 1u) ? o4[k] * scale : 0.f;
+        *reinterpret_cast<uint2*>(dxm + (size_t)row * D + (i * 64 + lane) * 4) =
+            uint2{pack_bf16x2(o4[0], o4[1]), pack_bf16x2(o4[2], o4[3])};
+      }
     }
   }
 #pragma unroll
@@ -497,15 +601,16 @@ PV_API long pv_layernorm_bwd_ws(int M, int D) {
 }
 
 // dgamma/dbeta are overwritten on the wave-per-row path (D in {256,512,768,1024}, ws given)
-PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma, const float* mean, const float* rstd,
-                            void* dx, float* dgamma, float* dbeta, float* ws, int M, int D, void* stream) {
+static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gamma, const float* mean,
+                              const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int D,
+                              void* dxm, int thr, float scale, unsigned seed, const unsigned* seed_ptr, void* stream) {
   const int blocks = ln_blocks(M);
   hipStream_t st = (hipStream_t)stream;
 #define PV_LN_ROWS(VPT)                                                                                          \
   {                                                                                                              \
     hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, st,                  \
                        (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,                \
-                       (unsigned short*)dx, ws, M);                                                              \
+                       (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr);            \
     PV_LAUNCH_CHECK();                                                                                           \
     float* ws2 = ws + (size_t)blocks * 2 * D;                                                                    \
     for (int half = 0; half < 2; ++half) {                                                                       \
@@ -535,10 +640,49 @@ PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma
     default: break;
   }
 #undef PV_LN_ROWS
+  if (dxm) return -1;  // the dropout-fused backward exists on the wave-per-row path only
   const int rpb = 32;
   hipLaunchKernelGGL(pv::tfm::layernorm_bwd_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 2 * D * sizeof(float),
                      (hipStream_t)stream, (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,
                      (unsigned short*)dx, dgamma, dbeta, M, D, rpb);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma, const float* mean, const float* rstd,
+                            void* dx, float* dgamma, float* dbeta, float* ws, int M, int D, void* stream) {
+  return layernorm_bwd_impl(dy, hsum, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, D, nullptr, 0, 1.f, 0u, nullptr,
+                            stream);
+}
+
+// dx = dL/dh (the residual input's gradient), dxm = dx * keep * scale (the dropout branch's),
+// keep regenerated from (seed + *seed_ptr, row, column) exactly as pv_add_ln_drop_fwd drew it.
+PV_API int pv_layernorm_bwd_drop(const void* dy, const void* hsum, const float* gamma, const float* mean,
+                                 const float* rstd, void* dx, void* dxm, float* dgamma, float* dbeta, float* ws, int M,
+                                 int D, int thr, float scale, unsigned seed, const unsigned* seed_ptr, void* stream) {
+  if (!ws || !ln_rows_ok(D)) return -1;
+  return layernorm_bwd_impl(dy, hsum, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, D, dxm, thr, scale, seed,
+                            seed_ptr, stream);
+}
+
+// Wave-per-row residual add (+ optional dropout on x) + LayerNorm, D in {256, 512, 768, 1024}.
+PV_API int pv_add_ln_drop_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, void* h,
+                              float* mean, float* rstd, int M, int D, float eps, int thr, float scale, unsigned seed,
+                              const unsigned* seed_ptr, void* stream) {
+  if (!ln_rows_ok(D) || thr < 0 || thr > 255) return -1;
+  const dim3 grid((M + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define PV_ADDLN(VPT)                                                                                          \
+  hipLaunchKernelGGL(pv::tfm::add_ln_drop_fwd_kernel<VPT>, grid, dim3(256), 0, st, (const unsigned short*)x,  \
+                     (const unsigned short*)r, gamma, beta, (unsigned short*)y, (unsigned short*)h, mean, rstd, \
+                     M, eps, thr, scale, seed, seed_ptr)
+  switch (D) {
+    case 256: PV_ADDLN(1); break;
+    case 512: PV_ADDLN(2); break;
+    case 768: PV_ADDLN(3); break;
+    default: PV_ADDLN(4); break;
+  }
+#undef PV_ADDLN
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -43,19 +43,18 @@ class BertLayer(nn.Module):
         self.ln2_g = nn.Parameter(torch.ones(H))
         self.ln2_b = nn.Parameter(torch.zeros(H))
 
-    def forward(self, x: torch.Tensor, mask: torch.Tensor, dt: torch.dtype, p_drop: float, training: bool):
+    def forward(self, x: torch.Tensor, mask: torch.Tensor, dt: torch.dtype, p_drop: float, training: bool,
+                seed: int = 0):
         N, L, H = x.shape
+        p = p_drop if training else 0.0
         qkv = tops.linear(x, self.wqkv, self.bqkv)            # (N, L, 3H) packed [slot][head][d]
         a = tops.fused_attention(qkv, mask, self.heads)       # (N, L, H), no permute copies
         o = tops.linear(a, self.wo, self.bo)
-        if training and p_drop > 0:
-            o = F.dropout(o, p_drop, True)
-        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b)
+        # hidden dropout fused into the residual add + LayerNorm (counter-hash masks)
+        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed)
         f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
         f2 = tops.linear(f, self.w2, self.b2)
-        if training and p_drop > 0:
-            f2 = F.dropout(f2, p_drop, True)
-        return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b)
+        return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF)
 
 
 class _RowGather(torch.autograd.Function):
@@ -98,7 +97,7 @@ class BertEncoder(nn.Module):
                 if p.dim() == 2:
                     p.normal_(0.0, 0.02, generator=gen)
 
-    def forward(self, ids: torch.Tensor, p_drop: float, training: bool) -> torch.Tensor:
+    def forward(self, ids: torch.Tensor, p_drop: float, training: bool, seed: int = 0) -> torch.Tensor:
         dt = torch.bfloat16 if ids.is_cuda else torch.float32
         ids = ids.long()
         N, L = ids.shape
@@ -108,8 +107,8 @@ class BertEncoder(nn.Module):
         x = tops.add_layernorm(x, None, self.ln_g, self.ln_b)
         if training and p_drop > 0:
             x = F.dropout(x, p_drop, True)
-        for layer in self.layers:
-            x = layer(x, mask, dt, p_drop, training)
+        for li, layer in enumerate(self.layers):
+            x = layer(x, mask, dt, p_drop, training, seed=(int(seed) * 1000003 + li * 7919) & 0xFFFFFFFF)
         cls = x[:, 0].float()
         return F.linear(cls, self.proj) if self.proj is not None else cls
 
@@ -132,7 +131,7 @@ class BertDualEncoder(TwoTowerModel):
 
     def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:
         enc = self.query_tower if tower == "query" else self.doc_towers[0]
-        return enc(ids, self.p_drop, training)
+        return enc(ids, self.p_drop, training, seed=seed)
 
 
 def bert_flops_per_token(cfg, L: int) -> float:

@@ -13,12 +13,26 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
 
+def _seed_ptr():
+    """Device seed offset of a captured hipGraph step (ops.conv_pool.set_seed_tensor): the
+    fused dropout kernels add it so each replay draws fresh masks."""
+    from . import conv_pool
+
+    return conv_pool._SEED_DEV
+
+
 class _AddLNFn(torch.autograd.Function):
+    """y = LayerNorm(dropout(x) + r).  D in {256, 512, 768, 1024}: one wave per row
+    (``pv_add_ln_drop_fwd``); the dropout mask is a counter hash of (seed, row, column)
+    (ops/reference.py::dropout_keep_mask, p quantised to 1/256), regenerated in the backward,
+    which writes both the residual gradient and the masked branch gradient in one pass."""
+
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps):
+    def forward(ctx, x, r, gamma, beta, eps, p, seed):
         x = x.to(torch.bfloat16).contiguous()
         r = r.to(torch.bfloat16).contiguous() if r is not None else None
         D = x.shape[-1]
@@ -27,15 +41,27 @@ class _AddLNFn(torch.autograd.Function):
         h = torch.empty_like(x)
         mean = torch.empty(M, dtype=torch.float32, device=x.device)
         rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-        check(lib().pv_add_layernorm_fwd(P(x), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D, eps,
-                                         stream(x.device)), "pv_add_layernorm_fwd")
-        ctx.save_for_backward(h, gamma, mean, rstd)
+        thr = ref.dropout_threshold(p) if p > 0 else 0
+        scale = 256.0 / (256.0 - thr)
+        sp = _seed_ptr() if thr > 0 else None
+        seed = int(seed) & 0xFFFFFFFF
+        if D in _LN_ROWS:
+            check(lib().pv_add_ln_drop_fwd(P(x), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D, eps,
+                                           thr, scale, seed, P(sp), stream(x.device)), "pv_add_ln_drop_fwd")
+        else:
+            if thr > 0:
+                raise ValueError(f"fused dropout + LayerNorm needs D in {_LN_ROWS}")
+            check(lib().pv_add_layernorm_fwd(P(x), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D, eps,
+                                             stream(x.device)), "pv_add_layernorm_fwd")
+        ctx.save_for_backward(h, gamma, mean, rstd, sp)
         ctx.has_r = r is not None
+        ctx.drop = (thr, scale, seed)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        h, gamma, mean, rstd = ctx.saved_tensors
+        h, gamma, mean, rstd, sp = ctx.saved_tensors
+        thr, scale, seed = ctx.drop
         D = h.shape[-1]
         M = h.numel() // D
         dy = dy.to(torch.bfloat16).contiguous()
@@ -46,15 +72,32 @@ class _AddLNFn(torch.autograd.Function):
         dg = alloc(gamma.shape, dtype=torch.float32, device=h.device)
         db = alloc(gamma.shape, dtype=torch.float32, device=h.device)
         ws = torch.empty(nws, dtype=torch.float32, device=h.device) if nws > 0 else None
-        check(L_.pv_layernorm_bwd(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dg), P(db), P(ws), M, D,
-                                  stream(h.device)), "pv_layernorm_bwd")
-        return dx, (dx if ctx.has_r else None), dg, db, None
+        if thr > 0:
+            dxm = torch.empty_like(h)
+            check(L_.pv_layernorm_bwd_drop(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dxm), P(dg), P(db),
+                                           P(ws), M, D, thr, scale, seed, P(sp), stream(h.device)),
+                  "pv_layernorm_bwd_drop")
+        else:
+            dxm = dx
+            check(L_.pv_layernorm_bwd(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dg), P(db), P(ws), M, D,
+                                      stream(h.device)), "pv_layernorm_bwd")
+        return dxm, (dx if ctx.has_r else None), dg, db, None, None, None
+
+
+_LN_ROWS = (256, 512, 768, 1024)
 
 
 def add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor,
-                  eps: float = 1e-12) -> torch.Tensor:
+                  eps: float = 1e-12, p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """LayerNorm(dropout_p(x) + r) (dropout only when p > 0: pass p = 0 outside training)."""
     if use_hip(x):
-        return _AddLNFn.apply(x, r, gamma, beta, eps)
+        if p > 0 and x.shape[-1] not in _LN_ROWS:
+            x = F.dropout(x, p, True)
+            p = 0.0
+        return _AddLNFn.apply(x, r, gamma, beta, eps, float(p), int(seed))
+    if p > 0:
+        keep = ref.dropout_keep_mask(seed, x.numel() // x.shape[-1], x.shape[-1], p, device=x.device)
+        x = x * keep.view(x.shape).to(x.dtype) * (256.0 / (256.0 - ref.dropout_threshold(p)))
     h = x if r is None else x + r
     return F.layer_norm(h.float(), (h.shape[-1],), gamma, beta, eps).to(x.dtype)
 

@@ -579,3 +579,39 @@ def test_adam_and_sumsq_large_flat(n):
     out.zero_()
     check(lib().pv_sumsq(P(g[1:]), n - 1, P(out), stream()), "pv_sumsq")  # misaligned start
     assert float(out[1]) == 1.0
+
+
+@pytest.mark.parametrize("D,p", [(768, 0.1), (768, 0.25), (256, 0.0), (1024, 0.5)])
+def test_add_layernorm_fused_dropout(D, p):
+    """LayerNorm(dropout(x) + r) (wave-per-row fused kernel, counter-hash mask) vs the fp32
+    reference with the same mask (ops/reference.py::dropout_keep_mask); gradients of x
+    (masked) and r (unmasked) from the one-pass backward."""
+    from dnn_page_vectors_amd.ops import transformer as tf
+
+    torch.manual_seed(3)
+    M = 300
+    x = bf(torch.randn(M, D, device=DEV)).requires_grad_(True)
+    r = bf(torch.randn(M, D, device=DEV)).requires_grad_(True)
+    g = (1.0 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    seed = 987654
+    y = tf.add_layernorm(x.to(torch.bfloat16), r.to(torch.bfloat16), g, b, 1e-12, p=p, seed=seed)
+    x2, r2 = x.detach().clone().requires_grad_(True), r.detach().clone().requires_grad_(True)
+    g2, b2 = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    if p > 0:
+        keep = ref.dropout_keep_mask(seed, M, D, p, device=DEV).float()
+        hh = x2 * keep * (256.0 / (256.0 - ref.dropout_threshold(p))) + r2
+    else:
+        hh = x2 + r2
+    yr = torch.nn.functional.layer_norm(hh, (D,), g2, b2, 1e-12)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    w = torch.randn(M, D, device=DEV)
+    (y.float() * w).sum().backward()
+    (yr * w).sum().backward()
+    for a_, b_ in ((x.grad, x2.grad), (r.grad, r2.grad)):
+        err = (a_.float() - b_).abs().max() / b_.abs().max()
+        assert err < 3e-2, float(err)
+    torch.testing.assert_close(g.grad, g2.grad, rtol=3e-2, atol=0.5)
+    torch.testing.assert_close(b.grad, b2.grad, rtol=3e-2, atol=0.5)
+    if p > 0:  # dropped positions get exactly zero gradient through the branch
+        assert float(x.grad[keep == 0].abs().max()) == 0.0
