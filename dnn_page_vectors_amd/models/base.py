@@ -83,9 +83,10 @@ class TwoTowerModel(nn.Module):
         self.eval()
         outs = []
         try:
-            for i in range(0, ids.shape[0], batch_size):
-                v = self.tower_forward(tower, ids[i:i + batch_size], False, 0)
-                outs.append(dops.l2_normalize(v) if normalize else v)
+            with torch.no_grad():  # no autograd graph: nothing saved for a backward
+                for i in range(0, ids.shape[0], batch_size):
+                    v = self.tower_forward(tower, ids[i:i + batch_size], False, 0)
+                    outs.append(dops.l2_normalize(v) if normalize else v)
         finally:
             self.train(was)
         return torch.cat(outs, 0) if outs else torch.empty(0, self.out_dim, device=ids.device)
