@@ -150,11 +150,12 @@ def hip(required: bool = True) -> Optional[ctypes.CDLL]:
             try:
                 import torch  # noqa: F401  (single HIP runtime, see module docstring)
 
-                if _autobuild() and not os.path.exists(_build.HIP_LIB):
+                path = os.environ.get("PAGEVEC_HIP_LIB") or _build.HIP_LIB  # variant A/B builds (tools/)
+                if path == _build.HIP_LIB and _autobuild() and not os.path.exists(path):
                     _build.build_hip()
-                if not os.path.exists(_build.HIP_LIB):
-                    raise NativeUnavailable(f"{_build.HIP_LIB} missing")
-                lib = ctypes.CDLL(_build.HIP_LIB)
+                if not os.path.exists(path):
+                    raise NativeUnavailable(f"{path} missing")
+                lib = ctypes.CDLL(path)
                 from .ops import _sigs
 
                 _sigs.declare(lib)

@@ -43,7 +43,11 @@ constexpr int S3 = 10;             // K-steps of 32 for k=3 (K = 312 -> 320)
 constexpr int S4 = 13;             // K-steps of 32 for k=4 (K = 416)
 constexpr int NT = 10;             // 16-column tiles per width (150 -> 160 filters)
 constexpr int FW = 150;            // real filters per width
-constexpr int R = 112;             // window rows per chunk (7 blocks; 3 staged pieces per thread)
+#ifndef PV_CONV_R
+#define PV_CONV_R 112                // tools/conv_variant_build.py builds other chunk sizes for A/B runs
+#endif
+constexpr int R = PV_CONV_R;       // window rows per chunk (7 blocks; 3 staged pieces per thread)
+static_assert(R % 16 == 0, "chunk = whole 16-window blocks");
 constexpr int CROWS = R + 3;       // LDS rows per chunk
 constexpr int NTHREADS = 512;
 constexpr int PPT = (CROWS * PIECES + NTHREADS - 1) / NTHREADS;  // pieces per thread (4)
