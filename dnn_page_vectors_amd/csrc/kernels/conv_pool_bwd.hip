@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool,
       const int v = ok ? ids[(size_t)n * L + t] : V;
       PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
       keys[s0 + j] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;
-      vals[s0 + j] = s0 + j;
+      if (vals) vals[s0 + j] = s0 + j;  // null: the sort generates the positions itself
     }
   }
 }

@@ -22,6 +22,8 @@ SIGS = {
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",
     "pv_sort_pairs_u32": "plpppp" "li" "p",
+    "pv_sort_iota_temp_bytes": "li",
+    "pv_sort_iota_u32": "plppp" "li" "p",
     # dense.hip
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
@@ -67,7 +69,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

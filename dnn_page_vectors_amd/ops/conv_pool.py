@@ -137,17 +137,16 @@ class _ConvPoolFn(torch.autograd.Function):
             M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
             u32 = torch.int32
             keys = torch.empty(M, dtype=u32, device=dev)
-            vals = torch.empty(M, dtype=u32, device=dev)
             rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
-            check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(vals), P(rec), N, L, V,
+            # entry i's value is its slot i: no value array, the sort reads a counting iterator
+            check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L, V,
                                             scale, s), "pv_conv_pool_bwd_emit3")
             end_bit = max(1, int(V).bit_length())
             skeys = torch.empty_like(keys)
-            svals = torch.empty_like(vals)
-            tb = int(L_.pv_sort_pairs_temp_bytes(M, end_bit))
+            svals = torch.empty_like(keys)
+            tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
             temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-            check(L_.pv_sort_pairs_u32(P(temp), tb, P(keys), P(skeys), P(vals), P(svals), M, end_bit, s),
-                  "pv_sort_pairs_u32")
+            check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
             # bf16 weight rows [2*FW][4][EP] (the operands the forward MFMAs used)
             wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)

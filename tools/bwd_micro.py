@@ -84,6 +84,17 @@ def main():
     def sort():
         check(L_.pv_sort_pairs_u32(P(temp), tb, P(keys), P(skeys), P(vals), P(svals), M, end_bit, s), "sort")
 
+    tbi = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
+    tempi = torch.empty(max(tbi, 1), dtype=torch.uint8, device=dev)
+    svals2 = torch.empty_like(vals)
+
+    def emit_novals():
+        check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L, V,
+                                        scale, s), "emit")
+
+    def sort_iota():
+        check(L_.pv_sort_iota_u32(P(tempi), tbi, P(keys), P(skeys), P(svals2), M, end_bit, s), "sort_iota")
+
     def dw():
         check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E,
                                      V, 7, None, 0, thr, 0, scale, s), "dw")
@@ -98,6 +109,9 @@ def main():
 
     emit()
     sort()
+    sort_iota()
+    torch.cuda.synchronize()
+    print(json.dumps({"sort_iota_vals_equal": bool(torch.equal(svals, svals2))}), flush=True)
     epws = [int(x) for x in a.epw.split(",")]
     ref = torch.zeros(V, E, device=dev)
     reduce(0, ref)
@@ -108,11 +122,13 @@ def main():
         reduce(epw, out)
         err = float((out - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         print(json.dumps({"epw": epw, "rel_err_vs_reduce4": err}), flush=True)
-    res = {k: [] for k in ["emit", "sort", "dw"] + [f"reduce_epw{e}" for e in epws]}
+    res = {k: [] for k in ["emit", "emit_novals", "sort", "sort_iota", "dw"] + [f"reduce_epw{e}" for e in epws]}
     scratch = torch.zeros(V, E, device=dev)
     for _ in range(a.rounds):
         res["emit"].append(ev_time(emit, a.iters))
         res["sort"].append(ev_time(sort, a.iters))
+        res["emit_novals"].append(ev_time(emit_novals, a.iters))
+        res["sort_iota"].append(ev_time(sort_iota, a.iters))
         res["dw"].append(ev_time(dw, a.iters))
         for epw in epws:
             res[f"reduce_epw{epw}"].append(ev_time(lambda: reduce(epw, scratch), a.iters))

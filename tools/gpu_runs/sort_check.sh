@@ -1,0 +1,10 @@
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "conv or hipgraph or cdssm" > gpurun_out/pytest_sort.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_sort.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python tools/bwd_micro.py --epw 512 --rounds 3 > gpurun_out/bwd_micro_iota.log 2>&1
+rc=$?; echo "micro rc=$rc"; tail -2 gpurun_out/bwd_micro_iota.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 30 --quality-steps 0 --eager-compare 0 > gpurun_out/bench_iota.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_iota.log | cut -c1-250
