@@ -91,3 +91,23 @@ def test_html_normalizer():
     s = T.normalize_html_line("<b>Hello</b>   World&amp;Co...  Mütze!")
     assert "<b>" not in s and "  " not in s
     assert " . " in s and "mütze" in s
+
+
+@settings(max_examples=100, deadline=None)
+@given(st.lists(st.text(alphabet=st.sampled_from(list("abcXYZ019 _.#$€äöüßÄÖÜé\n\U0001F600\U00010400")),
+                        min_size=0, max_size=40), min_size=1, max_size=5),
+       st.integers(min_value=1, max_value=30))
+def test_native_char_vocab_fuzz(texts, L):
+    """char mode with an exact vocabulary: the native code-point table (BMP) and the string
+    fallback (non-BMP code points, incl. a Deseret letter that lower-cases to another
+    non-BMP code point) agree with the Python rules; ids of characters missing from the
+    vocabulary are UNK; vocabulary edits after first use invalidate the table."""
+    toks = [T.split_features(t, "char") for t in texts[:2]]  # later texts: OOV chars possible
+    vocab = T.Vocab(T.build_vocab_counts(toks))
+    fz = Featurizer("char", vocab=vocab, nthreads=2)
+    got = fz(texts, L)
+    want = np.array(T.featurize_py(texts, "char", L, vocab=vocab), dtype=np.int32)
+    np.testing.assert_array_equal(got, want)
+    fz._lib.pv_vocab_add(fz.handle(), "ü".encode(), 77)  # edit after the table was built
+    got2 = fz(["über"], 4)
+    assert got2[0, 0] == 77
