@@ -168,7 +168,8 @@ __global__ __launch_bounds__(256) void add_ln_drop_fwd_kernel(const unsigned sho
                                                               float* __restrict__ mean_out,
                                                               float* __restrict__ rstd_out, int M, float eps,
                                                               int thr, float scale, unsigned seed,
-                                                              const unsigned* __restrict__ seed_ptr) {
+                                                              const unsigned* __restrict__ seed_ptr,
+                                                              const float* __restrict__ xb) {
   constexpr int D = 256 * VPT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + wave;
@@ -186,6 +187,11 @@ __global__ __launch_bounds__(256) void add_ln_drop_fwd_kernel(const unsigned sho
     v[i][1] = __uint_as_float(a.x & 0xFFFF0000u);
     v[i][2] = __uint_as_float(a.y << 16);
     v[i][3] = __uint_as_float(a.y & 0xFFFF0000u);
+    if (xb) {  // the branch's linear-layer bias (its GEMM runs without one)
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(xb + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[i][k] += b4[k];
+    }
     if (thr > 0) {
       const unsigned kb = keep4(hrow, c, thr);
 #pragma unroll
@@ -242,12 +248,13 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
                                                                  float* __restrict__ part, int M,
                                                                  unsigned short* __restrict__ dxm, int thr,
                                                                  float scale, unsigned seed,
-                                                                 const unsigned* __restrict__ seed_ptr) {
+                                                                 const unsigned* __restrict__ seed_ptr, int nparts) {
   constexpr int D = 256 * VPT;
-  if (dxm && seed_ptr) seed += *seed_ptr;
-  __shared__ float red[2][4][D];
+  if (thr > 0 && seed_ptr) seed += *seed_ptr;
+  __shared__ float red[3][4][D];
+  const bool want_db = nparts == 3;  // column sums of the branch gradient (its bias gradient)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float gm[VPT][4], ga[VPT][4], gb[VPT][4];
+  float gm[VPT][4], ga[VPT][4], gb[VPT][4], gc[VPT][4];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const f32x4 g4 = *reinterpret_cast<const f32x4*>(gamma + (i * 64 + lane) * 4);
@@ -256,6 +263,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
       gm[i][k] = g4[k];
       ga[i][k] = 0.f;
       gb[i][k] = 0.f;
+      gc[i][k] = 0.f;
     }
   }
   for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
@@ -288,12 +296,17 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
       for (int k = 0; k < 4; ++k) o4[k] = rs * (g[i][k] * gm[i][k] - a - xh[i][k] * b);
       *reinterpret_cast<uint2*>(dx + (size_t)row * D + (i * 64 + lane) * 4) =
           uint2{pack_bf16x2(o4[0], o4[1]), pack_bf16x2(o4[2], o4[3])};
-      if (dxm) {  // gradient of the dropout branch: dh * keep * scale (mask regenerated)
+      if (thr > 0) {  // gradient of the dropout branch: dh * keep * scale (mask regenerated)
         const unsigned kb = keep4(dropout_row_hash(seed, (unsigned)row), (i * 64 + lane) * 4, thr);
 #pragma unroll
         for (int k = 0; k < 4; ++k) o4[k] = ((kb >> k) & 1u) ? o4[k] * scale : 0.f;
+      }
+      if (dxm)
         *reinterpret_cast<uint2*>(dxm + (size_t)row * D + (i * 64 + lane) * 4) =
             uint2{pack_bf16x2(o4[0], o4[1]), pack_bf16x2(o4[2], o4[3])};
+      if (want_db) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gc[i][k] += o4[k];
       }
     }
   }
@@ -303,13 +316,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
     for (int k = 0; k < 4; ++k) {
       red[0][wave][(i * 64 + lane) * 4 + k] = ga[i][k];
       red[1][wave][(i * 64 + lane) * 4 + k] = gb[i][k];
+      red[2][wave][(i * 64 + lane) * 4 + k] = gc[i][k];
     }
   __syncthreads();
-  // per-block partials part[block][0:D] = dgamma, [D:2D] = dbeta (summed by colsum_*)
-  float* pb = part + (size_t)blockIdx.x * 2 * D;
+  // per-block partials part[block][0:D] = dgamma, [D:2D] = dbeta, [2D:3D] = dbias (colsum_*)
+  float* pb = part + (size_t)blockIdx.x * nparts * D;
   for (int c = threadIdx.x; c < D; c += 256) {
     pb[c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
     pb[D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    if (want_db) pb[2 * D + c] = red[2][0][c] + red[2][1][c] + red[2][2][c] + red[2][3][c];
   }
 }
 
@@ -597,28 +612,31 @@ static bool ln_rows_ok(int D) { return D == 256 || D == 512 || D == 768 || D == 
 // floats of workspace pv_layernorm_bwd needs (0: the generic kernel accumulates into
 // zeroed dgamma/dbeta with atomics)
 PV_API long pv_layernorm_bwd_ws(int M, int D) {
-  return ln_rows_ok(D) ? (long)ln_blocks(M) * 2 * D + 2L * pv::tfm::kColSplits * D : 0;
+  return ln_rows_ok(D) ? (long)ln_blocks(M) * 3 * D + 3L * pv::tfm::kColSplits * D : 0;  // room for dbias
 }
 
 // dgamma/dbeta are overwritten on the wave-per-row path (D in {256,512,768,1024}, ws given)
 static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gamma, const float* mean,
                               const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int D,
-                              void* dxm, int thr, float scale, unsigned seed, const unsigned* seed_ptr, void* stream) {
+                              void* dxm, int thr, float scale, unsigned seed, const unsigned* seed_ptr, float* dxb,
+                              void* stream) {
   const int blocks = ln_blocks(M);
   hipStream_t st = (hipStream_t)stream;
 #define PV_LN_ROWS(VPT)                                                                                          \
   {                                                                                                              \
+    const int np = dxb ? 3 : 2;                                                                                  \
     hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, st,                  \
                        (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,                \
-                       (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr);            \
+                       (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr, np);        \
     PV_LAUNCH_CHECK();                                                                                           \
-    float* ws2 = ws + (size_t)blocks * 2 * D;                                                                    \
-    for (int half = 0; half < 2; ++half) {                                                                       \
+    float* ws2 = ws + (size_t)blocks * np * D;                                                                   \
+    float* outs[3] = {dgamma, dbeta, dxb};                                                                       \
+    for (int part = 0; part < np; ++part) {                                                                      \
       hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0, st, \
-                         ws + half * D, ws2 + (size_t)half * pv::tfm::kColSplits * D, blocks, D, 2 * D);          \
+                         ws + part * D, ws2 + (size_t)part * pv::tfm::kColSplits * D, blocks, D, np * D);         \
       PV_LAUNCH_CHECK();                                                                                         \
       hipLaunchKernelGGL(pv::tfm::colsum_final_kernel, dim3((D + 255) / 256), dim3(256), 0, st,                  \
-                         ws2 + (size_t)half * pv::tfm::kColSplits * D, half ? dbeta : dgamma, pv::tfm::kColSplits, D); \
+                         ws2 + (size_t)part * pv::tfm::kColSplits * D, outs[part], pv::tfm::kColSplits, D);      \
       PV_LAUNCH_CHECK();                                                                                         \
     }                                                                                                            \
     return 0;                                                                                                    \
@@ -640,7 +658,7 @@ static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gam
     default: break;
   }
 #undef PV_LN_ROWS
-  if (dxm) return -1;  // the dropout-fused backward exists on the wave-per-row path only
+  if (dxm || dxb || thr > 0) return -1;  // the fused variants exist on the wave-per-row path only
   const int rpb = 32;
   hipLaunchKernelGGL(pv::tfm::layernorm_bwd_kernel, dim3((M + rpb - 1) / rpb), dim3(256), 2 * D * sizeof(float),
                      (hipStream_t)stream, (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,
@@ -652,30 +670,33 @@ static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gam
 PV_API int pv_layernorm_bwd(const void* dy, const void* hsum, const float* gamma, const float* mean, const float* rstd,
                             void* dx, float* dgamma, float* dbeta, float* ws, int M, int D, void* stream) {
   return layernorm_bwd_impl(dy, hsum, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, D, nullptr, 0, 1.f, 0u, nullptr,
-                            stream);
+                            nullptr, stream);
 }
 
-// dx = dL/dh (the residual input's gradient), dxm = dx * keep * scale (the dropout branch's),
-// keep regenerated from (seed + *seed_ptr, row, column) exactly as pv_add_ln_drop_fwd drew it.
+// dx = dL/dh (the residual input's gradient), dxm = dx * keep * scale (the dropout branch's;
+// null when thr = 0: then the branch gradient IS dx), keep regenerated from (seed + *seed_ptr,
+// row, column) exactly as pv_add_ln_drop_fwd drew it; dxb (optional) = column sums of the
+// branch gradient = the gradient of the bias pv_add_ln_drop_fwd added to x.
 PV_API int pv_layernorm_bwd_drop(const void* dy, const void* hsum, const float* gamma, const float* mean,
-                                 const float* rstd, void* dx, void* dxm, float* dgamma, float* dbeta, float* ws, int M,
-                                 int D, int thr, float scale, unsigned seed, const unsigned* seed_ptr, void* stream) {
-  if (!ws || !ln_rows_ok(D)) return -1;
+                                 const float* rstd, void* dx, void* dxm, float* dgamma, float* dbeta, float* dxb,
+                                 float* ws, int M, int D, int thr, float scale, unsigned seed,
+                                 const unsigned* seed_ptr, void* stream) {
+  if (!ws || !ln_rows_ok(D) || (thr > 0 && !dxm)) return -1;
   return layernorm_bwd_impl(dy, hsum, gamma, mean, rstd, dx, dgamma, dbeta, ws, M, D, dxm, thr, scale, seed,
-                            seed_ptr, stream);
+                            seed_ptr, dxb, stream);
 }
 
 // Wave-per-row residual add (+ optional dropout on x) + LayerNorm, D in {256, 512, 768, 1024}.
-PV_API int pv_add_ln_drop_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, void* h,
-                              float* mean, float* rstd, int M, int D, float eps, int thr, float scale, unsigned seed,
-                              const unsigned* seed_ptr, void* stream) {
+PV_API int pv_add_ln_drop_fwd(const void* x, const float* xb, const void* r, const float* gamma, const float* beta,
+                              void* y, void* h, float* mean, float* rstd, int M, int D, float eps, int thr, float scale,
+                              unsigned seed, const unsigned* seed_ptr, void* stream) {
   if (!ln_rows_ok(D) || thr < 0 || thr > 255) return -1;
   const dim3 grid((M + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
 #define PV_ADDLN(VPT)                                                                                          \
   hipLaunchKernelGGL(pv::tfm::add_ln_drop_fwd_kernel<VPT>, grid, dim3(256), 0, st, (const unsigned short*)x,  \
                      (const unsigned short*)r, gamma, beta, (unsigned short*)y, (unsigned short*)h, mean, rstd, \
-                     M, eps, thr, scale, seed, seed_ptr)
+                     M, eps, thr, scale, seed, seed_ptr, xb)
   switch (D) {
     case 256: PV_ADDLN(1); break;
     case 512: PV_ADDLN(2); break;

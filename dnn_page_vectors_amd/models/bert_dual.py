@@ -49,12 +49,14 @@ class BertLayer(nn.Module):
         p = p_drop if training else 0.0
         qkv = tops.linear(x, self.wqkv, self.bqkv)            # (N, L, 3H) packed [slot][head][d]
         a = tops.fused_attention(qkv, mask, self.heads)       # (N, L, H), no permute copies
-        o = tops.linear(a, self.wo, self.bo)
-        # hidden dropout fused into the residual add + LayerNorm (counter-hash masks)
-        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed)
+        o = tops.linear(a, self.wo)
+        # output bias + hidden dropout fused into the residual add + LayerNorm (counter-hash
+        # masks; the bias gradient is reduced in the LayerNorm backward)
+        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo)
         f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
-        f2 = tops.linear(f, self.w2, self.b2)
-        return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF)
+        f2 = tops.linear(f, self.w2)
+        return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
+                                  bias=self.b2)
 
 
 class _RowGather(torch.autograd.Function):

@@ -48,8 +48,8 @@ SIGS = {
     "pv_topk_cos": "pppppp" "iiiii" "p",
     # transformer.hip
     "pv_add_layernorm_fwd": "pppppppp" "iif" "p",
-    "pv_add_ln_drop_fwd": "pppppppp" "iif" "ifup" "p",
-    "pv_layernorm_bwd_drop": "ppppppp" "ppp" "ii" "ifup" "p",
+    "pv_add_ln_drop_fwd": "ppppppppp" "iif" "ifup" "p",
+    "pv_layernorm_bwd_drop": "ppppppp" "pppp" "ii" "ifup" "p",
     "pv_layernorm_bwd_ws": "ii",
     "pv_layernorm_bwd": "ppppppppp" "ii" "p",
     "pv_bias_gelu_fwd": "ppp" "li" "p",

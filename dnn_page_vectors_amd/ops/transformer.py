@@ -26,13 +26,15 @@ def _seed_ptr():
 
 
 class _AddLNFn(torch.autograd.Function):
-    """y = LayerNorm(dropout(x) + r).  D in {256, 512, 768, 1024}: one wave per row
+    """y = LayerNorm(dropout(x + xb) + r).  D in {256, 512, 768, 1024}: one wave per row
     (``pv_add_ln_drop_fwd``); the dropout mask is a counter hash of (seed, row, column)
     (ops/reference.py::dropout_keep_mask, p quantised to 1/256), regenerated in the backward,
-    which writes both the residual gradient and the masked branch gradient in one pass."""
+    which writes both the residual gradient and the masked branch gradient in one pass and
+    reduces the branch bias gradient (column sums) with the LayerNorm parameter gradients.
+    ``xb``: the bias of the linear layer producing x (that GEMM then runs without one)."""
 
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps, p, seed):
+    def forward(ctx, x, r, gamma, beta, eps, p, seed, xb):
         x = x.to(torch.bfloat16).contiguous()
         r = r.to(torch.bfloat16).contiguous() if r is not None else None
         D = x.shape[-1]
@@ -45,17 +47,19 @@ class _AddLNFn(torch.autograd.Function):
         scale = 256.0 / (256.0 - thr)
         sp = _seed_ptr() if thr > 0 else None
         seed = int(seed) & 0xFFFFFFFF
+        xbf = xb.float().contiguous() if xb is not None else None
         if D in _LN_ROWS:
-            check(lib().pv_add_ln_drop_fwd(P(x), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D, eps,
-                                           thr, scale, seed, P(sp), stream(x.device)), "pv_add_ln_drop_fwd")
+            check(lib().pv_add_ln_drop_fwd(P(x), P(xbf), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D,
+                                           eps, thr, scale, seed, P(sp), stream(x.device)), "pv_add_ln_drop_fwd")
         else:
-            if thr > 0:
-                raise ValueError(f"fused dropout + LayerNorm needs D in {_LN_ROWS}")
+            if thr > 0 or xb is not None:
+                raise ValueError(f"fused dropout / bias + LayerNorm needs D in {_LN_ROWS}")
             check(lib().pv_add_layernorm_fwd(P(x), P(r), P(gamma), P(beta), P(y), P(h), P(mean), P(rstd), M, D, eps,
                                              stream(x.device)), "pv_add_layernorm_fwd")
         ctx.save_for_backward(h, gamma, mean, rstd, sp)
         ctx.has_r = r is not None
         ctx.drop = (thr, scale, seed)
+        ctx.xb = None if xb is None else (xb.shape, xb.dtype)
         return y
 
     @staticmethod
@@ -72,29 +76,42 @@ class _AddLNFn(torch.autograd.Function):
         dg = alloc(gamma.shape, dtype=torch.float32, device=h.device)
         db = alloc(gamma.shape, dtype=torch.float32, device=h.device)
         ws = torch.empty(nws, dtype=torch.float32, device=h.device) if nws > 0 else None
-        if thr > 0:
-            dxm = torch.empty_like(h)
+        dxb = torch.empty(D, dtype=torch.float32, device=h.device) if ctx.xb is not None else None
+        if thr > 0 or dxb is not None:
+            dxm = torch.empty_like(h) if thr > 0 else None
             check(L_.pv_layernorm_bwd_drop(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dxm), P(dg), P(db),
-                                           P(ws), M, D, thr, scale, seed, P(sp), stream(h.device)),
+                                           P(dxb), P(ws), M, D, thr, scale, seed, P(sp), stream(h.device)),
                   "pv_layernorm_bwd_drop")
+            if dxm is None:
+                dxm = dx
         else:
             dxm = dx
             check(L_.pv_layernorm_bwd(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dg), P(db), P(ws), M, D,
                                       stream(h.device)), "pv_layernorm_bwd")
-        return dxm, (dx if ctx.has_r else None), dg, db, None, None, None
+        if dxb is not None and ctx.xb[1] != torch.float32:
+            dxb = dxb.to(ctx.xb[1])
+        return dxm, (dx if ctx.has_r else None), dg, db, None, None, None, dxb
 
 
 _LN_ROWS = (256, 512, 768, 1024)
 
 
 def add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor,
-                  eps: float = 1e-12, p: float = 0.0, seed: int = 0) -> torch.Tensor:
-    """LayerNorm(dropout_p(x) + r) (dropout only when p > 0: pass p = 0 outside training)."""
+                  eps: float = 1e-12, p: float = 0.0, seed: int = 0,
+                  bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LayerNorm(dropout_p(x + bias) + r) (dropout only when p > 0: pass p = 0 outside
+    training; ``bias`` = the bias of the linear layer that produced x, folded in here)."""
     if use_hip(x):
-        if p > 0 and x.shape[-1] not in _LN_ROWS:
-            x = F.dropout(x, p, True)
-            p = 0.0
-        return _AddLNFn.apply(x, r, gamma, beta, eps, float(p), int(seed))
+        if x.shape[-1] not in _LN_ROWS:
+            if bias is not None:
+                x = x + bias.to(x.dtype)
+                bias = None
+            if p > 0:
+                x = F.dropout(x, p, True)
+                p = 0.0
+        return _AddLNFn.apply(x, r, gamma, beta, eps, float(p), int(seed), bias)
+    if bias is not None:
+        x = x + bias.to(x.dtype)
     if p > 0:
         keep = ref.dropout_keep_mask(seed, x.numel() // x.shape[-1], x.shape[-1], p, device=x.device)
         x = x * keep.view(x.shape).to(x.dtype) * (256.0 / (256.0 - ref.dropout_threshold(p)))

@@ -581,11 +581,12 @@ def test_adam_and_sumsq_large_flat(n):
     assert float(out[1]) == 1.0
 
 
-@pytest.mark.parametrize("D,p", [(768, 0.1), (768, 0.25), (256, 0.0), (1024, 0.5)])
-def test_add_layernorm_fused_dropout(D, p):
-    """LayerNorm(dropout(x) + r) (wave-per-row fused kernel, counter-hash mask) vs the fp32
-    reference with the same mask (ops/reference.py::dropout_keep_mask); gradients of x
-    (masked) and r (unmasked) from the one-pass backward."""
+@pytest.mark.parametrize("D,p,with_bias", [(768, 0.1, True), (768, 0.25, False), (256, 0.0, True),
+                                            (256, 0.0, False), (1024, 0.5, True)])
+def test_add_layernorm_fused_dropout(D, p, with_bias):
+    """LayerNorm(dropout(x + xb) + r) (wave-per-row fused kernel, counter-hash mask, folded
+    linear bias) vs the fp32 reference with the same mask (ops/reference.py::dropout_keep_mask);
+    gradients of x (masked), r (unmasked) and xb (column sums) from the one-pass backward."""
     from dnn_page_vectors_amd.ops import transformer as tf
 
     torch.manual_seed(3)
@@ -594,21 +595,25 @@ def test_add_layernorm_fused_dropout(D, p):
     r = bf(torch.randn(M, D, device=DEV)).requires_grad_(True)
     g = (1.0 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
     b = (0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
+    xb = (0.2 * torch.randn(D, device=DEV)).requires_grad_(True) if with_bias else None
     seed = 987654
-    y = tf.add_layernorm(x.to(torch.bfloat16), r.to(torch.bfloat16), g, b, 1e-12, p=p, seed=seed)
+    y = tf.add_layernorm(x.to(torch.bfloat16), r.to(torch.bfloat16), g, b, 1e-12, p=p, seed=seed, bias=xb)
     x2, r2 = x.detach().clone().requires_grad_(True), r.detach().clone().requires_grad_(True)
     g2, b2 = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    xb2 = xb.detach().clone().requires_grad_(True) if with_bias else None
+    xin = x2 + xb2 if with_bias else x2
     if p > 0:
         keep = ref.dropout_keep_mask(seed, M, D, p, device=DEV).float()
-        hh = x2 * keep * (256.0 / (256.0 - ref.dropout_threshold(p))) + r2
+        hh = xin * keep * (256.0 / (256.0 - ref.dropout_threshold(p))) + r2
     else:
-        hh = x2 + r2
+        hh = xin + r2
     yr = torch.nn.functional.layer_norm(hh, (D,), g2, b2, 1e-12)
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
     w = torch.randn(M, D, device=DEV)
     (y.float() * w).sum().backward()
     (yr * w).sum().backward()
-    for a_, b_ in ((x.grad, x2.grad), (r.grad, r2.grad)):
+    pairs = [(x.grad, x2.grad), (r.grad, r2.grad)] + ([(xb.grad, xb2.grad)] if with_bias else [])
+    for a_, b_ in pairs:
         err = (a_.float() - b_).abs().max() / b_.abs().max()
         assert err < 3e-2, float(err)
     torch.testing.assert_close(g.grad, g2.grad, rtol=3e-2, atol=0.5)
