@@ -41,8 +41,11 @@ __host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
   return x;
 }
 
+// One lowbias32 round per row: mix32(seed) is loop-invariant in every caller (hoisted), so
+// a row costs one finaliser (two 32-bit multiplies) — the sparse backward kernels recompute
+// it for every gradient entry and are VALU-bound.
 __device__ __forceinline__ unsigned dropout_row_hash(unsigned seed, unsigned row) {
-  return mix32(seed ^ mix32(row));
+  return mix32(row ^ mix32(seed));
 }
 
 // Keep-bits for columns 4g..4g+3 of a row (byte b of the group hash >= thr).

@@ -107,10 +107,14 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
       for (int u = 0; u < 4; ++u) {
         if (u >= cnt) break;
         const float gj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g), sl[u]));
+        const f32x2 g2 = {gj, gj};
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          acc[2 * w] += gj * __uint_as_float(raw[u][w] << 16);
-          acc[2 * w + 1] += gj * __uint_as_float(raw[u][w] & 0xFFFF0000u);
+        for (int w = 0; w < 4; ++w) {  // packed fp32 FMA (v_pk_fma_f32): two columns per op
+          const f32x2 x2 = {__uint_as_float(raw[u][w] << 16), __uint_as_float(raw[u][w] & 0xFFFF0000u)};
+          f32x2 a2 = {acc[2 * w], acc[2 * w + 1]};
+          a2 = __builtin_elementwise_fma(g2, x2, a2);
+          acc[2 * w] = a2[0];
+          acc[2 * w + 1] = a2[1];
         }
       }
     }

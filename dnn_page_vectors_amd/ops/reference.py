@@ -45,14 +45,14 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r``.
 
     element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25):
-             h_row = mix(seed ^ mix(row)); nibble b of mix(h_row + g*0x9E3779B9) decides column
+             h_row = mix(row ^ mix(seed)); nibble b of mix(h_row + g*0x9E3779B9) decides column
              8g+b (kept iff nibble >= thr/16) — one hash per 8 columns;
     element, other thr: byte b of mix(h_row + g*0x9E3779B9) decides column 4g+b (>= thr);
     token:   one decision per row: byte 0 of h_row.
     """
     thr = dropout_threshold(p)
     rows = torch.arange(n_rows, dtype=torch.int64, device=device) + int(row_offset)
-    h_row = _mix32((int(seed) & _M32) ^ _mix32(rows))
+    h_row = _mix32(rows ^ _mix32(torch.tensor(int(seed) & _M32, dtype=torch.int64, device=device)))
     if mode == "token":
         b = h_row & 0xFF
         return (b >= thr).unsqueeze(1).expand(n_rows, width)

@@ -229,19 +229,20 @@ def test_cdssm_train_step_gpu():
     from dnn_page_vectors_amd.train.trainer import Trainer
 
     pdist.init_distributed()
+    # memorising one fixed batch (dropout on): a working fwd / sparse bwd / Adam chain drives
+    # the loss down fast (CPU reference: explicit 1.39 -> 0.02, in-batch 5.55 -> 0.56 in 40
+    # steps); 30 steps on fresh random batches barely move the gamma=10 clipped-cosine loss
     for mode in ("explicit", "cross_gpu"):
         cfg = Configuration(feature_level="ngram", vocab_hash_size=3000, batch_size=64, query_length=45,
-                            document_length=200, loss_mode=mode)
+                            document_length=200, loss_mode=mode, lr=1e-2)
         tr = Trainer(cfg, CDSSM(cfg, 3000), torch.device(DEV))
         g = torch.Generator(device="cpu").manual_seed(0)
         pages = torch.randint(1, 3000, (512, 200), generator=g, dtype=torch.int32).to(DEV)
-        losses = []
-        for _ in range(30):
-            idx = torch.randint(0, 512, (64, 4), generator=g).to(DEV)
-            q, d = pages[idx[:, 0], :45].contiguous(), pages[idx]
-            losses.append(float(tr.train_step(q, d)["loss"]))
+        idx = torch.randint(0, 512, (64, 4), generator=g).to(DEV)
+        q, d = pages[idx[:, 0], :45].contiguous(), pages[idx]
+        losses = [float(tr.train_step(q, d)["loss"]) for _ in range(40)]
         assert all(l == l for l in losses)
-        assert sum(losses[-5:]) < sum(losses[:5])
+        assert losses[-1] < 0.5 * losses[0], (mode, losses[::8])
 
 
 @pytest.mark.parametrize("plan,L,E", [("gather", 45, 512), ("counts", 300, 512), ("gather", 20, 64), ("counts", 20, 72)])
