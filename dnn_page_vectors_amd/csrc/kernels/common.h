@@ -53,6 +53,10 @@ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g
   return mix32(hrow + g * 0x9E3779B9u);
 }
 
+// Bytes in {0, 1} -> bytes in {0, 0xFF}: x * 255 as (x << 8) - x (two full-rate ops instead
+// of a quarter-rate v_mul_lo_u32; the sparse-backward kernels are VALU-bound).
+__device__ __forceinline__ unsigned bytes_to_mask(unsigned x) { return (x << 8) - x; }
+
 // Byte k of the result is 0xFF iff byte k of the group hash is >= thr (element 4g+k kept).
 // thr = 64 / 128 / 192 (p = 0.25 — the reference's rate — / 0.5 / 0.75) is a function of the
 // top two bits of each byte: 4 bit ops instead of 4 compares + selects.
@@ -69,7 +73,7 @@ __device__ __forceinline__ unsigned keep_bytes(unsigned h, int thr) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) b |= ((int)((h >> (8 * k)) & 0xFFu) >= thr ? 1u : 0u) << (8 * k);
   }
-  return b * 0xFFu;
+  return bytes_to_mask(b);
 }
 
 // AND-mask for the bf16 pair (elements 2j, 2j+1) of a packed dword, from keep_bytes (v_perm_b32).
@@ -98,8 +102,8 @@ __device__ __forceinline__ u32x4 keep_piece(unsigned hrow, int q, int thr) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) b |= (((h >> (4 * k)) & 0xFu) >= (unsigned)t ? 1u : 0u) << (4 * k);
     }
-    const unsigned lo = (b & 0x01010101u) * 0xFFu;         // byte j: column 2j (even nibbles)
-    const unsigned hi = ((b >> 4) & 0x01010101u) * 0xFFu;  // byte j: column 2j+1
+    const unsigned lo = bytes_to_mask(b & 0x01010101u);         // byte j: column 2j (even nibbles)
+    const unsigned hi = bytes_to_mask((b >> 4) & 0x01010101u);  // byte j: column 2j+1
     return u32x4{__builtin_amdgcn_perm(hi, lo, 0x04040000u), __builtin_amdgcn_perm(hi, lo, 0x05050101u),
                  __builtin_amdgcn_perm(hi, lo, 0x06060202u), __builtin_amdgcn_perm(hi, lo, 0x07070303u)};
   }

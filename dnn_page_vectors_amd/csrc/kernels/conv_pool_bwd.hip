@@ -80,6 +80,20 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         if (m) { m &= m - 1; ++cnt; }
       }
       u32x4 raw[4];
+      // dropout row hashes of the (up to) 4 samples of this round in ONE pass: lane 4u + j
+      // hashes row (n_u, a_u + j), then every lane fetches its row's hash with a bpermute
+      unsigned hq = 0u;
+      if (thr > 0) {
+        const int uu = (lane >> 2) & 3;
+        int su = sl[0];
+        su = uu == 1 ? sl[1] : su;
+        su = uu == 2 ? sl[2] : su;
+        su = uu == 3 ? sl[3] : su;
+        su = su < 0 ? sl[0] : su;
+        const int au = __builtin_amdgcn_ds_bpermute(su * 4, a);
+        hq = (lane < 16 && (lane & 3) < K) ? dropout_row_hash(seed, row_offset + (unsigned)((base + su) * L + au + (lane & 3)))
+                                           : 0u;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u >= cnt) break;
@@ -93,8 +107,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         const bool ok = pv_ && t >= 0 && t < V;
         raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (size_t)t * EP + pc * 8) : u32x4{0u, 0u, 0u, 0u};
         if (thr > 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
-          const unsigned hown = lane < K ? dropout_row_hash(seed, row_offset + (unsigned)(nn * L + a_ + lane)) : 0u;
-          const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute(jsel * 4, (int)hown);
+          const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, (int)hq);
           if (token_mode) {
             const unsigned k = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
             raw[u] &= u32x4{k, k, k, k};
