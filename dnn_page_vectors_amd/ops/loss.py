@@ -201,13 +201,16 @@ class _CrossGpuFn(torch.autograd.Function):
         # the forward and the tower's own backward (B*DP*2 bytes per rank)
         qall = torch.empty(B * W, DP, dtype=torch.bfloat16, device=qn.device)
         ctx.qwork = dist.all_gather_into_tensor(qall, qb, group=group, async_op=True)
-        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp, qall)
+        # a plain attribute, not a saved tensor: the in-flight collective writes qall after
+        # this point (gloo copies the result back on completion, bumping its version)
+        ctx.qall = qall
+        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp)
         ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
         return loss, torch.exp(-loss).detach()
 
     @staticmethod
     def backward(ctx, gl, _gp):
-        qb, db, dbl, pos_local, sumexp, qall = ctx.saved_tensors
+        qb, db, dbl, pos_local, sumexp = ctx.saved_tensors
         B, M, n, D, DP, gamma, clip, group, W = ctx.meta
         s = stream(qb.device)
         L_ = lib()
@@ -223,6 +226,7 @@ class _CrossGpuFn(torch.autograd.Function):
         check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
         ctx.qwork.wait()
         ctx.qwork = None
+        qall, ctx.qall = ctx.qall, None
         swork.wait()
         # dD of the local pages = sum over all W*B queries: no reduce-scatter of an (M, DP)
         # fp32 partial (W x the bytes of dd) over xGMI

@@ -69,8 +69,9 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-def test_cross_gpu_loss_two_ranks_one_gpu():
-    world, port = 2, _port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_cross_gpu_loss_ranks_one_gpu(world):
+    port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
