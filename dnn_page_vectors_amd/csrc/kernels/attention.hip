@@ -220,6 +220,33 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const unsigned short
   }
 }
 
+// Same D with all 64 lanes busy: a wave per row (n, q), lane l loads 4 consecutive columns
+// of each 256-column chunk c (head 4c + l/16), the per-head sums are 16-lane xor reductions
+// (4 shuffles per chunk) — for H = 12: 3 chunks, 12 shuffles per row instead of 12 full wave
+// reductions with half the lanes idle.  Requires H % 4 == 0 (H * 64 a multiple of 256).
+__global__ __launch_bounds__(256) void attn_bwd_prep4_kernel(const unsigned short* __restrict__ dout,
+                                                             const unsigned short* __restrict__ out,
+                                                             float* __restrict__ Dv, int NL, int L, int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // n*L + q
+  const int lane = threadIdx.x & 63;
+  if (row >= NL) return;
+  const int n = row / L, q = row - n * L;
+  const unsigned short* a = dout + (size_t)row * H * HD;
+  const unsigned short* b = out + (size_t)row * H * HD;
+  for (int c = 0; c < H / 4; ++c) {
+    const int col = c * 256 + lane * 4;
+    const uint2 x = *reinterpret_cast<const uint2*>(a + col);
+    const uint2 y = *reinterpret_cast<const uint2*>(b + col);
+    float acc = __uint_as_float(x.x << 16) * __uint_as_float(y.x << 16) +
+                __uint_as_float(x.x & 0xFFFF0000u) * __uint_as_float(y.x & 0xFFFF0000u) +
+                __uint_as_float(x.y << 16) * __uint_as_float(y.y << 16) +
+                __uint_as_float(x.y & 0xFFFF0000u) * __uint_as_float(y.y & 0xFFFF0000u);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if ((lane & 15) == 0) Dv[((size_t)n * H + 4 * c + (lane >> 4)) * L + q] = acc;
+  }
+}
+
 // grid (ceil(L/64) key blocks, H, N); wave w owns keys k0 + 16w .. +15 (lane column)
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned short* __restrict__ qkv,
                                                                const int* __restrict__ mask,
@@ -442,8 +469,12 @@ PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const 
   if (N <= 0 || L <= 0 || H <= 0) return -1;
   hipStream_t s = (hipStream_t)stream;
   const int NL = N * L;
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
-                     (const unsigned short*)out, D, NL, L, H);
+  if (H % 4 == 0)
+    hipLaunchKernelGGL(attn_bwd_prep4_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
+                       (const unsigned short*)out, D, NL, L, H);
+  else
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
+                       (const unsigned short*)out, D, NL, L, H);
   PV_LAUNCH_CHECK();
   dim3 grid((L + TB - 1) / TB, H, N);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, s, (const unsigned short*)qkv, mask,
