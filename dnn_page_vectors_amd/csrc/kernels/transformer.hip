@@ -402,12 +402,26 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   const int c = blockIdx.x * 64 + tx;
   const int per = (R + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * per, r1 = min(R, r0 + per);
+  part += (size_t)blockIdx.z * D;  // grid.z: several column sets of one row layout in one launch
+  part2 += (size_t)blockIdx.z * gridDim.y * D;
   float a = 0.f;
   if (c < D)
     for (int r = r0 + ty; r < r1; r += 4) a += part[(size_t)r * ld + c];
   sh[ty][tx] = a;
   __syncthreads();
   if (ty == 0 && c < D) part2[(size_t)blockIdx.y * D + c] = sh[0][tx] + sh[1][tx] + sh[2][tx] + sh[3][tx];
+}
+
+// final split sums of up to 3 column sets (grid.y = set) -> out0 / out1 / out2
+__global__ void colsum_final3_kernel(const float* __restrict__ part2, float* __restrict__ out0,
+                                     float* __restrict__ out1, float* __restrict__ out2, int S, int D) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  const int set = blockIdx.y;
+  const float* p = part2 + (size_t)set * S * D;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += p[(size_t)s * D + c];
+  (set == 0 ? out0 : set == 1 ? out1 : out2)[c] = a;
 }
 
 __global__ void colsum_final_kernel(const float* __restrict__ part2, float* __restrict__ out, int S, int D) {
@@ -630,15 +644,12 @@ static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gam
                        (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr, np);        \
     PV_LAUNCH_CHECK();                                                                                           \
     float* ws2 = ws + (size_t)blocks * np * D;                                                                   \
-    float* outs[3] = {dgamma, dbeta, dxb};                                                                       \
-    for (int part = 0; part < np; ++part) {                                                                      \
-      hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0, st, \
-                         ws + part * D, ws2 + (size_t)part * pv::tfm::kColSplits * D, blocks, D, np * D);         \
-      PV_LAUNCH_CHECK();                                                                                         \
-      hipLaunchKernelGGL(pv::tfm::colsum_final_kernel, dim3((D + 255) / 256), dim3(256), 0, st,                  \
-                         ws2 + (size_t)part * pv::tfm::kColSplits * D, outs[part], pv::tfm::kColSplits, D);      \
-      PV_LAUNCH_CHECK();                                                                                         \
-    }                                                                                                            \
+    hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits, np), dim3(256), 0,  \
+                       st, ws, ws2, blocks, D, np * D);                                                          \
+    PV_LAUNCH_CHECK();                                                                                           \
+    hipLaunchKernelGGL(pv::tfm::colsum_final3_kernel, dim3((D + 255) / 256, np), dim3(256), 0, st, ws2, dgamma,  \
+                       dbeta, dxb, pv::tfm::kColSplits, D);                                                      \
+    PV_LAUNCH_CHECK();                                                                                           \
     return 0;                                                                                                    \
   }
   if (ws) {

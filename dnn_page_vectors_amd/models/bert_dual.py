@@ -59,6 +59,19 @@ class BertLayer(nn.Module):
                                   bias=self.b2)
 
 
+    def forward_packed(self, x: torch.Tensor, masks, shapes, p_drop: float, training: bool, seed: int = 0):
+        """x (T, H): several sequence groups packed token-major (see BertEncoder.forward_multi)."""
+        p = p_drop if training else 0.0
+        qkv = tops.linear(x, self.wqkv, self.bqkv)            # (T, 3H): one GEMM for every group
+        a = tops.packed_attention(qkv, masks, shapes, self.heads)
+        o = tops.linear(a, self.wo)
+        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo)
+        f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
+        f2 = tops.linear(f, self.w2)
+        return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
+                                  bias=self.b2)
+
+
 class _RowGather(torch.autograd.Function):
     """Token-embedding lookup whose backward is an atomic row scatter (``index_add_``).
 
@@ -114,6 +127,38 @@ class BertEncoder(nn.Module):
         cls = x[:, 0].float()
         return F.linear(cls, self.proj) if self.proj is not None else cls
 
+    def forward_multi(self, ids_list, p_drop: float, training: bool, seed: int = 0):
+        """Several id batches (e.g. the queries (B, Lq) and the pages (B*S, Ld) of one step)
+        through the SAME encoder in one pass: every position-wise op (the four linear layers,
+        bias+GELU, residual+LayerNorm, their backward and weight gradients) runs once over the
+        packed tokens; only attention is per group.  Each weight then receives one gradient
+        (no accumulation adds) from one larger, better-filled GEMM.  Returns the per-group
+        CLS vectors (projected if configured)."""
+        dt = torch.bfloat16 if ids_list[0].is_cuda else torch.float32
+        xs, masks, shapes = [], [], []
+        for ids in ids_list:
+            ids = ids.long()
+            N, L = ids.shape
+            mask = (ids != 0)
+            mask[:, 0] = True
+            xs.append((_RowGather.apply(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
+                      .reshape(N * L, -1))
+            masks.append(mask)
+            shapes.append((N, L))
+        x = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
+        x = tops.add_layernorm(x, None, self.ln_g, self.ln_b)
+        if training and p_drop > 0:
+            x = F.dropout(x, p_drop, True)
+        for li, layer in enumerate(self.layers):
+            x = layer.forward_packed(x, masks, shapes, p_drop, training,
+                                     seed=(int(seed) * 1000003 + li * 7919) & 0xFFFFFFFF)
+        outs, off = [], 0
+        for N, L in shapes:
+            cls = x[off:off + N * L].view(N, L, -1)[:, 0].float()
+            off += N * L
+            outs.append(F.linear(cls, self.proj) if self.proj is not None else cls)
+        return outs
+
 
 class BertDualEncoder(TwoTowerModel):
     def __init__(self, cfg, vocab_size: int):
@@ -134,6 +179,19 @@ class BertDualEncoder(TwoTowerModel):
     def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:
         enc = self.query_tower if tower == "query" else self.doc_towers[0]
         return enc(ids, self.p_drop, training, seed=seed)
+
+    def forward(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int = 0, doc_hook=None):
+        """Siamese towers: queries and pages of the step go through the encoder as ONE packed
+        token batch (BertEncoder.forward_multi); separate towers use the base class path."""
+        if self.doc_towers[0] is not self.query_tower or not getattr(self.cfg, "bert_packed", True):
+            return super().forward(q_ids, d_ids, seed=seed, doc_hook=doc_hook)
+        B, S, Ld = d_ids.shape
+        qv, dv = self.query_tower.forward_multi([q_ids, d_ids.reshape(B * S, Ld)], self.p_drop, self.training,
+                                                seed=seed * 2 + 1)
+        d = dv.view(B, S, -1)
+        if doc_hook is not None:
+            doc_hook(d)
+        return qv, d
 
 
 def bert_flops_per_token(cfg, L: int) -> float:

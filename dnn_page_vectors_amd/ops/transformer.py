@@ -214,6 +214,70 @@ def fused_attention(qkv: torch.Tensor, mask: Optional[torch.Tensor], heads: int)
     return attention(q, k, v, mask).transpose(1, 2).reshape(N, L, heads * d)
 
 
+class _PackedAttnFn(torch.autograd.Function):
+    """Attention over several packed sequence groups in ONE token-major tensor: qkv (T, 3*H*64)
+    holds segments of (N_i, L_i) sequences back to back (the query and the page tower of the
+    siamese dual encoder); each segment runs the fused kernels on offset pointers into the
+    shared input / output / gradient buffers — no per-tower copies, slices or gradient adds."""
+
+    @staticmethod
+    def forward(ctx, qkv, masks, shapes, heads, scale):
+        qkv = qkv.to(torch.bfloat16).contiguous()
+        T, C = qkv.shape
+        H = heads
+        if C != 3 * H * 64:
+            raise ValueError("fused attention needs head dim 64")
+        out = torch.empty(T, H * 64, dtype=torch.bfloat16, device=qkv.device)
+        lses = []
+        off = 0
+        s = stream(qkv.device)
+        esz = qkv.element_size()
+        for (N, L), m in zip(shapes, masks):
+            lse = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
+            check(lib().pv_attn_fwd(qkv.data_ptr() + off * C * esz, P(m), out.data_ptr() + off * H * 64 * esz,
+                                    P(lse), N, L, H, float(scale), s), "pv_attn_fwd")
+            lses.append(lse)
+            off += N * L
+        if off != T:
+            raise ValueError("segment shapes do not cover the packed tensor")
+        ctx.save_for_backward(qkv, out, *masks, *lses)
+        ctx.meta = (H, float(scale), list(shapes), len(masks))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        H, scale, shapes, k = ctx.meta
+        saved = ctx.saved_tensors
+        qkv, out, masks, lses = saved[0], saved[1], saved[2:2 + k], saved[2 + k:]
+        T, C = qkv.shape
+        dout = dout.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        esz = qkv.element_size()
+        s = stream(qkv.device)
+        off = 0
+        for (N, L), m, lse in zip(shapes, masks, lses):
+            D = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
+            check(lib().pv_attn_bwd(qkv.data_ptr() + off * C * esz, P(m), out.data_ptr() + off * H * 64 * esz,
+                                    dout.data_ptr() + off * H * 64 * esz, P(lse), P(D),
+                                    dqkv.data_ptr() + off * C * esz, N, L, H, scale, s), "pv_attn_bwd")
+            off += N * L
+        return dqkv, None, None, None, None
+
+
+def packed_attention(qkv: torch.Tensor, masks, shapes, heads: int) -> torch.Tensor:
+    """qkv (T, 3*H*d) token-major with segments of shapes [(N_i, L_i)] back to back, masks
+    [(N_i, L_i)] -> (T, H*d)."""
+    d = qkv.shape[1] // (3 * heads)
+    if use_hip(qkv) and d == 64:
+        ms = [m.to(torch.int32).contiguous() for m in masks]
+        return _PackedAttnFn.apply(qkv, ms, [tuple(x) for x in shapes], heads, 1.0 / math.sqrt(d))
+    outs, off = [], 0
+    for (N, L), m in zip(shapes, masks):
+        outs.append(fused_attention(qkv[off:off + N * L].view(N, L, -1), m, heads).reshape(N * L, -1))
+        off += N * L
+    return torch.cat(outs, 0)
+
+
 # bf16 copies of fp32 master weights, refreshed once per optimizer step (generation counter
 # of models.base: bump_generation() after every update)
 _W16 = {}

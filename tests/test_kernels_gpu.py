@@ -621,3 +621,35 @@ def test_add_layernorm_fused_dropout(D, p, with_bias):
     torch.testing.assert_close(b.grad, b2.grad, rtol=3e-2, atol=0.5)
     if p > 0:  # dropped positions get exactly zero gradient through the branch
         assert float(x.grad[keep == 0].abs().max()) == 0.0
+
+
+def test_bert_packed_dual_tower_matches_separate_towers():
+    """BertDualEncoder.forward packs queries and pages into one token batch (one GEMM per
+    linear layer, per-group attention on offset pointers); outputs and every parameter
+    gradient must match running the two towers separately (no dropout)."""
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.models.base import TwoTowerModel
+
+    cfg = preset_config("bert_dp8").replace(bert_layers=2, bert_dropout=0.0, query_length=32, document_length=96)
+    m = build_model(cfg, cfg.vocab_hash_size).to(DEV).train()
+    g = torch.Generator().manual_seed(0)
+    q = torch.randint(1, 30000, (8, 32), generator=g, dtype=torch.int32).to(DEV)
+    d = torch.randint(1, 30000, (8, 2, 96), generator=g, dtype=torch.int32).to(DEV)
+    d[:, :, 80:] = 0  # padding in the pages
+    wq = torch.randn(8, 768, device=DEV)
+    wd = torch.randn(8, 2, 768, device=DEV)
+    grads = []
+    for packed in (True, False):
+        m.zero_grad(set_to_none=True)
+        qv, dv = m(q, d) if packed else TwoTowerModel.forward(m, q, d)
+        ((qv * wq).sum() + (dv * wd).sum()).backward()
+        grads.append((qv.detach(), dv.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None}))
+    (qa, da, ga), (qb, db, gb) = grads
+    torch.testing.assert_close(qa, qb, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(da, db, rtol=2e-2, atol=2e-2)
+    assert ga.keys() == gb.keys()
+    for n in ga:
+        err = float((ga[n] - gb[n]).abs().max() / gb[n].abs().max().clamp_min(1e-12))
+        assert err < 5e-2, (n, err)
