@@ -445,6 +445,40 @@ __global__ void bias_gelu_fwd_kernel(const unsigned short* __restrict__ x, const
   }
 }
 
+// x * sigmoid(2u) == 0.5 x (1 + tanh u): one v_exp + one v_rcp, no libm tanhf
+__device__ __forceinline__ float gelu_tanh_fast(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x * __frcp_rn(1.f + __expf(-2.f * u));
+}
+
+// Vectorised bias + GELU forward (D % 8 == 0): a thread owns 8 consecutive columns
+// (16-byte loads / stores, its 8 bias values in registers) for RPB rows.  The scalar kernel
+// above spent its time in a 64-bit `i % D` and libm tanhf per element pair (VALU-bound at
+// ~3 TB/s); grid = (ceil(D / 8 / 128), ceil(M / RPB)), 128 threads.
+constexpr int kGeluFwdRpb = 16;
+__global__ __launch_bounds__(128) void bias_gelu_fwd_vec_kernel(const unsigned short* __restrict__ x,
+                                                                const float* __restrict__ b,
+                                                                unsigned short* __restrict__ y, int M, int D) {
+  const int c8 = blockIdx.x * 128 + threadIdx.x;
+  if (c8 * 8 >= D) return;
+  const int col = c8 * 8;
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + col), b1 = *reinterpret_cast<const f32x4*>(b + col + 4);
+  const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  const int r0 = blockIdx.y * kGeluFwdRpb, r1 = min(M, r0 + kGeluFwdRpb);
+  for (int r = r0; r < r1; ++r) {
+    const size_t o = (size_t)r * D + col;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + o);
+    u32x4 w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a0 = __uint_as_float(v[k] << 16) + bb[2 * k];
+      const float a1 = __uint_as_float(v[k] & 0xFFFF0000u) + bb[2 * k + 1];
+      w[k] = pack_bf16x2(gelu_tanh_fast(a0), gelu_tanh_fast(a1));
+    }
+    *reinterpret_cast<u32x4*>(y + o) = w;
+  }
+}
+
 // dx = dy * gelu'(x + b); db += sum over rows (fp32 atomics from block partials)
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const unsigned short* __restrict__ x,
                                                             const float* __restrict__ b,
@@ -721,6 +755,14 @@ PV_API int pv_add_ln_drop_fwd(const void* x, const float* xb, const void* r, con
 
 PV_API int pv_bias_gelu_fwd(const void* x, const float* b, void* y, long n, int D, void* stream) {
   if (D % 2) return -1;
+  if (D % 8 == 0 && n / D <= 0x7FFFFFFFL) {
+    const int M = (int)(n / D);
+    dim3 grid((D / 8 + 127) / 128, (M + pv::tfm::kGeluFwdRpb - 1) / pv::tfm::kGeluFwdRpb);
+    hipLaunchKernelGGL(pv::tfm::bias_gelu_fwd_vec_kernel, grid, dim3(128), 0, (hipStream_t)stream,
+                       (const unsigned short*)x, b, (unsigned short*)y, M, D);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   long blocks = (n / 2 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(pv::tfm::bias_gelu_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
