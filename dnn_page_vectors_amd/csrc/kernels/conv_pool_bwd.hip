@@ -205,8 +205,11 @@ __device__ __forceinline__ void slot_decode(unsigned sl, unsigned& n, unsigned& 
   }
 }
 
+// KT: unsigned (any V) or unsigned short (V < 65535: 2-byte sort keys, a quarter less sort /
+// emit / reduce key traffic)
+template <typename KT>
 __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool, const float* pooled,
-                                                             const int* argmax, const int* ids, unsigned* keys,
+                                                             const int* argmax, const int* ids, KT* keys,
                                                              unsigned* vals, int2* rec, int N, int L, int V,
                                                              float scale) {
   const long pair = (long)blockIdx.x * 256 + threadIdx.x;
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool,
       const bool ok = live && t < L;
       const int v = ok ? ids[(size_t)n * L + t] : V;
       PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
-      keys[s0 + j] = (unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V;
+      keys[s0 + j] = (KT)((unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V);
       if (vals) vals[s0 + j] = s0 + j;  // null: the sort generates the positions itself
     }
   }
@@ -365,7 +368,8 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
 // Zipf token distribution of real (and synthetic) pages the most frequent rows otherwise
 // take thousands of serialised row-atomics at one L2 channel.  Entry metadata is software-
 // pipelined: keys/slots two sub-chunks ahead, the {g, argmax} record gather one ahead.
-__device__ __forceinline__ void rd_meta(const unsigned* __restrict__ skeys, const unsigned* __restrict__ svals,
+template <typename KT>
+__device__ __forceinline__ void rd_meta(const KT* __restrict__ skeys, const unsigned* __restrict__ svals,
                                         long i, long wend, unsigned V, unsigned& key, unsigned& sl) {
   key = V;
   sl = 0u;
@@ -376,7 +380,8 @@ __device__ __forceinline__ void rd_meta(const unsigned* __restrict__ skeys, cons
   }
 }
 
-__global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const unsigned* __restrict__ skeys,
+template <typename KT>
+__global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restrict__ skeys,
                                                                const unsigned* __restrict__ svals,
                                                                const int2* __restrict__ rec,
                                                                const unsigned short* __restrict__ wrow,
@@ -518,8 +523,8 @@ PV_API int pv_conv_pool_bwd_emit3(const float* gpool, const float* pooled, const
                                   void* stream) {
   using namespace pv::convbwd;
   const long pairs = (long)N * 2 * FW;
-  hipLaunchKernelGGL(conv_bwd_emit3_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale);
+  hipLaunchKernelGGL(conv_bwd_emit3_kernel<unsigned>, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -533,9 +538,37 @@ PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals
   using namespace pv::convbwd;
   if (E > EP || epw < 64 || (epw & 63)) return -1;
   const long waves = (M + epw - 1) / epw;
-  hipLaunchKernelGGL(conv_bwd_reduce5_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed,
                      seed_ptr, row_offset, thr, token_mode);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// 2-byte-key variants (V < 65535): emit -> pv_sort_iota_u16 -> reduce
+PV_API int pv_conv_pool_bwd_emit3_u16(const float* gpool, const float* pooled, const int* argmax, const int* ids,
+                                      void* keys, void* rec, int N, int L, int V, float scale, void* stream) {
+  using namespace pv::convbwd;
+  if (V >= 65535) return -1;
+  const long pairs = (long)N * 2 * FW;
+  hipLaunchKernelGGL(conv_bwd_emit3_kernel<unsigned short>, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, gpool, pooled, argmax, ids, (unsigned short*)keys, (unsigned*)nullptr,
+                     (int2*)rec, N, L, V, scale);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                        float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
+                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                                        void* stream) {
+  using namespace pv::convbwd;
+  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
+  const long waves = (M + epw - 1) / epw;
+  hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const unsigned short*)skeys, svals, (const int2*)rec,
+                     (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
+                     token_mode);
   PV_LAUNCH_CHECK();
   return 0;
 }

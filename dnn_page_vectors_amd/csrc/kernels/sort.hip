@@ -38,3 +38,21 @@ PV_API int pv_sort_iota_u32(void* temp, long temp_bytes, const unsigned* keys_in
                                            vals_out, (size_t)n, 0u, (unsigned)end_bit, (hipStream_t)stream);
   return (int)e;
 }
+
+// 2-byte keys (token ids < 65535), values = input positions (counting iterator)
+PV_API long pv_sort_iota_u16_temp_bytes(long n, int end_bit) {
+  size_t bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, bytes, (const unsigned short*)nullptr, (unsigned short*)nullptr,
+                            rocprim::counting_iterator<unsigned>(0u), (unsigned*)nullptr, (size_t)n, 0u,
+                            (unsigned)end_bit);
+  return (long)bytes;
+}
+
+PV_API int pv_sort_iota_u16(void* temp, long temp_bytes, const void* keys_in, void* keys_out, unsigned* vals_out,
+                            long n, int end_bit, void* stream) {
+  size_t bytes = (size_t)temp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(temp, bytes, (const unsigned short*)keys_in, (unsigned short*)keys_out,
+                                           rocprim::counting_iterator<unsigned>(0u), vals_out, (size_t)n, 0u,
+                                           (unsigned)end_bit, (hipStream_t)stream);
+  return (int)e;
+}

@@ -23,6 +23,10 @@ SIGS = {
     "pv_sort_pairs_temp_bytes": "li",
     "pv_sort_pairs_u32": "plpppp" "li" "p",
     "pv_sort_iota_temp_bytes": "li",
+    "pv_sort_iota_u16_temp_bytes": "li",
+    "pv_sort_iota_u16": "plppp" "li" "p",
+    "pv_conv_pool_bwd_emit3_u16": "pppppp" "iii" "f" "p",
+    "pv_conv_pool_bwd_reduce5_u16": "ppppp" "liiii" "upuii" "p",
     "pv_sort_iota_u32": "plppp" "li" "p",
     # dense.hip
     "pv_linear_act": "pipippp" "iiiiii" "p",
@@ -69,7 +73,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

@@ -136,23 +136,36 @@ class _ConvPoolFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
             u32 = torch.int32
-            keys = torch.empty(M, dtype=u32, device=dev)
-            rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
-            # entry i's value is its slot i: no value array, the sort reads a counting iterator
-            check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L, V,
-                                            scale, s), "pv_conv_pool_bwd_emit3")
             end_bit = max(1, int(V).bit_length())
+            rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
+            # entry i's value is its slot i: no value array, the sort reads a counting iterator;
+            # token ids < 65535 sort as 2-byte keys
+            k16 = V < 65535 and REDUCE_EPW > 0
+            keys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
             skeys = torch.empty_like(keys)
-            svals = torch.empty_like(keys)
-            tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
-            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-            check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
+            svals = torch.empty(M, dtype=u32, device=dev)
+            if k16:
+                check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L, V,
+                                                    scale, s), "pv_conv_pool_bwd_emit3_u16")
+                tb = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))
+                temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+                check(L_.pv_sort_iota_u16(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u16")
+            else:
+                check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
+                                                V, scale, s), "pv_conv_pool_bwd_emit3")
+                tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
+                temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+                check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
             # bf16 weight rows [2*FW][4][EP] (the operands the forward MFMAs used)
             wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)
             wrow[:FW, :3, :E] = w3.detach()
             wrow[FW:, :, :E] = w4.detach()
-            if REDUCE_EPW > 0:
+            if k16:
+                check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
+                      "pv_conv_pool_bwd_reduce5_u16")
+            elif REDUCE_EPW > 0:
                 check(L_.pv_conv_pool_bwd_reduce5(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E,
                                                   V, seed, P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce5")
             else:

@@ -95,6 +95,23 @@ def main():
     def sort_iota():
         check(L_.pv_sort_iota_u32(P(tempi), tbi, P(keys), P(skeys), P(svals2), M, end_bit, s), "sort_iota")
 
+    keys16 = torch.empty(M, dtype=torch.int16, device=dev)
+    skeys16 = torch.empty_like(keys16)
+    svals3 = torch.empty_like(vals)
+    tb16 = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))
+    temp16 = torch.empty(max(tb16, 1), dtype=torch.uint8, device=dev)
+
+    def emit16():
+        check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys16), P(rec), N, L, V,
+                                            scale, s), "emit16")
+
+    def sort16():
+        check(L_.pv_sort_iota_u16(P(temp16), tb16, P(keys16), P(skeys16), P(svals3), M, end_bit, s), "sort16")
+
+    def reduce16(out):
+        check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys16), P(svals3), P(rec), P(wrow), P(out), M, 512, L, E, V, 7,
+                                              None, 0, thr, 0, s), "reduce16")
+
     def dw():
         check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E,
                                      V, 7, None, 0, thr, 0, scale, s), "dw")
@@ -111,7 +128,11 @@ def main():
     sort()
     sort_iota()
     torch.cuda.synchronize()
-    print(json.dumps({"sort_iota_vals_equal": bool(torch.equal(svals, svals2))}), flush=True)
+    emit16()
+    sort16()
+    torch.cuda.synchronize()
+    print(json.dumps({"sort_iota_vals_equal": bool(torch.equal(svals, svals2)),
+                      "sort_u16_vals_equal": bool(torch.equal(svals, svals3))}), flush=True)
     epws = [int(x) for x in a.epw.split(",")]
     ref = torch.zeros(V, E, device=dev)
     reduce(0, ref)
@@ -122,13 +143,22 @@ def main():
         reduce(epw, out)
         err = float((out - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         print(json.dumps({"epw": epw, "rel_err_vs_reduce4": err}), flush=True)
-    res = {k: [] for k in ["emit", "emit_novals", "sort", "sort_iota", "dw"] + [f"reduce_epw{e}" for e in epws]}
+    out16 = torch.zeros(V, E, device=dev)
+    reduce16(out16)
+    torch.cuda.synchronize()
+    print(json.dumps({"reduce_u16_rel_err_vs_reduce4":
+                      float((out16 - ref).abs().max() / ref.abs().max().clamp_min(1e-30))}), flush=True)
+    res = {k: [] for k in ["emit", "emit_novals", "emit_u16", "sort", "sort_iota", "sort_u16", "dw", "reduce_u16"] +
+           [f"reduce_epw{e}" for e in epws]}
     scratch = torch.zeros(V, E, device=dev)
     for _ in range(a.rounds):
         res["emit"].append(ev_time(emit, a.iters))
         res["sort"].append(ev_time(sort, a.iters))
         res["emit_novals"].append(ev_time(emit_novals, a.iters))
         res["sort_iota"].append(ev_time(sort_iota, a.iters))
+        res["emit_u16"].append(ev_time(emit16, a.iters))
+        res["sort_u16"].append(ev_time(sort16, a.iters))
+        res["reduce_u16"].append(ev_time(lambda: reduce16(scratch), a.iters))
         res["dw"].append(ev_time(dw, a.iters))
         for epw in epws:
             res[f"reduce_epw{epw}"].append(ev_time(lambda: reduce(epw, scratch), a.iters))
