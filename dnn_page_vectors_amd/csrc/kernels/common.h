@@ -49,18 +49,8 @@ __device__ __forceinline__ unsigned dropout_row_hash(unsigned seed, unsigned row
 }
 
 // Keep-bits for columns 4g..4g+3 of a row (byte b of the group hash >= thr).
-// hrow is already a full lowbias32 output; one xorshift-multiply-xorshift round decorrelates
-// the groups of a row (one 32-bit multiply instead of two: the mask regeneration dominates
-// the VALU-bound sparse backward kernels)
-__device__ __forceinline__ unsigned mix32_half(unsigned x) {
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  return x;
-}
-
 __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
-  return mix32_half(hrow + g * 0x9E3779B9u);
+  return mix32(hrow + g * 0x9E3779B9u);
 }
 
 // Bytes in {0, 1} -> bytes in {0, 0xFF}: x * 255 as (x << 8) - x (two full-rate ops instead

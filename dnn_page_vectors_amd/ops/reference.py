@@ -24,14 +24,6 @@ BCE_EPS = 1e-7                                 # Keras epsilon() clip in binary_
 _M32 = 0xFFFFFFFF
 
 
-def _mix32_half(x: torch.Tensor) -> torch.Tensor:
-    """One xorshift-multiply-xorshift round (the group hash of csrc/kernels/common.h)."""
-    x = x & _M32
-    x = x ^ (x >> 16)
-    x = (x * 0x7FEB352D) & _M32
-    return x ^ (x >> 15)
-
-
 def _mix32(x: torch.Tensor) -> torch.Tensor:
     """lowbias32 finaliser on int64 tensors holding uint32 values."""
     x = x & _M32
@@ -53,7 +45,7 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r``.
 
     element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25):
-             h_row = mix(row ^ mix(seed)); nibble b of mix_half(h_row + g*0x9E3779B9) decides column
+             h_row = mix(row ^ mix(seed)); nibble b of mix(h_row + g*0x9E3779B9) decides column
              8g+b (kept iff nibble >= thr/16) — one hash per 8 columns;
     element, other thr: byte b of mix(h_row + g*0x9E3779B9) decides column 4g+b (>= thr);
     token:   one decision per row: byte 0 of h_row.
@@ -67,13 +59,13 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     if thr % 16 == 0:
         ng = (width + 7) // 8
         g = torch.arange(ng, dtype=torch.int64, device=device)
-        h = _mix32_half(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
+        h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
         shifts = torch.arange(0, 32, 4, dtype=torch.int64, device=device)
         nib = (h.unsqueeze(2) >> shifts) & 0xF  # (n, ng, 8)
         return nib.reshape(n_rows, ng * 8)[:, :width] >= thr // 16
     ng = (width + 3) // 4
     g = torch.arange(ng, dtype=torch.int64, device=device)
-    h = _mix32_half(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
+    h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
     shifts = torch.tensor([0, 8, 16, 24], dtype=torch.int64, device=device)
     bytes_ = (h.unsqueeze(2) >> shifts) & 0xFF  # (n, ng, 4)
     return (bytes_.reshape(n_rows, ng * 4)[:, :width] >= thr)
