@@ -653,3 +653,22 @@ def test_bert_packed_dual_tower_matches_separate_towers():
     for n in ga:
         err = float((ga[n] - gb[n]).abs().max() / gb[n].abs().max().clamp_min(1e-12))
         assert err < 5e-2, (n, err)
+
+
+def test_embedding_bag_counts_split_k():
+    """Counts plan at a vocabulary large enough for the V-split batched GEMM (V // 8 >= 2048)."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    torch.manual_seed(11)
+    V, N, L, E = 16384, 40, 300, 64
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV)
+    ids[:, 250:] = 0
+    W = bf(torch.randn(V, E, device=DEV)).requires_grad_(True)
+    out = eops.embedding_bag(ids, W, plan="counts")
+    Wr = W.detach().clone().requires_grad_(True)
+    outr = ref.embedding_bag_sum(ids, Wr, 0) / (ids != 0).sum(1, keepdim=True).float()
+    torch.testing.assert_close(out, outr, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(outr)
+    (out * g).sum().backward()
+    (outr * g).sum().backward()
+    torch.testing.assert_close(W.grad, Wr.grad, rtol=2e-2, atol=2e-2)
