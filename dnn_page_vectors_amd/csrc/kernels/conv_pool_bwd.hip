@@ -82,30 +82,33 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
       u32x4 raw[4];
       // dropout row hashes of the (up to) 4 samples of this round in ONE pass: lane 4u + j
       // hashes row (n_u, a_u + j), then every lane fetches its row's hash with a bpermute
+      // ... and the same lanes fetch the window's token ids of those samples (4 bpermutes for
+      // the round instead of 4 readlanes + 3 selects per sample)
       unsigned hq = 0u;
-      if (thr > 0) {
-        const int uu = (lane >> 2) & 3;
+      int tq;
+      {
+        const int uu = (lane >> 2) & 3, jq = lane & 3;
         int su = sl[0];
         su = uu == 1 ? sl[1] : su;
         su = uu == 2 ? sl[2] : su;
         su = uu == 3 ? sl[3] : su;
         su = su < 0 ? sl[0] : su;
-        const int au = __builtin_amdgcn_ds_bpermute(su * 4, a);
-        hq = (lane < 16 && (lane & 3) < K) ? dropout_row_hash(seed, row_offset + (unsigned)((base + su) * L + au + (lane & 3)))
-                                           : 0u;
+        int tv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tv[j] = __builtin_amdgcn_ds_bpermute(su * 4, tok[j]);
+        tq = jq == 0 ? tv[0] : jq == 1 ? tv[1] : jq == 2 ? tv[2] : tv[3];
+        if (thr > 0) {
+          const int au = __builtin_amdgcn_ds_bpermute(su * 4, a);
+          hq = (lane < 16 && jq < K) ? dropout_row_hash(seed, row_offset + (unsigned)((base + su) * L + au + jq)) : 0u;
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u >= cnt) break;
-        const int s_ = sl[u];
-        const int a_ = __builtin_amdgcn_readlane(a, s_);
-        const int nn = base + s_;
-        int tj[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tj[j] = __builtin_amdgcn_readlane(tok[j], s_);
-        const int t = jsel == 0 ? tj[0] : jsel == 1 ? tj[1] : jsel == 2 ? tj[2] : tj[3];
+        const int t = __builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, tq);
         const bool ok = pv_ && t >= 0 && t < V;
-        raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (size_t)t * EP + pc * 8) : u32x4{0u, 0u, 0u, 0u};
+        // 32-bit element offset (V * EP < 2^31): no 64-bit multiply per piece
+        raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (unsigned)(t * EP + pc * 8)) : u32x4{0u, 0u, 0u, 0u};
         if (thr > 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
           const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, (int)hq);
           if (token_mode) {
@@ -500,7 +503,7 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
                                unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
                                float scale, void* stream) {
   using namespace pv::convbwd;
-  if (E > EP || L < 4) return -1;
+  if (E > EP || L < 4 || (long)V * EP >= (1L << 31)) return -1;  // 32-bit table offsets in the kernel
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
