@@ -258,11 +258,11 @@ __device__ __forceinline__ void reduce4_flush(float* slab, const float (&acc)[8]
   const int c0 = lane, c1 = lane + 64;
   if (c0 < E) {
     const float v = slab[c0] + slab[EP + c0] + slab[2 * EP + c0] + slab[3 * EP + c0];
-    atomicAdd(&dtable[(size_t)key * E + c0], v);
+    atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c0)], v);
   }
   if (c1 < E) {
     const float v = slab[c1] + slab[EP + c1] + slab[2 * EP + c1] + slab[3 * EP + c1];
-    atomicAdd(&dtable[(size_t)key * E + c1], v);
+    atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c1)], v);
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // slab reads done before the next flush overwrites it
 }
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
       float v[8];
       {
         u32x4 w = u32x4{0u, 0u, 0u, 0u};
-        if (act) w = *reinterpret_cast<const u32x4*>(wrow + (size_t)f_j * EP + 8 * p);
+        if (act) w = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * p));
         if (thr > 0) {
           if (token_mode) {
             const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
@@ -539,7 +539,7 @@ PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals
                                     const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
                                     void* stream) {
   using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63)) return -1;
+  if (E > EP || epw < 64 || (epw & 63) || (long)V * E >= (1L << 32)) return -1;
   const long waves = (M + epw - 1) / epw;
   hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed,
@@ -581,7 +581,7 @@ PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals
                                     const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
                                     void* stream) {
   using namespace pv::convbwd;
-  if (E > EP) return -1;
+  if (E > EP || (long)V * E >= (1L << 32)) return -1;
   const long chunks = (M + 63) / 64;
   hipLaunchKernelGGL(conv_bwd_reduce4_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, L, E, V, seed,
