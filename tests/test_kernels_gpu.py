@@ -591,7 +591,7 @@ def test_add_layernorm_fused_dropout(D, p, with_bias):
     from dnn_page_vectors_amd.ops import transformer as tf
 
     torch.manual_seed(3)
-    M = 300
+    M = 301  # odd: the 2-rows-per-wave forward recomputes (but does not store) a tail row
     x = bf(torch.randn(M, D, device=DEV)).requires_grad_(True)
     r = bf(torch.randn(M, D, device=DEV)).requires_grad_(True)
     g = (1.0 + 0.1 * torch.randn(D, device=DEV)).requires_grad_(True)
