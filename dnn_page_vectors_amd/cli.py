@@ -82,11 +82,17 @@ def cmd_train(a) -> int:
     if cfg.backend != "auto":
         set_backend(cfg.backend)
     torch.manual_seed(cfg.seed)
+    # placement=tower (P9, cnn_dssm_tf.py:139-158) splits the J+1 doc SLOTS of one batch over
+    # the ranks and scores every rank's queries against the gathered slots: every rank must
+    # see the SAME batch (unsharded loader, rank-independent synthetic seed); data parallel
+    # gives each rank its own shard
+    replicated = getattr(cfg, "placement", "dp") == "tower"
+    d_rank, d_world = (0, 1) if replicated else (info.rank, info.world_size)
     if a.synthetic:
         V = cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000
         gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=a.synthetic_pages), info.device,
-                             seed=cfg.seed + info.rank)
-        steps = max(1, cfg.num_train_samples // (cfg.batch_size * info.world_size))
+                             seed=cfg.seed + d_rank)
+        steps = max(1, cfg.num_train_samples // (cfg.batch_size * d_world))
         train_loader = SyntheticLoader(gen, cfg.batch_size, steps)
         val_loader = SyntheticLoader(gen, cfg.batch_size, max(1, cfg.num_validation_samples // cfg.batch_size))
     else:
@@ -96,11 +102,10 @@ def cmd_train(a) -> int:
                               cfg.num_negative_examples)
         va = JsonlPairDataset(cfg.model_validation_data, fz, cfg.query_length, cfg.document_length,
                               cfg.num_negative_examples)
-        train_loader = PairLoader(tr, cfg.batch_size, shuffle=a.shuffle, seed=cfg.seed, rank=info.rank,
-                                  world_size=info.world_size, prefetch=cfg.prefetch, device=info.device)
-        val_loader = PairLoader(va, cfg.batch_size, rank=info.rank, world_size=info.world_size,
-                                device=info.device)
-        steps = min(train_loader.num_batches(), max(1, cfg.num_train_samples // (cfg.batch_size * info.world_size)))
+        train_loader = PairLoader(tr, cfg.batch_size, shuffle=a.shuffle, seed=cfg.seed, rank=d_rank,
+                                  world_size=d_world, prefetch=cfg.prefetch, device=info.device)
+        val_loader = PairLoader(va, cfg.batch_size, rank=d_rank, world_size=d_world, device=info.device)
+        steps = min(train_loader.num_batches(), max(1, cfg.num_train_samples // (cfg.batch_size * d_world)))
     model = build_model(cfg, V)
     if cfg.feature_level == "word" and cfg.vocab_hash_size <= 1 and os.path.exists(cfg.word_vectors_file):
         from .io.vectors import cached_word_vectors, init_embedding_

@@ -53,10 +53,19 @@ class _ExplicitFn(torch.autograd.Function):
         return dq * g[:, None], dd * g[:, None, None], None, None
 
 
+# limits of the fused explicit-loss kernel (pv_dssm_explicit: one wave per row, the 1+J
+# document vectors of a row staged in registers)
+EXPLICIT_MAX_J1 = 16
+EXPLICIT_MAX_D = 512
+
+
 def dssm_explicit_loss(qn: torch.Tensor, dn: torch.Tensor, gamma: float, clip: bool = True
                        ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """qn (B, D), dn (B, 1+J, D) normalised -> (per-row loss (B,), P(D+|Q) (B,))."""
-    if use_hip(qn, dn):
+    """qn (B, D), dn (B, 1+J, D) normalised -> (per-row loss (B,), P(D+|Q) (B,)).
+
+    GPU: the fused HIP kernel when 1+J <= 16 and D <= 512; wider heads (e.g. a BERT
+    tower without projection, D = 768) take the torch expression below on the device."""
+    if use_hip(qn, dn) and dn.shape[1] <= EXPLICIT_MAX_J1 and qn.shape[1] <= EXPLICIT_MAX_D:
         return _ExplicitFn.apply(qn, dn, float(gamma), bool(clip))
     R = torch.clamp((qn.unsqueeze(1) * dn).sum(-1), 0.0, 1.0) if clip else (qn.unsqueeze(1) * dn).sum(-1)
     e = torch.exp(gamma * R - gamma * R.max(dim=1, keepdim=True).values.detach())

@@ -92,6 +92,7 @@ class Trainer:
             raise ValueError(f"unknown placement {self.placement!r}")
         if self.placement == "tower" and cfg.loss_mode != "explicit":
             raise ValueError("tower placement splits the explicit J-negative slots; use loss_mode=explicit")
+        self._replica_checked = False
         self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg")
                         if self.info.enabled else None)
         self.step = 0
@@ -128,6 +129,8 @@ class Trainer:
         range_push("forward")
         tower = self.placement == "tower" and self.info.enabled
         pre = {}
+        if tower and not self._replica_checked:
+            self._check_replicated_batch(q_ids, d_ids)
         if tower:  # every rank: same query/head seed; doc slots on their owning ranks
             q, d = placement.placed_forward(self.model, q_ids, d_ids, self._base_seed())
             dn = dops.l2_normalize(d.reshape(B * S, -1))
@@ -155,6 +158,24 @@ class Trainer:
         if tower:  # W identical heads: back-propagate 1/W of each, gradients are SUM-reduced
             loss = placement.scale_grad(loss, 1.0 / self.info.world_size)
         return loss, P
+
+    def _check_replicated_batch(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> None:
+        """Tower placement scores this rank's queries against doc slots computed on OTHER
+        ranks: all ranks must hold the same batch.  A data-parallel (sharded) loader would
+        silently train on mismatched pairs, so the first step compares a checksum of the
+        ids over the ranks (one tiny all-reduce, once)."""
+        def fp(t: torch.Tensor) -> torch.Tensor:
+            x = t.reshape(-1).to(torch.int64)
+            w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.int64) % 65521 + 1
+            return torch.stack([(x * w).sum(), x.sum(), torch.tensor(x.numel(), device=x.device)])
+        c = torch.cat([fp(q_ids), fp(d_ids)]).to(self.device).double()
+        lo, hi = c.clone(), -c
+        pdist.all_reduce_max_(hi)
+        pdist.all_reduce_max_(lo)
+        if not torch.equal(-hi, c) or not torch.equal(lo, c):
+            raise ValueError("placement='tower' needs the SAME batch on every rank (unsharded loader, "
+                             "rank-independent seed); got different batches — use placement='dp' for sharded data")
+        self._replica_checked = True
 
     GRAPH_WARMUP = 2
 
@@ -343,4 +364,7 @@ class Trainer:
         self.epoch = int(st["epoch"])
         self.skipped_steps = int(st.get("skipped_steps", 0))
         self.opt.step_count = int(st.get("opt_step", self.step))
+        # the HIP Adam reads its bias corrections from the DEVICE step counter (captured
+        # steps replay without the host): it must resume at the same count as the host one
+        self.opt.t_dev.fill_(float(self.opt.step_count))
         bump_generation()

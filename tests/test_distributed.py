@@ -155,3 +155,66 @@ def test_tower_placement_matches_single_process():
         assert abs(a - b) < 1e-5
     torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
     torch.testing.assert_close(res[0][0], tr.flat.data, rtol=1e-4, atol=3e-5)
+
+
+def _tower_sharded_worker(rank, world, port, q):
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed(device="cpu")
+    cfg = _cfg("explicit", 4).replace(placement="tower")
+    tr = Trainer(cfg, CDSSM(cfg, 150))
+    qa, da = _data(8)[0]
+    sl = slice(rank * 4, (rank + 1) * 4)  # a data-parallel shard: different batch per rank
+    try:
+        tr.train_step(qa[sl], da[sl])
+        q.put((rank, "no error"))
+    except ValueError as e:
+        q.put((rank, str(e)))
+    pdist.destroy()
+
+
+def test_tower_placement_rejects_sharded_batches():
+    """tower placement pairs this rank's queries with other ranks' doc slots, so
+    sharded (per-rank) batches must be refused instead of training on mismatched pairs."""
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_tower_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=300) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    for r in range(world):
+        assert "SAME batch" in res[r], res
+
+
+def test_cli_train_tower_placement_two_ranks(tmp_path):
+    """`train --synthetic --set placement=tower` under the launcher (gloo, 2 ranks): the CLI
+    must feed every rank the same batch (the trainer's replica check would raise otherwise)
+    and both ranks end with identical weights."""
+    import json
+    import subprocess
+    import sys
+    import textwrap
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "w.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys, torch
+        from dnn_page_vectors_amd import cli
+        rc = cli.main(["train", "--synthetic", "--synthetic-pages", "256",
+                       "--set", "experiment_root_directory={tmp_path}", "--set", "feature_level=ngram",
+                       "--set", "vocab_hash_size=150", "--set", "query_length=8", "--set", "document_length=16",
+                       "--set", "batch_size=8", "--set", "embedding_dim=12", "--set", "hidden_dims=16",
+                       "--set", "num_train_samples=32", "--set", "num_validation_samples=8", "--set", "nb_epoch=1",
+                       "--set", "placement=tower", "--set", "loss_mode=explicit", "--set", "reuse_experiment_timestamp=True"])
+        sys.exit(rc)
+    """))
+    env = dict(os.environ, PYTHONPATH=repo, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "dnn_page_vectors_amd.launch", "--nproc", "2", "--", str(script)],
+                       env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    hist = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["history"]
+    assert len(hist["loss"]) == 1 and hist["loss"][0] == hist["loss"][0]

@@ -131,9 +131,11 @@ def test_l2norm():
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("clip", [True, False])
-def test_explicit_loss(clip):
-    B, J1, D = 40, 4, 150
+@pytest.mark.parametrize("clip,J1,D", [(True, 4, 150), (False, 4, 150), (True, 4, 768), (True, 20, 128)])
+def test_explicit_loss(clip, J1, D):
+    """Fused kernel (1+J <= 16, D <= 512) and the on-device torch route beyond its limits
+    (D = 768: BERT without projection; 1+J = 20) against the fp32 expression."""
+    B = 40
     q = torch.relu(torch.randn(B, D, device=DEV))
     d = torch.relu(torch.randn(B, J1, D, device=DEV))
     qn = ref.l2_normalize(q).requires_grad_(True)
@@ -699,3 +701,45 @@ def test_cdssm_recall_quality_guard():
     assert float(m["loss"]) == float(m["loss"])
     print(f"recall@10 after 1000 steps: {r:.4f}")
     assert r >= 0.19, r
+
+
+def test_resume_restores_device_adam_step(tmp_path):
+    """the HIP Adam takes its bias corrections from the DEVICE step
+    counter; a resumed run must continue at the same count.  Train 4 steps uninterrupted
+    vs 2 steps -> checkpoint -> fresh Trainer -> resume -> 2 steps: the last update of
+    both runs must agree (with t_dev restarting at 0 the resumed update is ~3x larger)."""
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.io import checkpoint as ck
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    cfg = Configuration(feature_level="ngram", vocab_hash_size=500, query_length=12, document_length=64,
+                        batch_size=32, loss_mode="explicit", experiment_root_directory=str(tmp_path))
+    g = torch.Generator().manual_seed(4)
+    data = [(torch.randint(1, 500, (32, 12), generator=g, dtype=torch.int32).to(DEV),
+             torch.randint(1, 500, (32, 4, 64), generator=g, dtype=torch.int32).to(DEV)) for _ in range(4)]
+    ta = Trainer(cfg, CDSSM(cfg, 500), torch.device(DEV))
+    for q, d in data[:3]:
+        ta.train_step(q, d)
+    before_a = ta.flat.data.clone()
+    ta.train_step(*data[3])
+    delta_a = ta.flat.data - before_a
+
+    tb = Trainer(cfg, CDSSM(cfg, 500), torch.device(DEV))
+    for q, d in data[:2]:
+        tb.train_step(q, d)
+    ck.save_epoch(tb, str(tmp_path / "ck"), 1)
+    tc = Trainer(cfg, CDSSM(cfg, 500), torch.device(DEV))
+    assert ck.resume(tc, str(tmp_path / "ck"))
+    assert tc.opt.step_count == 2 and float(tc.opt.t_dev) == 2.0
+    tc.train_step(*data[2])
+    before_c = tc.flat.data.clone()
+    tc.train_step(*data[3])
+    delta_c = tc.flat.data - before_c
+    torch.cuda.synchronize()
+    assert float(tc.opt.t_dev) == 4.0
+    rel = float((delta_c - delta_a).norm() / delta_a.norm())
+    assert rel < 0.05, rel
+    torch.testing.assert_close(tc.flat.data, ta.flat.data, rtol=1e-3, atol=2e-4)

@@ -30,7 +30,8 @@ def main():
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--loss", default="")
     ap.add_argument("--set", nargs="*", default=[])
-    ap.add_argument("--graph", type=int, default=0, help="hipGraph steps (fenced by a device sync per replay)")
+    ap.add_argument("--graph", type=int, default=0, help="hipGraph steps")
+    ap.add_argument("--graph-fence", type=int, default=1, help="device sync after every replay (Trainer graph_fence)")
     ap.add_argument("--sync-each", action="store_true", help="synchronize + print after every step (debug)")
     ap.add_argument("--no-initial-eval", action="store_true")
     ap.add_argument("--pool", type=int, default=0, help="pre-generate this many batches and cycle them (0 = fresh batch per step)")
@@ -48,12 +49,13 @@ def main():
     dev = info.device
     data = SyntheticPairs(spec_from_config(cfg, V, num_pages=65536), dev, seed=11)
     model = build_model(cfg, V)
-    tr = Trainer(cfg, model, dev, graph=bool(a.graph))
+    tr = Trainer(cfg, model, dev, graph=bool(a.graph), graph_fence=bool(a.graph_fence))
     qe, pe = data.eval_set(a.eval_pages)
     rel = torch.arange(a.eval_pages, device=dev)
     t0 = time.time()
 
     def evaluate(step, loss):
+        print(json.dumps({"eval_begin": step}), flush=True)
         r = recall_table(model.encode(qe, "query"), model.encode(pe, "doc"), rel, ks=(1, 10, 100))
         rec = {"preset": a.preset, "step": step, "pairs_seen": step * a.batch, "loss": round(loss, 4),
                **{k: round(v, 4) for k, v in r.items()}, "wall_s": round(time.time() - t0, 1)}
