@@ -170,7 +170,6 @@ def main():
     # quality phase (untimed): continue on fresh batches so Recall@10 reflects a trained model
     done = a.warmup + a.steps
     graph_used = trainer._graph is not None
-    trainer.graph_mode = False  # fresh per-step batches run eager (see Trainer graph_fence)
     for i in range(max(0, a.quality_steps - done)):
         m = trainer.train_step(*data.batch(a.batch))
     quality_loss = float(m["loss"])

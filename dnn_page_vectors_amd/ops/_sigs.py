@@ -28,6 +28,9 @@ SIGS = {
     "pv_conv_pool_bwd_emit3_u16": "pppppp" "iii" "f" "p",
     "pv_conv_pool_bwd_reduce5_u16": "ppppp" "liiii" "upuii" "p",
     "pv_sort_iota_u32": "plppp" "li" "p",
+    # radix_sort.hip
+    "pv_rsort_temp_bytes": "lii",
+    "pv_rsort_pairs": "plpppp" "lii" "p",
     # dense.hip
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
@@ -73,7 +76,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

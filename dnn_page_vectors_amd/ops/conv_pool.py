@@ -87,6 +87,36 @@ def _grid(device: torch.device) -> int:
     return _grid_cache[idx]
 
 
+# dTable sort: the in-tree LSD radix sort (radix_sort.hip: graph-safe, no memsets / atomics);
+# PAGEVEC_SORT=rocprim selects rocPRIM's onesweep sort (A/B and reference only: its
+# hipMemsetAsync-reset state faulted under long hipGraph replays, docs/PERF.md)
+SORT_IMPL = os.environ.get("PAGEVEC_SORT", "rsort")
+
+
+def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor, end_bit: int,
+                    impl: Optional[str] = None) -> None:
+    """Stable sort of ``keys`` (int16 / int32, read as unsigned) by bits [0, end_bit): sorted
+    keys -> ``skeys``, their input positions -> ``svals`` (int32)."""
+    L_ = lib()
+    M = keys.numel()
+    s = stream(keys.device)
+    kb = keys.element_size()
+    impl = impl or SORT_IMPL
+    if impl == "rocprim":
+        if kb == 2:
+            tb = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
+            check(L_.pv_sort_iota_u16(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u16")
+        else:
+            tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
+            check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
+        return
+    tb = int(L_.pv_rsort_temp_bytes(M, end_bit, kb))
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
+    check(L_.pv_rsort_pairs(P(temp), tb, P(keys), P(skeys), None, P(svals), M, end_bit, kb, s), "pv_rsort_pairs")
+
+
 class _ConvPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, table, w3, w4, bias, tbl16, wpack, p, seed, row_offset, training, mode):
@@ -147,15 +177,10 @@ class _ConvPoolFn(torch.autograd.Function):
             if k16:
                 check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L, V,
                                                     scale, s), "pv_conv_pool_bwd_emit3_u16")
-                tb = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))
-                temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-                check(L_.pv_sort_iota_u16(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u16")
             else:
                 check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
-                tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
-                temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-                check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
+            sort_pairs_iota(keys, skeys, svals, end_bit)
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
             # bf16 weight rows [2*FW][4][EP] (the operands the forward MFMAs used)
             wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)

@@ -77,7 +77,7 @@ class PhaseTimer:
 
 class Trainer:
     def __init__(self, cfg, model: TwoTowerModel, device: Optional[torch.device] = None,
-                 metrics: Optional[MetricsLogger] = None, graph: bool = False, graph_fence: bool = True):
+                 metrics: Optional[MetricsLogger] = None, graph: bool = False, graph_fence: bool = False):
         self.cfg = cfg
         self.info = pdist.info()
         self.device = device or self.info.device
@@ -105,13 +105,14 @@ class Trainer:
         # step (forward, backward, Adam) is captured once and replayed — one launch per step
         # instead of hundreds (the launch-bound MLP / BERT steps)
         self.graph_mode = bool(graph) and self.device.type == "cuda" and not self.info.enabled
-        # graph_fence: device-synchronize after every replay.  Measured on MI355X / ROCm 7.2 /
-        # torch 2.10: replays interleaved with eager allocating work (a fresh synthetic batch
-        # per step) and no device-wide sync hit an illegal-address fault after ~97 replays,
-        # deterministically; with a device sync per replay (or device-resident pre-built
-        # batches, bench.py) 100+ replays ran clean.  The fence costs one host round trip per
-        # step; bench.py turns it off because its batches are pre-built and nothing eager
-        # runs between replays.
+        # graph_fence: optional device sync after every replay (debugging aid, off by default).
+        # Round 1 needed it: replays interleaved with eager allocating work faulted after ~97
+        # CDSSM steps inside rocPRIM's onesweep radix sort (the dTable gradient's bucketing),
+        # whose ordered-block-id counter and look-back states are reset by hipMemsetAsync
+        # nodes inside the captured graph.  The conv backward now sorts with the in-tree
+        # radix sort (csrc/kernels/radix_sort.hip: no memsets, no atomics, no look-back) and
+        # 300 unfenced replays with a fresh eager batch per step run clean
+        # (test_hipgraph_cdssm_unfenced_fresh_batches, docs/PERF.md).
         self.graph_fence = bool(graph_fence)
         self._graph = None
         self._graph_key = None

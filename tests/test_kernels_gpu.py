@@ -743,3 +743,58 @@ def test_resume_restores_device_adam_step(tmp_path):
     rel = float((delta_c - delta_a).norm() / delta_a.norm())
     assert rel < 0.05, rel
     torch.testing.assert_close(tc.flat.data, ta.flat.data, rtol=1e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize("n,kbytes,end_bit", [(1, 2, 15), (100, 2, 15), (4095, 2, 15), (4096, 4, 15), (4097, 2, 8),
+                                              (1_000_003, 2, 15), (17_203_200, 2, 15), (300_001, 4, 23),
+                                              (70_000, 4, 32)])
+@pytest.mark.parametrize("impl", ["rsort", "rocprim"])
+def test_radix_sort_matches_stable_sort(n, kbytes, end_bit, impl):
+    """The dTable sort (radix_sort.hip, and rocPRIM as the A/B alternative) == torch's stable
+    sort: same keys, same input positions (stability) — Zipf-skewed keys with a sentinel."""
+    g = torch.Generator().manual_seed(n)
+    hi = min(1 << end_bit, 60000 if kbytes == 2 else 1 << 31)
+    k = (torch.rand(n, generator=g) ** 3 * (hi - 1)).long()  # skewed toward small keys
+    k[::7] = hi - 1  # many equal keys (the dead-entry sentinel pattern)
+    if kbytes == 4 and end_bit == 32:
+        k = torch.randint(0, 1 << 32, (n,), generator=g, dtype=torch.int64)
+    dt = torch.int16 if kbytes == 2 else torch.int32
+    keys = k.to(torch.int64)
+    kin = (keys - (1 << 16) * (keys >= (1 << 15)) if kbytes == 2 else keys - (1 << 32) * (keys >= (1 << 31))).to(dt)
+    kin = kin.to(DEV)
+    skeys = torch.empty_like(kin)
+    svals = torch.empty(n, dtype=torch.int32, device=DEV)
+    if impl == "rocprim" and end_bit == 32:
+        pytest.skip("rocPRIM path covers the conv backward's key widths only")
+    cops.sort_pairs_iota(kin, skeys, svals, end_bit, impl=impl)
+    ref_k, ref_i = torch.sort(keys, stable=True)
+    mask = (1 << 16) - 1 if kbytes == 2 else (1 << 32) - 1
+    got_k = skeys.cpu().to(torch.int64) & mask
+    assert torch.equal(got_k, ref_k)
+    assert torch.equal(svals.cpu().to(torch.int64), ref_i)
+
+
+def test_hipgraph_cdssm_unfenced_fresh_batches():
+    """CDSSM steps replayed from a hipGraph with NO per-replay sync while eager work (a fresh
+    synthetic batch, i.e. new allocations) runs between replays: the pattern that faulted in
+    rocPRIM's memset-reset onesweep sort after ~97 replays.  The in-tree radix sort makes the
+    captured step self-contained; 160 replays must run clean and keep learning signal finite."""
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    assert cops.SORT_IMPL == "rsort"
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=128, document_length=512)
+    data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=8192), DEV, seed=3)
+    tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device(DEV), graph=True, graph_fence=False)
+    losses = []
+    for _ in range(160):
+        q, d = data.batch(cfg.batch_size)
+        losses.append(tr.train_step(q, d)["loss"].clone())
+    torch.cuda.synchronize()
+    assert tr._graph is not None
+    vals = [float(l) for l in losses]
+    assert all(v == v and v < 50 for v in vals), vals[-5:]

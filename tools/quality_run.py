@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--loss", default="")
     ap.add_argument("--set", nargs="*", default=[])
     ap.add_argument("--graph", type=int, default=0, help="hipGraph steps")
-    ap.add_argument("--graph-fence", type=int, default=1, help="device sync after every replay (Trainer graph_fence)")
+    ap.add_argument("--graph-fence", type=int, default=0, help="device sync after every replay (Trainer graph_fence)")
     ap.add_argument("--sync-each", action="store_true", help="synchronize + print after every step (debug)")
     ap.add_argument("--no-initial-eval", action="store_true")
     ap.add_argument("--pool", type=int, default=0, help="pre-generate this many batches and cycle them (0 = fresh batch per step)")

@@ -1,0 +1,51 @@
+"""dTable sort A/B: in-tree LSD radix sort (radix_sort.hip) vs rocPRIM onesweep, same process,
+interleaved, at the conv-backward shapes (2-byte keys < 2^15, values = positions).
+
+    python tools/sort_micro.py --M 17203200 4300800
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from dnn_page_vectors_amd.ops import conv_pool as cops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, nargs="*", default=[17_203_200, 4_300_800])
+    ap.add_argument("--end-bit", type=int, default=15)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    for M in a.M:
+        # Zipf-like token keys with a dead-entry sentinel, as the emit kernel writes them
+        r = torch.rand(M, device=dev)
+        keys = (r ** 4 * 29999).to(torch.int16)
+        keys[::5] = 30000
+        skeys = torch.empty_like(keys)
+        svals = torch.empty(M, dtype=torch.int32, device=dev)
+        res = {}
+        for impl in ("rsort", "rocprim"):
+            cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=impl)  # warm
+        torch.cuda.synchronize()
+        times = {"rsort": [], "rocprim": []}
+        for _ in range(a.iters):
+            for impl in ("rsort", "rocprim"):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=impl)
+                e1.record()
+                e1.synchronize()
+                times[impl].append(e0.elapsed_time(e1))
+        for impl, t in times.items():
+            t.sort()
+            res[impl + "_ms_median"] = round(t[len(t) // 2], 4)
+        print(json.dumps({"M": M, **res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
