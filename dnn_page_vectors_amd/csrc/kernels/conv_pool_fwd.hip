@@ -121,7 +121,11 @@ __device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u
     int q = threadIdx.x + i * NTHREADS;
     int r = q / PIECES, pc = q - r * PIECES;
     int tok = (q < CROWS * PIECES) ? ids_lds[r] : -1;
-    if ((DBG & 1) == 0 && tok >= 0 && tok < p.V) {
+    if constexpr ((DBG & 128) != 0) {  // ablation: synthetic non-zero rows, no table gather
+      const unsigned h = mix32((unsigned)tok * 13u + (unsigned)pc);
+      const unsigned w = (h & 0x807F807Fu) | 0x3C003C00u;  // two bf16 of magnitude [2^-7, 2^-6)
+      v[i] = u32x4{w, w ^ 0x80008000u, w ^ 0x00400040u, w ^ 0x80408040u};
+    } else if ((DBG & 1) == 0 && tok >= 0 && tok < p.V) {
       v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)tok * EP + pc * 8);
     } else {
       v[i] = u32x4{0u, 0u, 0u, 0u};
@@ -132,7 +136,16 @@ __device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u
 // Apply dropout to the staged pieces and write them into the LDS chunk buffer.
 // hrow[r] holds the per-row hash of this chunk (computed once per row when its token id
 // was loaded), so each 16-byte piece costs only its two group hashes.
-template <int DBG>
+// DM (dropout mode, compile time): -1 runtime (p.thr / p.token_mode), 0 off, 1 element
+// dropout at thr = 64 (p = 0.25, the reference's rate: one nibble-decision group hash per
+// piece), 2 element dropout at any thr, 3 token dropout.  The compile-time forms drop the
+// runtime mode branches (and their code) from the staging path.
+template <int DM>
+__device__ __forceinline__ bool dm_on(const Params& p) {
+  return DM < 0 ? p.thr > 0 : DM != 0;
+}
+
+template <int DBG, int DM = -1>
 __device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsigned* hrow, u32x4 (&v)[PPT]) {
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
@@ -140,13 +153,13 @@ __device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsi
     if (q < CROWS * PIECES) {
       int r = q / PIECES, pc = q - r * PIECES;
       u32x4 x = v[i];
-      if ((DBG & 4) == 0 && p.thr > 0) {
+      if ((DBG & 4) == 0 && dm_on<DM>(p)) {
         const unsigned hr = hrow[r];
-        if (p.token_mode) {
+        if (DM == 3 || (DM < 0 && p.token_mode)) {
           unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
           x = x & u32x4{m, m, m, m};
         } else {
-          x &= keep_piece(hr, pc, p.thr);
+          x &= keep_piece(hr, pc, DM == 1 ? 64 : p.thr);
         }
       }
       *reinterpret_cast<u32x4*>(xl + r * ROWB + pc * 16) = x;
@@ -155,8 +168,9 @@ __device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsi
 }
 
 // per-row dropout hash of chunk (n,c) row r (0 when dropout is off)
+template <int DM = -1>
 __device__ __forceinline__ unsigned row_hash(const Params& p, const Cursor& cu, int r) {
-  if (p.thr <= 0) return 0u;
+  if (!dm_on<DM>(p)) return 0u;
   return dropout_row_hash(p.seed, p.row_offset + (unsigned)(cu.n * p.L + cu.c * R + r));
 }
 
@@ -409,7 +423,7 @@ __device__ __forceinline__ float max_tagged(float m, float x, unsigned keep, uns
   return r;
 }
 
-template <int N3, int N4, int PF, int DBG, int OPT = 0>
+template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1>
 __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4base, char* xl0, int* ids_lds) {
   const int lane = threadIdx.x & 63;
   constexpr int A3 = N3 > 0 ? N3 : 1, A4 = N4 > 0 ? N4 : 1;
@@ -444,24 +458,24 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
     const int r = threadIdx.x + i * NTHREADS;
     if (r < CROWS) {
       ids_lds[r] = tok[i];
-      hs[r] = row_hash(p, cur, r);
+      hs[r] = row_hash<DM>(p, cur, r);
     }
   }
   __syncthreads();
   load_rows<DBG>(p, ids_lds, stage);
-  store_rows<DBG>(p, xl0, hs, stage);
+  store_rows<DBG, DM>(p, xl0, hs, stage);
   load_ids(p, c1, tok);
 #pragma unroll
   for (int i = 0; i < IDS_PT; ++i) {
     const int r = threadIdx.x + i * NTHREADS;
     if (r < CROWS) {
       ids_lds[CROWS + r] = tok[i];
-      hs[CROWS + r] = row_hash(p, c1, r);
+      hs[CROWS + r] = row_hash<DM>(p, c1, r);
     }
   }
   load_ids(p, c2, tok);
 #pragma unroll
-  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, c2, threadIdx.x + i * NTHREADS);
+  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c2, threadIdx.x + i * NTHREADS);
   __syncthreads();
   load_rows<DBG>(p, ids_lds + CROWS, stage);  // rows of c1
   // slot bookkeeping: ids/hashes of chunk c live in slot (c parity); the stage regs hold c1
@@ -696,7 +710,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
       reset_state();
     }
     // stage chunk c1 into the idle buffer (its hashes are in slot par^1), publish c2's ids/hashes
-    store_rows<DBG>(p, xl0 + (par ^ 1) * (CROWS * ROWB), hs + (par ^ 1) * CROWS, stage);
+    store_rows<DBG, DM>(p, xl0 + (par ^ 1) * (CROWS * ROWB), hs + (par ^ 1) * CROWS, stage);
 #pragma unroll
     for (int i = 0; i < IDS_PT; ++i) {
       const int r = threadIdx.x + i * NTHREADS;
@@ -709,7 +723,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
     load_rows<DBG>(p, ids_lds + par * CROWS, stage);  // rows of c2
     load_ids(p, c3, tok);
 #pragma unroll
-    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash(p, c3, threadIdx.x + i * NTHREADS);
+    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c3, threadIdx.x + i * NTHREADS);
     cur = c1;
     c1 = c2;
     c2 = c3;
@@ -740,6 +754,32 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd2_kernel(Params p) {
     case 6: run_wave2<2, 1, PF, DBG, OPT>(p, 6, 6, xl, ids_lds); break;
     case 3: run_wave2<0, 2, PF, DBG, OPT>(p, 0, 7, xl, ids_lds); break;
     default: run_wave2<2, 1, PF, DBG, OPT>(p, 8, 9, xl, ids_lds); break;
+  }
+}
+
+// v3 = the v2 schedule with (a) the dropout mode as a template parameter (DM) and (b) ONE
+// inlined body per (k3 tiles, k4 tiles) shape — 3 bodies instead of 8, the tile bases are
+// wave-uniform runtime values — so the code the 8 waves of a CU execute is ~3x smaller
+// (the v2 kernel is ~118 KB of code for 8 specialised bodies).
+template <int PF, int DBG, int OPT, int DM>
+__global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd3_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
+  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr ((OPT & 1) != 0) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  // same tile assignment as v2: SIMD s hosts waves s and s+4
+  if (wave < 2) {
+    run_wave2<3, 0, PF, DBG, OPT, DM>(p, 3 * wave, 0, xl, ids_lds);           // k3 0-2 / 3-5
+  } else if (wave >= 6) {
+    const int w7 = wave - 6;
+    run_wave2<2, 1, PF, DBG, OPT, DM>(p, 6 + 2 * w7, 6 + 3 * w7, xl, ids_lds);  // k3 6-7 k4 6 / k3 8-9 k4 9
+  } else {
+    const int t4 = wave == 2 ? 4 : wave == 3 ? 7 : wave == 4 ? 0 : 2;
+    run_wave2<0, 2, PF, DBG, OPT, DM>(p, 0, t4, xl, ids_lds);                   // k4 pairs
   }
 }
 
@@ -808,12 +848,28 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #define PV_CONV_LAUNCH(PFV, DV) \
   hipLaunchKernelGGL((conv_pool_fwd_kernel<PFV, DV>), dim3(grid), dim3(NTHREADS), 0, st, p)
   switch (dbg) {
-    case 0:  // production: v2 schedule (double-buffered chunks, tag-encoded argmax) + OPT 13:
-             // s_setprio 1 for waves 4-7, the tag mask in a VGPR (one v_and_or_b32 per element)
-             // and the partial tail blocks peeled out of the hot loop.  Same-process A/B at the
-             // bench shape: OPT 1 6.065 ms, OPT 5 6.008, OPT 9 5.938, OPT 13 5.891 (v2 without
-             // setprio measured 6.04 vs 5.94 with it on another box); the pipelined epilogue
-             // (OPT 2) measured 6.18 ms and is kept only as a variant.
+    case 0:    // production: v3 (= v2 schedule + compile-time dropout mode, 3 wave bodies; same-process
+    case 512:  // A/B vs v2 OPT 13 at the bench shape: 5.797 vs 5.899 ms, bit-identical outputs)
+    {
+      const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+      switch (dm) {
+        case 0: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 13, 0>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        case 1: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 13, 2>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        default: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 13, 3>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+      }
+      break;
+    }
+#define PV_CONV3_ABL(D) \
+    case 512 + D: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, D, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    PV_CONV3_ABL(4) PV_CONV3_ABL(128) PV_CONV3_ABL(132) PV_CONV3_ABL(2) PV_CONV3_ABL(8)
+#undef PV_CONV3_ABL
+    case 2048 + 1: hipLaunchKernelGGL((conv_pool_fwd3_kernel<1, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 2048 + 3: hipLaunchKernelGGL((conv_pool_fwd3_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 2048 + 4: hipLaunchKernelGGL((conv_pool_fwd3_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 2048 + 12: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 12, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 1024:  // v2 schedule + OPT 13 (double-buffered chunks, tag-encoded argmax, s_setprio 1 for
+                // waves 4-7, tag mask in a VGPR, peeled tail blocks), runtime dropout mode, 8 bodies
       hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0, 13>), dim3(grid), dim3(NTHREADS), 0, st, p);
       break;
     case 128: PV_CONV_LAUNCH(2, 0); break;  // v1 schedule (two barriers per chunk, cmp/select argmax)
