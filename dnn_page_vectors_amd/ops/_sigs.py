@@ -19,6 +19,9 @@ SIGS = {
     "pv_conv_pool_bwd_reduce5": "ppppp" "liiii" "upuii" "p",
     "pv_conv_pool_bwd_emit3": "ppppppp" "iii" "f" "p",
     "pv_conv_bwd_slots_per_sample": "",
+    "pv_conv_dx_dense_maxl": "",
+    "pv_conv_pool_bwd_dx_dense": "ppppppp" "iiii" "upuii" "f" "p",
+    "pv_conv_bwd_rows_reduce": "pippp" "liii" "p",
     # sort.hip
     "pv_sort_pairs_temp_bytes": "li",
     "pv_sort_pairs_u32": "plpppp" "li" "p",

@@ -117,6 +117,23 @@ def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor
     check(L_.pv_rsort_pairs(P(temp), tb, P(keys), P(skeys), None, P(svals), M, end_bit, kb, s), "pv_rsort_pairs")
 
 
+# dTable of short sequences (the query towers) from per-sample dense dX rows (N*L rows sorted by
+# token) instead of N*1050 (f, j) entries through emit -> sort -> reduce.  Same-process A/B
+# (tools/qbwd_micro.py, whole conv backward incl. dW): 4096 x 45 0.445 vs 0.459 ms, but
+# 1024 x 250 0.293 vs 0.265 ms — so only up to DENSE_DX_MAXL tokens.  PAGEVEC_DENSE_DX=0: off.
+DENSE_DX = os.environ.get("PAGEVEC_DENSE_DX", "1") != "0"
+DENSE_DX_MAXL = 64
+
+
+def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
+    """bf16 weight rows [2*FW][4][EP] (zero padded): the operands the forward MFMAs used."""
+    F, _, E = w3.shape
+    wrow = torch.zeros(2 * F, 4, ep, dtype=torch.bfloat16, device=w3.device)
+    wrow[:F, :3, :E] = w3.detach()
+    wrow[F:, :, :E] = w4.detach()
+    return wrow
+
+
 class _ConvPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, table, w3, w4, bias, tbl16, wpack, p, seed, row_offset, training, mode):
@@ -163,7 +180,23 @@ class _ConvPoolFn(torch.autograd.Function):
         check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E, V,
                                      seed, P(sp), row_offset, thr, tok, scale, s_dw), "pv_conv_pool_bwd_dw")
         dtable = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl()):
+            # short sequences (query towers): per-sample dense dX rows (LDS), sorted by token,
+            # summed per token run: N*L rows instead of N*1050 (f, j) entries
+            R = N * L
+            k16 = V < 65535
+            keys = torch.empty(R, dtype=torch.int16 if k16 else torch.int32, device=dev)
+            rows = torch.empty(R, EP, dtype=torch.float32, device=dev)
+            check(L_.pv_conv_pool_bwd_dx_dense(P(gpool), P(pooled), P(argmax), P(ids), P(_weight_rows(w3, w4, EP)),
+                                               P(rows), P(keys), 2 if k16 else 4, N, L, V, seed, P(sp), row_offset,
+                                               thr, tok, scale, s), "pv_conv_pool_bwd_dx_dense")
+            skeys = torch.empty_like(keys)
+            svals = torch.empty(R, dtype=torch.int32, device=dev)
+            sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
+            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            check(L_.pv_conv_bwd_rows_reduce(P(skeys), 2 if k16 else 4, P(svals), P(rows), P(dtable), R, 256, E, V, s),
+                  "pv_conv_bwd_rows_reduce")
+        elif ctx.needs_input_grad[1]:
             M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
             u32 = torch.int32
             end_bit = max(1, int(V).bit_length())
@@ -182,10 +215,7 @@ class _ConvPoolFn(torch.autograd.Function):
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
             sort_pairs_iota(keys, skeys, svals, end_bit)
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
-            # bf16 weight rows [2*FW][4][EP] (the operands the forward MFMAs used)
-            wrow = torch.zeros(2 * FW, 4, EP, dtype=torch.bfloat16, device=dev)
-            wrow[:FW, :3, :E] = w3.detach()
-            wrow[FW:, :, :E] = w4.detach()
+            wrow = _weight_rows(w3, w4, EP)
             if k16:
                 check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
                                                       L, E, V, seed, P(sp), row_offset, thr, tok, s),

@@ -798,3 +798,34 @@ def test_hipgraph_cdssm_unfenced_fresh_batches():
     assert tr._graph is not None
     vals = [float(l) for l in losses]
     assert all(v == v and v < 50 for v in vals), vals[-5:]
+
+
+@pytest.mark.parametrize("L,p,mode", [(45, 0.25, "element"), (20, 0.0, "element"), (250, 0.25, "element"),
+                                      (64, 0.25, "token"), (37, 0.3, "element")])
+def test_dense_dx_matches_sort_path(L, p, mode):
+    """Short-sequence dTable (per-sample dense dX in LDS + row atomics) == the emit / sort /
+    reduce path on Zipf-skewed ids (fp32 atomics both ways: equal up to summation order)."""
+    torch.manual_seed(2)
+    V, E, F, N = 700, 100, 150, 96
+    ranks = torch.arange(1, V, dtype=torch.float64)
+    probs = ranks.pow(-1.1)
+    ids = (torch.multinomial(probs / probs.sum(), N * L, replacement=True) + 1).view(N, L).to(torch.int32).to(DEV)
+    table = bf(torch.randn(V, E, device=DEV) * 0.5)
+    w3, w4 = bf(torch.randn(F, 3, E, device=DEV) * 0.1), bf(torch.randn(F, 4, E, device=DEV) * 0.1)
+    b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
+    grads = []
+    saved = cops.DENSE_DX, cops.DENSE_DX_MAXL
+    cops.DENSE_DX_MAXL = 256
+    try:
+        for dense in (False, True):
+            cops.DENSE_DX = dense
+            t = table.clone().requires_grad_(True)
+            pooled, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], b, p, 77, True, mode)
+            (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
+            grads.append(t.grad)
+    finally:
+        cops.DENSE_DX, cops.DENSE_DX_MAXL = saved
+    # fp32 sums of hundreds of terms in different orders (hot Zipf rows): absolute tolerance
+    # relative to the largest gradient entry
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=2e-5 * float(grads[0].abs().max()))
+    assert grads[0].abs().sum() > 0
