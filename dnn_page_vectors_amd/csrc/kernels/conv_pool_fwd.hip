@@ -11,13 +11,14 @@
 //    LDS span X[t*EP, (t+k)*EP): no im2col, and the A fragment of K-step s is one
 //    16-byte-aligned ds_read_b128 at byte 208*t + 64*s + 16*(lane>>4).  Both widths
 //    share the A fragments of steps 0..9; k=4 adds steps 10..12.
-//  * All 2 x 150 filters (padded to 2 x 160 = 20 tiles of 16 columns) live in
-//    REGISTERS for the whole persistent workgroup.  8 waves, two per SIMD (waves w and
-//    w+4 share a SIMD under the dispatcher's cyclic wave->SIMD order): every SIMD owns
-//    {3 k3 + 2 k4} or {2 k3 + 3 k4} tiles => 56/59 MFMAs per 16-row block (97.5%
-//    balance), split over its two waves so each wave holds <= 144 weight VGPRs — no
-//    AGPR spills/copies — and one wave's max/argmax VALU epilogue overlaps its partner's
-//    MFMAs.  Weights are loaded once per workgroup, not per sample.
+//  * All 2 x 150 filters live in REGISTERS for the whole persistent workgroup, as 9 k3
+//    tiles + 9 k4 tiles of 16 columns + ONE mixed 13-step tile (k3 filters 144..149 with
+//    a zero 4th tap beside k4 filters 144..149; v4): 220 MFMAs per 16-row block (the
+//    plain 2 x 160 padding needs 230).  8 waves, two per SIMD (waves w and w+4 share a
+//    SIMD under the dispatcher's cyclic wave->SIMD order): per-SIMD loads {56,56,56,52}
+//    MFMAs per block, split over its two waves so each wave holds <= 120 weight VGPRs —
+//    no AGPR spills/copies — and one wave's max/argmax VALU epilogue overlaps its
+//    partner's MFMAs.  Weights are loaded once per workgroup, not per sample.
 //  * Conv activations never leave registers: each lane keeps a running max and the
 //    argmax row for its 4 accumulator rows; the cross-lane reduction happens once per
 //    sample.  ReLU(max + bias) == max(ReLU(conv + bias)) because ReLU is monotone.
@@ -87,8 +88,10 @@ __device__ __forceinline__ int chunk_of_kq(int kq) { return kq == 1 ? 2 : (kq ==
 
 // fragment base index of tile T in wpack (tiles 0..9 k3 with S3 steps, 10..19 k4 with S4)
 __device__ __forceinline__ int tile_base(int T) {
-  return T < NT ? T * S3 : NT * S3 + (T - NT) * S4;
+  return T < NT ? T * S3 : NT * S3 + (T - NT) * S4;  // T = 2*NT: the mixed tile (v4), after all others
 }
+constexpr int MIXT = 2 * NT;  // mixed tile: k3 filters 144..149 (cols 0-5) + k4 filters 144..149 (cols 6-11)
+constexpr int MIXC = 6;       // k3 columns of the mixed tile
 
 struct Cursor {
   int n, c, nchunks;
@@ -423,7 +426,7 @@ __device__ __forceinline__ float max_tagged(float m, float x, unsigned keep, uns
   return r;
 }
 
-template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1>
+template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1, bool MIX = false>
 __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4base, char* xl0, int* ids_lds) {
   const int lane = threadIdx.x & 63;
   constexpr int A3 = N3 > 0 ? N3 : 1, A4 = N4 > 0 ? N4 : 1;
@@ -436,7 +439,8 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
 #pragma unroll
   for (int i = 0; i < N4; ++i)
 #pragma unroll
-    for (int s = 0; s < S4; ++s) w4[i][s] = p.wpack[(tile_base(NT + t4base + i) + s) * 64 + lane];
+    for (int s = 0; s < S4; ++s)
+      w4[i][s] = p.wpack[(tile_base((MIX && i == N4 - 1) ? MIXT : NT + t4base + i) + s) * 64 + lane];
 
   const int nchunks = (p.L - 3 + 1 + R - 1) / R;
   // chunk cursors: cur (MFMA), c1 (staged in regs / stored this iteration), c2 (ids in LDS), c3 (ids in regs)
@@ -490,6 +494,8 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
   };
   reset_state();
   const int rsub = lane & 15, kq = lane >> 4;
+  // valid-window limit of k4 tile i in a partial block (the mixed tile's k3 columns reach one more window)
+  auto lim4 = [&](int i) { return (MIX && i == N4 - 1 && rsub < MIXC) ? nw3 : nw4; };
   unsigned keep = ~TAGM;
   if constexpr ((OPT & 4) != 0) {
     // the tag mask in a VGPR: (x & keep) | btag can then be ONE v_and_or_b32 (VGPR, VGPR, SGPR)
@@ -581,7 +587,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
             if (row < nw3) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
 #pragma unroll
           for (int i = 0; i < N4; ++i)
-            if (row < nw4) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+            if (row < lim4(i)) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
         }
       }
     };
@@ -666,7 +672,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
               if (row < nw3) m3[i][r] = max_tagged(m3[i][r], c3[i][r], keep, btag);
   #pragma unroll
             for (int i = 0; i < N4; ++i)
-              if (row < nw4) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
+              if (row < lim4(i)) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
           }
         }
       }
@@ -674,7 +680,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
     // sample epilogue: decode (value, window) per register, reduce over regs and lane groups
     if (cur.c == cur.nchunks - 1) {
       flush_pending();
-      auto finish = [&](f32x4& m, int colbase) {
+      auto finish = [&](f32x4& m, int colbase, bool mixed = false) {
         float bv = -INFINITY;
         int bi = 0;
 #pragma unroll
@@ -694,7 +700,9 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
           bv = take ? ov : bv;
           bi = take ? oi : bi;
         }
-        const int col = colbase + rsub;
+        // the mixed tile's lanes map to k3 filter 144+rsub (rsub < 6) or k4 filter 144+rsub-6 (rsub < 12)
+        const int col = mixed ? (rsub < MIXC ? 144 + rsub : rsub < 2 * MIXC ? 160 + 144 + rsub - MIXC : 159)
+                              : colbase + rsub;
         if (kq == 0 && (col % 160) < FW) {
           const int f = (col / 160) * FW + (col % 160);
           PV_CHECK(bi >= 0 && bi < (col < 160 ? nw3 : nw4), PV_ERR_ARGMAX);
@@ -706,7 +714,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
 #pragma unroll
       for (int i = 0; i < N3; ++i) finish(m3[i], (t3base + i) * 16);
 #pragma unroll
-      for (int i = 0; i < N4; ++i) finish(m4[i], 160 + (t4base + i) * 16);
+      for (int i = 0; i < N4; ++i) finish(m4[i], 160 + (t4base + i) * 16, MIX && i == N4 - 1);
       reset_state();
     }
     // stage chunk c1 into the idle buffer (its hashes are in slot par^1), publish c2's ids/hashes
@@ -783,6 +791,30 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd3_kernel(Params p) {
   }
 }
 
+// v4 = v3 with the padding columns packed: 9 k3 tiles (filters 0..143), 9 k4 tiles and ONE
+// mixed 13-step tile holding k3 filters 144..149 (zero 4th tap) beside k4 filters 144..149.
+// 220 MFMAs per 16-window block instead of 230, and the per-SIMD load {56,56,56,52}
+// instead of {56,56,59,59}: the chunk barrier waits for the slowest SIMD.
+template <int PF, int DBG, int OPT, int DM>
+__global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd4_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
+  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr ((OPT & 1) != 0) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  // SIMD s hosts waves s and s+4: {k3 0-2 | k4 0-1}, {k3 3-5 | k4 2-3}, {k3 6-8 | k4 4-5}, {k4 6-7 | k4 8 + mixed}
+  if (wave < 3) {
+    run_wave2<3, 0, PF, DBG, OPT, DM>(p, 3 * wave, 0, xl, ids_lds);
+  } else if (wave == 7) {
+    run_wave2<0, 2, PF, DBG, OPT, DM, true>(p, 0, 8, xl, ids_lds);
+  } else {
+    run_wave2<0, 2, PF, DBG, OPT, DM>(p, 0, wave == 3 ? 6 : 2 * (wave - 4), xl, ids_lds);
+  }
+}
+
 PV_DEBUG_EXPORT(convfwd)
 }  // namespace convpool
 }  // namespace pv
@@ -801,6 +833,12 @@ __global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E
   int k = (T < NT) ? 3 : 4;
   const float* w = (T < NT) ? w3 : w4;
   int col = (T % NT) * 16 + (lane & 15);
+  if (T == MIXT) {  // mixed tile (v4): k3 filters 144..149, then k4 filters 144..149, then zeros
+    const int c = lane & 15;
+    k = c < MIXC ? 3 : 4;
+    w = c < MIXC ? w3 : w4;
+    col = c < MIXC ? 144 + c : c < 2 * MIXC ? 144 + c - MIXC : FW;
+  }
   bf16x8 v;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -816,7 +854,7 @@ __global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E
 PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* out, void* stream) {
   using namespace pv::convpool;
   if (E > EP) return -1;
-  int nfrag = NT * S3 + NT * S4;
+  int nfrag = NT * S3 + NT * S4 + S4;  // + the mixed tile of v4
   hipLaunchKernelGGL(pack_conv_weights_kernel, dim3(nfrag), dim3(64), 0, (hipStream_t)stream, w3, w4, E,
                      (bf16x8*)out);
   PV_LAUNCH_CHECK();
@@ -825,7 +863,7 @@ PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* o
 
 PV_API int pv_conv_packed_size() {
   using namespace pv::convpool;
-  return (NT * S3 + NT * S4) * 64 * 8;  // bf16 elements
+  return (NT * S3 + NT * S4 + S4) * 64 * 8;  // bf16 elements
 }
 
 // Diagnostic ablation switch (tools/conv_micro.py): 0 in production.
@@ -848,8 +886,8 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #define PV_CONV_LAUNCH(PFV, DV) \
   hipLaunchKernelGGL((conv_pool_fwd_kernel<PFV, DV>), dim3(grid), dim3(NTHREADS), 0, st, p)
   switch (dbg) {
-    case 0:    // production: v3 (= v2 schedule + compile-time dropout mode, 3 wave bodies; same-process
-    case 512:  // A/B vs v2 OPT 13 at the bench shape: 5.797 vs 5.899 ms, bit-identical outputs)
+    case 512:  // v3 (= v2 schedule + compile-time dropout mode, 3 wave bodies; same-process
+               // A/B vs v2 OPT 13 at the bench shape: 5.797 vs 5.899 ms, bit-identical outputs)
     {
       const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
       switch (dm) {
@@ -868,6 +906,17 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
     case 2048 + 3: hipLaunchKernelGGL((conv_pool_fwd3_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 4: hipLaunchKernelGGL((conv_pool_fwd3_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 12: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, 0, 12, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 0:       // production: v4 (same-process A/B vs v3 at the bench shape: 5.528 vs 5.691 ms,
+    case 4096: {  // bit-identical): padding columns packed into one mixed tile (220 MFMAs per block)
+      const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+      switch (dm) {
+        case 0: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 0>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        case 1: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        case 2: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 2>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+        default: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 3>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+      }
+      break;
+    }
     case 1024:  // v2 schedule + OPT 13 (double-buffered chunks, tag-encoded argmax, s_setprio 1 for
                 // waves 4-7, tag mask in a VGPR, peeled tail blocks), runtime dropout mode, 8 bodies
       hipLaunchKernelGGL((conv_pool_fwd2_kernel<2, 0, 13>), dim3(grid), dim3(NTHREADS), 0, st, p);
