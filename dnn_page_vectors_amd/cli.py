@@ -1,4 +1,4 @@
-"""Command line: ``python -m dnn_page_vectors_amd {setup,train,encode,eval,bench}``.
+"""Command line: ``python -m dnn_page_vectors_amd {setup,w2v,train,encode,eval,bench}``.
 
 The reference has no CLI — each script runs at module level with hard-coded settings
 (SURVEY §5.6).  Every subcommand here takes ``--preset``, ``--config file.yaml`` and
@@ -128,6 +128,36 @@ def cmd_train(a) -> int:
     return 0
 
 
+def cmd_w2v(a) -> int:
+    """Train word vectors on the experiment's text (reference train_word2vec,
+    dssm_cnn_v2/w2v.py:8-53) and write them where ``train`` looks for pretrained vectors
+    (``word_vectors_file``, word2vec text format); the model itself goes to
+    ``vectors/word2vec_models/<name>`` (loaded instead of retrained when present)."""
+    from .data.featurize import iter_jsonl_texts
+    from .data.text import split_features
+    from .models.word2vec import Word2Vec, model_name
+
+    cfg = _config(a)
+    files = a.input or [f for f in (cfg.model_training_data, cfg.model_validation_data) if os.path.exists(f)]
+    if not files:
+        raise SystemExit("no training text: run `setup` first or pass --input")
+    path = os.path.join(cfg.vectors_directory, "word2vec_models", model_name(cfg.embedding_dim, a.min_count, a.window))
+    if Word2Vec.exists(path) and not a.force:
+        model = Word2Vec.load(path)
+    else:
+        sents = [split_features(t, "word") for fn in files for row in iter_jsonl_texts(fn, cfg.num_negative_examples)
+                 for t in row]
+        model = Word2Vec(sents, size=cfg.embedding_dim, window=a.window, min_count=a.min_count, sample=1e-3,
+                         sg=int(a.sg), iter=a.iter, seed=cfg.seed)
+        model.init_sims(replace=True)
+        model.save(path)
+    os.makedirs(os.path.dirname(cfg.word_vectors_file), exist_ok=True)
+    model.save_word2vec_format(cfg.word_vectors_file)
+    print(json.dumps({"model": path, "vectors": cfg.word_vectors_file, "words": len(model.index2word),
+                      "dim": model.vector_size}))
+    return 0
+
+
 def cmd_encode(a) -> int:
     import numpy as np
     import torch
@@ -186,6 +216,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.add_argument("--input", default=None, help="local JSONL dataset to import")
     p.add_argument("--link", action="store_true")
     p.set_defaults(fn=cmd_setup)
+    p = sub.add_parser("w2v", help="train word2vec vectors on the experiment text (reference w2v.py)")
+    _common(p)
+    p.add_argument("--input", action="append", default=None, help="JSONL file(s); default: the train/val split")
+    p.add_argument("--window", type=int, default=10)
+    p.add_argument("--min-count", type=int, default=1)
+    p.add_argument("--iter", type=int, default=5)
+    p.add_argument("--sg", action="store_true", help="skip-gram instead of CBOW")
+    p.add_argument("--force", action="store_true", help="retrain even if the model exists")
+    p.set_defaults(fn=cmd_w2v)
     p = sub.add_parser("train")
     _common(p)
     p.add_argument("--synthetic", action="store_true")

@@ -34,6 +34,8 @@ SIGS = {
     # radix_sort.hip
     "pv_rsort_temp_bytes": "lii",
     "pv_rsort_pairs": "plpppp" "lii" "p",
+    # w2v.hip
+    "pv_w2v_train": "pppppp" "ll" "iiii" "u" "f" "i" "p",
     # dense.hip
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",

@@ -24,6 +24,9 @@ def test_cli_setup_train_encode(tmp_path):
               "--set", "embedding_dim=16", "--set", "hidden_dims=8", "--set", "num_train_samples=24",
               "--set", "num_validation_samples=8", "--set", "nb_epoch=2"]
     _run(["setup", "--input", str(src)] + common, tmp_path)
+    # word vectors trained on the split (reference w2v.py), then picked up by `train`
+    w = json.loads(_run(["w2v", "--iter", "2", "--window", "3"] + common, tmp_path).strip().splitlines()[-1])
+    assert os.path.exists(w["vectors"]) and w["dim"] == 16 and w["words"] > 10
     out = _run(["train"] + common, tmp_path)
     hist = json.loads(out.strip().splitlines()[-1])["history"]
     assert len(hist["loss"]) == 2 and len(hist["val_loss"]) == 2
