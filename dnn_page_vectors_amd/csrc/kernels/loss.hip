@@ -20,6 +20,7 @@
 //       ib_pos      : the positive logit (same bf16 inputs) and the one-hot term of
 //                     the gradient, -gscale*g*clip' * {d_pos, q}.
 #include "common.h"
+#include <type_traits>
 
 namespace pv {
 namespace loss {
@@ -185,11 +186,14 @@ __device__ __forceinline__ void load_xb(const unsigned short* __restrict__ X, in
   }
 }
 
-template <int KS>
+// CLIP (compile time) and FULL (a uniform branch per tile: only a split's last tile can be
+// partial) keep the per-element epilogue to fmed3 + fma + exp2 + add: the exp epilogue, not
+// the MFMAs, bounds these kernels (one exp per 320 MFMA FLOPs at D = 160).
+template <int KS, bool CLIP>
 __global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Y,
                                                          float* __restrict__ part, int nx, int ny, int per_split,
-                                                         float gamma, int clip) {
+                                                         float gamma) {
   using T = IbTile<KS>;
   __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
@@ -207,21 +211,27 @@ __global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __
   for (int c0 = c_begin; c0 < c_end; c0 += TD, buf ^= 1) {
     const bool more = c0 + TD < c_end;
     if (more) ib_load<KS>(Y, c0 + TD, c_end, st);
-    const bool full = c0 + TD <= c_end;
     f32x4 acc[4][2];
     st_tile<KS>(xb, yt[buf], acc);
+    auto epi = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool yv = full || c0 + c * 16 + 4 * g + r < c_end;
+        for (int r = 0; r < 4; ++r) {
+          const bool yv = FULL || c0 + c * 16 + 4 * g + r < c_end;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float v = acc[c][i][r];
-          if (clip) v = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
-          rs[i] += yv ? __builtin_amdgcn_exp2f(__builtin_fmaf(v, gl, -gl)) : 0.f;
+          for (int i = 0; i < 2; ++i) {
+            float v = acc[c][i][r];
+            if constexpr (CLIP) v = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+            float x = __builtin_fmaf(v, gl, -gl);
+            if constexpr (!FULL) x = yv ? x : -INFINITY;
+            rs[i] += __builtin_amdgcn_exp2f(x);
+          }
         }
-      }
+    };
+    if (c0 + TD <= c_end) epi(std::true_type{});
+    else epi(std::false_type{});
     if (more) ib_store<KS>(yt[buf ^ 1], st);
     __syncthreads();
   }
@@ -249,16 +259,16 @@ __global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restri
 // Each split writes its partial product with plain stores into out (a single split) or
 // into its slice of the workspace ws[split][nx][DP]; ib_split_reduce sums the slices
 // (fp32 atomics from 16-32 splits cost ~4x more than the extra write + read).
-template <int KS, bool ROW>
+template <int KS, bool ROW, bool CLIP>
 __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Y,
                                                          const float* __restrict__ scale, float* __restrict__ out,
                                                          float* __restrict__ ws, int nx, int ny, int per_split,
-                                                         float gamma, int clip) {
+                                                         float gamma) {
   using T = IbTile<KS>;
   constexpr int NC = T::DP / 16;
   __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
-  __shared__ float ysc[2][TD];
+  __shared__ __attribute__((aligned(16))) float ysc[2][TD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int r0 = blockIdx.x * TQ + wave * 32;
   const int c_begin = blockIdx.y * per_split, c_end = min(ny, c_begin + per_split);
@@ -298,26 +308,40 @@ __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __
     f32x4 acc[4][2];
     st_tile<KS>(xb, yb, acc);
     // G^T in registers -> bf16 B fragments gb[s2][i] (s2: 32-row k-step of the tile);
-    // exp(g*(v-1)) = exp2(v*gl - gl) with gl = g*log2(e)
-    const bool full = c0 + TD <= c_end;
+    // exp(g*(v-1)) = exp2(v*gl - gl) with gl = g*log2(e).  A dropped element (outside the
+    // clip range, or past the split's last row) gets exponent -inf: exp2 returns 0, one
+    // select instead of a compare-and-select on the product.
     u32x4 gp[2][2];
+    auto epi = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c) {
+        f32x4 ysv;
+        if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[buf][c * 16 + 4 * g]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        float gv[4];
+        for (int i = 0; i < 2; ++i) {
+          float gv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int yr = c * 16 + 4 * g + r;
-          const float v = acc[c][i][r];
-          const float vc = clip ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
-          const bool ok = (!clip || vc == v) && (full || c0 + yr < c_end);
-          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(vc, gl, -gl));
-          gv[r] = ok ? (ROW ? rsc[i] : ysc[buf][yr]) * e : 0.f;
+          for (int r = 0; r < 4; ++r) {
+            const int yr = c * 16 + 4 * g + r;
+            const float v = acc[c][i][r];
+            float x;
+            if constexpr (CLIP) {
+              const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+              x = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
+            } else {
+              x = __builtin_fmaf(v, gl, -gl);
+            }
+            if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
+            gv[r] = (ROW ? rsc[i] : ysv[r]) * __builtin_amdgcn_exp2f(x);
+          }
+          gp[c >> 1][i][(c & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
+          gp[c >> 1][i][(c & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
         }
-        gp[c >> 1][i][(c & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
-        gp[c >> 1][i][(c & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
       }
+    };
+    if (c0 + TD <= c_end) epi(std::true_type{});
+    else epi(std::false_type{});
     // out^T[feat][x] += Y^T[feat][y] . G^T[y][x]
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -478,9 +502,15 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
   const int ns = ib_fwd_splits(nx, ny);
   const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
   dim3 grid((nx + TQ - 1) / TQ, ns);
-  IB_DISPATCH(DP / 32, hipLaunchKernelGGL(ib_fwd_kernel<KS>, grid, dim3(256), 0, (hipStream_t)stream,
-                                          (const unsigned short*)X, (const unsigned short*)Y, ws, nx, ny, per,
-                                          gamma, clip));
+  if (clip) {
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_fwd_kernel<KS, true>), grid, dim3(256), 0, (hipStream_t)stream,
+                                            (const unsigned short*)X, (const unsigned short*)Y, ws, nx, ny, per,
+                                            gamma));
+  } else {
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_fwd_kernel<KS, false>), grid, dim3(256), 0, (hipStream_t)stream,
+                                            (const unsigned short*)X, (const unsigned short*)Y, ws, nx, ny, per,
+                                            gamma));
+  }
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, sumexp, nx, ns);
   PV_LAUNCH_CHECK();
@@ -513,15 +543,16 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   if (ns > 1 && !ws) return -3;
   dim3 grid((nx + TQ - 1) / TQ, ns);
   hipStream_t s = (hipStream_t)stream;
+#define PV_IB_BWD(ROWV, CLIPV)                                                                              \
+  IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, ROWV, CLIPV>), grid, dim3(256), 0, s,           \
+                                          (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, \
+                                          ny, per, gamma))
   if (row_scale) {
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true>), grid, dim3(256), 0, s,
-                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx,
-                                            ny, per, gamma, clip));
+    if (clip) { PV_IB_BWD(true, true); } else { PV_IB_BWD(true, false); }
   } else {
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, false>), grid, dim3(256), 0, s,
-                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx,
-                                            ny, per, gamma, clip));
+    if (clip) { PV_IB_BWD(false, true); } else { PV_IB_BWD(false, false); }
   }
+#undef PV_IB_BWD
   PV_LAUNCH_CHECK();
   if (ns > 1) {
     const long n4 = (long)nx * DP / 4;
