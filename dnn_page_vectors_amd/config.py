@@ -114,6 +114,7 @@ class Configuration:
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
     grad_bucket_mb: float = 32.0
+    query_stream: bool = True             # query tower (fwd, hence bwd) on a side HIP stream
     placement: str = "dp"                # dp (data parallel) | tower (slots over ranks, cnn_dssm_tf.py:139-158)
     log_every: int = 10
     skip_nonfinite: bool = True

@@ -72,8 +72,35 @@ class TwoTowerModel(nn.Module):
                              for s in range(S)], dim=1)
         if doc_hook is not None:
             doc_hook(d)
-        q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
+        side = self._query_stream(q_ids)
+        if side is None:
+            q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
+            return q, d
+        # The query tower on a side stream: autograd runs each backward op on the stream of
+        # its forward op, so the query tower's backward (its own sparse conv backward, sort,
+        # dense GEMMs) overlaps the page tower's on the main stream; the engine joins the
+        # streams before backward() returns.
+        main = torch.cuda.current_stream(q_ids.device)
+        side.wait_stream(main)
+        q_ids.record_stream(side)
+        with torch.cuda.stream(side):
+            q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
+        main.wait_stream(side)
+        q.record_stream(main)
         return q, d
+
+    def _query_stream(self, q_ids: torch.Tensor) -> Optional[torch.cuda.Stream]:
+        if not (q_ids.is_cuda and self.training and getattr(self.cfg, "query_stream", False)):
+            return None
+        if torch.cuda.is_current_stream_capturing():  # hipGraph capture: one stream
+            return None
+        st = getattr(self, "_qstreams", None)
+        if st is None:
+            st = self._qstreams = {}
+        dev = q_ids.device.index
+        if dev not in st:
+            st[dev] = torch.cuda.Stream(device=q_ids.device)
+        return st[dev]
 
     @torch.no_grad()
     def encode(self, ids: torch.Tensor, tower: str = "doc", batch_size: int = 4096,
