@@ -259,12 +259,18 @@ __global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restri
 // Each split writes its partial product with plain stores into out (a single split) or
 // into its slice of the workspace ws[split][nx][DP]; ib_split_reduce sums the slices
 // (fp32 atomics from 16-32 splits cost ~4x more than the extra write + read).
-template <int KS, bool ROW, bool CLIP>
+// FWD (with ROW, X = queries): the forward pass that also produces the query gradient's
+// normaliser-free part U = sum_j exp(g*(S_ij - 1)) * clip'_ij * Y_j, and the row sums
+// sum_j exp(g*(S_ij - 1)) into `part` like ib_fwd.  dQ_i is a per-row multiple of U_i
+// (scale_i = g_up_i * gamma / sumexp_i, known only in backward, is a row scalar), so the
+// backward's dQ pass — a third recomputation of S — disappears: dQ = scale * U.
+template <int KS, bool ROW, bool CLIP, bool FWD = false>
 __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Y,
                                                          const float* __restrict__ scale, float* __restrict__ out,
                                                          float* __restrict__ ws, int nx, int ny, int per_split,
-                                                         float gamma) {
+                                                         float gamma, float* __restrict__ part = nullptr) {
+  static_assert(!FWD || ROW, "the fused forward runs over query rows");
   using T = IbTile<KS>;
   constexpr int NC = T::DP / 16;
   __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
@@ -276,11 +282,12 @@ __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __
   bf16x8 xb[2][KS];
   load_xb<KS>(X, r0, nx, xb);
   float rsc[2] = {0.f, 0.f};
+  float rs[2] = {0.f, 0.f};  // FWD: row sums of exp(g*(S-1))
   if (ROW) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r = r0 + i * 16 + (lane & 15);
-      rsc[i] = r < nx ? scale[r] : 0.f;
+      rsc[i] = FWD ? 1.f : r < nx ? scale[r] : 0.f;
     }
   }
   f32x4 o[NC][2];
@@ -326,6 +333,15 @@ __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __
             const int yr = c * 16 + 4 * g + r;
             const float v = acc[c][i][r];
             float x;
+            if constexpr (FWD) {  // every valid element counts in the row sum; clip' masks G
+              const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
+              x = __builtin_fmaf(vc, gl, -gl);
+              if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
+              const float e = __builtin_amdgcn_exp2f(x);
+              rs[i] += e;
+              gv[r] = (!CLIP || vc == v) ? e : 0.f;
+              continue;
+            }
             if constexpr (CLIP) {
               const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
               x = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
@@ -361,6 +377,16 @@ __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __
       if (!ROW && threadIdx.x < TD) ysc[buf ^ 1][threadIdx.x] = scv;
     }
     __syncthreads();
+  }
+  if constexpr (FWD) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int r = r0 + i * 16 + (lane & 15);
+      if (g == 0 && r < nx) part[(size_t)blockIdx.y * nx + r] = v;  // summed in split order by ib_rowsum
+    }
   }
   // o[n][i][r] = out[x = r0 + i*16 + (lane&15)][feat = n*16 + 4g + r]
   float* dst = gridDim.y == 1 ? out : ws + (size_t)blockIdx.y * nx * T::DP;
@@ -559,6 +585,44 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
     long blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(ib_split_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, out, n4, ns);
+    PV_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+// Fused forward + dQ part (see ib_bwd_kernel FWD): sumexp (nx), U (nx, DP) fp32 fully
+// written; ws_u = pv_ib_bwd_ws(nx, ny, DP) floats, part = pv_ib_fwd_dq_parts(nx, ny) floats.
+PV_API long pv_ib_fwd_dq_parts(int nx, int ny) {
+  using namespace pv::loss;
+  int ns = ib2_splits(nx, ny);
+  const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
+  return (long)((ny + per - 1) / per) * nx;
+}
+
+PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, float* ws_u, float* part, int nx,
+                        int ny, int DP, float gamma, int clip, void* stream) {
+  using namespace pv::loss;
+  if (DP % 32 || DP > 192) return -2;
+  int ns = ib2_splits(nx, ny);
+  const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
+  ns = (ny + per - 1) / per;
+  if (ns > 1 && !ws_u) return -3;
+  dim3 grid((nx + TQ - 1) / TQ, ns);
+  hipStream_t s = (hipStream_t)stream;
+#define PV_IB_FWDDQ(CLIPV)                                                                                    \
+  IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true, CLIPV, true>), grid, dim3(256), 0, s,       \
+                                          (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u,  \
+                                          nx, ny, per, gamma, part))
+  if (clip) { PV_IB_FWDDQ(true); } else { PV_IB_FWDDQ(false); }
+#undef PV_IB_FWDDQ
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, s, part, sumexp, nx, ns);
+  PV_LAUNCH_CHECK();
+  if (ns > 1) {
+    const long n4 = (long)nx * DP / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(ib_split_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws_u, U, n4, ns);
     PV_LAUNCH_CHECK();
   }
   return 0;

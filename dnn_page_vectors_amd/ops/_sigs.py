@@ -49,6 +49,8 @@ SIGS = {
     "pv_ib_bwd_ws": "iii",
     "pv_attn_fwd": "pppp" "iii" "f" "p",
     "pv_attn_bwd": "ppppppp" "iii" "f" "p",
+    "pv_ib_fwd_dq_parts": "ii",
+    "pv_ib_fwd_dq": "pppppp" "iiif" "i" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
@@ -81,7 +83,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
 }
 
-_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

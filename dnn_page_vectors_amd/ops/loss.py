@@ -81,6 +81,25 @@ def _pad_bf16(x: torch.Tensor, DP: int) -> torch.Tensor:
     return out
 
 
+def _ib_forward(qb: torch.Tensor, db: torch.Tensor, B: int, M: int, DP: int, gamma: float, clip: int,
+                with_dq: bool) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """sumexp (B,) and, when the query gradient will be needed, its normaliser-free part
+    U (B, DP) from the SAME pass over S (pv_ib_fwd_dq): the backward's dQ = scale * U."""
+    s = stream(qb.device)
+    L_ = lib()
+    sumexp = torch.empty(B, dtype=torch.float32, device=qb.device)
+    if not with_dq:
+        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qb.device)
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        return sumexp, None
+    U = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
+    ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), 1), dtype=torch.float32, device=qb.device)
+    part = torch.empty(L_.pv_ib_fwd_dq_parts(B, M), dtype=torch.float32, device=qb.device)
+    check(L_.pv_ib_fwd_dq(P(qb), P(db), P(sumexp), P(U), P(ws), P(part), B, M, DP, float(gamma), int(clip), s),
+          "pv_ib_fwd_dq")
+    return sumexp, U
+
+
 class _InBatchFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qn, dn, pos, gamma, clip):
@@ -93,31 +112,33 @@ class _InBatchFn(torch.autograd.Function):
         qb = _pad_bf16(qn.detach(), DP)
         db = _pad_bf16(dn.detach(), DP)
         pos = pos.to(torch.int32).contiguous()
-        sumexp = torch.empty(B, dtype=torch.float32, device=qn.device)
         spos = torch.empty(B, dtype=torch.float32, device=qn.device)
         L_ = lib()
-        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qn.device)
-        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        sumexp, U = _ib_forward(qb, db, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
               "pv_ib_pos")
         loss = gamma + torch.log(sumexp) - spos
-        ctx.save_for_backward(qb, db, pos, sumexp)
+        ctx.save_for_backward(qb, db, pos, sumexp, U)
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
         return loss, torch.exp(-loss).detach()
 
     @staticmethod
     def backward(ctx, gl, _gp):
-        qb, db, pos, sumexp = ctx.saved_tensors
+        qb, db, pos, sumexp, U = ctx.saved_tensors
         B, M, D, DP, gamma, clip = ctx.meta
         s = stream(qb.device)
         L_ = lib()
         g = gl.contiguous().float()
         scale = (g * gamma / sumexp).contiguous()
-        dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
         dd = torch.empty(M, DP, dtype=torch.float32, device=qb.device)
-        ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
-                         dtype=torch.float32, device=qb.device)
-        check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
+        ws = torch.empty(max(L_.pv_ib_bwd_ws(M, B, DP), 1), dtype=torch.float32, device=qb.device)
+        if U is not None:
+            dq = U * scale[:, None]
+        else:
+            dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
+            ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
+                             dtype=torch.float32, device=qb.device)
+            check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
         check(L_.pv_ib_bwd(P(db), P(qb), P(scale), P(dd), P(ws), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
         return dq[:, :D], dd[:, :D], None, None, None
@@ -197,11 +218,9 @@ class _CrossGpuFn(torch.autograd.Function):
             dist.all_gather_into_tensor(db, dbl, group=group)
         pos_local = pos_local.to(torch.int32).contiguous()
         pos = (pos_local + rank * n).contiguous()
-        sumexp = torch.empty(B, dtype=torch.float32, device=qn.device)
         spos = torch.empty(B, dtype=torch.float32, device=qn.device)
         L_ = lib()
-        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qn.device)
-        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
+        sumexp, U = _ib_forward(qb, db, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
               "pv_ib_pos")
         loss = gamma + torch.log(sumexp) - spos
@@ -213,13 +232,13 @@ class _CrossGpuFn(torch.autograd.Function):
         # a plain attribute, not a saved tensor: the in-flight collective writes qall after
         # this point (gloo copies the result back on completion, bumping its version)
         ctx.qall = qall
-        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp)
+        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp, U)
         ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
         return loss, torch.exp(-loss).detach()
 
     @staticmethod
     def backward(ctx, gl, _gp):
-        qb, db, dbl, pos_local, sumexp = ctx.saved_tensors
+        qb, db, dbl, pos_local, sumexp, U = ctx.saved_tensors
         B, M, n, D, DP, gamma, clip, group, W = ctx.meta
         s = stream(qb.device)
         L_ = lib()
@@ -228,11 +247,14 @@ class _CrossGpuFn(torch.autograd.Function):
         # every rank's per-query softmax scale (B floats each), gathered while dQ runs
         scale_all = torch.empty(B * W, dtype=torch.float32, device=qb.device)
         swork = dist.all_gather_into_tensor(scale_all, scale, group=group, async_op=True)
-        dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
         dd = torch.empty(n, DP, dtype=torch.float32, device=qb.device)
         ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(n, B * W, DP), 1),
                          dtype=torch.float32, device=qb.device)
-        check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
+        if U is not None:  # the forward already summed exp * clip' * d over ALL ranks' pages
+            dq = U * scale[:, None]
+        else:
+            dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
+            check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
         ctx.qwork.wait()
         ctx.qwork = None
         qall, ctx.qall = ctx.qall, None
