@@ -902,6 +902,8 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
     case 512 + D: hipLaunchKernelGGL((conv_pool_fwd3_kernel<2, D, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     PV_CONV3_ABL(4) PV_CONV3_ABL(128) PV_CONV3_ABL(132) PV_CONV3_ABL(2) PV_CONV3_ABL(8)
 #undef PV_CONV3_ABL
+    case 4096 + 512 + 4: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 4, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    case 4096 + 512 + 2: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 2, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 1: hipLaunchKernelGGL((conv_pool_fwd4_kernel<1, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 3: hipLaunchKernelGGL((conv_pool_fwd4_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 4: hipLaunchKernelGGL((conv_pool_fwd4_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;

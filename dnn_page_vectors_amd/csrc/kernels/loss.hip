@@ -245,13 +245,22 @@ __global__ __launch_bounds__(256, 2) void ib_fwd_kernel(const unsigned short* __
   }
 }
 
-// sumexp[r] = sum_s part[s][r] in a fixed order (the forward loss is bit-reproducible)
-__global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restrict__ out, int nx, int ns) {
+// sumexp[r] = sum_s part[s][r] in a fixed order (the forward loss is bit-reproducible);
+// with spos (the positive logit g*clip(cos+), ib_pos) also the per-row loss
+// g + log(sumexp) - spos (= -log P+ of the softmax over exp(g*(S-1))) and P+ = exp(-loss).
+__global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restrict__ out, int nx, int ns,
+                                 const float* __restrict__ spos = nullptr, float* __restrict__ loss = nullptr,
+                                 float* __restrict__ prob = nullptr, float gamma = 0.f) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nx) return;
   float a = 0.f;
   for (int s = 0; s < ns; ++s) a += part[(size_t)s * nx + r];
   out[r] = a;
+  if (spos) {
+    const float l = gamma + __logf(a) - spos[r];
+    loss[r] = l;
+    prob[r] = __expf(-l);
+  }
 }
 
 // ROW = true : X = queries, Y = docs,    out = dQ, scale indexed by X row
@@ -522,7 +531,7 @@ PV_API long pv_ib_fwd_ws(int nx, int ny, int DP) {
 }
 
 PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int nx, int ny, int DP, float gamma,
-                     int clip, void* stream) {
+                     int clip, const float* spos, float* loss, float* prob, void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
   const int ns = ib_fwd_splits(nx, ny);
@@ -538,7 +547,8 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
                                             gamma));
   }
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, sumexp, nx, ns);
+  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, sumexp, nx, ns,
+                     spos, loss, prob, gamma);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -600,7 +610,8 @@ PV_API long pv_ib_fwd_dq_parts(int nx, int ny) {
 }
 
 PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, float* ws_u, float* part, int nx,
-                        int ny, int DP, float gamma, int clip, void* stream) {
+                        int ny, int DP, float gamma, int clip, const float* spos, float* loss, float* prob,
+                        void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
   int ns = ib2_splits(nx, ny);
@@ -616,7 +627,8 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   if (clip) { PV_IB_FWDDQ(true); } else { PV_IB_FWDDQ(false); }
 #undef PV_IB_FWDDQ
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, s, part, sumexp, nx, ns);
+  hipLaunchKernelGGL(ib_rowsum_kernel, dim3((nx + 255) / 256), dim3(256), 0, s, part, sumexp, nx, ns, spos, loss,
+                     prob, gamma);
   PV_LAUNCH_CHECK();
   if (ns > 1) {
     const long n4 = (long)nx * DP / 4;

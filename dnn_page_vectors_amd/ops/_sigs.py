@@ -43,14 +43,14 @@ SIGS = {
     "pv_act_bwd": "ppp" "li" "p",
     # loss.hip
     "pv_dssm_explicit": "pppppp" "iii" "ffi" "p",
-    "pv_ib_fwd": "pppp" "iii" "fi" "p",
+    "pv_ib_fwd": "pppp" "iii" "fi" "ppp" "p",
     "pv_ib_fwd_ws": "iii",
     "pv_ib_bwd": "ppppp" "iii" "fii" "p",
     "pv_ib_bwd_ws": "iii",
     "pv_attn_fwd": "pppp" "iii" "f" "p",
     "pv_attn_bwd": "ppppppp" "iii" "f" "p",
     "pv_ib_fwd_dq_parts": "ii",
-    "pv_ib_fwd_dq": "pppppp" "iiif" "i" "p",
+    "pv_ib_fwd_dq": "pppppp" "iiif" "i" "ppp" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip

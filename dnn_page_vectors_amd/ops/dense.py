@@ -88,10 +88,18 @@ class _L2NormFn(torch.autograd.Function):
         M, D = x2.shape
         y = torch.empty_like(x2)
         inv = torch.empty(M, dtype=torch.float32, device=x.device)
-        check(lib().pv_l2norm_fwd(P(x2), P(y), P(inv), None, M, D, D, stream(x.device)), "pv_l2norm_fwd")
+        # the cosine-softmax losses read the vectors as zero-padded bf16 rows (32-multiple
+        # width): written by the same kernel, handed over as an attribute of the output
+        DP = (D + 31) // 32 * 32
+        ybf = torch.empty(M, DP, dtype=torch.bfloat16, device=x.device) if DP <= 192 else None
+        check(lib().pv_l2norm_fwd(P(x2), P(y), P(inv), P(ybf), M, D, DP if ybf is not None else D, stream(x.device)),
+              "pv_l2norm_fwd")
         ctx.save_for_backward(x2, y, inv)
         ctx.shape = x.shape
-        return y.view(x.shape)
+        out = y.view(x.shape)
+        if ybf is not None and len(x.shape) == 2:
+            out._pv_bf16 = ybf
+        return out
 
     @staticmethod
     def backward(ctx, dy):

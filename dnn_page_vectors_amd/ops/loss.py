@@ -75,29 +75,40 @@ def dssm_explicit_loss(qn: torch.Tensor, dn: torch.Tensor, gamma: float, clip: b
 
 
 def _pad_bf16(x: torch.Tensor, DP: int) -> torch.Tensor:
+    pre = getattr(x, "_pv_bf16", None)  # written by the L2-normalise kernel (ops/dense.py)
+    if pre is not None and pre.shape == (x.shape[0], DP) and pre.device == x.device:
+        return pre
     n, D = x.shape
     out = torch.zeros(n, DP, dtype=torch.bfloat16, device=x.device)
-    out[:, :D] = x
+    out[:, :D] = x.detach()
     return out
 
 
-def _ib_forward(qb: torch.Tensor, db: torch.Tensor, B: int, M: int, DP: int, gamma: float, clip: int,
-                with_dq: bool) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """sumexp (B,) and, when the query gradient will be needed, its normaliser-free part
-    U (B, DP) from the SAME pass over S (pv_ib_fwd_dq): the backward's dQ = scale * U."""
+def _ib_forward(qb: torch.Tensor, db: torch.Tensor, pos: torch.Tensor, B: int, M: int, DP: int, gamma: float,
+                clip: int, with_dq: bool):
+    """-> (per-row loss, P+, sumexp, U).  The positive logit first (ib_pos), then ONE pass
+    over S whose row-sum kernel also finalises loss = g + log(sumexp) - spos and P+.
+    When the query gradient will be needed, the same pass produces its normaliser-free
+    part U (B, DP) (pv_ib_fwd_dq): the backward's dQ = scale * U."""
     s = stream(qb.device)
     L_ = lib()
-    sumexp = torch.empty(B, dtype=torch.float32, device=qb.device)
+    dev = qb.device
+    spos = torch.empty(B, dtype=torch.float32, device=dev)
+    check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s), "pv_ib_pos")
+    sumexp = torch.empty(B, dtype=torch.float32, device=dev)
+    loss = torch.empty(B, dtype=torch.float32, device=dev)
+    prob = torch.empty(B, dtype=torch.float32, device=dev)
     if not with_dq:
-        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=qb.device)
-        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), s), "pv_ib_fwd")
-        return sumexp, None
-    U = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
-    ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), 1), dtype=torch.float32, device=qb.device)
-    part = torch.empty(L_.pv_ib_fwd_dq_parts(B, M), dtype=torch.float32, device=qb.device)
-    check(L_.pv_ib_fwd_dq(P(qb), P(db), P(sumexp), P(U), P(ws), P(part), B, M, DP, float(gamma), int(clip), s),
-          "pv_ib_fwd_dq")
-    return sumexp, U
+        part = torch.empty(L_.pv_ib_fwd_ws(B, M, DP), dtype=torch.float32, device=dev)
+        check(L_.pv_ib_fwd(P(qb), P(db), P(sumexp), P(part), B, M, DP, float(gamma), int(clip), P(spos), P(loss),
+                           P(prob), s), "pv_ib_fwd")
+        return loss, prob, sumexp, None
+    U = torch.empty(B, DP, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), 1), dtype=torch.float32, device=dev)
+    part = torch.empty(L_.pv_ib_fwd_dq_parts(B, M), dtype=torch.float32, device=dev)
+    check(L_.pv_ib_fwd_dq(P(qb), P(db), P(sumexp), P(U), P(ws), P(part), B, M, DP, float(gamma), int(clip), P(spos),
+                          P(loss), P(prob), s), "pv_ib_fwd_dq")
+    return loss, prob, sumexp, U
 
 
 class _InBatchFn(torch.autograd.Function):
@@ -108,19 +119,14 @@ class _InBatchFn(torch.autograd.Function):
         DP = (D + 31) // 32 * 32
         if DP > 192:
             raise ValueError("in-batch loss kernel supports D <= 192")
-        s = stream(qn.device)
-        qb = _pad_bf16(qn.detach(), DP)
-        db = _pad_bf16(dn.detach(), DP)
+        qb = _pad_bf16(qn, DP)
+        db = _pad_bf16(dn, DP)
         pos = pos.to(torch.int32).contiguous()
-        spos = torch.empty(B, dtype=torch.float32, device=qn.device)
-        L_ = lib()
-        sumexp, U = _ib_forward(qb, db, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
-        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
-              "pv_ib_pos")
-        loss = gamma + torch.log(sumexp) - spos
+        loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
         ctx.save_for_backward(qb, db, pos, sumexp, U)
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
-        return loss, torch.exp(-loss).detach()
+        ctx.mark_non_differentiable(prob)
+        return loss, prob
 
     @staticmethod
     def backward(ctx, gl, _gp):
@@ -180,7 +186,7 @@ class PageGather:
         W = dist.get_world_size(group)
         self.D = dn.shape[1]
         self.DP = (self.D + 31) // 32 * 32
-        self.dbl = _pad_bf16(dn.detach(), self.DP)
+        self.dbl = _pad_bf16(dn, self.DP)
         self.db = torch.empty(dn.shape[0] * W, self.DP, dtype=torch.bfloat16, device=dn.device)
         self.work = dist.all_gather_into_tensor(self.db, self.dbl, group=group, async_op=True)
         self.source = dn
@@ -208,22 +214,17 @@ class _CrossGpuFn(torch.autograd.Function):
         n = dn.shape[0]
         M = n * W
         DP = (D + 31) // 32 * 32
-        s = stream(qn.device)
-        qb = _pad_bf16(qn.detach(), DP)
+        qb = _pad_bf16(qn, DP)
         if pre is not None:
             dbl, db = pre.wait()
         else:
-            dbl = _pad_bf16(dn.detach(), DP)
+            dbl = _pad_bf16(dn, DP)
             db = torch.empty(M, DP, dtype=torch.bfloat16, device=qn.device)
             dist.all_gather_into_tensor(db, dbl, group=group)
         pos_local = pos_local.to(torch.int32).contiguous()
         pos = (pos_local + rank * n).contiguous()
-        spos = torch.empty(B, dtype=torch.float32, device=qn.device)
-        L_ = lib()
-        sumexp, U = _ib_forward(qb, db, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
-        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
-              "pv_ib_pos")
-        loss = gamma + torch.log(sumexp) - spos
+        loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
+        ctx.mark_non_differentiable(prob)
         # the backward scores the LOCAL pages against ALL ranks' queries (dD needs no
         # cross-rank sum then): gather the bf16 queries now, in flight during the rest of
         # the forward and the tower's own backward (B*DP*2 bytes per rank)
@@ -234,7 +235,7 @@ class _CrossGpuFn(torch.autograd.Function):
         ctx.qall = qall
         ctx.save_for_backward(qb, db, dbl, pos_local, sumexp, U)
         ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
-        return loss, torch.exp(-loss).detach()
+        return loss, prob
 
     @staticmethod
     def backward(ctx, gl, _gp):
