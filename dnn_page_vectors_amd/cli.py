@@ -1,4 +1,4 @@
-"""Command line: ``python -m dnn_page_vectors_amd {setup,w2v,train,encode,eval,bench}``.
+"""Command line: ``python -m dnn_page_vectors_amd {setup,w2v,train,encode,eval,serve,bench}``.
 
 The reference has no CLI — each script runs at module level with hard-coded settings
 (SURVEY §5.6).  Every subcommand here takes ``--preset``, ``--config file.yaml`` and
@@ -205,6 +205,39 @@ def cmd_eval(a) -> int:
     return 0
 
 
+def cmd_serve(a) -> int:
+    """HTTP serving (serve/server.py): encode, index pages, search by query text."""
+    import uvicorn
+
+    from .serve.server import build_service, create_app
+
+    from .io.checkpoint import FINAL_WEIGHTS
+
+    cfg = _config(a)
+    final = os.path.join(cfg.trained_model_dir, FINAL_WEIGHTS)
+    weights = a.weights or (final if os.path.exists(final) else None)
+    engine, index = build_service(cfg, weights, max_batch=a.max_batch, max_wait_ms=a.max_wait_ms,
+                                  index_path=a.index)
+    if a.pages:
+        batch_ids, batch_txt = [], []
+        with open(a.pages, encoding="utf-8") as f:
+            for line in f:
+                if not line.strip():
+                    continue
+                rec = json.loads(line)
+                batch_ids.append(rec["id"])
+                batch_txt.append(rec["text"])
+                if len(batch_txt) == a.max_batch:
+                    index.add(engine.encode(batch_txt, "doc"), batch_ids, normalize=False)
+                    batch_ids, batch_txt = [], []
+        if batch_txt:
+            index.add(engine.encode(batch_txt, "doc"), batch_ids, normalize=False)
+        log.info("indexed %d pages", len(index))
+    uvicorn.run(create_app(engine, index), host=a.host, port=a.port, log_level="info")
+    engine.close()
+    return 0
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     from .log import setup_logging
 
@@ -245,6 +278,16 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.add_argument("--pages", type=int, default=2048)
     p.add_argument("--metrics", default=None, help="append the eval record to this metrics JSONL")
     p.set_defaults(fn=cmd_eval)
+    p = sub.add_parser("serve", help="HTTP page-vector service: /encode, /index/add, /search")
+    _common(p)
+    p.add_argument("--weights", default=None)
+    p.add_argument("--pages", default=None, help='JSONL {"id": ..., "text": ...} to index at startup')
+    p.add_argument("--index", default=None, help="saved PageIndex path to load")
+    p.add_argument("--host", default="127.0.0.1")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--max-batch", type=int, default=4096)
+    p.add_argument("--max-wait-ms", type=float, default=2.0)
+    p.set_defaults(fn=cmd_serve)
     p = sub.add_parser("bench", help="run bench.py (headline benchmark)")
     p.add_argument("rest", nargs=argparse.REMAINDER)
     p.set_defaults(fn=lambda a: __import__("subprocess").call([sys.executable, os.path.join(

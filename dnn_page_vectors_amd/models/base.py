@@ -12,6 +12,7 @@ the compute-cache refresh hook used after optimizer steps.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -91,6 +92,8 @@ class TwoTowerModel(nn.Module):
 
     def _query_stream(self, q_ids: torch.Tensor) -> Optional[torch.cuda.Stream]:
         if not (q_ids.is_cuda and self.training and getattr(self.cfg, "query_stream", False)):
+            return None
+        if os.environ.get("PAGEVEC_QUERY_STREAM", "1") == "0":  # A/B switch
             return None
         if torch.cuda.is_current_stream_capturing():  # hipGraph capture: one stream
             return None

@@ -33,17 +33,42 @@ def topk_cos(qn: torch.Tensor, pn: torch.Tensor, k: int = 10, block: int = 65536
 
 
 _KS = (1, 2, 3, 4, 5, 6, 8, 12, 16, 24)
+MAX_K = 16  # register-resident sorted lists of the kernel (topk.hip K)
+
+
+def padded_width(D: int) -> int:
+    """Zero-padded feature width: one of the kernel's compiled 32-multiples (topk.hip)."""
+    return 32 * next(ks for ks in _KS if 32 * ks >= D)
+
+
+def pad_bf16(x: torch.Tensor, DP: int) -> torch.Tensor:
+    out = torch.zeros(x.shape[0], DP, dtype=torch.bfloat16, device=x.device)
+    out[:, :x.shape[1]] = x
+    return out
+
+
+def topk_cos_padded(qb: torch.Tensor, pb: torch.Tensor, k: int, n: int = -1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k over the first ``n`` rows of PRE-PADDED bf16 pages ``pb`` (N_cap, DP) for
+    pre-padded bf16 queries ``qb`` (B, DP) — the serving index keeps its pages in this
+    layout so a search does not re-pad the collection.  k <= MAX_K; GPU only."""
+    n = pb.shape[0] if n < 0 else n
+    B, DP = qb.shape
+    vals = torch.empty(B, k, dtype=torch.float32, device=qb.device)
+    idx = torch.empty(B, k, dtype=torch.int32, device=qb.device)
+    ns = int(lib().pv_topk_splits(B, n))
+    pv = torch.full((B, ns, 4, 16), float("-inf"), dtype=torch.float32, device=qb.device)
+    pi = torch.full((B, ns, 4, 16), -1, dtype=torch.int32, device=qb.device)
+    check(lib().pv_topk_cos(P(qb), P(pb), P(vals), P(idx), P(pv), P(pi), B, n, DP, k, ns, stream(qb.device)),
+          "pv_topk_cos")
+    return vals, idx.long()
 
 
 def _topk_hip(qn, pn, k):
     B, D = qn.shape
     N = pn.shape[0]
-    # zero-padded feature width: one of the kernel's compiled 32-multiples (topk.hip)
-    DP = 32 * next(ks for ks in _KS if 32 * ks >= D)
-    qb = torch.zeros(B, DP, dtype=torch.bfloat16, device=qn.device)
-    qb[:, :D] = qn
-    pb = torch.zeros(N, DP, dtype=torch.bfloat16, device=qn.device)
-    pb[:, :D] = pn
+    DP = padded_width(D)
+    qb = pad_bf16(qn, DP)
+    pb = pad_bf16(pn, DP)
     vals = torch.empty(B, k, dtype=torch.float32, device=qn.device)
     idx = torch.empty(B, k, dtype=torch.int32, device=qn.device)
     ns = int(lib().pv_topk_splits(B, N))
