@@ -456,7 +456,7 @@ def test_debug_kernels_flag_bad_ids_without_faulting():
         _native.use_debug_kernels(False)
 
 
-@pytest.mark.parametrize("L,H", [(32, 4), (37, 4), (64, 12), (200, 4), (300, 6)])
+@pytest.mark.parametrize("L,H", [(32, 4), (37, 4), (64, 12), (65, 4), (200, 4), (256, 12), (300, 6)])
 def test_fused_attention_packed_qkv(L, H):
     """attention.hip (online softmax fwd, dK/dV + dQ bwd) vs an fp32 reference on the same
     bf16 packed QKV, with key padding."""
@@ -483,6 +483,40 @@ def test_fused_attention_packed_qkv(L, H):
         scale = gr[:, :, slot].abs().max()
         err = (g[:, :, slot] - gr[:, :, slot]).abs().max() / scale
         assert err < 3e-2, (slot, float(err))
+
+
+def test_packed_attention_qkv_projection_grads():
+    """Packed query (L 32) + page (L 256) segments through the QKV projection and the fused
+    attention: the projection's weight and bias gradients match fp32 torch."""
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    torch.manual_seed(5)
+    H, d, Hd = 4, 64, 256
+    shapes = [(6, 32), (3, 256)]
+    T = sum(N * L for N, L in shapes)
+    x = (torch.randn(T, Hd, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(3 * H * d, Hd, device=DEV) * 0.05).requires_grad_(True)
+    b = (torch.randn(3 * H * d, device=DEV) * 0.1).requires_grad_(True)
+    masks = [torch.ones(N, L, dtype=torch.int32, device=DEV) for N, L in shapes]
+    masks[1][1, 200:] = 0
+    out = tops.packed_attention(tops.linear(x, w, b), masks, shapes, H)
+    do = torch.randn_like(out.float())
+    (out.float() * do).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().bfloat16().float().requires_grad_(True)
+    qr = xr @ wr.t() + br
+    outs, off = [], 0
+    for (N, L), m in zip(shapes, masks):
+        qkv_s = qr[off:off + N * L].view(N, L, 3, H, d).permute(2, 0, 3, 1, 4)
+        s_ = (qkv_s[0] @ qkv_s[1].transpose(-1, -2)) / 8.0
+        s_ = s_.masked_fill(~m.bool()[:, None, None, :], float("-inf"))
+        outs.append((torch.softmax(s_, -1) @ qkv_s[2]).transpose(1, 2).reshape(N * L, H * d))
+        off += N * L
+    (torch.cat(outs) * do).sum().backward()
+    for got, want in ((w.grad, wr.grad), (b.grad, br.grad)):
+        err = (got.float() - want).abs().max() / want.abs().max()
+        assert err < 3e-2, float(err)
 
 
 @pytest.mark.parametrize("model", ["cdssm", "mlp"])

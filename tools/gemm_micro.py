@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--tokens", type=int, nargs="+", default=[65536, 8192])
     a = ap.parse_args()
     dev = "cuda"
+    a_ = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    b_ = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: a_ @ b_, iters=10)
+    print(json.dumps({"square_8192": f"{t:.3f} ms {2 * 8192 ** 3 / t / 1e9:.0f} TF/s"}), flush=True)
     shapes = [(768, 2304), (768, 768), (768, 3072), (3072, 768)]
     for T in a.tokens:
         for K, N in shapes:
