@@ -15,6 +15,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, need, stream, use_hip
 
@@ -154,6 +155,7 @@ class _ConvPoolFn(torch.autograd.Function):
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
+        ctx.params = (table, w3, w4)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return pooled, argmax
 
     @staticmethod
@@ -164,8 +166,14 @@ class _ConvPoolFn(torch.autograd.Function):
         dev = ids.device
         s = stream(dev)
         gpool = gpool.contiguous().float()
-        dw3 = torch.zeros_like(w3)
-        dw4 = torch.zeros_like(w4)
+        # the backward kernels accumulate atomically: they can add straight into the flat
+        # gradient buffer (no zeroed temporaries, no AccumulateGrad adds)
+        ptable, pw3, pw4 = ctx.params
+        t_tab = grad_sink.accum_target(ptable) if ctx.needs_input_grad[1] else None
+        t3 = grad_sink.accum_target(pw3) if ctx.needs_input_grad[2] else None
+        t4 = grad_sink.accum_target(pw4) if ctx.needs_input_grad[3] else None
+        dw3 = t3 if t3 is not None else torch.zeros_like(w3)
+        dw4 = t4 if t4 is not None else torch.zeros_like(w4)
         db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
         L_ = lib()
         # every buffer the side stream touches is allocated on the main stream above/before
@@ -193,7 +201,7 @@ class _ConvPoolFn(torch.autograd.Function):
             skeys = torch.empty_like(keys)
             svals = torch.empty(R, dtype=torch.int32, device=dev)
             sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
-            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
             check(L_.pv_conv_bwd_rows_reduce(P(skeys), 2 if k16 else 4, P(svals), P(rows), P(dtable), R, 256, E, V, s),
                   "pv_conv_bwd_rows_reduce")
         elif ctx.needs_input_grad[1]:
@@ -214,7 +222,7 @@ class _ConvPoolFn(torch.autograd.Function):
                 check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
             sort_pairs_iota(keys, skeys, svals, end_bit)
-            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
             wrow = _weight_rows(w3, w4, EP)
             if k16:
                 check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
@@ -228,7 +236,13 @@ class _ConvPoolFn(torch.autograd.Function):
                                                   P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
         if side is not None:
             main.wait_stream(side)
-        return None, dtable, dw3, dw4, db, None, None, None, None, None, None, None
+        for t, prm in ((t_tab, ptable), (t3, pw3), (t4, pw4)):
+            if t is not None:
+                grad_sink.done(prm)
+        if t_tab is not None:
+            dtable = None
+        return (None, dtable, None if t3 is not None else dw3, None if t4 is not None else dw4, db,
+                None, None, None, None, None, None, None)
 
 
 def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, biases, p: float, seed: int,

@@ -11,6 +11,7 @@ from typing import Optional
 
 import torch
 
+from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
@@ -35,6 +36,7 @@ class _LinearActFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w, y if act in ("relu", "tanh") else None, b)
         ctx.act = act
         ctx.xshape = x.shape
+        ctx.params = (w, b)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -57,22 +59,34 @@ class _LinearActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dz @ w.float()).view(ctx.xshape).to(x2.dtype)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dz, xf).to(w.dtype)
+            tw = grad_sink.write_target(ctx.params[0])  # straight into the flat gradient (ops/grad_sink.py)
+            if tw is not None:
+                _wgrad(dz, xf, out=tw)
+                grad_sink.done(ctx.params[0])
+            else:
+                dw = _wgrad(dz, xf).to(w.dtype)
         if b is not None and ctx.needs_input_grad[2]:
-            db = dz.sum(0)
+            tb = grad_sink.write_target(ctx.params[1])
+            if tb is not None:
+                torch.sum(dz, 0, out=tb)
+                grad_sink.done(ctx.params[1])
+            else:
+                db = dz.sum(0)
         return dx, dw, db, None
 
 
-def _wgrad(dz: torch.Tensor, xf: torch.Tensor) -> torch.Tensor:
+def _wgrad(dz: torch.Tensor, xf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dz^T x split over the row axis into batched GEMMs (the single GEMM of a 150 x 300
-    output over 16384 rows runs on a handful of workgroups: 126 us in the CDSSM profile)."""
+    output over 16384 rows runs on a handful of workgroups: 126 us in the CDSSM profile).
+    ``out``: fp32 destination (a flat-gradient view), overwritten."""
     from .transformer import _wgrad_splits
 
     T = dz.shape[0]
     sk = _wgrad_splits(T)
     if sk == 1:
-        return dz.t() @ xf
-    return torch.bmm(dz.view(sk, T // sk, -1).transpose(1, 2), xf.view(sk, T // sk, -1)).sum(0)
+        return torch.mm(dz.t(), xf, out=out)
+    part = torch.bmm(dz.view(sk, T // sk, -1).transpose(1, 2), xf.view(sk, T // sk, -1))
+    return torch.sum(part, 0, out=out)
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "relu") -> torch.Tensor:

@@ -18,6 +18,7 @@ from typing import Optional
 
 import torch
 
+from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
@@ -69,14 +70,25 @@ class _BagFn(torch.autograd.Function):
             out = _counts_gemm(C[:, :V], W16) * scale[:, None]
         ctx.save_for_backward(C, scale)
         ctx.V = V
+        ctx.W = W  # the parameter itself (its flat-gradient view is the direct-write target)
         return out
 
     @staticmethod
     def backward(ctx, g):
         C, scale = ctx.saved_tensors
         gs = (g.float() * scale[:, None]).to(torch.bfloat16)
-        dW = (C[:, :ctx.V].t() @ gs).float()
-        return None, dW, None, None, None, None
+        Ct = C[:, :ctx.V].t()
+        if ctx.needs_input_grad[1]:
+            W = ctx.W
+            tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
+            if tw is not None:
+                try:
+                    torch.mm(Ct, gs, out_dtype=torch.float32, out=tw)
+                except (TypeError, RuntimeError, NotImplementedError):
+                    tw.copy_(Ct @ gs)
+                grad_sink.done(W)
+                return None, None, None, None, None, None
+        return None, (Ct @ gs).float(), None, None, None, None
 
 
 def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor] = None, pad: int = 0,

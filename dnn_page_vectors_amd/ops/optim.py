@@ -38,14 +38,29 @@ class FlatParams:
         self.numel = off
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        # direct gradient writes (ops/grad_sink.py): params written this step, flat-grad
+        # addresses, and a hook marking params that autograd's AccumulateGrad wrote
+        self.written = set()
+        self._gptr: Dict[int, int] = {}
+        self._hooks = []
         for n, p in self.named:
             o, k, shp = self.offsets[n]
             self.data[o:o + k].copy_(p.data.reshape(-1).float())
             p.data = self.data[o:o + k].view(shp)
             p.grad = self.grad[o:o + k].view(shp)
+            self._gptr[id(p)] = p.grad.data_ptr()
+            p._pv_flat = self
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._mark))
+
+    def _mark(self, p) -> None:
+        self.written.add(id(p))
+
+    def owns_grad(self, p) -> bool:
+        return p.grad is not None and self._gptr.get(id(p)) == p.grad.data_ptr()
 
     def zero_grad(self) -> None:
         self.grad.zero_()
+        self.written.clear()
 
     def reattach_grads(self) -> None:
         """Re-point param.grad at the flat buffer (if something replaced them)."""

@@ -13,6 +13,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
 
@@ -60,6 +61,7 @@ class _AddLNFn(torch.autograd.Function):
         ctx.has_r = r is not None
         ctx.drop = (thr, scale, seed)
         ctx.xb = None if xb is None else (xb.shape, xb.dtype)
+        ctx.params = (gamma, beta, xb)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return y
 
     @staticmethod
@@ -73,10 +75,16 @@ class _AddLNFn(torch.autograd.Function):
         L_ = lib()
         nws = int(L_.pv_layernorm_bwd_ws(M, D))
         alloc = torch.empty if nws > 0 else torch.zeros  # generic kernel accumulates atomically
-        dg = alloc(gamma.shape, dtype=torch.float32, device=h.device)
-        db = alloc(gamma.shape, dtype=torch.float32, device=h.device)
+        # the workspace path overwrites dg / db / dxb: write them straight into the flat
+        # gradient when this is the parameters' first contribution (ops/grad_sink.py)
+        tgt = [grad_sink.write_target(q) if (nws > 0 and ctx.needs_input_grad[i]) else None
+               for q, i in zip(ctx.params, (2, 3, 7))]
+        dg = tgt[0] if tgt[0] is not None else alloc(gamma.shape, dtype=torch.float32, device=h.device)
+        db = tgt[1] if tgt[1] is not None else alloc(gamma.shape, dtype=torch.float32, device=h.device)
         ws = torch.empty(nws, dtype=torch.float32, device=h.device) if nws > 0 else None
-        dxb = torch.empty(D, dtype=torch.float32, device=h.device) if ctx.xb is not None else None
+        dxb = None
+        if ctx.xb is not None:
+            dxb = tgt[2] if tgt[2] is not None else torch.empty(D, dtype=torch.float32, device=h.device)
         if thr > 0 or dxb is not None:
             dxm = torch.empty_like(h) if thr > 0 else None
             check(L_.pv_layernorm_bwd_drop(P(dy), P(h), P(gamma), P(mean), P(rstd), P(dx), P(dxm), P(dg), P(db),
@@ -90,7 +98,12 @@ class _AddLNFn(torch.autograd.Function):
                                       stream(h.device)), "pv_layernorm_bwd")
         if dxb is not None and ctx.xb[1] != torch.float32:
             dxb = dxb.to(ctx.xb[1])
-        return dxm, (dx if ctx.has_r else None), dg, db, None, None, None, dxb
+        outs = [dg, db, dxb]
+        for j, (t, q) in enumerate(zip(tgt, ctx.params)):
+            if t is not None:
+                grad_sink.done(q)
+                outs[j] = None
+        return dxm, (dx if ctx.has_r else None), outs[0], outs[1], None, None, None, outs[2]
 
 
 _LN_ROWS = (256, 512, 768, 1024)
@@ -127,6 +140,7 @@ class _BiasGeluFn(torch.autograd.Function):
         D = x.shape[-1]
         check(lib().pv_bias_gelu_fwd(P(x), P(b), P(y), x.numel(), D, stream(x.device)), "pv_bias_gelu_fwd")
         ctx.save_for_backward(x, b)
+        ctx.params = (b,)
         return y
 
     @staticmethod
@@ -136,10 +150,18 @@ class _BiasGeluFn(torch.autograd.Function):
         M = x.numel() // D
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(x)
-        db = torch.empty_like(b) if D % 8 == 0 else torch.zeros_like(b)  # vector path overwrites db
+        tb = grad_sink.write_target(ctx.params[0]) if (D % 8 == 0 and b.dtype == torch.float32
+                                                       and ctx.needs_input_grad[1]) else None
+        if tb is not None:
+            db = tb
+        else:
+            db = torch.empty_like(b) if D % 8 == 0 else torch.zeros_like(b)  # vector path overwrites db
         L_ = lib()
         ws = torch.empty(L_.pv_bias_gelu_bwd_ws(M, D), dtype=torch.float32, device=x.device) if D % 8 == 0 else None
         check(L_.pv_bias_gelu_bwd(P(x), P(b), P(dy), P(dx), P(db), P(ws), M, D, stream(x.device)), "pv_bias_gelu_bwd")
+        if tb is not None:
+            grad_sink.done(ctx.params[0])
+            db = None
         return dx, db
 
 
@@ -302,7 +324,7 @@ def _wgrad_splits(T: int) -> int:
     return sk
 
 
-def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dW = dy^T x (bf16 operands, fp32 result) for T >> N, K.
 
     A single GEMM has only (N/256)(K/256) output tiles (36 for 768 x 3072) for a 65536-long
@@ -310,17 +332,19 @@ def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     tools/gemm_micro.py).  Splitting the token axis into up to 16 batched fp32-output GEMMs
     and summing the partials in fp32 fills the chip: 1.82 -> 1.03 ms per BERT layer at
     T = 65536 (bmm out_dtype=fp32; same fp32 accumulation, different summation order).
+    ``out``: fp32 destination (a flat-gradient view, ops/grad_sink.py), overwritten.
     """
     T = dy2.shape[0]
     sk = _wgrad_splits(T)
     try:
         if sk == 1:
-            return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+            return torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=out)
         dy3 = dy2.view(sk, T // sk, dy2.shape[1])
         x3 = x2.view(sk, T // sk, x2.shape[1])
-        return torch.bmm(dy3.transpose(1, 2), x3, out_dtype=torch.float32).sum(0)
+        return torch.sum(torch.bmm(dy3.transpose(1, 2), x3, out_dtype=torch.float32), 0, out=out)
     except (TypeError, RuntimeError, NotImplementedError):  # no mm/bmm out_dtype (CPU)
-        return (dy2.t().float() @ x2.float())
+        r = dy2.t().float() @ x2.float()
+        return r if out is None else out.copy_(r)
 
 
 class _Linear16Fn(torch.autograd.Function):
@@ -337,15 +361,28 @@ class _Linear16Fn(torch.autograd.Function):
         ctx.save_for_backward(x2, w16)
         ctx.has_b = b is not None
         ctx.shape = x.shape
+        ctx.params = (w, b)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return y.view(*x.shape[:-1], w16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w16 = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16)
-        dx = (dy2 @ w16).view(ctx.shape)
-        dw = wgrad_f32(dy2, x2)
-        db = dy2.sum(0, dtype=torch.float32) if ctx.has_b else None
+        dx = (dy2 @ w16).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        pw, pb = ctx.params
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            tw = grad_sink.write_target(pw)
+            dw = wgrad_f32(dy2, x2, out=tw)
+            if tw is not None:
+                grad_sink.done(pw)
+                dw = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            tb = grad_sink.write_target(pb)
+            db = torch.sum(dy2, 0, dtype=torch.float32, out=tb)
+            if tb is not None:
+                grad_sink.done(pb)
+                db = None
         return dx, dw, db, None
 
 

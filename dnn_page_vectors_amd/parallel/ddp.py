@@ -21,6 +21,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import grad_sink
 from ..ops.optim import FlatParams
 
 
@@ -60,13 +61,16 @@ class GradBuckets:
                 cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
         if cur_lo is not None:
             self._add(cur_lo, cur_hi, members)
-        self.pending = [0] * len(self.buckets)
+        self.pending: List[set] = [set() for _ in self.buckets]
         self.handles: List[Optional[object]] = [None] * len(self.buckets)
         self._hooks = []
         if self.overlap:
             for name, p in flat.named:
                 bi = self.param_bucket[name]
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
+                hook = self._make_hook(bi)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                # ops that write the flat gradient directly fire this instead (ops/grad_sink.py)
+                self._hooks.append(_Remover(grad_sink.add_hook(p, hook)))
 
     def _add(self, lo: int, hi: int, members: List[str]) -> None:
         bi = len(self.buckets)
@@ -75,9 +79,10 @@ class GradBuckets:
             self.param_bucket[m] = bi
 
     def _make_hook(self, bi: int):
-        def hook(_p):
-            self.pending[bi] += 1
-            if self.pending[bi] == self.buckets[bi][2] and self.handles[bi] is None:
+        def hook(p):
+            seen = self.pending[bi]
+            seen.add(id(p))  # a set: a parameter reached twice counts once
+            if len(seen) == self.buckets[bi][2] and self.handles[bi] is None:
                 self._launch(bi)
         return hook
 
@@ -90,7 +95,7 @@ class GradBuckets:
             self.handles[bi] = dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True)
 
     def start_step(self) -> None:
-        self.pending = [0] * len(self.buckets)
+        self.pending = [set() for _ in self.buckets]
         self.handles = [None] * len(self.buckets)
 
     def finish(self) -> None:
@@ -111,6 +116,11 @@ class GradBuckets:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+class _Remover:
+    def __init__(self, fn):
+        self.remove = fn
 
 
 def broadcast_params(flat: FlatParams, src: int = 0) -> None:

@@ -872,3 +872,79 @@ def test_dense_dx_matches_sort_path(L, p, mode):
     # relative to the largest gradient entry
     torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=2e-5 * float(grads[0].abs().max()))
     assert grads[0].abs().sum() > 0
+
+
+@pytest.mark.parametrize("model", ["cdssm", "mlp", "bert"])
+def test_direct_flat_grad_writes_match_autograd(model, monkeypatch):
+    """ops/grad_sink.py: ops writing parameter gradients straight into the flat buffer give
+    the gradients autograd's AccumulateGrad path gives (one step, same data and init)."""
+    from dnn_page_vectors_amd.config import Configuration, preset_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.ops import grad_sink
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    if model == "bert":
+        cfg = preset_config("bert_dp8").replace(bert_layers=2, batch_size=16, document_length=64, query_length=16,
+                                                bert_dropout=0.0)
+        V = cfg.vocab_hash_size
+    else:
+        cfg = Configuration(model=model, feature_level="ngram", vocab_hash_size=500, query_length=12,
+                            document_length=64, batch_size=32, embedding_dim=100, dropout_prob=(0.0, 0.5),
+                            loss_mode="in_batch", mlp_dims=(64, 64, 32), hidden_dims=64)
+        V = 500
+    if model == "bert":
+        from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+
+        q, d = SyntheticPairs(spec_from_config(cfg, V, num_pages=512), DEV, seed=5).batch(cfg.batch_size)
+    else:
+        g = torch.Generator().manual_seed(4)
+        q = torch.randint(1, V, (32, 12), generator=g, dtype=torch.int32).to(DEV)
+        d = torch.randint(1, V, (32, 4, 64), generator=g, dtype=torch.int32).to(DEV)
+    grads = []
+    for enabled in (False, True):
+        monkeypatch.setattr(grad_sink, "ENABLED", enabled)
+        torch.manual_seed(0)
+        tr = Trainer(cfg, build_model(cfg, V), torch.device(DEV))
+        tr.train_step(q, d)
+        torch.cuda.synchronize()
+        grads.append((tr.flat.grad.clone(), len(tr.flat.written)))
+    (ga, _), (gb, n_written) = grads
+    assert n_written == len(tr.flat.named)
+    assert float(ga.abs().sum()) > 0
+    err = float((ga - gb).abs().max() / ga.abs().max())
+    assert err < 1e-2, err
+
+
+def test_direct_grad_weight_used_twice(monkeypatch):
+    """A weight reached by two ops in one backward: the first writes the flat gradient, the
+    second falls back to autograd's accumulate (grad_sink.write_target's written set)."""
+    from dnn_page_vectors_amd.ops import grad_sink
+    from dnn_page_vectors_amd.ops.optim import FlatParams
+
+    x1 = bf(torch.randn(256, 96, device=DEV))
+    x2 = bf(torch.randn(128, 96, device=DEV))
+    res = []
+    for enabled in (True, False):
+        monkeypatch.setattr(grad_sink, "ENABLED", enabled)
+        torch.manual_seed(1)
+        lin = torch.nn.Linear(96, 64).to(DEV)
+        lin.weight.data = bf(lin.weight.data)
+        flat = FlatParams(lin.named_parameters())
+        flat.zero_grad()
+        y = dops.linear_act(x1, lin.weight, lin.bias, "relu").sum() + dops.linear_act(x2, lin.weight, lin.bias,
+                                                                                       "tanh").sum()
+        y.backward()
+        assert lin.weight.grad.data_ptr() == flat.grad.data_ptr()
+        res.append((lin.weight.grad.clone(), lin.bias.grad.clone(), lin.weight.detach().clone(),
+                    lin.bias.detach().clone()))
+    (gw, gb, w0, b0), (gw2, gb2, _, _) = res
+    torch.testing.assert_close(gw, gw2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gb, gb2, rtol=1e-5, atol=1e-5)
+    wr = w0.requires_grad_(True)
+    br = b0.requires_grad_(True)
+    (torch.relu(x1 @ wr.t() + br).sum() + torch.tanh(x2 @ wr.t() + br).sum()).backward()
+    for got, want in ((gw, wr.grad), (gb, br.grad)):
+        err = float((got - want).abs().max() / want.abs().max())
+        assert err < 2e-2, err
