@@ -17,6 +17,13 @@ kernels), returning ``None`` to autograd for that input:
 * ``done(p)``          — mark ``p`` written this step and fire the data-parallel bucket
   hooks (parallel/ddp.py) that ``register_post_accumulate_grad_hook`` would have fired.
 
+Data parallel: a bucket's all-reduce is launched from ``done`` as soon as all its
+parameters are written.  A parameter that ALSO receives a gradient from another node of
+the same graph would get that later contribution added while its bucket is already in
+flight, so ``mark_multi_use(loss, flat)`` walks the autograd graph once (per input shape)
+before backward and excludes every parameter with more than one consumer edge.
+(Without data parallelism the ``written`` set alone keeps every case exact.)
+
 ``PAGEVEC_DIRECT_GRAD=0`` disables direct writes (A/B measurement, debugging).
 """
 from __future__ import annotations
@@ -37,7 +44,7 @@ def accum_target(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if p is None or torch.is_grad_enabled():  # create_graph backward: keep autograd's path
         return None
     f = _flat(p)
-    if f is None or p.grad is None or p.grad.dtype != torch.float32 or not f.owns_grad(p):
+    if f is None or p.grad is None or p.grad.dtype != torch.float32 or not f.owns_grad(p) or id(p) in f.multi:
         return None
     return p.grad
 
@@ -64,3 +71,28 @@ def add_hook(p: torch.Tensor, fn: Callable[[torch.Tensor], None]) -> Callable[[]
     def remove():
         p._pv_sink_hooks = tuple(h for h in getattr(p, "_pv_sink_hooks", ()) if h is not fn)
     return remove
+
+
+def mark_multi_use(root: torch.Tensor, flat) -> int:
+    """Count the autograd edges into each parameter's AccumulateGrad node under ``root``;
+    parameters of ``flat`` reached more than once are excluded from direct writes.
+    Returns the number of such parameters."""
+    counts = {}
+    seen = set()
+    stack = [root.grad_fn]
+    while stack:
+        fn = stack.pop()
+        if fn is None or fn in seen:
+            continue
+        seen.add(fn)
+        for nxt, _ in fn.next_functions:
+            if nxt is None:
+                continue
+            var = getattr(nxt, "variable", None)
+            if var is not None:  # AccumulateGrad
+                counts[id(var)] = counts.get(id(var), 0) + 1
+            else:
+                stack.append(nxt)
+    ids = {id(p) for _, p in flat.named}
+    flat.multi = {i for i, c in counts.items() if c > 1 and i in ids}
+    return len(flat.multi)

@@ -41,6 +41,7 @@ class FlatParams:
         # direct gradient writes (ops/grad_sink.py): params written this step, flat-grad
         # addresses, and a hook marking params that autograd's AccumulateGrad wrote
         self.written = set()
+        self.multi = set()  # params with several consumers (grad_sink.mark_multi_use)
         self._gptr: Dict[int, int] = {}
         self._hooks = []
         for n, p in self.named:

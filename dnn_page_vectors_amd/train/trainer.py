@@ -28,6 +28,7 @@ import torch
 
 from ..models.base import TwoTowerModel, bump_generation
 from ..ops import dense as dops
+from ..ops import grad_sink
 from ..ops import loss as lops
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
@@ -93,6 +94,7 @@ class Trainer:
         if self.placement == "tower" and cfg.loss_mode != "explicit":
             raise ValueError("tower placement splits the explicit J-negative slots; use loss_mode=explicit")
         self._replica_checked = False
+        self._sink_scanned = set()
         self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg")
                         if self.info.enabled else None)
         self.step = 0
@@ -243,6 +245,11 @@ class Trainer:
         loss, P = self.compute_loss(q_ids, d_ids, seed)
         if timer:
             timer.mark()
+        if self.buckets is not None and self.buckets.overlap:
+            key = (tuple(q_ids.shape), tuple(d_ids.shape))
+            if key not in self._sink_scanned:  # once per input shape (ops/grad_sink.py)
+                grad_sink.mark_multi_use(loss, self.flat)
+                self._sink_scanned.add(key)
         range_push("backward")
         loss.backward()
         range_pop()

@@ -84,3 +84,61 @@ def test_cross_gpu_loss_ranks_one_gpu(world):
         assert e_loss < 1e-4, res
         assert e_q < 5e-2 and e_d < 5e-2, res  # bf16 G vs fp32 oracle
         assert h_q < 1e-4 and h_d < 1e-4, res  # vs the single-process HIP path
+
+
+def _ddp_worker(rank, world, port, model, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
+    try:
+        from dnn_page_vectors_amd.config import Configuration
+        from dnn_page_vectors_amd.models import build_model
+        from dnn_page_vectors_amd.ops import grad_sink
+        from dnn_page_vectors_amd.parallel import dist as pdist
+        from dnn_page_vectors_amd.train.trainer import Trainer
+
+        info = pdist.init_distributed()
+        dev = info.device
+        cfg = Configuration(model=model, feature_level="ngram", vocab_hash_size=500, query_length=12,
+                            document_length=64, batch_size=32, embedding_dim=100, dropout_prob=(0.0, 0.5),
+                            loss_mode="in_batch", mlp_dims=(64, 64, 32), hidden_dims=64, grad_bucket_mb=0.05)
+        g = torch.Generator().manual_seed(10 + rank)
+        qi = torch.randint(1, 500, (32, 12), generator=g, dtype=torch.int32).to(dev)
+        di = torch.randint(1, 500, (32, 4, 64), generator=g, dtype=torch.int32).to(dev)
+        grads = []
+        for enabled in (False, True):
+            grad_sink.ENABLED = enabled
+            torch.manual_seed(0)
+            tr = Trainer(cfg, build_model(cfg, 500), dev)
+            assert tr.buckets is not None and len(tr.buckets.buckets) > 1
+            tr.train_step(qi, di)
+            torch.cuda.synchronize()
+            grads.append(tr.flat.grad.clone())
+        diff = float((grads[0] - grads[1]).abs().max() / grads[0].abs().max())
+        s = torch.stack([grads[1].double().sum(), grads[1].double().abs().sum()]).cpu()
+        allsum = [torch.zeros_like(s) for _ in range(world)]
+        torch.distributed.all_gather(allsum, s)
+        agree = max(float((a - s).abs().max() / s.abs().max()) for a in allsum)
+        q.put((rank, (diff, agree)))
+        pdist.destroy()
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("model", ["cdssm", "mlp"])
+def test_ddp_buckets_with_direct_grad_writes(model):
+    """Bucketed, backward-overlapped all-reduce (parallel/ddp.py) fired from the direct
+    flat-gradient writes (ops/grad_sink.py): the reduced gradients equal those of the
+    AccumulateGrad-hook path, and every rank holds the same gradient."""
+    world = 2
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, model, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=300) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+        diff, agree = res[r]
+        assert diff < 1e-3, res
+        assert agree < 1e-6, res
