@@ -6,7 +6,9 @@
 //   the host can ship raw bytes and let the GPU hash them (DSSM "word hashing").
 // * embedding_bag: out[n,:] = scale_n * sum_{t: ids[n,t] != pad} W[ids[n,t], :] — the
 //   multi-hot x W1 first layer of the DSSM MLP tower, for short bags (queries):
-//   one wave per sample, 16-byte row chunks per lane, 4 rows in flight.
+//   one wave per sample, 16-byte row chunks per lane, 4 rows in flight; it also emits the
+//   16-bit sort keys of the sparse backward (bag_bwd_sorted: sort (token, slot) entries
+//   by token, sum each token's run of dY rows, one atomic add per run and column).
 // * bag_counts: for LONG bags (2k-token pages) the same product is computed as a dense
 //   GEMM  C (N x V counts, bf16) x W  on the matrix cores (hipBLASLt), and the backward
 //   dW = C^T x dY likewise — 126 GFLOP of MFMA instead of 8 GB of gathers / 4G float
@@ -40,6 +42,7 @@ __global__ void trigram_hash_kernel(const unsigned char* __restrict__ text, cons
 __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restrict__ ids,
                                                             const unsigned short* __restrict__ W,
                                                             float* __restrict__ out, float* __restrict__ lens_out,
+                                                            unsigned short* __restrict__ keys_out,
                                                             int N, int L, int E, int V, int pad, int mean) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -56,8 +59,11 @@ __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restric
     const int tl = t0 + lane;
     const int myid = tl < L ? row[tl] : pad;
     PV_CHECK(myid == pad || (myid >= 0 && myid < V), PV_ERR_ID);
-    unsigned long long m = __ballot(myid != pad && myid >= 0 && myid < V);
+    const bool live = myid != pad && myid >= 0 && myid < V;
+    unsigned long long m = __ballot(live);
     cnt += __popcll(m);
+    // the sparse backward's sort keys: token id, or the sentinel V (sorts last) for pads
+    if (keys_out && tl < L) keys_out[(size_t)n * L + tl] = (unsigned short)(live ? myid : V);
     while (m) {
       int src[4];
       int k = 0;
@@ -109,6 +115,104 @@ __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restric
     }
   }
   if (lens_out && lane == 0) lens_out[n] = (float)cnt;
+}
+
+// Sparse bag backward (short bags): dW[tok] += scale_n * g[n] over the N*L (token, slot)
+// entries sorted by token (keys from embedding_bag_kernel, values = slot = n*L + t).  Wave w
+// walks sorted entries [w*EPW, (w+1)*EPW) run by run (sentinel keys V sort last and end the
+// walk), 8 rows in flight, and adds each run's sum into dW: runs wholly inside the range
+// with a plain vector read-modify-write (no other writer), the two boundary runs with float
+// atomics (a hot token's run spreads over many waves and stays exact).
+// Lane l owns columns {4l + 256 j}, j < NJ (E <= 256 NJ, E % 4 == 0).  dW may be the flat
+// gradient buffer itself (accumulate semantics, ops/grad_sink.py).
+template <int NJ>
+__global__ __launch_bounds__(256) void bag_bwd_sorted_kernel(const unsigned short* __restrict__ skeys,
+                                                             const unsigned* __restrict__ svals,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ lens, float* __restrict__ dW,
+                                                             long M, int EPW, int L, int E, int V, int mean) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
+  if (wbeg >= M) return;
+  const long wend = min(M, wbeg + (long)EPW);
+  const unsigned UV = (unsigned)V;
+  // runs shared with the neighbouring waves: the one entering at wbeg, the one leaving at wend
+  const unsigned k_in = wbeg > 0 ? (unsigned)skeys[wbeg - 1] : UV;
+  const unsigned k_out = wend < M ? (unsigned)skeys[wend] : UV;
+  unsigned cur = UV;
+  bool first = true;
+  f32x4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto flush = [&](bool last) {
+    if (cur < UV) {
+      float* drow = dW + (size_t)cur * E;
+      // a run wholly inside this wave's range has no other writer: vector read-modify-write;
+      // a boundary run may be split over waves: float atomics
+      if ((first && cur == k_in) || (last && cur == k_out)) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = 4 * lane + 256 * j;
+          if (c < E) {
+            atomicAdd(&drow[c + 0], acc[j][0]);
+            atomicAdd(&drow[c + 1], acc[j][1]);
+            atomicAdd(&drow[c + 2], acc[j][2]);
+            atomicAdd(&drow[c + 3], acc[j][3]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = 4 * lane + 256 * j;
+          if (c < E) {
+            f32x4* p = reinterpret_cast<f32x4*>(drow + c);
+            *p = *p + acc[j];
+          }
+        }
+      }
+      first = false;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  for (long i0 = wbeg; i0 < wend; i0 += 64) {
+    const long il = i0 + lane;
+    const unsigned kl = il < wend ? (unsigned)skeys[il] : UV;
+    const unsigned rl = (il < wend && kl < UV) ? svals[il] : 0u;
+    const int n = __popcll(__ballot(kl < UV));  // live entries are a prefix (sorted)
+    for (int e0 = 0; e0 < n; e0 += 8) {
+      f32x4 x[8][NJ];
+      unsigned kk[8];
+      float sc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u < n ? e0 + u : e0;
+        kk[u] = (unsigned)__builtin_amdgcn_readlane((int)kl, e);
+        const unsigned slot = (unsigned)__builtin_amdgcn_readlane((int)rl, e);
+        PV_CHECK((long)slot < M, PV_ERR_SLOT);
+        const unsigned smp = slot / (unsigned)L;
+        sc[u] = mean ? 1.f / fmaxf(lens[smp], 1.f) : 1.f;
+        const float* src = g + (size_t)smp * E;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = 4 * lane + 256 * j;
+          x[u][j] = c < E ? *reinterpret_cast<const f32x4*>(src + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (e0 + u >= n) break;
+        if (kk[u] != cur) {
+          flush(false);
+          cur = kk[u];
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] += sc[u] * x[u][j];
+      }
+    }
+    if (n < 64) break;
+  }
+  flush(true);
 }
 
 // counts: (N, ldc) bf16, zeroed; lens: (N) float (non-pad tokens per bag)
@@ -201,11 +305,33 @@ PV_API int pv_trigram_hash(const void* text, const int* lens, int* out, int N, i
   return 0;
 }
 
-PV_API int pv_embedding_bag(const int* ids, const void* W, float* out, float* lens, int N, int L, int E, int V, int pad,
-                            int mean, void* stream) {
+PV_API int pv_embedding_bag(const int* ids, const void* W, float* out, float* lens, void* keys, int N, int L, int E,
+                            int V, int pad, int mean, void* stream) {
   if (E % 8 || E > 1024) return -1;
+  if (keys && V >= 65535) return -2;  // 16-bit sort keys (sentinel V)
   hipLaunchKernelGGL(pv::embed::embedding_bag_kernel, dim3((N + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids,
-                     (const unsigned short*)W, out, lens, N, L, E, V, pad, mean);
+                     (const unsigned short*)W, out, lens, (unsigned short*)keys, N, L, E, V, pad, mean);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Sparse bag backward over sorted (token, slot) entries: dW (V, E) fp32 += ... (atomics).
+PV_API int pv_bag_bwd_sorted(const void* skeys, const unsigned* svals, const float* g, const float* lens, float* dW,
+                             long M, int epw, int L, int E, int V, int mean, void* stream) {
+  if (E % 4 || E > 1024 || epw < 8 || V >= 65535) return -1;
+  const long waves = (M + epw - 1) / epw;
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned short* k = (const unsigned short*)skeys;
+  if (E <= 256)
+    hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<1>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
+                       E, V, mean);
+  else if (E <= 512)
+    hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<2>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
+                       E, V, mean);
+  else
+    hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<4>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
+                       E, V, mean);
   PV_LAUNCH_CHECK();
   return 0;
 }

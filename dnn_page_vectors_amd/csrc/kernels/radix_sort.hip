@@ -69,7 +69,7 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned* ws, un
 }
 
 // ---- pass kernel 1: per-tile digit histogram -> hist[d * nb + tile] ----------------------
-template <typename KT>
+template <typename KT, int IPT_>
 __global__ __launch_bounds__(BT) void rs_count_kernel(const KT* __restrict__ keys, long n, int shift, int nbits,
                                                       unsigned* __restrict__ hist, int nb) {
   __shared__ unsigned cnt[NW][RADIX];
@@ -77,15 +77,15 @@ __global__ __launch_bounds__(BT) void rs_count_kernel(const KT* __restrict__ key
   for (int i = threadIdx.x; i < NW * RADIX; i += BT) (&cnt[0][0])[i] = 0u;
   __syncthreads();
   const unsigned mask = (1u << nbits) - 1u;
-  const long base = (long)blockIdx.x * TILE + (long)w * WTILE;
-  unsigned d[IPT];
+  const long base = (long)blockIdx.x * (BT * IPT_) + (long)w * (WAVE * IPT_);
+  unsigned d[IPT_];
 #pragma unroll
-  for (int j = 0; j < IPT; ++j) {
+  for (int j = 0; j < IPT_; ++j) {
     const long i = base + j * WAVE + lane;
     d[j] = i < n ? ((unsigned)keys[i] >> shift) & mask : 0xFFFFFFFFu;
   }
 #pragma unroll
-  for (int j = 0; j < IPT; ++j) {
+  for (int j = 0; j < IPT_; ++j) {
     const bool valid = d[j] != 0xFFFFFFFFu;
     const unsigned long long pm = peers_of(d[j], valid, nbits);
     const bool leader = valid && (pm & lanemask_lt()) == 0ull;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(BT) void rs_scan_kernel(unsigned* __restrict__ hist
 // ---- pass kernel 3: stable scatter ---------------------------------------------------------
 // vals_in == nullptr: values are the input positions (iota), i.e. the first pass of a sort
 // whose payload is "where did this key come from".
-template <typename KT>
+template <typename KT, int IPT_>
 __global__ __launch_bounds__(BT) void rs_scatter_kernel(const KT* __restrict__ keys_in,
                                                         const unsigned* __restrict__ vals_in,
                                                         KT* __restrict__ keys_out, unsigned* __restrict__ vals_out,
@@ -130,8 +130,8 @@ __global__ __launch_bounds__(BT) void rs_scatter_kernel(const KT* __restrict__ k
   __shared__ unsigned dstart[RADIX];    // first in-tile position of each digit
   __shared__ unsigned gbase[RADIX];     // global position of (digit, this tile)'s first item
   __shared__ unsigned ws[NW];
-  __shared__ KT kst[TILE];
-  __shared__ unsigned vst[TILE];
+  __shared__ KT kst[(BT * IPT_)];
+  __shared__ unsigned vst[(BT * IPT_)];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, t = threadIdx.x;
   for (int i = t; i < NW * RADIX; i += BT) (&cnt[0][0])[i] = 0u;
   {  // global base of each digit: exclusive scan of the digit totals + this tile's offset
@@ -141,20 +141,20 @@ __global__ __launch_bounds__(BT) void rs_scatter_kernel(const KT* __restrict__ k
   }
   __syncthreads();
   const unsigned mask = (1u << nbits) - 1u;
-  const long tbase = (long)blockIdx.x * TILE;
-  const long base = tbase + (long)w * WTILE;
-  KT k[IPT];
-  unsigned v[IPT];
+  const long tbase = (long)blockIdx.x * (BT * IPT_);
+  const long base = tbase + (long)w * (WAVE * IPT_);
+  KT k[IPT_];
+  unsigned v[IPT_];
 #pragma unroll
-  for (int j = 0; j < IPT; ++j) {
+  for (int j = 0; j < IPT_; ++j) {
     const long i = base + j * WAVE + lane;
     const bool ok = i < n;
     k[j] = ok ? keys_in[i] : (KT)0;
     v[j] = ok ? (vals_in ? vals_in[i] : (unsigned)i) : 0u;
   }
-  unsigned rank[IPT];
+  unsigned rank[IPT_];
 #pragma unroll
-  for (int j = 0; j < IPT; ++j) {
+  for (int j = 0; j < IPT_; ++j) {
     const long i = base + j * WAVE + lane;
     const bool valid = i < n;
     const unsigned d = ((unsigned)k[j] >> shift) & mask;
@@ -178,18 +178,18 @@ __global__ __launch_bounds__(BT) void rs_scatter_kernel(const KT* __restrict__ k
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < IPT; ++j) {
+  for (int j = 0; j < IPT_; ++j) {
     const long i = base + j * WAVE + lane;
     if (i < n) {
       const unsigned d = ((unsigned)k[j] >> shift) & mask;
       const unsigned pos = dstart[d] + cnt[w][d] + rank[j];
-      PV_CHECK(pos < (unsigned)TILE, PV_ERR_LDS);
+      PV_CHECK(pos < (unsigned)(BT * IPT_), PV_ERR_LDS);
       kst[pos] = k[j];
       vst[pos] = v[j];
     }
   }
   __syncthreads();
-  const int tn = (int)min((long)TILE, n - tbase);
+  const int tn = (int)min((long)(BT * IPT_), n - tbase);
   for (int i = t; i < tn; i += BT) {
     const KT kk = kst[i];
     const unsigned d = ((unsigned)kk >> shift) & mask;
@@ -209,9 +209,14 @@ struct Layout {
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Items per thread: 16 (4096-item tiles) for large sorts; small ones (the sparse bag
+// backward's ~200k keys) use 1024-item tiles so the grid still covers the CUs.
+__host__ inline int pick_ipt(long n) { return n <= (1L << 20) ? 4 : IPT; }
+
 __host__ inline Layout layout(long n, int end_bit, int key_bytes) {
   Layout L{};
-  L.nb = (int)((n + TILE - 1) / TILE);
+  const long tile = (long)BT * pick_ipt(n);
+  L.nb = (int)((n + tile - 1) / tile);
   L.passes = (end_bit + 7) / 8;
   size_t o = 0;
   L.ktmp = o;
@@ -247,10 +252,17 @@ int sort_impl(void* temp, long temp_bytes, const KT* keys_in, KT* keys_out, cons
     const bool to_out = ((L.passes - 1 - p) & 1) == 0;
     KT* kout = to_out ? keys_out : ktmp;
     unsigned* vout = to_out ? vals_out : vtmp;
-    hipLaunchKernelGGL(rs_count_kernel<KT>, dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
+    if (pick_ipt(n) == 4)
+      hipLaunchKernelGGL((rs_count_kernel<KT, 4>), dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
+    else
+      hipLaunchKernelGGL((rs_count_kernel<KT, IPT>), dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
     hipLaunchKernelGGL(rs_scan_kernel, dim3(RADIX), dim3(BT), 0, st, hist, L.nb, totals);
-    hipLaunchKernelGGL(rs_scatter_kernel<KT>, dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift, nbits,
-                       (const unsigned*)hist, (const unsigned*)totals, L.nb);
+    if (pick_ipt(n) == 4)
+      hipLaunchKernelGGL((rs_scatter_kernel<KT, 4>), dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift,
+                         nbits, (const unsigned*)hist, (const unsigned*)totals, L.nb);
+    else
+      hipLaunchKernelGGL((rs_scatter_kernel<KT, IPT>), dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift,
+                         nbits, (const unsigned*)hist, (const unsigned*)totals, L.nb);
     PV_LAUNCH_CHECK();
     kin = kout;
     vin = vout;

@@ -55,7 +55,8 @@ SIGS = {
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
-    "pv_embedding_bag": "pppp" "iiiiii" "p",
+    "pv_embedding_bag": "ppppp" "iiiiii" "p",
+    "pv_bag_bwd_sorted": "ppppp" "liiiii" "p",
     "pv_bag_counts": "ppp" "iiiiii" "p",
     # topk.hip
     "pv_topk_splits": "ii",

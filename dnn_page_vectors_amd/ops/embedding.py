@@ -10,10 +10,15 @@ Two execution plans for ``bag = scale * onehot_counts(ids) @ W``:
   scatter atomics at all).  For 2k-token pages at V = 30k, E = 512 this is ~0.13 TFLOP
   of MFMA instead of ~8 GB of row gathers (fwd) + ~16 GB of float atomics (bwd).
 
-The backward always uses the counts GEMM.  CPU: plain torch.
+Backward: the counts GEMM C^T @ dY for the counts plan; for the gather plan (short bags,
+V < 65535) a sparse path — the forward also emits 16-bit sort keys (token id, pad -> V),
+the backward sorts the N*L (token, slot) entries and ``pv_bag_bwd_sorted`` sums each
+token's run of dY rows into dW (MLP query tower, N 4096 x L 45: ~0.19 ms of counts build +
+126 GFLOP GEMM replaced by a 184k-entry sort + ~0.4 GB of row reads).  CPU: plain torch.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -21,6 +26,7 @@ import torch
 from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
+from .conv_pool import sort_pairs_iota
 
 
 _HIST_MAX = 38912  # csrc/kernels/embedding.hip HIST_MAX
@@ -54,40 +60,76 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor) -> torch.Tensor:
     return (C @ W16).float()
 
 
+SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
+BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
+
+
 class _BagFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, W, W16, pad, mean, plan):
         ids = ids.to(torch.int32).contiguous()
         N, L = ids.shape
         V, E = W.shape
-        C, lens = _counts(ids, V, pad)
-        scale = (1.0 / lens.clamp(min=1.0)) if mean else torch.ones_like(lens)
-        if plan == "gather":
-            out = torch.empty(N, E, dtype=torch.float32, device=ids.device)
-            check(lib().pv_embedding_bag(P(ids), P(W16), P(out), None, N, L, E, V, pad, int(mean),
-                                         stream(ids.device)), "pv_embedding_bag")
-        else:
-            out = _counts_gemm(C[:, :V], W16) * scale[:, None]
-        ctx.save_for_backward(C, scale)
         ctx.V = V
         ctx.W = W  # the parameter itself (its flat-gradient view is the direct-write target)
+        ctx.mean = bool(mean)
+        if plan == "gather":
+            # short bags: row gather forward; the backward is sparse (sort the (token, slot)
+            # entries, sum each token's run of dY rows) -- no N x V counts matrix at all
+            sparse = SPARSE_BWD and V < 65535 and E % 4 == 0 and N * L < (1 << 31)
+            want_keys = sparse and ctx.needs_input_grad[1]
+            out = torch.empty(N, E, dtype=torch.float32, device=ids.device)
+            lens = torch.empty(N, dtype=torch.float32, device=ids.device)
+            keys = torch.empty(N * L, dtype=torch.int16, device=ids.device) if want_keys else None
+            check(lib().pv_embedding_bag(P(ids), P(W16), P(out), P(lens), P(keys), N, L, E, V, pad, int(mean),
+                                         stream(ids.device)), "pv_embedding_bag")
+            if want_keys or not ctx.needs_input_grad[1]:
+                ctx.sparse = (L, E)
+                ctx.save_for_backward(keys, lens)
+                return out
+            C, lens = _counts(ids, V, pad)
+        else:
+            C, lens = _counts(ids, V, pad)
+            scale = (1.0 / lens.clamp(min=1.0)) if mean else torch.ones_like(lens)
+            out = _counts_gemm(C[:, :V], W16) * scale[:, None]
+        ctx.sparse = None
+        ctx.save_for_backward(C, lens)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        C, scale = ctx.saved_tensors
-        gs = (g.float() * scale[:, None]).to(torch.bfloat16)
-        Ct = C[:, :ctx.V].t()
-        if ctx.needs_input_grad[1]:
-            W = ctx.W
-            tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
+        if not ctx.needs_input_grad[1]:
+            return None, None, None, None, None, None
+        W = ctx.W
+        V = ctx.V
+        if ctx.sparse is not None:
+            keys, lens = ctx.saved_tensors
+            L, E = ctx.sparse
+            M = keys.numel()
+            skeys = torch.empty_like(keys)
+            svals = torch.empty(M, dtype=torch.int32, device=keys.device)
+            sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
+            tw = grad_sink.accum_target(W)  # the kernel accumulates atomically
+            dW = tw if tw is not None else torch.zeros(V, E, dtype=torch.float32, device=keys.device)
+            g = g.contiguous().float()
+            check(lib().pv_bag_bwd_sorted(P(skeys), P(svals), P(g), P(lens), P(dW), M, BAG_EPW, L, E, V,
+                                          int(ctx.mean), stream(g.device)), "pv_bag_bwd_sorted")
             if tw is not None:
-                try:
-                    torch.mm(Ct, gs, out_dtype=torch.float32, out=tw)
-                except (TypeError, RuntimeError, NotImplementedError):
-                    tw.copy_(Ct @ gs)
                 grad_sink.done(W)
                 return None, None, None, None, None, None
+            return None, dW, None, None, None, None
+        C, lens = ctx.saved_tensors
+        scale = (1.0 / lens.clamp(min=1.0)) if ctx.mean else torch.ones_like(lens)
+        gs = (g.float() * scale[:, None]).to(torch.bfloat16)
+        Ct = C[:, :V].t()
+        tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
+        if tw is not None:
+            try:
+                torch.mm(Ct, gs, out_dtype=torch.float32, out=tw)
+            except (TypeError, RuntimeError, NotImplementedError):
+                tw.copy_(Ct @ gs)
+            grad_sink.done(W)
+            return None, None, None, None, None, None
         return None, (Ct @ gs).float(), None, None, None, None
 
 

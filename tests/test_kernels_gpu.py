@@ -247,7 +247,8 @@ def test_cdssm_train_step_gpu():
         assert losses[-1] < 0.5 * losses[0], (mode, losses[::8])
 
 
-@pytest.mark.parametrize("plan,L,E", [("gather", 45, 512), ("counts", 300, 512), ("gather", 20, 64), ("counts", 20, 72)])
+@pytest.mark.parametrize("plan,L,E", [("gather", 45, 512), ("counts", 300, 512), ("gather", 20, 64), ("counts", 20, 72),
+                                      ("gather", 33, 1000)])
 def test_embedding_bag(plan, L, E):
     from dnn_page_vectors_amd.ops import embedding as eops
 
@@ -264,6 +265,32 @@ def test_embedding_bag(plan, L, E):
     (out * g).sum().backward()
     (outr * g).sum().backward()
     torch.testing.assert_close(W.grad, Wr.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_embedding_bag_sparse_backward_hot_tokens():
+    """Gather plan's sparse backward (sort (token, slot) entries, sum runs, atomics): a hot
+    token whose run spans hundreds of waves, pads, and the MLP query shape (N 4096, L 45,
+    V 30000, E 512) against the fp32 reference."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    V, N, L, E = 30000, 4096, 45, 512
+    g0 = torch.Generator(device=DEV).manual_seed(2)
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV, generator=g0)
+    ids[torch.rand(N, L, device=DEV, generator=g0) < 0.3] = 7       # ~55k-entry run
+    ids[torch.rand(N, L, device=DEV, generator=g0) < 0.4] = 0       # pads
+    ids[:5] = 0                                                      # empty bags
+    W = bf(torch.randn(V, E, device=DEV, generator=g0) * 0.1).requires_grad_(True)
+    Wr = W.detach().clone().requires_grad_(True)
+    out = eops.embedding_bag(ids, W, pad=0, mean=True, plan="gather")
+    cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
+    outr = ref.embedding_bag_sum(ids, Wr, 0) / cnt
+    torch.testing.assert_close(out, outr, rtol=2e-2, atol=2e-2)
+    gy = torch.randn(N, E, device=DEV, generator=g0)
+    (out * gy).sum().backward()
+    (outr * gy).sum().backward()
+    err = float((W.grad - Wr.grad).abs().max() / Wr.grad.abs().max())
+    assert err < 1e-4, err
+    assert float(W.grad[0].abs().max()) == 0.0
 
 
 def test_trigram_hash_device():
@@ -790,7 +817,7 @@ def test_resume_restores_device_adam_step(tmp_path):
 
 @pytest.mark.parametrize("n,kbytes,end_bit", [(1, 2, 15), (100, 2, 15), (4095, 2, 15), (4096, 4, 15), (4097, 2, 8),
                                               (1_000_003, 2, 15), (17_203_200, 2, 15), (300_001, 4, 23),
-                                              (70_000, 4, 32)])
+                                              (70_000, 4, 32), (184_320, 2, 15), (2_000_000, 4, 20)])
 @pytest.mark.parametrize("impl", ["rsort", "rocprim"])
 def test_radix_sort_matches_stable_sort(n, kbytes, end_bit, impl):
     """The dTable sort (radix_sort.hip, and rocPRIM as the A/B alternative) == torch's stable
