@@ -110,6 +110,7 @@ class Configuration:
     beta1: float = 0.9
     beta2: float = 0.999
     adam_eps: float = 1e-8
+    lazy_embedding_adam: bool = False    # Adam skips embedding rows with an all-zero gradient (large vocabularies)
     dtype: str = "fp32"                   # fp32 | bf16 (compute dtype of hot kernels)
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)

@@ -82,6 +82,75 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 __global__ void step_inc_kernel(float* t) { *t += 1.f; }
 
+// Lazy (sparse-row) Adam over an embedding table (rows, cols) of the flat buffer: a row
+// whose gradient is all zero this step (its tokens were not in the batch) keeps p, m and v
+// untouched, so the step reads 4 B and writes nothing for it instead of the dense 28 B per
+// parameter (TF LazyAdam semantics; the bias corrections use the global step *tdev).
+// LPR lanes per row (cols <= 4 LPR, or LPR = 64 with up to 4 column groups per lane), so a
+// 100-wide table puts two rows in each wave; two row groups per trip keep loads in flight.
+template <int LPR>
+__global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                             float* __restrict__ m, float* __restrict__ v, long rows,
+                                                             int cols, float lr, float b1, float b2, float eps,
+                                                             float wd, int torch_style,
+                                                             const float* __restrict__ skip,
+                                                             const float* __restrict__ tdev) {
+  constexpr int NJ = LPR == 64 ? 4 : 1;  // column groups per lane
+  constexpr int RPW = 64 / LPR;          // rows per wave and trip
+  if (skip && *skip != 0.f) return;
+  const float t = *tdev;
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float lr_t = torch_style ? lr / bc1 : lr * sqrtf(bc2) / bc1;
+  const float bc2_sqrt_inv = torch_style ? rsqrtf(bc2) : 1.f;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, ln = lane % LPR;
+  const unsigned long long gmask = LPR == 64 ? ~0ull : (((1ull << LPR) - 1ull) << (sub * LPR));
+  const long wave0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long r0 = wave0 * 2 * RPW; r0 < rows; r0 += nwaves * 2 * RPW) {
+    f32x4 gg[2][NJ];
+    bool live[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long r = r0 + h * RPW + sub;
+      bool nz = false;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = 4 * ln + 4 * LPR * j;
+        gg[h][j] = (r < rows && c < cols) ? *reinterpret_cast<const f32x4*>(g + (size_t)r * cols + c)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        nz |= gg[h][j][0] != 0.f || gg[h][j][1] != 0.f || gg[h][j][2] != 0.f || gg[h][j][3] != 0.f;
+      }
+      live[h] = (__ballot(nz) & gmask) != 0ull;  // any column of MY row
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long r = r0 + h * RPW + sub;
+      if (!live[h] || r >= rows) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = 4 * ln + 4 * LPR * j;
+        if (c >= cols) continue;
+        const size_t o = (size_t)r * cols + c;
+        f32x4 pp = *reinterpret_cast<f32x4*>(p + o);
+        f32x4 mm = *reinterpret_cast<f32x4*>(m + o);
+        f32x4 vv = *reinterpret_cast<f32x4*>(v + o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float gk = gg[h][j][k] + wd * pp[k];
+          mm[k] = b1 * mm[k] + (1.f - b1) * gk;
+          vv[k] = b2 * vv[k] + (1.f - b2) * gk * gk;
+          const float den = torch_style ? (sqrtf(vv[k]) * bc2_sqrt_inv + eps) : (sqrtf(vv[k]) + eps);
+          pp[k] -= lr_t * mm[k] / den;
+        }
+        *reinterpret_cast<f32x4*>(p + o) = pp;
+        *reinterpret_cast<f32x4*>(m + o) = mm;
+        *reinterpret_cast<f32x4*>(v + o) = vv;
+      }
+    }
+  }
+}
+
 // fp32 (rows, cols) -> bf16 (rows, ldo) with zero padding of columns cols..ldo-1
 __global__ void cast_pad_bf16_kernel(const float* __restrict__ in, unsigned short* __restrict__ out, long rows, int cols,
                                      int ldo) {
@@ -167,6 +236,43 @@ PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                      lr, b1, b2, eps, wd, torch_style, 1.f, skip, (const float*)tdev);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Segmented step (lazy embedding rows): pv_step_inc once, then one pv_adam_seg per range of
+// the flat buffer — row_len 0: dense update of n elements; row_len > 0: lazy rows of an
+// (n / row_len, row_len) table.
+PV_API int pv_step_inc(float* tdev, void* stream) {
+  hipLaunchKernelGGL(pv::optim::step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, tdev);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_adam_seg(float* p, const float* g, float* m, float* v, long n, int row_len, const float* tdev, float lr,
+                       float b1, float b2, float eps, float wd, int torch_style, const float* skip, void* stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+  if (n <= 0) return 0;
+  if (row_len == 0) {
+    hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                       lr, b1, b2, eps, wd, torch_style, 1.f, skip, tdev);
+  } else {
+    if (row_len % 4 || row_len > 1024 || n % row_len) return -2;
+    const long rows = n / row_len;
+    const int lpr = row_len <= 32 ? 8 : row_len <= 64 ? 16 : row_len <= 128 ? 32 : 64;
+    long blocks = (rows + 8L * (64 / lpr) - 1) / (8L * (64 / lpr));  // 4 waves x 2 row groups
+    if (blocks > 16384) blocks = 16384;
+    const dim3 grid((unsigned)blocks);
+    hipStream_t st = (hipStream_t)stream;
+#define PV_LAZY(LPR)                                                                                          \
+  hipLaunchKernelGGL(pv::optim::adam_lazy_rows_kernel<LPR>, grid, dim3(256), 0, st, p, g, m, v, rows, row_len, lr, \
+                     b1, b2, eps, wd, torch_style, skip, tdev)
+    if (lpr == 8) PV_LAZY(8);
+    else if (lpr == 16) PV_LAZY(16);
+    else if (lpr == 32) PV_LAZY(32);
+    else PV_LAZY(64);
+#undef PV_LAZY
+  }
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -78,6 +78,8 @@ SIGS = {
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip
     "pv_adam_dev": "pppp" "l" "p" "fffff" "i" "p" "p",
+    "pv_step_inc": "p" "p",
+    "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "p" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
     "pv_sumsq": "p" "l" "p" "p",

@@ -79,8 +79,20 @@ class FlatParams:
 
 class FlatAdam:
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, torch_style: bool = False):
+                 weight_decay: float = 0.0, torch_style: bool = False, lazy: Optional[Iterable[str]] = None):
+        """lazy: names of 2-D embedding tables updated LazyAdam-style — a row whose gradient is
+        all zero this step (none of its tokens in the batch) keeps its weights and moments
+        (optim.hip::adam_lazy_rows_kernel; the step then streams ~4 B instead of 28 B per
+        untouched parameter, which is what makes word-level vocabularies of millions of rows
+        cheap).  Default: dense Adam everywhere (Keras parity)."""
         self.flat = flat
+        # [(offset, numel, row_len)] sorted by offset; rows of 4k floats (16-byte aligned)
+        self.lazy: List[Tuple[int, int, int]] = []
+        for name in (lazy or ()):
+            o, k, shp = flat.offsets[name]
+            if len(shp) == 2 and shp[1] % 4 == 0 and shp[1] <= 1024:
+                self.lazy.append((o, k, int(shp[1])))
+        self.lazy.sort()
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
         self.torch_style = torch_style
         self.m = torch.zeros_like(flat.data)
@@ -95,12 +107,20 @@ class FlatAdam:
         self.step_count += 1
         t = self.step_count
         if use_hip(self.flat.data):
+            if self.lazy:
+                self._step_segments(skip_flag)
+                return
             check(lib().pv_adam_dev(P(self.flat.data), P(self.flat.grad), P(self.m), P(self.v), self.flat.numel,
                                     P(self.t_dev), self.lr, self.b1, self.b2, self.eps, self.wd,
                                     int(self.torch_style), P(skip_flag), stream(self.flat.data.device)), "pv_adam_dev")
             return
         if skip_flag is not None and float(skip_flag) != 0.0:
             return
+        keep = []
+        for o, k, rl in self.lazy:  # CPU: dense update, then restore the untouched rows
+            untouched = (self.flat.grad[o:o + k].view(-1, rl) == 0).all(1)
+            keep.append((o, k, rl, untouched, [t[o:o + k].view(-1, rl)[untouched].clone()
+                                                for t in (self.flat.data, self.m, self.v)]))
         with torch.no_grad():
             g = self.flat.grad + self.wd * self.flat.data if self.wd else self.flat.grad
             if self.torch_style:
@@ -111,6 +131,31 @@ class FlatAdam:
                 self.flat.data.addcdiv_(self.m, (self.v.sqrt() / math.sqrt(bc2)).add_(self.eps), value=-self.lr / bc1)
             else:
                 ref.adam_keras_([self.flat.data], [g], [self.m], [self.v], t, self.lr, self.b1, self.b2, self.eps)
+            for o, k, rl, untouched, saved in keep:
+                for tt, sv in zip((self.flat.data, self.m, self.v), saved):
+                    tt[o:o + k].view(-1, rl)[untouched] = sv
+
+    def _step_segments(self, skip_flag: Optional[torch.Tensor]) -> None:
+        """Device step count +1, then dense updates of the gaps between lazy tables and lazy
+        row updates of the tables (all reading the device counter: hipGraph-replayable)."""
+        L_ = lib()
+        s = stream(self.flat.data.device)
+        check(L_.pv_step_inc(P(self.t_dev), s), "pv_step_inc")
+        pos = 0
+        segs = []
+        for o, k, rl in self.lazy:
+            if o > pos:
+                segs.append((pos, o - pos, 0))
+            segs.append((o, k, rl))
+            pos = o + (k + 63) // 64 * 64
+        if pos < self.flat.numel:
+            segs.append((pos, self.flat.numel - pos, 0))
+        esz = self.flat.data.element_size()
+        base = [t.data_ptr() for t in (self.flat.data, self.flat.grad, self.m, self.v)]
+        for o, n, rl in segs:
+            ptrs = [b + o * esz for b in base]
+            check(L_.pv_adam_seg(ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, rl, P(self.t_dev), self.lr, self.b1, self.b2,
+                                 self.eps, self.wd, int(self.torch_style), P(skip_flag), s), "pv_adam_seg")
 
     def state_dict(self) -> Dict[str, object]:
         return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr}

@@ -86,8 +86,11 @@ class Trainer:
         self.flat = FlatParams(self.model.named_parameters())
         broadcast_params(self.flat)
         bump_generation()
+        lazy = None
+        if getattr(cfg, "lazy_embedding_adam", False):
+            lazy = [n for n, p in self.flat.named if n.rsplit(".", 1)[-1] in ("embedding", "word") and p.dim() == 2]
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
-                            torch_style=(cfg.model == "bert"))
+                            torch_style=(cfg.model == "bert"), lazy=lazy)
         self.placement = getattr(cfg, "placement", "dp")
         if self.placement not in ("dp", "tower"):
             raise ValueError(f"unknown placement {self.placement!r}")

@@ -975,3 +975,39 @@ def test_direct_grad_weight_used_twice(monkeypatch):
     for got, want in ((gw, wr.grad), (gb, br.grad)):
         err = float((got - want).abs().max() / want.abs().max())
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("torch_style,E", [(False, 96), (True, 96), (False, 20), (False, 60), (True, 300)])
+def test_lazy_embedding_adam_matches_cpu(torch_style, E):
+    """FlatAdam(lazy=[table]): untouched embedding rows keep weights and moments; touched rows
+    and every other parameter get the dense update (HIP segmented step vs the CPU path)."""
+    from dnn_page_vectors_amd.ops.optim import FlatAdam, FlatParams
+
+    def make(dev):
+        torch.manual_seed(0)
+        m = torch.nn.ModuleDict({"lin": torch.nn.Linear(33, 17), "tok": torch.nn.Embedding(301, E)})
+        return m.to(dev)
+
+    res = []
+    for dev in ("cpu", DEV):
+        m = make(dev)
+        flat = FlatParams(m.named_parameters())
+        opt = FlatAdam(flat, lr=1e-2, torch_style=torch_style, lazy=["tok.weight"])
+        assert opt.lazy
+        g = torch.Generator().manual_seed(1)
+        for t in range(4):
+            gr = torch.randn(flat.numel, generator=g)
+            o, k, _ = flat.offsets["tok.weight"]
+            tab = gr[o:o + k].view(301, E)
+            tab[torch.arange(301) % (t + 2) != 0] = 0.0   # a different row subset each step
+            gr[o + k:o + (k + 63) // 64 * 64] = 0.0        # alignment padding carries no gradient
+            flat.grad.copy_(gr.to(dev))
+            opt.step()
+        res.append((flat.data.cpu(), opt.m.cpu(), opt.v.cpu()))
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    # rows never touched (odd rows with t+2 in {2,3,4,5} all skipping them: rows % 60 == 1) keep init
+    o, k, _ = flat.offsets["tok.weight"]
+    mv = res[1][1][o:o + k].view(301, E)
+    never = [r for r in range(301) if all(r % (t + 2) != 0 for t in range(4))]
+    assert never and float(mv[never].abs().max()) == 0.0

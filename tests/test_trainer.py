@@ -104,3 +104,27 @@ def test_metrics_jsonl_has_step_breakdown(tmp_path):
         for k in ("forward_ms", "backward_ms", "allreduce_ms", "optimizer_ms", "step_ms", "pairs_per_s", "hbm_gb"):
             assert k in r, r
         assert abs(r["step_ms"] - (r["forward_ms"] + r["backward_ms"] + r["allreduce_ms"] + r["optimizer_ms"])) < 0.01
+
+
+def test_lazy_embedding_adam_keeps_untouched_rows(tmp_path):
+    """cfg.lazy_embedding_adam: an embedding row whose tokens are absent from a step keeps its
+    weights (dense Adam would keep moving it on its momentum); dense parameters still train."""
+    moved = {}
+    for lazy in (True, False):
+        cfg = _cfg(tmp_path).replace(lazy_embedding_adam=lazy, dropout_prob=(0.0, 0.0))
+        torch.manual_seed(0)
+        tr = Trainer(cfg, CDSSM(cfg, 200))
+        assert bool(tr.opt.lazy) == lazy
+        emb = tr.model.doc_towers[0].embedding
+        g = torch.Generator().manual_seed(0)
+        q = torch.randint(1, 150, (cfg.batch_size, cfg.query_length), dtype=torch.int32, generator=g)
+        d1 = torch.randint(1, 150, (cfg.batch_size, cfg.J + 1, cfg.document_length), dtype=torch.int32, generator=g)
+        d2 = torch.randint(1, 100, (cfg.batch_size, cfg.J + 1, cfg.document_length), dtype=torch.int32, generator=g)
+        tr.train_step(q, d1)
+        after1 = emb.detach().clone()
+        conv1 = tr.model.doc_towers[0].conv_w[0].detach().clone()
+        tr.train_step(q, d2)
+        moved[lazy] = float((emb.detach()[100:150] - after1[100:150]).abs().max())
+        assert not torch.equal(emb.detach()[1:100], after1[1:100])
+        assert not torch.equal(tr.model.doc_towers[0].conv_w[0].detach(), conv1)
+    assert moved[True] == 0.0 and moved[False] > 0.0, moved

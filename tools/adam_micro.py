@@ -1,7 +1,11 @@
 """Flat-buffer Adam bandwidth: pv_adam (HIP) vs torch.optim.Adam(fused=True) on the same
 16 M fp32 parameters (28 bytes moved per parameter).
 
-    python tools/adam_micro.py [--n 16777216]
+    python tools/adam_micro.py [--n 16777216] [--lazy-rows 7500000 --lazy-cols 100 --touched 0.01]
+
+--lazy-rows: also time the lazy embedding-row update (pv_adam_seg row_len > 0) on a
+(rows, cols) table with a fraction ``--touched`` of rows carrying a gradient, against the
+dense update of the same table (a word-level vocabulary of millions of rows).
 """
 import argparse
 import json
@@ -26,12 +30,35 @@ def ev(fn, iters=20):
     return a.elapsed_time(b) / iters
 
 
+def lazy(a):
+    from dnn_page_vectors_amd.ops._common import P, check, lib, stream
+
+    R, C = a.lazy_rows, a.lazy_cols
+    n = R * C
+    p, m, v = (torch.zeros(n, device="cuda") for _ in range(3))
+    g = torch.zeros(R, C, device="cuda")
+    rows = torch.randperm(R, device="cuda")[:max(1, int(R * a.touched))]
+    g[rows] = torch.randn(rows.numel(), C, device="cuda")
+    t = torch.ones(1, device="cuda")
+    L = lib()
+    res = {}
+    for name, rl in (("dense", 0), ("lazy", C)):
+        res[name + "_ms"] = round(ev(lambda: check(L.pv_adam_seg(P(p), P(g), P(m), P(v), n, rl, P(t), 1e-3, 0.9, 0.999,
+                                                                  1e-8, 0.0, 0, None, stream()), "seg")), 4)
+    print(json.dumps({"rows": R, "cols": C, "touched": a.touched, **res}), flush=True)
+
+
 def main():
     from dnn_page_vectors_amd.ops._common import P, check, lib, stream
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16 * 1024 * 1024)
+    ap.add_argument("--lazy-rows", type=int, default=0)
+    ap.add_argument("--lazy-cols", type=int, default=100)
+    ap.add_argument("--touched", type=float, default=0.01)
     a = ap.parse_args()
+    if a.lazy_rows:
+        lazy(a)
     n = a.n
     p, g, m, v = (torch.randn(n, device="cuda") for _ in range(4))
     v.abs_()
