@@ -215,6 +215,74 @@ __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restr
   }
 }
 
+// Column sums (the bias / split-K reductions of the backward and the split-K forward):
+//   s[c] = sum_{r < R} x[r * ldx + c]
+// mode 0: out[c] = s[c]                      (one row split; overwrite)
+// mode 1: out[c] += s[c]  (float atomics)    (row splits; out pre-zeroed or a flat-gradient
+//                                             region, ops/grad_sink.py)
+// mode 2: out[c] = act(scale[c / E] * s[c] + bias[c % E])  (one row split; scale / bias
+//                                             optional: the counts-GEMM bag epilogue)
+// Block = QB column quads (4 consecutive columns: 16-byte fp32 / 8-byte bf16 loads) x
+// RG = 256 / QB row groups; the row groups meet in LDS, then one store / atomic per column
+// and block (<= 64 row splits: bounded same-address atomics).  blockIdx.y = row split.
+template <typename TX, int QB>
+__global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, long R, long C, long ldx,
+                                                     float* __restrict__ out, long rps, int mode,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ bias, int E, int act) {
+  constexpr int RG = 256 / QB;
+  __shared__ f32x4 red[RG][QB];
+  const int qi = threadIdx.x % QB, rg = threadIdx.x / QB;
+  const long c = 4 * ((long)blockIdx.x * QB + qi);
+  const bool live = c < C;
+  const long r0 = (long)blockIdx.y * rps;
+  const long r1 = min(R, r0 + rps);
+  auto ld4 = [&](long r) -> f32x4 {
+    if constexpr (sizeof(TX) == 4) {
+      return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(x) + r * ldx + c);
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(x) + r * ldx + c);
+      return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+                   __uint_as_float(u.y & 0xFFFF0000u)};
+    }
+  };
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  if (live) {
+    long r = r0 + rg;
+    for (; r + 3 * RG < r1; r += 4 * RG) {
+      a0 += ld4(r);
+      a1 += ld4(r + RG);
+      a2 += ld4(r + 2 * RG);
+      a3 += ld4(r + 3 * RG);
+    }
+    for (; r < r1; r += RG) a0 += ld4(r);
+  }
+  red[rg][qi] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (rg != 0 || !live) return;
+  f32x4 s4 = red[0][qi];
+#pragma unroll 4
+  for (int g = 1; g < RG; ++g) s4 += red[g][qi];
+  if (mode == 1) {
+    atomicAdd(out + c + 0, s4[0]);
+    atomicAdd(out + c + 1, s4[1]);
+    atomicAdd(out + c + 2, s4[2]);
+    atomicAdd(out + c + 3, s4[3]);
+    return;
+  }
+  if (mode == 2) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long cc = c + k;
+      float y = s4[k];
+      if (scale) y *= scale[cc / E];
+      if (bias) y += bias[cc % E];
+      s4[k] = act_fn(y, act);
+    }
+  }
+  *reinterpret_cast<f32x4*>(out + c) = s4;
+}
+
 }  // namespace dense
 }  // namespace pv
 
@@ -266,6 +334,45 @@ PV_API int pv_act_bwd(const float* y, const float* dy, float* dz, long n, int ac
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, n, act);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// xdt: 0 fp32, 1 bf16.  mode / epilogue: see colsum_kernel.  Narrow sums (bias gradients,
+// C <= 4096) use 16 quads x 16 row groups per block, wide ones (split-K partials) 64 x 4;
+// mode 1 adds row splits (<= 64) until the launch covers the chip.
+PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* out, int mode, const float* scale,
+                     const float* bias, int E, int act, void* stream) {
+  using namespace pv::dense;
+  if (C % 4 || ldx % 4 || R < 1 || ((uintptr_t)out & 15) || ((uintptr_t)x & (xdt ? 7 : 15))) return -1;
+  if (mode == 2 && E < 1) return -2;
+  const long quads = C / 4;
+  const bool narrow = quads <= 1024;
+  const int QB = narrow ? 16 : 64, RG = 256 / QB;
+  const long gx = (quads + QB - 1) / QB;
+  long splits = 1;
+  if (mode == 1) {
+    splits = (1024 + gx - 1) / gx;
+    const long maxs = (R + 4 * RG - 1) / (4 * RG);  // >= 4 rows per thread
+    if (splits > maxs) splits = maxs;
+    if (splits > 64) splits = 64;
+    if (splits < 1) splits = 1;
+  }
+  const long rps = (R + splits - 1) / splits;
+  splits = (R + rps - 1) / rps;
+  const dim3 grid((unsigned)gx, (unsigned)splits);
+  hipStream_t st = (hipStream_t)stream;
+#define PV_COLSUM(T, Q)                                                                                          \
+  hipLaunchKernelGGL((colsum_kernel<T, Q>), grid, dim3(256), 0, st, (const T*)x, R, C, ldx, out, rps, mode, scale, \
+                     bias, E, act)
+  if (xdt == 1) {
+    if (narrow) PV_COLSUM(unsigned short, 16);
+    else PV_COLSUM(unsigned short, 64);
+  } else {
+    if (narrow) PV_COLSUM(float, 16);
+    else PV_COLSUM(float, 64);
+  }
+#undef PV_COLSUM
   PV_LAUNCH_CHECK();
   return 0;
 }

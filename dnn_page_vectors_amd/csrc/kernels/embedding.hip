@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restric
                                                             const unsigned short* __restrict__ W,
                                                             float* __restrict__ out, float* __restrict__ lens_out,
                                                             unsigned short* __restrict__ keys_out,
+                                                            const float* __restrict__ bias, int act,
                                                             int N, int L, int E, int V, int pad, int mean) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -108,8 +109,15 @@ __global__ __launch_bounds__(256) void embedding_bag_kernel(const int* __restric
   for (int c = 0; c < 2; ++c) {
     const int ch = lane + 64 * c;
     if (ch < nchunk) {
-      f32x4 lo = {acc[c][0] * s, acc[c][1] * s, acc[c][2] * s, acc[c][3] * s};
-      f32x4 hi = {acc[c][4] * s, acc[c][5] * s, acc[c][6] * s, acc[c][7] * s};
+      // epilogue: act(mean + bias) (the MLP tower's first layer, fused)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float y = acc[c][k] * s;
+        if (bias) y += bias[ch * 8 + k];
+        acc[c][k] = act == 1 ? fmaxf(y, 0.f) : act == 3 ? tanhf(y) : y;
+      }
+      f32x4 lo = {acc[c][0], acc[c][1], acc[c][2], acc[c][3]};
+      f32x4 hi = {acc[c][4], acc[c][5], acc[c][6], acc[c][7]};
       *reinterpret_cast<f32x4*>(out + (size_t)n * E + ch * 8) = lo;
       *reinterpret_cast<f32x4*>(out + (size_t)n * E + ch * 8 + 4) = hi;
     }
@@ -305,12 +313,13 @@ PV_API int pv_trigram_hash(const void* text, const int* lens, int* out, int N, i
   return 0;
 }
 
-PV_API int pv_embedding_bag(const int* ids, const void* W, float* out, float* lens, void* keys, int N, int L, int E,
-                            int V, int pad, int mean, void* stream) {
-  if (E % 8 || E > 1024) return -1;
+// act: 0 none, 1 relu, 3 tanh (applied after the optional bias)
+PV_API int pv_embedding_bag(const int* ids, const void* W, float* out, float* lens, void* keys, const float* bias,
+                            int act, int N, int L, int E, int V, int pad, int mean, void* stream) {
+  if (E % 8 || E > 1024 || (act != 0 && act != 1 && act != 3)) return -1;
   if (keys && V >= 65535) return -2;  // 16-bit sort keys (sentinel V)
   hipLaunchKernelGGL(pv::embed::embedding_bag_kernel, dim3((N + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids,
-                     (const unsigned short*)W, out, lens, (unsigned short*)keys, N, L, E, V, pad, mean);
+                     (const unsigned short*)W, out, lens, (unsigned short*)keys, bias, act, N, L, E, V, pad, mean);
   PV_LAUNCH_CHECK();
   return 0;
 }

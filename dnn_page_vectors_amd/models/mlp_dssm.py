@@ -58,12 +58,17 @@ class MLPTower(nn.Module):
         if ids.dtype != torch.int32:
             ids = ids.to(torch.int32)
         cache = cache or {}
+        if self.act in ("none", "relu", "tanh"):  # first bias + activation fused into the bag kernel
+            h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True, bias=self.b1,
+                                   act=self.act)
+            return self.dense_stack(h, cache, first_done=True)
         h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True)
         return self.dense_stack(h, cache)
 
-    def dense_stack(self, h: torch.Tensor, cache=None) -> torch.Tensor:
+    def dense_stack(self, h: torch.Tensor, cache=None, first_done: bool = False) -> torch.Tensor:
         cache = cache or {}
-        h = _bias_act(h, self.b1, self.act)
+        if not first_done:
+            h = _bias_act(h, self.b1, self.act)
         n = len(self.ws)
         w8 = cache.get("w8")
         for i, (w, b) in enumerate(zip(self.ws, self.bs)):

@@ -55,7 +55,7 @@ SIGS = {
     "pv_ib_rows": "pppp" "ii" "fi" "p",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
-    "pv_embedding_bag": "ppppp" "iiiiii" "p",
+    "pv_embedding_bag": "ppppp" "pi" "iiiiii" "p",
     "pv_bag_bwd_sorted": "ppppp" "liiiii" "p",
     "pv_bag_counts": "ppp" "iiiiii" "p",
     # topk.hip
@@ -78,6 +78,7 @@ SIGS = {
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip
     "pv_adam_dev": "pppp" "l" "p" "fffff" "i" "p" "p",
+    "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
     "pv_step_inc": "p" "p",
     "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "p" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",

@@ -7,6 +7,7 @@ GEMMs for plain GEMMs, hand-written kernels for the fused hot ops).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -68,11 +69,74 @@ class _LinearActFn(torch.autograd.Function):
         if b is not None and ctx.needs_input_grad[2]:
             tb = grad_sink.write_target(ctx.params[1])
             if tb is not None:
-                torch.sum(dz, 0, out=tb)
+                colsum(dz, out=tb, accumulate=True)  # first contribution: the region is zero
                 grad_sink.done(ctx.params[1])
             else:
-                db = dz.sum(0)
+                db = colsum(dz)
         return dx, dw, db, None
+
+
+_COLSUM_HIP = os.environ.get("PAGEVEC_COLSUM", "1") != "0"  # 0: torch reductions (A/B)
+
+
+def _colsum_ok(x: torch.Tensor, C: int, ldx: int) -> bool:
+    return (_COLSUM_HIP and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and C % 4 == 0 and ldx % 4 == 0
+            and x.data_ptr() % 16 == 0)
+
+
+def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False, scale=None, bias=None,
+           act: str = "none") -> torch.Tensor:
+    """Sum over the leading axis of x (R, ...) -> fp32 (...) on the HIP column-sum kernel
+    (dense.hip::colsum_kernel): the bias gradients and split-K partial sums of the backward.
+    ``accumulate``: add into ``out`` (a zeroed buffer or a flat-gradient region).
+    ``scale`` (rows of the result) / ``bias`` (its last axis) / ``act``: fused epilogue
+    act(scale * sum + bias) of the split-K forward (no accumulate)."""
+    R = x.shape[0]
+    tail = x.shape[1:]
+    C = 1
+    for d in tail:
+        C *= int(d)
+    epi = scale is not None or bias is not None or act != "none"
+    x2 = x.reshape(R, C) if x.is_contiguous() else x.contiguous().reshape(R, C)
+    if use_hip(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)):
+        E = int(tail[-1]) if len(tail) else 1
+        if epi:
+            mode = 2
+        elif accumulate or R > 64:
+            mode = 1
+        else:
+            mode = 0
+        if out is None:
+            out = (torch.zeros if mode == 1 else torch.empty)(tail, dtype=torch.float32, device=x.device)
+        elif mode == 1 and not accumulate:
+            out.zero_()
+        sc = scale.float().contiguous() if scale is not None else None
+        bb = bias.float().contiguous() if bias is not None else None
+        check(lib().pv_colsum(P(x2), 1 if x2.dtype == torch.bfloat16 else 0, R, C, C, P(out), mode, P(sc), P(bb), E,
+                              _ACT[act], stream(x.device)), "pv_colsum")
+        return out
+    if not epi and out is not None and not accumulate and out.dtype == torch.float32:
+        return torch.sum(x, 0, dtype=torch.float32, out=out)
+    y = torch.sum(x, 0, dtype=torch.float32)
+    if epi:
+        if scale is not None:
+            y = y * scale.reshape(-1, *([1] * (y.dim() - 1))).float()
+        if bias is not None:
+            y = y + bias.float()
+        y = _torch_act(y, act)
+    if out is None:
+        return y
+    return out.add_(y) if accumulate else out.copy_(y)
+
+
+def _torch_act(y: torch.Tensor, act: str) -> torch.Tensor:
+    if act == "relu":
+        return torch.relu(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    if act == "gelu":
+        return torch.nn.functional.gelu(y, approximate="tanh")
+    return y
 
 
 def _wgrad(dz: torch.Tensor, xf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -86,7 +150,7 @@ def _wgrad(dz: torch.Tensor, xf: torch.Tensor, out: Optional[torch.Tensor] = Non
     if sk == 1:
         return torch.mm(dz.t(), xf, out=out)
     part = torch.bmm(dz.view(sk, T // sk, -1).transpose(1, 2), xf.view(sk, T // sk, -1))
-    return torch.sum(part, 0, out=out)
+    return colsum(part, out=out)
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "relu") -> torch.Tensor:

@@ -23,6 +23,7 @@ from typing import Optional
 
 import torch
 
+from . import dense as dops
 from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
@@ -43,7 +44,8 @@ def _counts(ids: torch.Tensor, V: int, pad: int):
     return C, lens
 
 
-def _counts_gemm(C: torch.Tensor, W16: torch.Tensor) -> torch.Tensor:
+def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, scale: Optional[torch.Tensor] = None,
+                 bias: Optional[torch.Tensor] = None, act: str = "none") -> torch.Tensor:
     """C (N, V) @ W16 (V, E) in fp32.  The (N, E) output has only (N/256)(E/256) = 32 tiles for
     the MLP page bags (N 4096, E 512) over a 30000-long reduction, so the single GEMM runs on
     a fraction of the CUs; split V into 8 batched fp32-output GEMMs and sum the partials:
@@ -54,25 +56,43 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor) -> torch.Tensor:
     if sk > 1 and N * E <= 8 * 1024 * 1024:
         try:
             Cb = C.unflatten(1, (sk, V // sk)).transpose(0, 1)
-            return torch.bmm(Cb, W16.reshape(sk, V // sk, E), out_dtype=torch.float32).sum(0)
+            part = torch.bmm(Cb, W16.reshape(sk, V // sk, E), out_dtype=torch.float32)
         except (TypeError, RuntimeError, NotImplementedError):
-            pass
-    return (C @ W16).float()
+            part = None
+        if part is not None:  # split-K sum fused with the bag-mean scale / bias / activation
+            return dops.colsum(part, scale=scale, bias=bias, act=act)
+    out = (C @ W16).float()
+    if scale is not None:
+        out = out * scale[:, None]
+    if bias is not None:
+        out = out + bias.float()
+    return dops._torch_act(out, act)
 
 
 SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
 BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
 
 
+_BAG_ACT = {"none": 0, "relu": 1, "tanh": 3}
+
+
 class _BagFn(torch.autograd.Function):
+    """act(scale * counts(ids) @ W + bias): the bag, its mean, and (optionally) the MLP
+    tower's first bias + activation in the producing kernel (gather epilogue / split-K sum
+    epilogue); the backward runs the activation mask, the bias column sum and dW."""
+
     @staticmethod
-    def forward(ctx, ids, W, W16, pad, mean, plan):
+    def forward(ctx, ids, W, W16, pad, mean, plan, bias, act):
         ids = ids.to(torch.int32).contiguous()
         N, L = ids.shape
         V, E = W.shape
         ctx.V = V
-        ctx.W = W  # the parameter itself (its flat-gradient view is the direct-write target)
+        ctx.W = W  # the parameters themselves (flat-gradient direct-write targets)
+        ctx.bias = bias
+        ctx.act = act
         ctx.mean = bool(mean)
+        bf = bias.float().contiguous() if bias is not None else None
+        C = None
         if plan == "gather":
             # short bags: row gather forward; the backward is sparse (sort the (token, slot)
             # entries, sum each token's run of dY rows) -- no N x V counts matrix at all
@@ -81,29 +101,41 @@ class _BagFn(torch.autograd.Function):
             out = torch.empty(N, E, dtype=torch.float32, device=ids.device)
             lens = torch.empty(N, dtype=torch.float32, device=ids.device)
             keys = torch.empty(N * L, dtype=torch.int16, device=ids.device) if want_keys else None
-            check(lib().pv_embedding_bag(P(ids), P(W16), P(out), P(lens), P(keys), N, L, E, V, pad, int(mean),
-                                         stream(ids.device)), "pv_embedding_bag")
-            if want_keys or not ctx.needs_input_grad[1]:
-                ctx.sparse = (L, E)
-                ctx.save_for_backward(keys, lens)
-                return out
-            C, lens = _counts(ids, V, pad)
+            check(lib().pv_embedding_bag(P(ids), P(W16), P(out), P(lens), P(keys), P(bf), _BAG_ACT[act], N, L, E, V,
+                                         pad, int(mean), stream(ids.device)), "pv_embedding_bag")
+            if not want_keys and ctx.needs_input_grad[1]:
+                C, lens = _counts(ids, V, pad)
         else:
             C, lens = _counts(ids, V, pad)
-            scale = (1.0 / lens.clamp(min=1.0)) if mean else torch.ones_like(lens)
-            out = _counts_gemm(C[:, :V], W16) * scale[:, None]
-        ctx.sparse = None
-        ctx.save_for_backward(C, lens)
+            scale = (1.0 / lens.clamp(min=1.0)) if mean else None
+            out = _counts_gemm(C[:, :V], W16, scale, bf, act)
+            keys = None
+        ctx.sparse = (L, E) if C is None else None
+        ctx.save_for_backward(keys if C is None else C, lens, out if act != "none" else None)
         return out
 
     @staticmethod
     def backward(ctx, g):
+        W, V, bias = ctx.W, ctx.V, ctx.bias
+        first, lens, y = ctx.saved_tensors
+        g = g.contiguous().float()
+        if y is not None:  # activation mask: dpre = dy * act'(y)
+            dz = torch.empty_like(g)
+            check(lib().pv_act_bwd(P(y), P(g), P(dz), g.numel(), _BAG_ACT[ctx.act], stream(g.device)), "pv_act_bwd")
+            g = dz
+        db = None
+        if bias is not None and ctx.needs_input_grad[6]:
+            tb = grad_sink.write_target(bias)
+            db = dops.colsum(g, out=tb, accumulate=tb is not None)  # a first contribution's region is zero
+            if tb is not None:
+                grad_sink.done(bias)
+                db = None
+            elif db.dtype != bias.dtype:
+                db = db.to(bias.dtype)
         if not ctx.needs_input_grad[1]:
-            return None, None, None, None, None, None
-        W = ctx.W
-        V = ctx.V
+            return None, None, None, None, None, None, db, None
         if ctx.sparse is not None:
-            keys, lens = ctx.saved_tensors
+            keys = first
             L, E = ctx.sparse
             M = keys.numel()
             skeys = torch.empty_like(keys)
@@ -111,16 +143,15 @@ class _BagFn(torch.autograd.Function):
             sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
             tw = grad_sink.accum_target(W)  # the kernel accumulates atomically
             dW = tw if tw is not None else torch.zeros(V, E, dtype=torch.float32, device=keys.device)
-            g = g.contiguous().float()
             check(lib().pv_bag_bwd_sorted(P(skeys), P(svals), P(g), P(lens), P(dW), M, BAG_EPW, L, E, V,
                                           int(ctx.mean), stream(g.device)), "pv_bag_bwd_sorted")
             if tw is not None:
                 grad_sink.done(W)
-                return None, None, None, None, None, None
-            return None, dW, None, None, None, None
-        C, lens = ctx.saved_tensors
+                dW = None
+            return None, dW, None, None, None, None, db, None
+        C = first
         scale = (1.0 / lens.clamp(min=1.0)) if ctx.mean else torch.ones_like(lens)
-        gs = (g.float() * scale[:, None]).to(torch.bfloat16)
+        gs = (g * scale[:, None]).to(torch.bfloat16)
         Ct = C[:, :V].t()
         tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
         if tw is not None:
@@ -129,25 +160,29 @@ class _BagFn(torch.autograd.Function):
             except (TypeError, RuntimeError, NotImplementedError):
                 tw.copy_(Ct @ gs)
             grad_sink.done(W)
-            return None, None, None, None, None, None
-        return None, (Ct @ gs).float(), None, None, None, None
+            return None, None, None, None, None, None, db, None
+        return None, (Ct @ gs).float(), None, None, None, None, db, None
 
 
 def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor] = None, pad: int = 0,
-                  mean: bool = True, plan: str = "auto") -> torch.Tensor:
-    """(N, L) ids -> (N, E): sum (or mean) of the rows of W over non-pad tokens."""
-    if use_hip(ids, W):
+                  mean: bool = True, plan: str = "auto", bias: Optional[torch.Tensor] = None,
+                  act: str = "none") -> torch.Tensor:
+    """(N, L) ids -> (N, E): act(sum (or mean) of the rows of W over non-pad tokens + bias).
+    ``act`` in {none, relu, tanh}; bias / act are fused into the producing kernel on the GPU."""
+    if use_hip(ids, W) and act in _BAG_ACT:
         if W16 is None:
             W16 = W.detach().to(torch.bfloat16).contiguous()
         if plan == "auto":
             plan = "gather" if ids.shape[1] <= 256 else "counts"
         if W.shape[1] % 8:
             plan = "counts"
-        return _BagFn.apply(ids, W, W16, pad, mean, plan)
+        return _BagFn.apply(ids, W, W16, pad, mean, plan, bias, act)
     out = ref.embedding_bag_sum(ids, W, pad)
     if mean:
         out = out / (ids != pad).sum(dim=1, keepdim=True).clamp(min=1).to(out.dtype)
-    return out
+    if bias is not None:
+        out = out + bias
+    return dops._torch_act(out, act)
 
 
 def trigram_hash(text: torch.Tensor, lens: torch.Tensor, L: int, hash_size: int) -> torch.Tensor:

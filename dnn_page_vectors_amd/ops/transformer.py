@@ -13,6 +13,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from . import dense as dops
 from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
@@ -341,7 +342,7 @@ def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] =
             return torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=out)
         dy3 = dy2.view(sk, T // sk, dy2.shape[1])
         x3 = x2.view(sk, T // sk, x2.shape[1])
-        return torch.sum(torch.bmm(dy3.transpose(1, 2), x3, out_dtype=torch.float32), 0, out=out)
+        return dops.colsum(torch.bmm(dy3.transpose(1, 2), x3, out_dtype=torch.float32), out=out)
     except (TypeError, RuntimeError, NotImplementedError):  # no mm/bmm out_dtype (CPU)
         r = dy2.t().float() @ x2.float()
         return r if out is None else out.copy_(r)
@@ -379,7 +380,7 @@ class _Linear16Fn(torch.autograd.Function):
                 dw = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             tb = grad_sink.write_target(pb)
-            db = torch.sum(dy2, 0, dtype=torch.float32, out=tb)
+            db = dops.colsum(dy2, out=tb, accumulate=tb is not None)  # a first contribution's region is zero
             if tb is not None:
                 grad_sink.done(pb)
                 db = None

@@ -1011,3 +1011,53 @@ def test_lazy_embedding_adam_matches_cpu(torch_style, E):
     mv = res[1][1][o:o + k].view(301, E)
     never = [r for r in range(301) if all(r % (t + 2) != 0 for t in range(4))]
     assert never and float(mv[never].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("R,shape,dt", [(4096, (512,), torch.float32), (65536, (768,), torch.bfloat16),
+                                        (8, (4096, 512), torch.float32), (3, (100,), torch.float32),
+                                        (1000, (36,), torch.bfloat16)])
+def test_colsum_modes(R, shape, dt):
+    """dense.hip::colsum_kernel (bias gradients, split-K sums) vs the fp32 torch sum:
+    overwrite, accumulate into a non-zero buffer, and the scale / bias / activation epilogue."""
+    g0 = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(R, *shape, device=DEV, generator=g0).to(dt)
+    want = x.float().sum(0)
+    got = dops.colsum(x)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-3)
+    base = torch.randn(*shape, device=DEV, generator=g0)
+    acc = base.clone()
+    dops.colsum(x, out=acc, accumulate=True)
+    torch.testing.assert_close(acc, base + want, rtol=1e-4, atol=1e-3)
+    if len(shape) == 2:
+        scale = torch.rand(shape[0], device=DEV, generator=g0)
+        bias = torch.randn(shape[1], device=DEV, generator=g0)
+        y = dops.colsum(x, scale=scale, bias=bias, act="tanh")
+        torch.testing.assert_close(y, torch.tanh(want * scale[:, None] + bias), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("plan,L,act", [("gather", 45, "tanh"), ("counts", 300, "tanh"), ("gather", 20, "relu"),
+                                        ("counts", 2000, "relu")])
+def test_embedding_bag_fused_bias_act(plan, L, act):
+    """act(mean bag + bias) with the bias / activation in the producing kernel (gather
+    epilogue, split-K column-sum epilogue): values and W / bias gradients vs fp32 torch."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    V, N, E = 30000, 96, 512
+    g0 = torch.Generator(device=DEV).manual_seed(3)
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV, generator=g0)
+    ids[:, L // 3:] *= (torch.rand(N, L - L // 3, device=DEV, generator=g0) < 0.5).int()
+    W = bf(torch.randn(V, E, device=DEV, generator=g0)).requires_grad_(True)
+    b = (torch.randn(E, device=DEV, generator=g0) * 0.3).requires_grad_(True)
+    Wr = W.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    y = eops.embedding_bag(ids, W, pad=0, mean=True, plan=plan, bias=b, act=act)
+    cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
+    pre = ref.embedding_bag_sum(ids, Wr, 0) / cnt + br
+    yr = torch.tanh(pre) if act == "tanh" else torch.relu(pre)
+    torch.testing.assert_close(y, yr, rtol=2e-2, atol=2e-2)
+    gy = torch.randn_like(yr)
+    (y * gy).sum().backward()
+    (yr * gy).sum().backward()
+    for got, want in ((W.grad, Wr.grad), (b.grad, br.grad)):
+        err = float((got - want).abs().max() / want.abs().max())
+        assert err < 2e-2, err
