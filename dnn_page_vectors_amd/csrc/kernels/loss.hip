@@ -483,6 +483,58 @@ __global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, con
   }
 }
 
+// Batch statistics of the per-row loss in one workgroup: mean loss and accuracy
+// (fraction of rows with P+ > 0.5) -- the training step's scalar loss and metric without
+// torch's mean / compare / cast / mean launches.
+__global__ __launch_bounds__(256) void loss_stats_kernel(const float* __restrict__ loss,
+                                                         const float* __restrict__ prob, int B,
+                                                         float* __restrict__ out_loss, float* __restrict__ out_acc) {
+  float s = 0.f, a = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) {
+    s += loss[i];
+    a += prob[i] > 0.5f ? 1.f : 0.f;
+  }
+  s = wave_sum(s);
+  a = wave_sum(a);
+  __shared__ float ws[4], wa[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    ws[w] = s;
+    wa[w] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float inv = 1.f / (float)B;
+    *out_loss = (ws[0] + ws[1] + ws[2] + ws[3]) * inv;
+    if (out_acc) *out_acc = (wa[0] + wa[1] + wa[2] + wa[3]) * inv;
+  }
+}
+
+// Backward prologue of the in-batch / cross-GPU loss: per-row upstream gradient g (a scalar
+// mean-loss gradient broadcast as g0 * invB, or a (B,) vector), the softmax scale
+// gamma * g / sumexp, and (when the forward kept U) dQ = scale * U -- one launch instead of
+// the fill / copy / mul / div / mul of the eager expression.  Thread = one (row, 4 columns).
+__global__ __launch_bounds__(256) void ib_grad_scale_kernel(const float* __restrict__ gl, int scalar, float invB,
+                                                            const float* __restrict__ sumexp, int B, float gamma,
+                                                            const float* __restrict__ U, int DP,
+                                                            float* __restrict__ dq, float* __restrict__ scale,
+                                                            float* __restrict__ grow) {
+  const int per = U ? DP / 4 : 1;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)B * per) return;
+  const int i = (int)(t / per), c4 = (int)(t - (long)i * per);
+  const float g = scalar ? gl[0] * invB : gl[i];
+  const float sc = g * gamma / sumexp[i];
+  if (c4 == 0) {
+    scale[i] = sc;
+    grow[i] = g;
+  }
+  if (U) {
+    const f32x4 u = *reinterpret_cast<const f32x4*>(U + (size_t)i * DP + 4 * c4);
+    *reinterpret_cast<f32x4*>(dq + (size_t)i * DP + 4 * c4) = u * sc;
+  }
+}
+
 PV_DEBUG_EXPORT(loss)
 }  // namespace loss
 }  // namespace pv
@@ -653,6 +705,25 @@ PV_API int pv_ib_rows(float* S, const int* pos, const float* gscale, float* loss
                       void* stream) {
   hipLaunchKernelGGL(pv::loss::ib_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, pos, gscale,
                      loss, B, M, gamma, clip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+PV_API int pv_loss_stats(const float* loss, const float* prob, int B, float* out_loss, float* out_acc, void* stream) {
+  if (B < 1) return -1;
+  hipLaunchKernelGGL(pv::loss::loss_stats_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, loss, prob, B, out_loss,
+                     out_acc);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// gl: scalar (scalar = 1, gradient of the mean: g = gl[0] * invB) or (B,) per-row gradient.
+PV_API int pv_ib_grad_scale(const float* gl, int scalar, float invB, const float* sumexp, int B, float gamma,
+                            const float* U, int DP, float* dq, float* scale, float* grow, void* stream) {
+  if (B < 1 || (U && (DP % 4 || !dq))) return -1;
+  const long n = (long)B * (U ? DP / 4 : 1);
+  hipLaunchKernelGGL(pv::loss::ib_grad_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, gl, scalar, invB, sumexp, B, gamma, U, DP, dq, scale, grow);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -78,6 +78,8 @@ SIGS = {
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip
     "pv_adam_dev": "pppp" "l" "p" "fffff" "i" "p" "p",
+    "pv_loss_stats": "pp" "i" "pp" "p",
+    "pv_ib_grad_scale": "p" "i" "f" "p" "i" "f" "p" "i" "ppp" "p",
     "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
     "pv_step_inc": "p" "p",
     "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "p" "p",

@@ -111,9 +111,31 @@ def _ib_forward(qb: torch.Tensor, db: torch.Tensor, pos: torch.Tensor, B: int, M
     return loss, prob, sumexp, U
 
 
+def _loss_stats(loss: torch.Tensor, prob: torch.Tensor):
+    """(mean loss, accuracy) as 0-dim device tensors from one kernel (loss.hip::loss_stats_kernel)."""
+    lm = torch.empty((), dtype=torch.float32, device=loss.device)
+    acc = torch.empty((), dtype=torch.float32, device=loss.device)
+    check(lib().pv_loss_stats(P(loss), P(prob), loss.shape[0], P(lm), P(acc), stream(loss.device)), "pv_loss_stats")
+    return lm, acc
+
+
+def _grad_prologue(gl: torch.Tensor, reduce: bool, B: int, gamma: float, sumexp: torch.Tensor,
+                   U: Optional[torch.Tensor], DP: int):
+    """-> (softmax scale (B,), per-row upstream gradient (B,), dQ = scale * U or None) in one
+    launch (loss.hip::ib_grad_scale_kernel); ``reduce``: gl is the mean loss's 0-dim gradient."""
+    dev = sumexp.device
+    g_in = gl.contiguous().float()
+    scale = torch.empty(B, dtype=torch.float32, device=dev)
+    grow = torch.empty(B, dtype=torch.float32, device=dev)
+    dq = torch.empty(B, DP, dtype=torch.float32, device=dev) if U is not None else None
+    check(lib().pv_ib_grad_scale(P(g_in), int(reduce), 1.0 / B, P(sumexp), B, float(gamma), P(U), DP, P(dq),
+                                 P(scale), P(grow), stream(dev)), "pv_ib_grad_scale")
+    return scale, grow, dq
+
+
 class _InBatchFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qn, dn, pos, gamma, clip):
+    def forward(ctx, qn, dn, pos, gamma, clip, reduce=False):
         B, D = qn.shape
         M = dn.shape[0]
         DP = (D + 31) // 32 * 32
@@ -125,29 +147,31 @@ class _InBatchFn(torch.autograd.Function):
         loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
         ctx.save_for_backward(qb, db, pos, sumexp, U)
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
+        ctx.reduce = bool(reduce)
         ctx.mark_non_differentiable(prob)
+        if reduce:
+            lm, acc = _loss_stats(loss, prob)
+            ctx.mark_non_differentiable(acc)
+            return lm, prob, acc
         return loss, prob
 
     @staticmethod
-    def backward(ctx, gl, _gp):
+    def backward(ctx, gl, _gp, _ga=None):
         qb, db, pos, sumexp, U = ctx.saved_tensors
         B, M, D, DP, gamma, clip = ctx.meta
         s = stream(qb.device)
         L_ = lib()
-        g = gl.contiguous().float()
-        scale = (g * gamma / sumexp).contiguous()
+        scale, g, dq = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, U, DP)
         dd = torch.empty(M, DP, dtype=torch.float32, device=qb.device)
         ws = torch.empty(max(L_.pv_ib_bwd_ws(M, B, DP), 1), dtype=torch.float32, device=qb.device)
-        if U is not None:
-            dq = U * scale[:, None]
-        else:
+        if U is None:
             dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
             ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(M, B, DP), 1),
                              dtype=torch.float32, device=qb.device)
             check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
         check(L_.pv_ib_bwd(P(db), P(qb), P(scale), P(dd), P(ws), M, B, DP, gamma, clip, 0, s), "pv_ib_bwd(dD)")
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
-        return dq[:, :D], dd[:, :D], None, None, None
+        return dq[:, :D], dd[:, :D], None, None, None, None
 
 
 class _InBatchRowsFn(torch.autograd.Function):
@@ -207,7 +231,7 @@ def start_page_gather(dn: torch.Tensor, group=None) -> Optional[PageGather]:
 
 class _CrossGpuFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qn, dn, pos_local, gamma, clip, group, pre):
+    def forward(ctx, qn, dn, pos_local, gamma, clip, group, pre, reduce=False):
         W = dist.get_world_size(group)
         rank = dist.get_rank(group)
         B, D = qn.shape
@@ -235,25 +259,27 @@ class _CrossGpuFn(torch.autograd.Function):
         ctx.qall = qall
         ctx.save_for_backward(qb, db, dbl, pos_local, sumexp, U)
         ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
+        ctx.reduce = bool(reduce)
+        if reduce:
+            lm, acc = _loss_stats(loss, prob)
+            ctx.mark_non_differentiable(acc)
+            return lm, prob, acc
         return loss, prob
 
     @staticmethod
-    def backward(ctx, gl, _gp):
+    def backward(ctx, gl, _gp, _ga=None):
         qb, db, dbl, pos_local, sumexp, U = ctx.saved_tensors
         B, M, n, D, DP, gamma, clip, group, W = ctx.meta
         s = stream(qb.device)
         L_ = lib()
-        g = gl.contiguous().float()
-        scale = (g * gamma / sumexp).contiguous()
+        scale, g, dq = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, U, DP)
         # every rank's per-query softmax scale (B floats each), gathered while dQ runs
         scale_all = torch.empty(B * W, dtype=torch.float32, device=qb.device)
         swork = dist.all_gather_into_tensor(scale_all, scale, group=group, async_op=True)
         dd = torch.empty(n, DP, dtype=torch.float32, device=qb.device)
         ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), L_.pv_ib_bwd_ws(n, B * W, DP), 1),
                          dtype=torch.float32, device=qb.device)
-        if U is not None:  # the forward already summed exp * clip' * d over ALL ranks' pages
-            dq = U * scale[:, None]
-        else:
+        if U is None:  # (else the forward already summed exp * clip' * d over ALL ranks' pages)
             dq = torch.empty(B, DP, dtype=torch.float32, device=qb.device)
             check(L_.pv_ib_bwd(P(qb), P(db), P(scale), P(dq), P(ws), B, M, DP, gamma, clip, 1, s), "pv_ib_bwd(dQ)")
         ctx.qwork.wait()
@@ -266,31 +292,40 @@ class _CrossGpuFn(torch.autograd.Function):
               "pv_ib_bwd(dD)")
         check(L_.pv_ib_pos(P(qb), P(dbl), P(pos_local), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s),
               "pv_ib_pos(bwd)")
-        return dq[:, :D], dd[:, :D], None, None, None, None, None
+        return dq[:, :D], dd[:, :D], None, None, None, None, None, None
+
+
+def _reduce_rows(loss: torch.Tensor, prob: torch.Tensor):
+    return loss.mean(), prob, (prob > 0.5).float().mean()
 
 
 def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, gamma: float, clip: bool = True,
-                   group=None, gathered: Optional[PageGather] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                   group=None, gathered: Optional[PageGather] = None, reduce: bool = False):
     """qn (B, D) and the LOCAL page vectors dn (n, D), normalised; pos_local (B,) indexes dn.
     Every query is scored against the pages of all ranks (rank r's pages at rows r*n...).
-    ``gathered``: the PageGather started on ``dn`` right after the doc tower."""
+    ``gathered``: the PageGather started on ``dn`` right after the doc tower.
+    -> (per-row loss, P+); ``reduce``: (mean loss, P+, accuracy), the mean and metric
+    computed in the loss kernels' epilogue (no separate reductions)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return inbatch_loss(qn, dn, pos_local, gamma, clip)
+        return inbatch_loss(qn, dn, pos_local, gamma, clip, reduce=reduce)
     if use_hip(qn, dn) and qn.shape[1] <= 192:
         if gathered is not None and gathered.source is not dn:
             raise ValueError("the prefetched gather belongs to another page tensor")
-        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group, gathered)
+        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group, gathered, bool(reduce))
     from ..parallel.dist import all_gather_autograd
     docs = all_gather_autograd(dn)
     pos = pos_local + dist.get_rank(group) * dn.shape[0]
-    return inbatch_loss(qn, docs, pos, gamma, clip)
+    return inbatch_loss(qn, docs, pos, gamma, clip, reduce=reduce)
 
 
-def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, gamma: float, clip: bool = True
-                 ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """qn (B, D), dn (M, D) normalised; pos_index (B,) -> (per-row loss, P_pos)."""
+def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, gamma: float, clip: bool = True,
+                 reduce: bool = False):
+    """qn (B, D), dn (M, D) normalised; pos_index (B,) -> (per-row loss, P_pos);
+    ``reduce``: (mean loss, P_pos, accuracy)."""
     if use_hip(qn, dn):
         if qn.shape[1] > 192:
-            return _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
-        return _InBatchFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
-    return ref.inbatch_softmax_loss(qn, dn, pos_index, gamma, clip)
+            out = _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
+            return _reduce_rows(*out) if reduce else out
+        return _InBatchFn.apply(qn, dn, pos_index, float(gamma), bool(clip), bool(reduce))
+    out = ref.inbatch_softmax_loss(qn, dn, pos_index, gamma, clip)
+    return _reduce_rows(*out) if reduce else out

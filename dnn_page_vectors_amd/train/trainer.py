@@ -98,6 +98,8 @@ class Trainer:
             raise ValueError("tower placement splits the explicit J-negative slots; use loss_mode=explicit")
         self._replica_checked = False
         self._sink_scanned = set()
+        self._pos = {}
+        self._acc = None
         self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg")
                         if self.info.enabled else None)
         self.step = 0
@@ -149,21 +151,33 @@ class Trainer:
             dn = pre["dn"]
         qn = dops.l2_normalize(q)
         clip = bool(getattr(cfg, "cos_clip", True))
+        self._acc = None
         if cfg.loss_mode == "explicit":
             per_row, P = lops.dssm_explicit_loss(qn, dn.view(B, S, -1), cfg.GAMMA, clip)
+            loss = per_row.mean()
         elif cfg.loss_mode in ("in_batch", "cross_gpu"):
-            pos = torch.arange(B, device=q.device, dtype=torch.int32) * S
+            pos = self._pos_cache(B, S, q.device)
+            # mean loss and accuracy straight from the loss kernels (reduce=True)
             if cfg.loss_mode == "cross_gpu" and self.info.enabled:
-                per_row, P = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip, gathered=pre.get("gather"))
+                loss, P, self._acc = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip, gathered=pre.get("gather"),
+                                                         reduce=True)
             else:
-                per_row, P = lops.inbatch_loss(qn, dn, pos, cfg.GAMMA, clip)
+                loss, P, self._acc = lops.inbatch_loss(qn, dn, pos, cfg.GAMMA, clip, reduce=True)
         else:
             raise ValueError(f"unknown loss_mode {cfg.loss_mode!r}")
         range_pop()
-        loss = per_row.mean()
         if tower:  # W identical heads: back-propagate 1/W of each, gradients are SUM-reduced
             loss = placement.scale_grad(loss, 1.0 / self.info.world_size)
         return loss, P
+
+    def _pos_cache(self, B: int, S: int, device) -> torch.Tensor:
+        """Positive-document index of each query (row b -> page b*S), built once per shape."""
+        key = (B, S, str(device))
+        pos = self._pos.get(key)
+        if pos is None:
+            pos = torch.arange(B, device=device, dtype=torch.int32) * S
+            self._pos = {key: pos}
+        return pos
 
     def _check_replicated_batch(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> None:
         """Tower placement scores this rank's queries against doc slots computed on OTHER
@@ -274,7 +288,8 @@ class Trainer:
             timer.mark()
             self._timer = timer
         self.step += 1
-        return {"loss": loss.detach(), "acc": (P > 0.5).float().mean(), "grad_sumsq": stats[0],
+        acc = self._acc if self._acc is not None else (P > 0.5).float().mean()
+        return {"loss": loss.detach(), "acc": acc, "grad_sumsq": stats[0],
                 "nonfinite": stats[1]}
 
     @torch.no_grad()
@@ -282,7 +297,7 @@ class Trainer:
         self.model.eval()
         loss, P = self.compute_loss(q_ids, d_ids, 0)
         self.model.train()
-        return {"loss": loss, "acc": (P > 0.5).float().mean()}
+        return {"loss": loss, "acc": self._acc if self._acc is not None else (P > 0.5).float().mean()}
 
     # ------------------------------------------------------------------ loops
     def _run_epoch(self, batches: Iterator, steps: int, train: bool) -> Dict[str, float]:

@@ -1061,3 +1061,32 @@ def test_embedding_bag_fused_bias_act(plan, L, act):
     for got, want in ((W.grad, Wr.grad), (b.grad, br.grad)):
         err = float((got - want).abs().max() / want.abs().max())
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("with_dq", [True, False])
+def test_inbatch_loss_reduce_matches_mean(with_dq):
+    """inbatch_loss(reduce=True): mean loss / accuracy from the loss_stats kernel and the
+    fused backward prologue (ib_grad_scale) equal per-row loss -> torch mean -> backward."""
+    B, M, D = 300, 1200, 150
+    g0 = torch.Generator(device=DEV).manual_seed(5)
+    q0 = torch.nn.functional.normalize(torch.randn(B, D, device=DEV, generator=g0), dim=1)
+    d0 = torch.nn.functional.normalize(torch.randn(M, D, device=DEV, generator=g0), dim=1)
+    d0[::4][:B] = torch.nn.functional.normalize(q0 + 0.5 * d0[::4][:B], dim=1)
+    pos = torch.arange(B, device=DEV, dtype=torch.int32) * 4
+    res = []
+    for reduce in (False, True):
+        q = q0.clone().requires_grad_(with_dq)
+        d = d0.clone().requires_grad_(True)
+        out = lops.inbatch_loss(q, d, pos, 10.0, True, reduce=reduce)
+        if reduce:
+            loss, P, acc = out
+        else:
+            loss, P = out
+            loss, acc = loss.mean(), (P > 0.5).float().mean()
+        loss.backward()
+        res.append((float(loss), float(acc), q.grad, d.grad))
+    (l0, a0, gq0, gd0), (l1, a1, gq1, gd1) = res
+    assert abs(l0 - l1) < 1e-5 * max(1.0, abs(l0)) and a0 == a1
+    torch.testing.assert_close(gd1, gd0, rtol=1e-5, atol=1e-7)
+    if with_dq:
+        torch.testing.assert_close(gq1, gq0, rtol=1e-5, atol=1e-7)
