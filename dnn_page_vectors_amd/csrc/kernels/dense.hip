@@ -225,7 +225,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restr
 // Block = QB column quads (4 consecutive columns: 16-byte fp32 / 8-byte bf16 loads) x
 // RG = 256 / QB row groups; the row groups meet in LDS, then one store / atomic per column
 // and block (<= 64 row splits: bounded same-address atomics).  blockIdx.y = row split.
-template <typename TX, int QB>
+template <typename TX, int QB, int VEC>
 __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, long R, long C, long ldx,
                                                      float* __restrict__ out, long rps, int mode,
                                                      const float* __restrict__ scale,
@@ -233,12 +233,15 @@ __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, l
   constexpr int RG = 256 / QB;
   __shared__ f32x4 red[RG][QB];
   const int qi = threadIdx.x % QB, rg = threadIdx.x / QB;
-  const long c = 4 * ((long)blockIdx.x * QB + qi);
+  const long c = VEC * ((long)blockIdx.x * QB + qi);
   const bool live = c < C;
   const long r0 = (long)blockIdx.y * rps;
   const long r1 = min(R, r0 + rps);
   auto ld4 = [&](long r) -> f32x4 {
-    if constexpr (sizeof(TX) == 4) {
+    if constexpr (VEC == 1) {
+      if constexpr (sizeof(TX) == 4) return f32x4{reinterpret_cast<const float*>(x)[r * ldx + c], 0.f, 0.f, 0.f};
+      else return f32x4{bf16_to_f32(reinterpret_cast<const unsigned short*>(x)[r * ldx + c]), 0.f, 0.f, 0.f};
+    } else if constexpr (sizeof(TX) == 4) {
       return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(x) + r * ldx + c);
     } else {
       const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(x) + r * ldx + c);
@@ -264,15 +267,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, l
 #pragma unroll 4
   for (int g = 1; g < RG; ++g) s4 += red[g][qi];
   if (mode == 1) {
-    atomicAdd(out + c + 0, s4[0]);
-    atomicAdd(out + c + 1, s4[1]);
-    atomicAdd(out + c + 2, s4[2]);
-    atomicAdd(out + c + 3, s4[3]);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) atomicAdd(out + c + k, s4[k]);
     return;
   }
   if (mode == 2) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < VEC; ++k) {
       const long cc = c + k;
       float y = s4[k];
       if (scale) y *= scale[cc / E];
@@ -280,7 +281,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, l
       s4[k] = act_fn(y, act);
     }
   }
-  *reinterpret_cast<f32x4*>(out + c) = s4;
+  if constexpr (VEC == 4) *reinterpret_cast<f32x4*>(out + c) = s4;
+  else out[c] = s4[0];
 }
 
 }  // namespace dense
@@ -344,12 +346,15 @@ PV_API int pv_act_bwd(const float* y, const float* dy, float* dz, long n, int ac
 PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* out, int mode, const float* scale,
                      const float* bias, int E, int act, void* stream) {
   using namespace pv::dense;
-  if (C % 4 || ldx % 4 || R < 1 || ((uintptr_t)out & 15) || ((uintptr_t)x & (xdt ? 7 : 15))) return -1;
+  if (R < 1 || C < 1) return -1;
   if (mode == 2 && E < 1) return -2;
-  const long quads = C / 4;
-  const bool narrow = quads <= 1024;
+  // 4 columns per thread when rows and pointers allow 16-byte (fp32) / 8-byte (bf16) loads
+  const bool vec = C % 4 == 0 && ldx % 4 == 0 && !((uintptr_t)out & 15) && !((uintptr_t)x & (xdt ? 7 : 15));
+  const int V = vec ? 4 : 1;
+  const long units = C / V;
+  const bool narrow = units <= 1024;
   const int QB = narrow ? 16 : 64, RG = 256 / QB;
-  const long gx = (quads + QB - 1) / QB;
+  const long gx = (units + QB - 1) / QB;
   long splits = 1;
   if (mode == 1) {
     splits = (1024 + gx - 1) / gx;
@@ -362,15 +367,17 @@ PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* ou
   splits = (R + rps - 1) / rps;
   const dim3 grid((unsigned)gx, (unsigned)splits);
   hipStream_t st = (hipStream_t)stream;
-#define PV_COLSUM(T, Q)                                                                                          \
-  hipLaunchKernelGGL((colsum_kernel<T, Q>), grid, dim3(256), 0, st, (const T*)x, R, C, ldx, out, rps, mode, scale, \
-                     bias, E, act)
+#define PV_COLSUM(T, Q, VV)                                                                                    \
+  hipLaunchKernelGGL((colsum_kernel<T, Q, VV>), grid, dim3(256), 0, st, (const T*)x, R, C, ldx, out, rps, mode, \
+                     scale, bias, E, act)
   if (xdt == 1) {
-    if (narrow) PV_COLSUM(unsigned short, 16);
-    else PV_COLSUM(unsigned short, 64);
+    if (!vec) PV_COLSUM(unsigned short, 16, 1);
+    else if (narrow) PV_COLSUM(unsigned short, 16, 4);
+    else PV_COLSUM(unsigned short, 64, 4);
   } else {
-    if (narrow) PV_COLSUM(float, 16);
-    else PV_COLSUM(float, 64);
+    if (!vec) PV_COLSUM(float, 16, 1);
+    else if (narrow) PV_COLSUM(float, 16, 4);
+    else PV_COLSUM(float, 64, 4);
   }
 #undef PV_COLSUM
   PV_LAUNCH_CHECK();

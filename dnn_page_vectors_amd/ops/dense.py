@@ -80,8 +80,7 @@ _COLSUM_HIP = os.environ.get("PAGEVEC_COLSUM", "1") != "0"  # 0: torch reduction
 
 
 def _colsum_ok(x: torch.Tensor, C: int, ldx: int) -> bool:
-    return (_COLSUM_HIP and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and C % 4 == 0 and ldx % 4 == 0
-            and x.data_ptr() % 16 == 0)
+    return _COLSUM_HIP and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)
 
 
 def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False, scale=None, bias=None,
@@ -98,7 +97,7 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
         C *= int(d)
     epi = scale is not None or bias is not None or act != "none"
     x2 = x.reshape(R, C) if x.is_contiguous() else x.contiguous().reshape(R, C)
-    if use_hip(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)):
+    if use_hip(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.dtype == torch.float32)):
         E = int(tail[-1]) if len(tail) else 1
         if epi:
             mode = 2
