@@ -111,6 +111,7 @@ class Configuration:
     beta2: float = 0.999
     adam_eps: float = 1e-8
     lazy_embedding_adam: bool = False    # Adam skips embedding rows with an all-zero gradient (large vocabularies)
+    optimizer_bf16_mirror: bool = True   # the Adam kernel also writes the bf16 compute copies of big weights
     dtype: str = "fp32"                   # fp32 | bf16 (compute dtype of hot kernels)
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)

@@ -14,11 +14,18 @@
 namespace pv {
 namespace optim {
 
+__device__ __forceinline__ void store_bf16x4(unsigned short* dst, const f32x4& v) {
+  const unsigned lo = (unsigned)f32_to_bf16(v[0]) | ((unsigned)f32_to_bf16(v[1]) << 16);
+  const unsigned hi = (unsigned)f32_to_bf16(v[2]) | ((unsigned)f32_to_bf16(v[3]) << 16);
+  *reinterpret_cast<uint2*>(dst) = uint2{lo, hi};
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
                                                    float b1, float b2, float eps, float wd, int torch_style,
                                                    float bc2_sqrt_inv, const float* __restrict__ skip,
-                                                   const float* __restrict__ tdev) {
+                                                   const float* __restrict__ tdev,
+                                                   unsigned short* __restrict__ p16) {
   if (skip && *skip != 0.f) return;  // non-finite guard: skip the whole step
   if (tdev) {  // step count on the device (hipGraph replays): bias corrections computed here
     const float t = *tdev, lr = lr_t;
@@ -54,6 +61,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     f32x4 v0 = reinterpret_cast<f32x4*>(v)[i], v1 = reinterpret_cast<f32x4*>(v)[j];
     upd(p0, g0, m0, v0);
     upd(p1, g1, m1, v1);
+    if (p16) {  // bf16 compute copy of the updated weights (consumers skip their cast kernel)
+      store_bf16x4(p16 + 4 * i, p0);
+      store_bf16x4(p16 + 4 * j, p1);
+    }
     reinterpret_cast<f32x4*>(p)[i] = p0;
     reinterpret_cast<f32x4*>(m)[i] = m0;
     reinterpret_cast<f32x4*>(v)[i] = v0;
@@ -67,6 +78,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
     f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
     upd(pp, gg, mm, vv);
+    if (p16) store_bf16x4(p16 + 4 * i, pp);
     reinterpret_cast<f32x4*>(p)[i] = pp;
     reinterpret_cast<f32x4*>(m)[i] = mm;
     reinterpret_cast<f32x4*>(v)[i] = vv;
@@ -77,6 +89,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     v[i] = b2 * v[i] + (1.f - b2) * gk * gk;
     float den = torch_style ? (sqrtf(v[i]) * bc2_sqrt_inv + eps) : (sqrtf(v[i]) + eps);
     p[i] -= lr_t * m[i] / den;
+    if (p16) p16[i] = f32_to_bf16(p[i]);
   }
 }
 
@@ -94,7 +107,8 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
                                                              int cols, float lr, float b1, float b2, float eps,
                                                              float wd, int torch_style,
                                                              const float* __restrict__ skip,
-                                                             const float* __restrict__ tdev) {
+                                                             const float* __restrict__ tdev,
+                                                             unsigned short* __restrict__ p16) {
   constexpr int NJ = LPR == 64 ? 4 : 1;  // column groups per lane
   constexpr int RPW = 64 / LPR;          // rows per wave and trip
   if (skip && *skip != 0.f) return;
@@ -146,6 +160,7 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
         *reinterpret_cast<f32x4*>(p + o) = pp;
         *reinterpret_cast<f32x4*>(m + o) = mm;
         *reinterpret_cast<f32x4*>(v + o) = vv;
+        if (p16) store_bf16x4(p16 + o, pp);
       }
     }
   }
@@ -235,7 +250,7 @@ PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
   hipLaunchKernelGGL(pv::optim::step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, tdev);
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                     lr, b1, b2, eps, wd, torch_style, 1.f, skip, (const float*)tdev);
+                     lr, b1, b2, eps, wd, torch_style, 1.f, skip, (const float*)tdev, (unsigned short*)nullptr);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -249,13 +264,16 @@ PV_API int pv_step_inc(float* tdev, void* stream) {
   return 0;
 }
 
+// p16: optional bf16 copy of the segment written with the update (8-byte aligned).
 PV_API int pv_adam_seg(float* p, const float* g, float* m, float* v, long n, int row_len, const float* tdev, float lr,
-                       float b1, float b2, float eps, float wd, int torch_style, const float* skip, void* stream) {
-  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
+                       float b1, float b2, float eps, float wd, int torch_style, const float* skip, void* p16,
+                       void* stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15 || ((uintptr_t)p16 & 7)) return -1;
   if (n <= 0) return 0;
+  unsigned short* h = (unsigned short*)p16;
   if (row_len == 0) {
     hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                       lr, b1, b2, eps, wd, torch_style, 1.f, skip, tdev);
+                       lr, b1, b2, eps, wd, torch_style, 1.f, skip, tdev, h);
   } else {
     if (row_len % 4 || row_len > 1024 || n % row_len) return -2;
     const long rows = n / row_len;
@@ -266,7 +284,7 @@ PV_API int pv_adam_seg(float* p, const float* g, float* m, float* v, long n, int
     hipStream_t st = (hipStream_t)stream;
 #define PV_LAZY(LPR)                                                                                          \
   hipLaunchKernelGGL(pv::optim::adam_lazy_rows_kernel<LPR>, grid, dim3(256), 0, st, p, g, m, v, rows, row_len, lr, \
-                     b1, b2, eps, wd, torch_style, skip, tdev)
+                     b1, b2, eps, wd, torch_style, skip, tdev, h)
     if (lpr == 8) PV_LAZY(8);
     else if (lpr == 16) PV_LAZY(16);
     else if (lpr == 32) PV_LAZY(32);
@@ -289,7 +307,7 @@ PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int ste
     lr_t = (float)(lr * sqrt(bc2) / bc1);
   }
   hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip, (const float*)nullptr);
+                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip, (const float*)nullptr, (unsigned short*)nullptr);
   PV_LAUNCH_CHECK();
   return 0;
 }

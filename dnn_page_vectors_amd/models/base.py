@@ -48,6 +48,11 @@ class TwoTowerModel(nn.Module):
         """Derived low-precision copies of the parameters used by the fused kernels."""
         return {}
 
+    def bf16_mirror_params(self):
+        """Names of parameters whose bf16 copy the optimizer should write with each update
+        (ops/optim.py::mirror_for); default none."""
+        return []
+
     # ---- shared ------------------------------------------------------------------
     def compute_cache(self) -> Dict[str, object]:
         if self._cache_gen != _GENERATION[0] or not self._cache:

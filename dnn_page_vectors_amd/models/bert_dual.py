@@ -176,6 +176,9 @@ class BertDualEncoder(TwoTowerModel):
     def out_dim(self) -> int:
         return self.cfg.bert_out_dim or self.cfg.bert_hidden
 
+    def bf16_mirror_params(self):
+        return [n for n, _ in self.named_parameters() if n.rsplit(".", 1)[-1] in ("wqkv", "wo", "w1", "w2")]
+
     def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:
         enc = self.query_tower if tower == "query" else self.doc_towers[0]
         return enc(ids, self.p_drop, training, seed=seed)

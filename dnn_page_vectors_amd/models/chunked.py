@@ -35,6 +35,9 @@ class ChunkedPageEncoder(TwoTowerModel):
     def out_dim(self) -> int:
         return self.cfg.mlp_dims[-1]
 
+    def bf16_mirror_params(self):
+        return [n for n, _ in self.named_parameters() if n.endswith(".embedding")]
+
     def build_cache(self):
         if not self.query_tower.embedding.is_cuda:
             return {}

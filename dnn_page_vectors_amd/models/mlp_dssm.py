@@ -24,6 +24,7 @@ import torch.nn as nn
 from ..ops import dense as dops
 from ..ops import embedding as eops
 from ..ops import fp8 as fops
+from ..ops.optim import mirror_for
 from .base import TwoTowerModel
 from .cdssm import glorot_uniform_
 
@@ -49,7 +50,8 @@ class MLPTower(nn.Module):
         self.act = act
 
     def build_cache(self):
-        c = {"emb16": self.embedding.detach().to(torch.bfloat16).contiguous()}
+        m = mirror_for(self.embedding)  # written by the optimizer kernel with the last update
+        c = {"emb16": m if m is not None else self.embedding.detach().to(torch.bfloat16).contiguous()}
         if self.use_fp8:
             c["w8"] = [fops.quantize(w.detach()) for w in self.ws]
         return c
@@ -101,6 +103,9 @@ class MLPDSSM(TwoTowerModel):
     @property
     def out_dim(self) -> int:
         return self.cfg.mlp_dims[-1]
+
+    def bf16_mirror_params(self):
+        return [n for n, _ in self.named_parameters() if n.endswith(".embedding")]
 
     def build_cache(self):
         c = {}

@@ -82,7 +82,7 @@ SIGS = {
     "pv_ib_grad_scale": "p" "i" "f" "p" "i" "f" "p" "i" "ppp" "p",
     "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
     "pv_step_inc": "p" "p",
-    "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "p" "p",
+    "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "pp" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
     "pv_sumsq": "p" "l" "p" "p",

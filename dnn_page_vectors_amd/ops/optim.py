@@ -79,12 +79,17 @@ class FlatParams:
 
 class FlatAdam:
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, torch_style: bool = False, lazy: Optional[Iterable[str]] = None):
+                 weight_decay: float = 0.0, torch_style: bool = False, lazy: Optional[Iterable[str]] = None,
+                 mirror: Optional[Iterable[str]] = None):
         """lazy: names of 2-D embedding tables updated LazyAdam-style — a row whose gradient is
         all zero this step (none of its tokens in the batch) keeps its weights and moments
         (optim.hip::adam_lazy_rows_kernel; the step then streams ~4 B instead of 28 B per
         untouched parameter, which is what makes word-level vocabularies of millions of rows
-        cheap).  Default: dense Adam everywhere (Keras parity)."""
+        cheap).  Default: dense Adam everywhere (Keras parity).
+
+        mirror: names of parameters whose bf16 compute copy the update kernel writes in the
+        same pass (``mirror_for(p)``): the forward's bf16 operands (MLP embedding tables,
+        BERT projection weights) then need no per-step cast kernel."""
         self.flat = flat
         # [(offset, numel, row_len)] sorted by offset; rows of 4k floats (16-byte aligned)
         self.lazy: List[Tuple[int, int, int]] = []
@@ -93,6 +98,19 @@ class FlatAdam:
             if len(shp) == 2 and shp[1] % 4 == 0 and shp[1] <= 1024:
                 self.lazy.append((o, k, int(shp[1])))
         self.lazy.sort()
+        # ONE bf16 copy of the whole flat buffer, written by the same (single) update launch;
+        # the named parameters' mirrors are views of it
+        self.mirror16: Optional[torch.Tensor] = None
+        self.mirrors: Dict[str, torch.Tensor] = {}
+        if mirror and use_hip(flat.data):
+            self.mirror16 = flat.data.detach().to(torch.bfloat16)
+            named = dict(flat.named)
+            for name in mirror:
+                o, k, shp = flat.offsets[name]
+                p = named[name]
+                self.mirrors[name] = p._pv_mirror = self.mirror16[o:o + k].view(shp)
+                p._pv_mirror_owner = flat
+            flat.mirror_gen = _generation()  # mirrors equal the weights as of this generation
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, betas[0], betas[1], eps, weight_decay
         self.torch_style = torch_style
         self.m = torch.zeros_like(flat.data)
@@ -107,8 +125,12 @@ class FlatAdam:
         self.step_count += 1
         t = self.step_count
         if use_hip(self.flat.data):
-            if self.lazy:
+            if self.lazy or self.mirrors:
                 self._step_segments(skip_flag)
+                # the trainer bumps the generation right after the step: the mirrors hold
+                # exactly the weights of that next generation
+                if self.mirrors:
+                    self.flat.mirror_gen = _generation() + 1
                 return
             check(lib().pv_adam_dev(P(self.flat.data), P(self.flat.grad), P(self.m), P(self.v), self.flat.numel,
                                     P(self.t_dev), self.lr, self.b1, self.b2, self.eps, self.wd,
@@ -141,21 +163,36 @@ class FlatAdam:
         L_ = lib()
         s = stream(self.flat.data.device)
         check(L_.pv_step_inc(P(self.t_dev), s), "pv_step_inc")
-        pos = 0
-        segs = []
-        for o, k, rl in self.lazy:
-            if o > pos:
-                segs.append((pos, o - pos, 0))
-            segs.append((o, k, rl))
-            pos = o + (k + 63) // 64 * 64
-        if pos < self.flat.numel:
-            segs.append((pos, self.flat.numel - pos, 0))
+        if not hasattr(self, "_segs"):
+            pos = 0
+            segs = []
+            for o, k, rl in self.lazy:
+                if o > pos:
+                    segs.append((pos, o - pos, 0))
+                segs.append((o, k, rl))
+                pos = o + (k + 63) // 64 * 64
+            if pos < self.flat.numel:
+                segs.append((pos, self.flat.numel - pos, 0))
+            self._segs = segs
         esz = self.flat.data.element_size()
         base = [t.data_ptr() for t in (self.flat.data, self.flat.grad, self.m, self.v)]
-        for o, n, rl in segs:
+        m16 = self.mirror16
+        for o, n, rl in self._segs:
             ptrs = [b + o * esz for b in base]
+            mp = m16.data_ptr() + 2 * o if m16 is not None else None
             check(L_.pv_adam_seg(ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, rl, P(self.t_dev), self.lr, self.b1, self.b2,
-                                 self.eps, self.wd, int(self.torch_style), P(skip_flag), s), "pv_adam_seg")
+                                 self.eps, self.wd, int(self.torch_style), P(skip_flag), mp, s), "pv_adam_seg")
+
+    def note_external_step(self) -> None:
+        """A replayed hipGraph ran this optimizer's captured update (mirrors included)."""
+        if self.mirrors:
+            self.flat.mirror_gen = _generation() + 1
+
+    def refresh_mirrors(self) -> None:
+        """Re-cast the bf16 mirrors from the fp32 weights (after a checkpoint load / broadcast)."""
+        if self.mirror16 is not None:
+            self.mirror16.copy_(self.flat.data)
+            self.flat.mirror_gen = _generation()
 
     def state_dict(self) -> Dict[str, object]:
         return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr}
@@ -165,6 +202,23 @@ class FlatAdam:
         self.v.copy_(d["v"])
         self.step_count = int(d["step"])
         self.t_dev.fill_(float(self.step_count))
+
+
+def _generation() -> int:
+    from ..models.base import _GENERATION
+
+    return _GENERATION[0]
+
+
+def mirror_for(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The bf16 copy of ``p`` the optimizer wrote with its last update, if it is current
+    (FlatAdam(mirror=...)); None -> the caller casts.  A generation bump that did not
+    follow a mirrored step (checkpoint load, broadcast) makes it stale until the next step
+    or ``refresh_mirrors``."""
+    m = getattr(p, "_pv_mirror", None)
+    if m is None or getattr(p._pv_mirror_owner, "mirror_gen", -1) != _generation():
+        return None
+    return m
 
 
 def grad_sumsq_and_finite(flat_grad: torch.Tensor) -> torch.Tensor:

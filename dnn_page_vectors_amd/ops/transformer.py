@@ -308,6 +308,11 @@ _W16 = {}
 
 def weight_bf16(w: torch.Tensor) -> torch.Tensor:
     from ..models.base import _GENERATION
+    from .optim import mirror_for
+
+    m = mirror_for(w)  # the optimizer kernel's bf16 copy (FlatAdam(mirror=...))
+    if m is not None:
+        return m
 
     key = id(w)
     ent = _W16.get(key)

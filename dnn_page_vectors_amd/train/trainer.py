@@ -89,8 +89,12 @@ class Trainer:
         lazy = None
         if getattr(cfg, "lazy_embedding_adam", False):
             lazy = [n for n, p in self.flat.named if n.rsplit(".", 1)[-1] in ("embedding", "word") and p.dim() == 2]
+        # bf16 compute copies written by the optimizer kernel itself (no per-step casts)
+        mirror = [n for n in self.model.bf16_mirror_params() if n in self.flat.offsets] \
+            if (hasattr(self.model, "bf16_mirror_params") and getattr(cfg, "optimizer_bf16_mirror", True)
+                and os.environ.get("PAGEVEC_NO_MIRROR", "0") != "1") else None
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
-                            torch_style=(cfg.model == "bert"), lazy=lazy)
+                            torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror)
         self.placement = getattr(cfg, "placement", "dp")
         if self.placement not in ("dp", "tower"):
             raise ValueError(f"unknown placement {self.placement!r}")
@@ -241,6 +245,7 @@ class Trainer:
         if self.graph_fence:
             torch.cuda.synchronize(self.device)
         self.opt.step_count += 1
+        self.opt.note_external_step()  # the captured update also rewrote the bf16 mirrors
         bump_generation()
         self.step += 1
         return self._gout
@@ -394,3 +399,4 @@ class Trainer:
         # steps replay without the host): it must resume at the same count as the host one
         self.opt.t_dev.fill_(float(self.opt.step_count))
         bump_generation()
+        self.opt.refresh_mirrors()

@@ -1091,3 +1091,63 @@ def test_inbatch_loss_reduce_matches_mean(with_dq):
     torch.testing.assert_close(gd1, gd0, rtol=1e-5, atol=1e-7)
     if with_dq:
         torch.testing.assert_close(gq1, gq0, rtol=1e-5, atol=1e-7)
+
+
+def test_adam_bf16_mirror_tracks_weights():
+    """FlatAdam(mirror=...): the update kernel writes bf16(p) with every step (dense and lazy
+    segments); mirror_for() serves it only while it is current."""
+    from dnn_page_vectors_amd.models.base import bump_generation
+    from dnn_page_vectors_amd.ops.optim import FlatAdam, FlatParams, mirror_for
+
+    torch.manual_seed(0)
+    m = torch.nn.ModuleDict({"lin": torch.nn.Linear(33, 17), "tok": torch.nn.Embedding(301, 96),
+                             "tok2": torch.nn.Embedding(50, 40)}).to(DEV)
+    flat = FlatParams(m.named_parameters())
+    opt = FlatAdam(flat, lr=1e-2, lazy=["tok2.weight"], mirror=["tok.weight", "lin.weight", "tok2.weight"])
+    for name in ("tok.weight", "lin.weight", "tok2.weight"):
+        p = dict(flat.named)[name]
+        assert mirror_for(p) is not None
+    for _ in range(3):
+        flat.grad.copy_(torch.randn_like(flat.grad))
+        opt.step()
+        bump_generation()
+        for name in ("tok.weight", "lin.weight", "tok2.weight"):
+            p = dict(flat.named)[name]
+            mm = mirror_for(p)
+            assert mm is not None and torch.equal(mm, p.detach().to(torch.bfloat16)), name
+    bump_generation()  # e.g. a checkpoint load: stale until refreshed
+    assert mirror_for(m.tok.weight) is None
+    with torch.no_grad():
+        m.tok.weight.mul_(0.5)
+    opt.refresh_mirrors()
+    assert torch.equal(mirror_for(m.tok.weight), m.tok.weight.detach().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("preset", ["mlp", "bert"])
+def test_bf16_mirror_training_matches_cast(preset):
+    """Same trajectory with the optimizer-written bf16 weights as with per-step casts."""
+    from dnn_page_vectors_amd.config import Configuration, preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    if preset == "bert":
+        cfg = preset_config("bert_dp8").replace(bert_layers=2, batch_size=16, document_length=64, query_length=16,
+                                                bert_dropout=0.0)
+    else:
+        cfg = Configuration(model="mlp", feature_level="ngram", vocab_hash_size=500, query_length=12,
+                            document_length=64, batch_size=32, embedding_dim=64, loss_mode="in_batch",
+                            mlp_dims=(64, 64, 32))
+    data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=512), DEV, seed=5)
+    pool = [data.batch(cfg.batch_size) for _ in range(4)]
+    runs = []
+    for mirror in (False, True):
+        torch.manual_seed(0)
+        tr = Trainer(cfg.replace(optimizer_bf16_mirror=mirror), build_model(cfg, cfg.vocab_hash_size),
+                     torch.device(DEV))
+        assert bool(tr.opt.mirrors) == mirror
+        runs.append([float(tr.train_step(*pool[i % 4])["loss"]) for i in range(5)])
+    for a, b in zip(*runs):
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), runs
