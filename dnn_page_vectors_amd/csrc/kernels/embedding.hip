@@ -15,6 +15,7 @@
 //   atomics per step.  This kernel builds C (and the bag lengths) with one atomic
 //   increment per token into a zeroed buffer (counts <= 256 are exact in bf16).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pv {
 namespace embed {
@@ -298,6 +299,46 @@ __global__ __launch_bounds__(1024) void bag_counts_lds_kernel(const int* __restr
   }
 }
 
+// Same, with two 16-bit counters per LDS word (bag length < 65536, so a counter never
+// carries into its neighbour): half the LDS (60 KB at V = 30 k), two blocks per CU, so one
+// block's histogram phase overlaps the other's row write.  Word w holds ids (2w, 2w+1) in
+// (low, high) halves: exactly the bf16 pair order of the output row.
+__global__ __launch_bounds__(1024) void bag_counts_lds16_kernel(const int* __restrict__ ids,
+                                                                unsigned short* __restrict__ counts,
+                                                                float* __restrict__ lens, int N, int L, int V,
+                                                                int ldc, int pad) {
+  extern __shared__ unsigned hist2[];
+  __shared__ int part[16];
+  const int n = blockIdx.x;
+  const int words = ldc / 2;
+  for (int c = threadIdx.x; c < words; c += blockDim.x) hist2[c] = 0u;
+  __syncthreads();
+  const int* row = ids + (size_t)n * L;
+  int local = 0;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    const int v = row[t];
+    PV_CHECK(v == pad || (v >= 0 && v < V), PV_ERR_ID);
+    if (v != pad && v >= 0 && v < V) {
+      ++local;
+      atomicAdd(&hist2[v >> 1], 1u << ((v & 1) * 16));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
+  __syncthreads();
+  uint2* crow = reinterpret_cast<uint2*>(counts + (size_t)n * ldc);
+  for (int c4 = threadIdx.x; c4 < ldc / 4; c4 += blockDim.x) {
+    const unsigned a = hist2[2 * c4], b = hist2[2 * c4 + 1];
+    crow[c4] = uint2{pack_bf16x2((float)(a & 0xFFFFu), (float)(a >> 16)),
+                     pack_bf16x2((float)(b & 0xFFFFu), (float)(b >> 16))};
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    lens[n] = (float)s;
+  }
+}
+
 PV_DEBUG_EXPORT(embed)
 }  // namespace embed
 }  // namespace pv
@@ -351,6 +392,23 @@ PV_API int pv_bag_bwd_sorted(const void* skeys, const unsigned* svals, const flo
 PV_API int pv_bag_counts(const int* ids, void* counts, float* lens, int N, int L, int V, int ldc, int pad,
                          int zeroed, void* stream) {
   if (ldc < V || (ldc & 1)) return -1;
+  static const bool packed16 = [] {  // PAGEVEC_BAG_COUNTS16=0: one u32 counter per id (A/B switch)
+    const char* e = getenv("PAGEVEC_BAG_COUNTS16");
+    return !(e && e[0] == '0');
+  }();
+  if (packed16 && L < 65536 && ldc <= 40960 && (ldc & 3) == 0) {
+    static bool attr16 = false;
+    if (!attr16) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&pv::embed::bag_counts_lds16_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 40960 * 2) != hipSuccess)
+        return -3;
+      attr16 = true;
+    }
+    hipLaunchKernelGGL(pv::embed::bag_counts_lds16_kernel, dim3(N), dim3(1024), (ldc / 2) * sizeof(unsigned),
+                       (hipStream_t)stream, ids, (unsigned short*)counts, lens, N, L, V, ldc, pad);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   if (ldc <= pv::embed::HIST_MAX && (ldc & 3) == 0) {
     static bool attr = false;
     if (!attr) {  // > 64 KB of dynamic LDS (gfx950: 160 KB per CU)

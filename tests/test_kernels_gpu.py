@@ -1151,3 +1151,24 @@ def test_bf16_mirror_training_matches_cast(preset):
         runs.append([float(tr.train_step(*pool[i % 4])["loss"]) for i in range(5)])
     for a, b in zip(*runs):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), runs
+
+
+@pytest.mark.parametrize("V,L", [(30000, 2000), (1001, 300), (38000, 64)])
+def test_bag_counts_matrix_exact(V, L):
+    """LDS-histogram count matrix (16-bit packed counters below V 40960, u32 otherwise) vs a
+    bincount reference: every entry, pads excluded, odd / even neighbours and repeats."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    N = 37
+    g0 = torch.Generator(device=DEV).manual_seed(9)
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV, generator=g0)
+    ids[:, ::7] = 5           # a repeated token (count L/7 <= 286)
+    ids[:, 1::11] = 6         # its odd neighbour
+    ids[:, L // 2:] *= (torch.rand(N, L - L // 2, device=DEV, generator=g0) < 0.5).int()  # pads
+    C, lens = eops._counts(ids, V, 0)
+    ref_c = torch.zeros(N, V, device=DEV)
+    ref_c.scatter_add_(1, ids.long(), torch.ones(N, L, device=DEV))
+    ref_c[:, 0] = 0
+    got = C[:, :V].float()
+    torch.testing.assert_close(got, ref_c.bfloat16().float(), rtol=0, atol=0)
+    torch.testing.assert_close(lens, (ids != 0).sum(1).float(), rtol=0, atol=0)
