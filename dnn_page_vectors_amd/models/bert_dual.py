@@ -47,29 +47,33 @@ class BertLayer(nn.Module):
                 seed: int = 0):
         N, L, H = x.shape
         p = p_drop if training else 0.0
-        qkv = tops.linear(x, self.wqkv, self.bqkv)            # (N, L, 3H) packed [slot][head][d]
+        r1, r2 = tops.ResidualLink(), tops.ResidualLink()
+        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1)    # (N, L, 3H) packed [slot][head][d]
         a = tops.fused_attention(qkv, mask, self.heads)       # (N, L, H), no permute copies
         o = tops.linear(a, self.wo)
         # output bias + hidden dropout fused into the residual add + LayerNorm (counter-hash
         # masks; the bias gradient is reduced in the LayerNorm backward)
-        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo)
-        f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
+        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo, res=r1)
+        f = tops.bias_gelu(tops.linear(x, self.w1, res=r2), self.b1)
         f2 = tops.linear(f, self.w2)
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
-                                  bias=self.b2)
+                                  bias=self.b2, res=r2)
 
 
     def forward_packed(self, x: torch.Tensor, masks, shapes, p_drop: float, training: bool, seed: int = 0):
         """x (T, H): several sequence groups packed token-major (see BertEncoder.forward_multi)."""
         p = p_drop if training else 0.0
-        qkv = tops.linear(x, self.wqkv, self.bqkv)            # (T, 3H): one GEMM for every group
+        # each x feeds a linear layer and a residual add: their gradients meet in the
+        # linear's dX GEMM (tops.ResidualLink) instead of an autograd add
+        r1, r2 = tops.ResidualLink(), tops.ResidualLink()
+        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1)    # (T, 3H): one GEMM for every group
         a = tops.packed_attention(qkv, masks, shapes, self.heads)
         o = tops.linear(a, self.wo)
-        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo)
-        f = tops.bias_gelu(tops.linear(x, self.w1), self.b1)
+        x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo, res=r1)
+        f = tops.bias_gelu(tops.linear(x, self.w1, res=r2), self.b1)
         f2 = tops.linear(f, self.w2)
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
-                                  bias=self.b2)
+                                  bias=self.b2, res=r2)
 
 
 class _RowGather(torch.autograd.Function):

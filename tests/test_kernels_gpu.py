@@ -1172,3 +1172,26 @@ def test_bag_counts_matrix_exact(V, L):
     got = C[:, :V].float()
     torch.testing.assert_close(got, ref_c.bfloat16().float(), rtol=0, atol=0)
     torch.testing.assert_close(lens, (ids != 0).sum(1).float(), rtol=0, atol=0)
+
+
+def test_bert_residual_link_matches_autograd_sum(monkeypatch):
+    """ops/transformer.py::ResidualLink: the residual gradient added in the linear layer's dX
+    GEMM equals autograd's separate sum (2-layer BERT, every parameter and the input)."""
+    from dnn_page_vectors_amd.models.bert_dual import BertEncoder
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(1, 500, (6, 40), generator=g).to(DEV)
+    ids[:, 30:] = 0
+    grads = []
+    for fuse in (False, True):
+        monkeypatch.setattr(tops, "RESID_FUSE", fuse)
+        enc = BertEncoder(500, 256, 512, 4, 2, 64, 32, torch.Generator().manual_seed(1)).to(DEV)
+        out = enc(ids, 0.0, True)
+        (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+        grads.append({n: p.grad.detach().clone() for n, p in enc.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 10
+    for n in grads[0]:
+        a, b = grads[0][n].float(), grads[1][n].float()
+        err = float((a - b).abs().max() / a.abs().max().clamp_min(1e-12))
+        assert err < 3e-2, (n, err)
