@@ -1,0 +1,50 @@
+"""CPU semantics of the fused-op entry points (the reference path the HIP kernels are
+checked against on the GPU): column sums with accumulate / epilogue, the bag with fused
+bias + activation, and the loss ``reduce`` mode."""
+import torch
+
+from dnn_page_vectors_amd.ops import dense as dops
+from dnn_page_vectors_amd.ops import embedding as eops
+from dnn_page_vectors_amd.ops import loss as lops
+
+
+def test_colsum_cpu_modes():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(37, 6, 8, generator=g)
+    torch.testing.assert_close(dops.colsum(x), x.sum(0))
+    out = torch.ones(6, 8)
+    dops.colsum(x, out=out, accumulate=True)
+    torch.testing.assert_close(out, 1 + x.sum(0))
+    scale, bias = torch.rand(6, generator=g), torch.randn(8, generator=g)
+    y = dops.colsum(x, scale=scale, bias=bias, act="tanh")
+    torch.testing.assert_close(y, torch.tanh(x.sum(0) * scale[:, None] + bias))
+
+
+def test_embedding_bag_bias_act_cpu():
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, 50, (9, 12), generator=g, dtype=torch.int32)
+    ids[:, 8:] = 0
+    W = torch.randn(50, 16, generator=g, requires_grad=True)
+    b = torch.randn(16, generator=g, requires_grad=True)
+    y = eops.embedding_bag(ids, W, pad=0, mean=True, bias=b, act="relu")
+    cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
+    W2 = W.detach().clone().requires_grad_(True)
+    b2 = b.detach().clone().requires_grad_(True)
+    want = torch.relu(torch.nn.functional.embedding(ids.long(), W2).mul((ids != 0).unsqueeze(-1)).sum(1) / cnt + b2)
+    torch.testing.assert_close(y, want)
+    y.sum().backward()
+    want.sum().backward()
+    torch.testing.assert_close(W.grad, W2.grad)
+    torch.testing.assert_close(b.grad, b2.grad)
+
+
+def test_inbatch_loss_reduce_cpu():
+    g = torch.Generator().manual_seed(2)
+    q = torch.nn.functional.normalize(torch.randn(8, 16, generator=g), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(32, 16, generator=g), dim=1)
+    pos = torch.arange(8, dtype=torch.int32) * 4
+    per_row, P = lops.inbatch_loss(q, d, pos, 10.0, True)
+    lm, P2, acc = lops.inbatch_loss(q, d, pos, 10.0, True, reduce=True)
+    torch.testing.assert_close(lm, per_row.mean())
+    torch.testing.assert_close(P2, P)
+    torch.testing.assert_close(acc, (P > 0.5).float().mean())
