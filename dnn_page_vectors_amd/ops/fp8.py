@@ -50,22 +50,44 @@ class _FP8LinearFn(torch.autograd.Function):
         y = torch.empty(M, N, dtype=torch.float32, device=x.device)
         check(lib().pv_fp8_linear(P(xq), P(w8), P(ax), P(aw), P(b) if b is not None else None, P(y), None, M, N, K,
                                   _ACT[act], stream(x.device)), "pv_fp8_linear")
-        ctx.save_for_backward(x2, w, y, b)
+        ctx.save_for_backward(x2, y if act != "none" else None)
         ctx.act, ctx.xshape = act, x.shape
+        ctx.params = (w, b)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, y, b = ctx.saved_tensors
-        dz = dy.reshape(-1, dy.shape[-1]).float()
-        if ctx.act == "relu":
-            dz = dz * (y > 0)
-        elif ctx.act == "tanh":
-            dz = dz * (1 - y * y)
+        from . import dense as dops
+        from . import grad_sink
+        from .transformer import weight_bf16, wgrad_f32
+
+        x2, y = ctx.saved_tensors
+        w, b = ctx.params
+        dz = dy.reshape(-1, dy.shape[-1]).contiguous().float()
+        if y is not None:  # activation mask in one kernel
+            dzm = torch.empty_like(dz)
+            check(lib().pv_act_bwd(P(y), P(dz), P(dzm), dz.numel(), _ACT[ctx.act], stream(dz.device)), "pv_act_bwd")
+            dz = dzm
         dzb = dz.to(torch.bfloat16)
-        dx = (dzb @ w.detach().to(torch.bfloat16)).float().view(ctx.xshape)
-        dw = (dzb.t() @ x2.to(torch.bfloat16)).float()
-        db = dz.sum(0) if b is not None else None
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            try:
+                dx = torch.mm(dzb, weight_bf16(w), out_dtype=torch.float32)
+            except (TypeError, RuntimeError, NotImplementedError):
+                dx = (dzb @ weight_bf16(w)).float()
+            dx = dx.view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            tw = grad_sink.write_target(w)
+            dw = wgrad_f32(dzb, x2.to(torch.bfloat16), out=tw)  # split-K fp32, straight into the flat grad
+            if tw is not None:
+                grad_sink.done(w)
+                dw = None
+        if b is not None and ctx.needs_input_grad[2]:
+            tb = grad_sink.write_target(b)
+            db = dops.colsum(dz, out=tb, accumulate=tb is not None)
+            if tb is not None:
+                grad_sink.done(b)
+                db = None
         return dx, dw, db, None, None
 
 
