@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import grad_sink
 from ..ops import transformer as tops
 from .base import TwoTowerModel
 
@@ -90,13 +91,20 @@ class _RowGather(torch.autograd.Function):
         flat = ids.reshape(-1)
         ctx.save_for_backward(flat)
         ctx.shape = W.shape
+        ctx.W = W  # flat-gradient direct-write target (ops/grad_sink.py)
         return W.index_select(0, flat).view(*ids.shape, W.shape[1])
 
     @staticmethod
     def backward(ctx, g):
         (flat,) = ctx.saved_tensors
+        gf = g.reshape(-1, ctx.shape[1]).float()
+        tw = grad_sink.accum_target(ctx.W)  # the scatter accumulates: add straight into the flat grad
+        if tw is not None:
+            tw.index_add_(0, flat, gf)
+            grad_sink.done(ctx.W)
+            return None, None
         gW = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
-        gW.index_add_(0, flat, g.reshape(-1, ctx.shape[1]).float())
+        gW.index_add_(0, flat, gf)
         return None, gW
 
 
