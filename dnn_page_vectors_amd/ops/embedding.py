@@ -52,7 +52,9 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, scale: Optional[torch.Tenso
     0.293 -> 0.148 ms (tools/bag_gemm_micro.py), and the result is no longer rounded to bf16."""
     N, V = C.shape
     E = W16.shape[1]
-    sk = next((k for k in (8, 4, 2) if V % k == 0 and V // k >= 2048), 1)
+    sk = _BAG_SPLITK or next((k for k in (8, 4, 2) if V % k == 0 and V // k >= 2048), 1)
+    if V % sk:
+        sk = 1
     if sk > 1 and N * E <= 8 * 1024 * 1024:
         try:
             Cb = C.unflatten(1, (sk, V // sk)).transpose(0, 1)
@@ -70,6 +72,7 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, scale: Optional[torch.Tenso
 
 
 SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
+_BAG_SPLITK = int(os.environ.get("PAGEVEC_BAG_SPLITK", "0"))  # override of the vocabulary split (A/B)
 BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
 
 
