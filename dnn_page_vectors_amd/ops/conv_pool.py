@@ -183,10 +183,19 @@ class _ConvPoolFn(torch.autograd.Function):
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
             s_dw = side.cuda_stream
-        else:
-            s_dw = s
-        check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E, V,
-                                     seed, P(sp), row_offset, thr, tok, scale, s_dw), "pv_conv_pool_bwd_dw")
+
+        def launch_dw():
+            check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L,
+                                         E, V, seed, P(sp), row_offset, thr, tok, scale, s_dw if side is not None else s),
+                  "pv_conv_pool_bwd_dw")
+
+        # Order: the side-stream variant starts dW first (it runs beside the table chain);
+        # on one stream the TABLE gradient goes first and its data-parallel bucket (the
+        # table has a bucket of its own, parallel/ddp.py) is released as soon as the
+        # reduce is enqueued, so its all-reduce (12 MB for the 30k x 100 table) overlaps
+        # the dW kernel instead of trailing the whole backward.
+        if side is not None:
+            launch_dw()
         dtable = None
         if ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl()):
             # short sequences (query towers): per-sample dense dX rows (LDS), sorted by token,
@@ -234,9 +243,15 @@ class _ConvPoolFn(torch.autograd.Function):
             else:
                 check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
                                                   P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
-        if side is not None:
+        if side is None:
+            if t_tab is not None:
+                grad_sink.done(ptable)  # fires the table's bucket: enqueued after the reduce above
+            launch_dw()
+        else:
             main.wait_stream(side)
-        for t, prm in ((t_tab, ptable), (t3, pw3), (t4, pw4)):
+            if t_tab is not None:
+                grad_sink.done(ptable)
+        for t, prm in ((t3, pw3), (t4, pw4)):
             if t is not None:
                 grad_sink.done(prm)
         if t_tab is not None:

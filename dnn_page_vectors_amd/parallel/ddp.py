@@ -27,6 +27,7 @@ from ..ops.optim import FlatParams
 
 class GradBuckets:
     MIN_SPLIT_BYTES = 1 << 20  # module-boundary cuts only once the open bucket holds >= 1 MB
+    OWN_BUCKET_LEAVES = ("embedding", "word")  # >= 1 MB embedding tables: one bucket each
 
     def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg"):
         """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients)."""
@@ -48,6 +49,15 @@ class GradBuckets:
             o, k, _ = flat.offsets[name]
             end = o + (k + 63) // 64 * 64
             mod = name.split(".", 1)[0]
+            if name.rsplit(".", 1)[-1] in self.OWN_BUCKET_LEAVES and (end - o) >= min_split:
+                # embedding tables get a bucket of their own: the sparse table backward
+                # releases it before the tower's weight gradients are done (ops/conv_pool.py)
+                if cur_lo is not None:
+                    self._add(cur_lo, cur_hi, members)
+                self._add(o, end, [name])
+                cur_lo = cur_hi = cur_mod = None
+                members = []
+                continue
             if cur_lo is None:
                 cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
             elif mod != cur_mod and (cur_hi - cur_lo) >= min_split:

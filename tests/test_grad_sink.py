@@ -56,3 +56,26 @@ def test_mark_multi_use_finds_shared_parameters(monkeypatch):
         assert grad_sink.write_target(m["b"].weight) is not None
     y2 = m["b"](m["a"](x)).sum()
     assert grad_sink.mark_multi_use(y2, flat) == 0
+
+
+def test_embedding_tables_get_their_own_bucket():
+    """parallel/ddp.py: each >= 1 MB embedding table is one bucket, so the sparse table
+    backward (ops/conv_pool.py) can release it before the tower's weight gradients."""
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel.ddp import GradBuckets
+
+    cfg = Configuration(feature_level="ngram", vocab_hash_size=30000)
+    m = CDSSM(cfg, cfg.vocab_hash_size)
+    flat = FlatParams(m.named_parameters())
+    gb = GradBuckets(flat, bucket_mb=32.0)
+    tables = [n for n, _ in flat.named if n.endswith("embedding")]
+    assert len(tables) == 2
+    for n in tables:
+        bi = gb.param_bucket[n]
+        assert gb.buckets[bi][2] == 1
+    # every parameter is in exactly one bucket and the buckets tile disjoint ranges
+    assert set(gb.param_bucket) == {n for n, _ in flat.named}
+    spans = sorted((lo, hi) for lo, hi, _ in gb.buckets)
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    assert sum(c for _, _, c in gb.buckets) == len(flat.named)
