@@ -492,6 +492,130 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
   if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
 }
 
+// reduce6 = reduce5 with the weight-row gathers of RB rounds (4 entries each) issued
+// together before any is consumed: reduce5 waits on each round's 16-byte L2 gather before
+// its FMAs (one load in flight per wave); here RB loads are in flight per wave.  Same
+// per-entry arithmetic and flush order as reduce5 (identical per-wave partial sums).
+template <typename KT, int RB>
+__global__ __launch_bounds__(256) void conv_bwd_reduce6_kernel(const KT* __restrict__ skeys,
+                                                               const unsigned* __restrict__ svals,
+                                                               const int2* __restrict__ rec,
+                                                               const unsigned short* __restrict__ wrow,
+                                                               float* __restrict__ dtable, long M, int EPW, int L,
+                                                               int E, int V, unsigned seed, const unsigned* seed_ptr,
+                                                               unsigned row_offset, int thr, int token_mode) {
+  static_assert(RB >= 1 && 16 % RB == 0, "RB rounds of 4 entries tile a 64-entry sub-chunk");
+  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
+  if (seed_ptr) seed += *seed_ptr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, p = lane & 15;
+  float* slab = slabs[wave];
+  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
+  if (wbeg >= M) return;
+  const long wend = min(M, wbeg + (long)EPW);
+  const unsigned UV = (unsigned)V;
+  unsigned k0, s0, k1, s1, k2, s2;
+  rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
+  rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
+  auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
+    if (!(key < UV && PV_OK((long)sl < M, PV_ERR_SLOT))) return int2{0, 0};
+    unsigned nn, f, j;
+    slot_decode(sl, nn, f, j);
+    return rec[nn * (2 * FW) + f];
+  };
+  int2 r0 = ld_rec(k0, s0);
+  unsigned cur = UV;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const bool act = p < RPIECES;
+  for (long b = wbeg; b < wend; b += 64) {
+    rd_meta(skeys, svals, b + 128 + lane, wend, UV, k2, s2);
+    const int2 r1 = ld_rec(k1, s1);
+    const unsigned key = k0;
+    unsigned fj = 0, hr = 0;
+    float gg = 0.f;
+    if (key < UV) {
+      unsigned nn, f, j;
+      slot_decode(s0, nn, f, j);
+      fj = (f << 2) | j;
+      gg = __int_as_float(r0.x);
+      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
+    }
+    const int n = __popcll(__ballot(key < UV));
+    if (n == 0) break;
+    if (cur == UV) cur = __builtin_amdgcn_readfirstlane(key);
+    const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);
+    for (int qb = 0; qb < n; qb += 4 * RB) {
+      unsigned kgs[RB], hes[RB];
+      float ges[RB];
+      u32x4 ws[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {  // issue: every round's metadata exchange + row gather
+        const int e = qb + 4 * r + g;
+        const bool valid = e < n;
+        const int src = (valid ? e : 0) * 4;
+        kgs[r] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
+        const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
+        ges[r] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
+        hes[r] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
+        if (!valid) {
+          ges[r] = 0.f;
+          kgs[r] = klast;
+        }
+        ws[r] = u32x4{0u, 0u, 0u, 0u};
+        if (act && valid) ws[r] = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * p));
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {  // consume in entry order (reduce5's arithmetic)
+        if (qb + 4 * r >= n) break;
+        u32x4 w = ws[r];
+        if (thr > 0) {
+          if (token_mode) {
+            const unsigned k = ((int)(hes[r] & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+            w &= u32x4{k, k, k, k};
+          } else {
+            w &= keep_piece(hes[r], p, thr);
+          }
+        }
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
+          v[k] = ges[r] * __uint_as_float(wk);
+        }
+        const unsigned kg = kgs[r];
+        const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
+        const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
+        if (ka == cur && kb == cur) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += v[k];
+          continue;
+        }
+        bool done = false;
+        for (int it = 0; it < 5; ++it) {
+          const bool mine = !done && kg == cur;
+          if (mine) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += v[k];
+            done = true;
+          }
+          const unsigned long long left = __ballot(!done);
+          if (left == 0) break;
+          reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+          cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
+        }
+      }
+    }
+    if (n < 64) break;
+    k0 = k1; s0 = s1; r0 = r1;
+    k1 = k2; s1 = s2;
+  }
+  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+}
+
 
 // ---- dTable for short sequences (query towers: L <= DENSE_MAXL) ------------------------------
 // A 45-token query has ~45 touched embedding rows but 1050 (f, j) gradient entries, so the
@@ -782,6 +906,32 @@ PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals
                      (hipStream_t)stream, (const unsigned short*)skeys, svals, (const int2*)rec,
                      (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
                      token_mode);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// reduce6 (RB rounds of row gathers in flight per wave); rb in {2, 4, 8, 16}, 2-byte keys.
+PV_API int pv_conv_pool_bwd_reduce6_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                        float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
+                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode, int rb,
+                                        void* stream) {
+  using namespace pv::convbwd;
+  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
+  const long waves = (M + epw - 1) / epw;
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define PV_R6(RBV)                                                                                                   \
+  hipLaunchKernelGGL((conv_bwd_reduce6_kernel<unsigned short, RBV>), grid, dim3(256), 0, st,                         \
+                     (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, \
+                     L, E, V, seed, seed_ptr, row_offset, thr, token_mode)
+  switch (rb) {
+    case 2: PV_R6(2); break;
+    case 4: PV_R6(4); break;
+    case 8: PV_R6(8); break;
+    case 16: PV_R6(16); break;
+    default: return -2;
+  }
+#undef PV_R6
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -58,10 +58,14 @@ _grid_cache = {}
 
 # sorted dTable entries per wave in the reduce (conv_bwd_reduce5_kernel); 0 = 64-entry reduce4
 REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
+# reduce6: weight-row gathers of RB 4-entry rounds in flight per wave (0 = reduce5)
+REDUCE_RB = int(os.environ.get("PAGEVEC_REDUCE_RB", "0"))
 
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
 # (both halves are gather/latency-bound and leave CU slots idle when run back to back)
-DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "0") != "0"  # measured: no gain (9.30 vs 9.30 ms)
+# (round 1: no gain, 9.30 vs 9.30 ms; with the round-2 backward, same box: 7.535 / 7.555 vs
+# 7.596 / 7.624 ms per headline step, so on by default for long sequences)
+DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "1") != "0"
 _side = {}
 
 
@@ -178,7 +182,10 @@ class _ConvPoolFn(torch.autograd.Function):
         L_ = lib()
         # every buffer the side stream touches is allocated on the main stream above/before
         # and the main stream joins the side stream before returning: no cross-stream reuse
-        side = _side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] else None
+        dense_dx = ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl())
+        # the page tower's dW beside its table chain (not inside a hipGraph capture: one stream)
+        side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] and not dense_dx
+                and not torch.cuda.is_current_stream_capturing() else None)
         if side is not None:
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
@@ -190,14 +197,14 @@ class _ConvPoolFn(torch.autograd.Function):
                   "pv_conv_pool_bwd_dw")
 
         # Order: the side-stream variant starts dW first (it runs beside the table chain);
-        # on one stream the TABLE gradient goes first and its data-parallel bucket (the
-        # table has a bucket of its own, parallel/ddp.py) is released as soon as the
-        # reduce is enqueued, so its all-reduce (12 MB for the 30k x 100 table) overlaps
+        # on one stream the TABLE gradient goes first.  Either way the table's data-parallel
+        # bucket (a bucket of its own, parallel/ddp.py) is released as soon as its reduce is
+        # enqueued on this stream, so its all-reduce (12 MB for the 30k x 100 table) overlaps
         # the dW kernel instead of trailing the whole backward.
         if side is not None:
             launch_dw()
         dtable = None
-        if ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl()):
+        if dense_dx:
             # short sequences (query towers): per-sample dense dX rows (LDS), sorted by token,
             # summed per token run: N*L rows instead of N*1050 (f, j) entries
             R = N * L
@@ -233,7 +240,11 @@ class _ConvPoolFn(torch.autograd.Function):
             sort_pairs_iota(keys, skeys, svals, end_bit)
             dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
             wrow = _weight_rows(w3, w4, EP)
-            if k16:
+            if k16 and REDUCE_RB > 0:
+                check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, REDUCE_RB, s),
+                      "pv_conv_pool_bwd_reduce6_u16")
+            elif k16:
                 check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
                                                       L, E, V, seed, P(sp), row_offset, thr, tok, s),
                       "pv_conv_pool_bwd_reduce5_u16")
@@ -243,14 +254,12 @@ class _ConvPoolFn(torch.autograd.Function):
             else:
                 check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
                                                   P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
+        if t_tab is not None:
+            grad_sink.done(ptable)  # fires the table's bucket: enqueued after the reduce above
         if side is None:
-            if t_tab is not None:
-                grad_sink.done(ptable)  # fires the table's bucket: enqueued after the reduce above
             launch_dw()
         else:
             main.wait_stream(side)
-            if t_tab is not None:
-                grad_sink.done(ptable)
         for t, prm in ((t3, pw3), (t4, pw4)):
             if t is not None:
                 grad_sink.done(prm)

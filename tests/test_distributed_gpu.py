@@ -86,7 +86,7 @@ def test_cross_gpu_loss_ranks_one_gpu(world):
         assert h_q < 1e-4 and h_d < 1e-4, res  # vs the single-process HIP path
 
 
-def _ddp_worker(rank, world, port, model, q):
+def _ddp_worker(rank, world, port, model, q, ld=64):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
     try:
@@ -99,11 +99,11 @@ def _ddp_worker(rank, world, port, model, q):
         info = pdist.init_distributed()
         dev = info.device
         cfg = Configuration(model=model, feature_level="ngram", vocab_hash_size=500, query_length=12,
-                            document_length=64, batch_size=32, embedding_dim=100, dropout_prob=(0.0, 0.5),
+                            document_length=ld, batch_size=32, embedding_dim=100, dropout_prob=(0.0, 0.5),
                             loss_mode="in_batch", mlp_dims=(64, 64, 32), hidden_dims=64, grad_bucket_mb=0.05)
         g = torch.Generator().manual_seed(10 + rank)
         qi = torch.randint(1, 500, (32, 12), generator=g, dtype=torch.int32).to(dev)
-        di = torch.randint(1, 500, (32, 4, 64), generator=g, dtype=torch.int32).to(dev)
+        di = torch.randint(1, 500, (32, 4, ld), generator=g, dtype=torch.int32).to(dev)
         grads = []
         for enabled in (False, True):
             grad_sink.ENABLED = enabled
@@ -124,16 +124,18 @@ def _ddp_worker(rank, world, port, model, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("model", ["cdssm", "mlp"])
-def test_ddp_buckets_with_direct_grad_writes(model):
+@pytest.mark.parametrize("model,ld", [("cdssm", 64), ("cdssm", 96), ("mlp", 64)])
+def test_ddp_buckets_with_direct_grad_writes(model, ld):
     """Bucketed, backward-overlapped all-reduce (parallel/ddp.py) fired from the direct
     flat-gradient writes (ops/grad_sink.py): the reduced gradients equal those of the
-    AccumulateGrad-hook path, and every rank holds the same gradient."""
+    AccumulateGrad-hook path, and every rank holds the same gradient.  ld = 96 takes the
+    long-sequence conv backward (emit / sort / reduce, dW on the side stream, the table's
+    own bucket released before dW)."""
     world = 2
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, model, q)) for r in range(world)]
+    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, model, q, ld)) for r in range(world)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=300) for _ in ps)
     [p.join(timeout=60) for p in ps]
