@@ -62,6 +62,9 @@ def parse():
                     help="after the timed steps, keep training (untimed, fresh synthetic batches, eager) until "
                          "this many optimizer steps in total, then measure Recall@10 on held-out pairs; "
                          "-1 = auto (1000 for cdssm / mlp, 0 = none for bert / chunked)")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="deterministic reduction mode (ops/determinism.py): order-free fixed-point "
+                         "gradient sums, one stream, no hipGraph")
     ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "cdssm_char"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5; "
                          "cdssm_char = the reference's default run (char level, 250 / 5000 tokens), per-GPU "
@@ -126,7 +129,8 @@ def main():
         if a.batch == 4096:
             a.batch = 1024
     batch = a.batch if a.model in ("cdssm", "cdssm_char") or a.batch != 4096 else cfg.batch_size
-    cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode)
+    cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode,
+                      deterministic=bool(a.deterministic))
     a.batch = batch
     V = cfg.vocab_hash_size
     dev = info.device
@@ -219,7 +223,8 @@ def main():
             "data": "synthetic (device-resident pre-featurized Zipf trigram-id pages; random-init weights)",
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
-                       "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend},
+                       "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend,
+                       "deterministic": bool(a.deterministic)},
             "recall_at_10": None if recall is None else round(recall, 4),
             "recall_after_steps": max(done, a.quality_steps),
             "final_loss": round(final_loss, 4),

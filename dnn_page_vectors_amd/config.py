@@ -117,6 +117,7 @@ class Configuration:
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
     grad_bucket_mb: float = 32.0
     query_stream: bool = True             # query tower (fwd, hence bwd) on a side HIP stream
+    deterministic: bool = False           # order-free (fixed-point) GPU reductions, one stream (ops/determinism.py)
     placement: str = "dp"                # dp (data parallel) | tower (slots over ranks, cnn_dssm_tf.py:139-158)
     log_every: int = 10
     skip_nonfinite: bool = True

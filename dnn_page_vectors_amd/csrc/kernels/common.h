@@ -171,6 +171,25 @@ enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3, PV_ERR_A
 #define PV_DEBUG_EXPORT(tu)
 #endif
 
+// ---- deterministic reduction mode (ops/determinism.py, det.hip) ---------------
+// Float atomics make a cross-workgroup sum depend on arrival order.  In deterministic mode
+// the kernels that combine partial sums across workgroups add int64 fixed-point values
+// (resolution 2^-40, range +-2^23) instead: integer addition is associative, so the total
+// is the same for every arrival order, and det_flush adds it into the float target in one
+// ordered pass.  Partial sums inside a workgroup are already formed in a fixed order.
+namespace pv {
+constexpr float PV_FX_SCALE = 1099511627776.0f;  // 2^40
+__device__ __forceinline__ void fx_add(long long* fx, size_t i, float v) {
+  const float x = fminf(fmaxf(v * PV_FX_SCALE, -9.0e18f), 9.0e18f);  // saturate, never wrap
+  atomicAdd(reinterpret_cast<unsigned long long*>(fx) + i, (unsigned long long)__float2ll_rn(x));
+}
+bool det_on();
+// n zeroed int64 accumulators, stream-ordered (one process-wide buffer: deterministic mode
+// runs every kernel of a step on one stream); nullptr on allocation failure
+long long* det_scratch(size_t n, hipStream_t st);
+int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st);  // dst += fx * 2^-40
+}  // namespace pv
+
 #define PV_LAUNCH_CHECK() \
   do {                    \
     hipError_t e__ = hipGetLastError(); \

@@ -45,7 +45,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
                                           const unsigned short* __restrict__ table, float* __restrict__ dw,
                                           float* __restrict__ db, float* red, int L, int E, int V, int fg, int fl,
                                           int n0, int n1, unsigned seed, unsigned row_offset, int thr, int token_mode,
-                                          float scale) {
+                                          float scale, long long* fxw, long long* fxb) {
   constexpr int NP = K * PIECES_ROW;  // pieces per window (39 / 52)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -145,14 +145,21 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
   for (int x = threadIdx.x; x < K * EP; x += 256) {
     float v = red[x] + red[K * EP + x] + red[2 * K * EP + x] + red[3 * K * EP + x];
     int j = x / EP, e = x % EP;
-    if (e < E && v != 0.f) atomicAdd(&dw[((size_t)fl * K + j) * E + e], v * scale);
+    if (e < E && v != 0.f) {
+      const size_t o = ((size_t)fl * K + j) * E + e;
+      if (fxw) fx_add(fxw, o, v * scale);  // deterministic mode (common.h)
+      else atomicAdd(&dw[o], v * scale);
+    }
   }
   __shared__ float gsw[4];
   if (lane == 0) gsw[wave] = gs;
   __syncthreads();
   if (threadIdx.x == 0) {
     float t = gsw[0] + gsw[1] + gsw[2] + gsw[3];
-    if (t != 0.f) atomicAdd(&db[fg], t);
+    if (t != 0.f) {
+      if (fxb) fx_add(fxb, fg, t);
+      else atomicAdd(&db[fg], t);
+    }
   }
 }
 
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
                                                           float* dw4, float* db, int N, int L, int E, int V, int nsplit,
                                                           unsigned seed, const unsigned* seed_ptr,
                                                           unsigned row_offset, int thr, int token_mode, float scale,
-                                                          int xcd_map) {
+                                                          int xcd_map, long long* fx) {
   __shared__ float red[4 * 4 * EP];
   if (seed_ptr) seed += *seed_ptr;  // device seed offset (captured hipGraph steps)
   // XCD-aware work mapping: workgroups are dealt round-robin to the 8 XCDs (each with its
@@ -180,10 +187,10 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
   const int n0 = split * per, n1 = min(N, n0 + per);
   if (f < FW)
     dw_filter<3>(gpool, pooled, argmax, ids, table, dw3, db, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
-                 token_mode, scale);
+                 token_mode, scale, fx, fx ? fx + (size_t)7 * FW * E : nullptr);
   else
     dw_filter<4>(gpool, pooled, argmax, ids, table, dw4, db, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
-                 token_mode, scale);
+                 token_mode, scale, fx ? fx + (size_t)3 * FW * E : nullptr, fx ? fx + (size_t)7 * FW * E : nullptr);
 }
 
 // ---- dTable emit (compact): keys + slot values + one 8-byte record per (n,f) pair -------
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool,
 // 256-byte-shaped atomic instructions.
 constexpr int RPIECES = EP / 8;  // 13 pieces of 8 columns
 __device__ __forceinline__ void reduce4_flush(float* slab, const float (&acc)[8], int g, int p, int lane, int E,
-                                              unsigned key, float* __restrict__ dtable) {
+                                              unsigned key, float* __restrict__ dtable, long long* fx) {
   if (p < RPIECES) {
     *reinterpret_cast<f32x4*>(slab + g * EP + 8 * p) = f32x4{acc[0], acc[1], acc[2], acc[3]};
     *reinterpret_cast<f32x4*>(slab + g * EP + 8 * p + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
@@ -258,11 +265,13 @@ __device__ __forceinline__ void reduce4_flush(float* slab, const float (&acc)[8]
   const int c0 = lane, c1 = lane + 64;
   if (c0 < E) {
     const float v = slab[c0] + slab[EP + c0] + slab[2 * EP + c0] + slab[3 * EP + c0];
-    atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c0)], v);
+    if (fx) fx_add(fx, (unsigned)(key * (unsigned)E + c0), v);  // deterministic mode
+    else atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c0)], v);
   }
   if (c1 < E) {
     const float v = slab[c1] + slab[EP + c1] + slab[2 * EP + c1] + slab[3 * EP + c1];
-    atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c1)], v);
+    if (fx) fx_add(fx, (unsigned)(key * (unsigned)E + c1), v);
+    else atomicAdd(&dtable[(unsigned)(key * (unsigned)E + c1)], v);
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // slab reads done before the next flush overwrites it
 }
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
                                                                const unsigned short* __restrict__ wrow,
                                                                float* __restrict__ dtable, long M, int L, int E,
                                                                int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode) {
+                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
   __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
   if (seed_ptr) seed += *seed_ptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -355,13 +364,13 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* _
       }
       const unsigned long long left = __ballot(!done);
       if (left == 0) break;
-      reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+      reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = 0.f;
       cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
     }
   }
-  reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+  reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 }
 
 // ---- dTable reduce, long runs: each wave owns EPW consecutive sorted entries --------------
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
                                                                const unsigned short* __restrict__ wrow,
                                                                float* __restrict__ dtable, long M, int EPW, int L,
                                                                int E, int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode) {
+                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
   __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
   if (seed_ptr) seed += *seed_ptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
         }
         const unsigned long long left = __ballot(!done);
         if (left == 0) break;
-        reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+        reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] = 0.f;
         cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
@@ -489,7 +498,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
     k0 = k1; s0 = s1; r0 = r1;
     k1 = k2; s1 = s2;
   }
-  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 }
 
 // reduce6 = reduce5 with the weight-row gathers of RB rounds (4 entries each) issued
@@ -503,7 +512,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce6_kernel(const KT* __restr
                                                                const unsigned short* __restrict__ wrow,
                                                                float* __restrict__ dtable, long M, int EPW, int L,
                                                                int E, int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode) {
+                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
   static_assert(RB >= 1 && 16 % RB == 0, "RB rounds of 4 entries tile a 64-entry sub-chunk");
   __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
   if (seed_ptr) seed += *seed_ptr;
@@ -602,7 +611,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce6_kernel(const KT* __restr
           }
           const unsigned long long left = __ballot(!done);
           if (left == 0) break;
-          reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+          reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc[k] = 0.f;
           cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
@@ -613,7 +622,7 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce6_kernel(const KT* __restr
     k0 = k1; s0 = s1; r0 = r1;
     k1 = k2; s1 = s2;
   }
-  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable);
+  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 }
 
 
@@ -773,7 +782,7 @@ __global__ __launch_bounds__(256) void conv_bwd_rows_reduce_kernel(const KT* __r
                                                                    const unsigned* __restrict__ svals,
                                                                    const float* __restrict__ rows,
                                                                    float* __restrict__ dtable, long M, int EPW,
-                                                                   int E, int V) {
+                                                                   int E, int V, long long* fx) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
   if (wbeg >= M) return;
@@ -784,9 +793,14 @@ __global__ __launch_bounds__(256) void conv_bwd_rows_reduce_kernel(const KT* __r
   float a0 = 0.f, a1 = 0.f;
   auto flush = [&]() {
     if (cur < UV) {
-      float* drow = dtable + (size_t)cur * E;
-      if (c0 < E) atomicAdd(&drow[c0], a0);
-      if (c1 < E) atomicAdd(&drow[c1], a1);
+      if (fx) {  // deterministic mode
+        if (c0 < E) fx_add(fx, (size_t)cur * E + c0, a0);
+        if (c1 < E) fx_add(fx, (size_t)cur * E + c1, a1);
+      } else {
+        float* drow = dtable + (size_t)cur * E;
+        if (c0 < E) atomicAdd(&drow[c0], a0);
+        if (c1 < E) atomicAdd(&drow[c1], a1);
+      }
     }
     a0 = 0.f;
     a1 = 0.f;
@@ -832,6 +846,21 @@ PV_DEBUG_EXPORT(convbwd)
 
 using namespace pv;
 
+// deterministic mode (common.h): fixed-point accumulators for an n-float target, flushed
+// into it after the kernel; a no-op otherwise
+struct DetAcc {
+  long long* fx = nullptr;
+  int err = 0;
+  DetAcc(size_t n, hipStream_t st) {
+    if (pv::det_on()) {
+      fx = pv::det_scratch(n, st);
+      if (!fx) err = -4;
+    }
+  }
+  int finish(float* dst, size_t n, hipStream_t st) const { return fx ? pv::det_flush(fx, dst, n, st) : 0; }
+};
+
+
 PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                                const void* table, float* dw3, float* dw4, float* db, int N, int L, int E, int V,
                                unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
@@ -845,10 +874,21 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
     const char* e = getenv("PAGEVEC_DW_XCD");
     return (e && e[0] == '0') ? 0 : 1;
   }();
-  hipLaunchKernelGGL(conv_bwd_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, (hipStream_t)stream, gpool, pooled,
+  hipStream_t st = (hipStream_t)stream;
+  // deterministic mode: fixed-point accumulators [dW3 | dW4 | db], flushed in order below
+  const size_t nfx = (size_t)7 * FW * E + 2 * FW;
+  long long* fx = det_on() ? det_scratch(nfx, st) : nullptr;
+  if (det_on() && !fx) return -4;
+  hipLaunchKernelGGL(conv_bwd_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled,
                      argmax, ids, (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr,
-                     row_offset, thr, token_mode, scale, xcd_map);
+                     row_offset, thr, token_mode, scale, xcd_map, fx);
   PV_LAUNCH_CHECK();
+  if (fx) {
+    int rc = det_flush(fx, dw3, (size_t)3 * FW * E, st);
+    if (!rc) rc = det_flush(fx + (size_t)3 * FW * E, dw4, (size_t)4 * FW * E, st);
+    if (!rc) rc = det_flush(fx + (size_t)7 * FW * E, db, 2 * FW, st);
+    return rc;
+  }
   return 0;
 }
 
@@ -875,11 +915,13 @@ PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals
   using namespace pv::convbwd;
   if (E > EP || epw < 64 || (epw & 63) || (long)V * E >= (1L << 32)) return -1;
   const long waves = (M + epw - 1) / epw;
+  const DetAcc det((size_t)V * E, (hipStream_t)stream);
+  if (det.err) return det.err;
   hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed,
-                     seed_ptr, row_offset, thr, token_mode);
+                     seed_ptr, row_offset, thr, token_mode, det.fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
 }
 
 // 2-byte-key variants (V < 65535): emit -> pv_sort_iota_u16 -> reduce
@@ -902,12 +944,14 @@ PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals
   using namespace pv::convbwd;
   if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
   const long waves = (M + epw - 1) / epw;
+  const DetAcc det((size_t)V * E, (hipStream_t)stream);
+  if (det.err) return det.err;
   hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                      (hipStream_t)stream, (const unsigned short*)skeys, svals, (const int2*)rec,
                      (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
-                     token_mode);
+                     token_mode, det.fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
 }
 
 // reduce6 (RB rounds of row gathers in flight per wave); rb in {2, 4, 8, 16}, 2-byte keys.
@@ -920,10 +964,12 @@ PV_API int pv_conv_pool_bwd_reduce6_u16(const void* skeys, const unsigned* svals
   const long waves = (M + epw - 1) / epw;
   const dim3 grid((unsigned)((waves + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
+  const DetAcc det((size_t)V * E, st);
+  if (det.err) return det.err;
 #define PV_R6(RBV)                                                                                                   \
   hipLaunchKernelGGL((conv_bwd_reduce6_kernel<unsigned short, RBV>), grid, dim3(256), 0, st,                         \
                      (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, \
-                     L, E, V, seed, seed_ptr, row_offset, thr, token_mode)
+                     L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx)
   switch (rb) {
     case 2: PV_R6(2); break;
     case 4: PV_R6(4); break;
@@ -933,7 +979,7 @@ PV_API int pv_conv_pool_bwd_reduce6_u16(const void* skeys, const unsigned* svals
   }
 #undef PV_R6
   PV_LAUNCH_CHECK();
-  return 0;
+  return det.finish(dtable, (size_t)V * E, st);
 }
 
 // Short-sequence dTable, step 1: rows (N*L, EP) fp32 (touched rows written), keys (N*L) u16
@@ -979,14 +1025,16 @@ PV_API int pv_conv_bwd_rows_reduce(const void* skeys, int key_bytes, const unsig
   if (E > EP || epw < 64 || (epw & 63)) return -1;
   const long waves = (M + epw - 1) / epw;
   hipStream_t st = (hipStream_t)stream;
+  const DetAcc det((size_t)V * E, st);
+  if (det.err) return det.err;
   if (key_bytes == 2)
     hipLaunchKernelGGL(conv_bwd_rows_reduce_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                       st, (const unsigned short*)skeys, svals, rows, dtable, M, epw, E, V);
+                       st, (const unsigned short*)skeys, svals, rows, dtable, M, epw, E, V, det.fx);
   else
     hipLaunchKernelGGL(conv_bwd_rows_reduce_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                       (const unsigned*)skeys, svals, rows, dtable, M, epw, E, V);
+                       (const unsigned*)skeys, svals, rows, dtable, M, epw, E, V, det.fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return det.finish(dtable, (size_t)V * E, st);
 }
 
 PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
@@ -996,10 +1044,12 @@ PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals
   using namespace pv::convbwd;
   if (E > EP || (long)V * E >= (1L << 32)) return -1;
   const long chunks = (M + 63) / 64;
+  const DetAcc det((size_t)V * E, (hipStream_t)stream);
+  if (det.err) return det.err;
   hipLaunchKernelGGL(conv_bwd_reduce4_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, L, E, V, seed,
-                     seed_ptr, row_offset, thr, token_mode);
+                     seed_ptr, row_offset, thr, token_mode, det.fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
 }
 

@@ -356,7 +356,9 @@ PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* ou
   const int QB = narrow ? 16 : 64, RG = 256 / QB;
   const long gx = (units + QB - 1) / QB;
   long splits = 1;
-  if (mode == 1) {
+  // deterministic mode (common.h): one row split, so each column gets a single atomic add
+  // per launch (order-free) instead of <= 64 same-address ones
+  if (mode == 1 && !pv::det_on()) {
     splits = (1024 + gx - 1) / gx;
     const long maxs = (R + 4 * RG - 1) / (4 * RG);  // >= 4 rows per thread
     if (splits > maxs) splits = maxs;

@@ -1,0 +1,56 @@
+// Deterministic reduction mode: the fixed-point accumulator buffer and its flush
+// (see common.h, "deterministic reduction mode").  pv_set_deterministic(1) switches the
+// conv backward (dW, db, dTable), the column-sum kernel and the gradient-norm kernel from
+// float atomics to fixed-point ones; ops/determinism.py also keeps a training step on one
+// HIP stream while it is on.
+#include "common.h"
+
+namespace pv {
+namespace {
+int g_det = 0;
+long long* g_fx = nullptr;
+size_t g_cap = 0;
+
+__global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restrict__ fx, float* __restrict__ dst,
+                                                       long n) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long v = fx[i];
+    if (v != 0) dst[i] += (float)((double)v * (1.0 / 1099511627776.0));
+  }
+}
+}  // namespace
+
+bool det_on() { return g_det != 0; }
+
+long long* det_scratch(size_t n, hipStream_t st) {
+  if (n > g_cap) {
+    if (g_fx) {
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+      (void)hipFree(g_fx);
+      g_fx = nullptr;
+      g_cap = 0;
+    }
+    const size_t cap = n < ((size_t)1 << 20) ? ((size_t)1 << 20) : n;
+    if (hipMalloc(&g_fx, cap * sizeof(long long)) != hipSuccess) {
+      g_fx = nullptr;
+      return nullptr;
+    }
+    g_cap = cap;
+  }
+  if (hipMemsetAsync(g_fx, 0, n * sizeof(long long), st) != hipSuccess) return nullptr;
+  return g_fx;
+}
+
+int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st) {
+  if (n == 0) return 0;
+  long blocks = ((long)n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(fx_flush_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fx, dst, (long)n);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+}  // namespace pv
+
+PV_API void pv_set_deterministic(int on) { pv::g_det = on ? 1 : 0; }
+PV_API int pv_get_deterministic() { return pv::g_det; }

@@ -190,7 +190,8 @@ __device__ __forceinline__ void sq_acc(const f32x4& v, float& s, float& bad) {
   }
 }
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ out2) {
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ out2,
+                                                    long long* fx) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   const long n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
@@ -219,7 +220,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) {
     float tot = ws[0] + ws[1] + ws[2] + ws[3];
     float b = fmaxf(fmaxf(wb[0], wb[1]), fmaxf(wb[2], wb[3]));
-    atomicAdd(&out2[0], tot);
+    if (fx) fx_add(fx, 0, tot);  // deterministic mode (common.h)
+    else atomicAdd(&out2[0], tot);
     if (b != 0.f) atomicExch(&out2[1], 1.f);
   }
 }
@@ -322,9 +324,12 @@ PV_API int pv_cast_pad_bf16(const float* in, void* out, long rows, int cols, int
 PV_API int pv_sumsq(const float* x, long n, float* out2, void* stream) {
   unsigned blocks = grid_for(n, 16);
   if (blocks > 512) blocks = 512;
-  hipLaunchKernelGGL(pv::optim::sumsq_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, out2);
+  hipStream_t st = (hipStream_t)stream;
+  long long* fx = pv::det_on() ? pv::det_scratch(1, st) : nullptr;
+  if (pv::det_on() && !fx) return -4;
+  hipLaunchKernelGGL(pv::optim::sumsq_kernel, dim3(blocks), dim3(256), 0, st, x, n, out2, fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return fx ? pv::det_flush(fx, out2, 1, st) : 0;
 }
 
 PV_API int pv_scale(float* x, long n, float s, void* stream) {

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import dense as dops
+from ..ops import determinism
 
 _GENERATION = [0]
 
@@ -101,6 +102,8 @@ class TwoTowerModel(nn.Module):
         if os.environ.get("PAGEVEC_QUERY_STREAM", "1") == "0":  # A/B switch
             return None
         if torch.cuda.is_current_stream_capturing():  # hipGraph capture: one stream
+            return None
+        if determinism.enabled():  # deterministic mode: one stream (ops/determinism.py)
             return None
         st = getattr(self, "_qstreams", None)
         if st is None:

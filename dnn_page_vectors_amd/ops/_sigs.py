@@ -12,6 +12,9 @@ SIGS = {
     "pv_conv_pack_weights": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
+    # det.hip (deterministic reduction mode, ops/determinism.py)
+    "pv_set_deterministic": "i",
+    "pv_get_deterministic": "",
     "pv_conv_pool_fwd": "pppppp" "iii" "upu" "ii" "f" "i" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",

@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from . import grad_sink
+from . import determinism, grad_sink
 from . import reference as ref
 from ._common import P, check, lib, need, stream, use_hip
 
@@ -185,7 +185,7 @@ class _ConvPoolFn(torch.autograd.Function):
         dense_dx = ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl())
         # the page tower's dW beside its table chain (not inside a hipGraph capture: one stream)
         side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] and not dense_dx
-                and not torch.cuda.is_current_stream_capturing() else None)
+                and not torch.cuda.is_current_stream_capturing() and not determinism.enabled() else None)
         if side is not None:
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)

@@ -1,0 +1,42 @@
+"""Deterministic reduction mode ("two runs give equal loss with deterministic
+reduction mode").
+
+The fast GPU training step is reproducible only to rounding: the sparse conv backward
+(dW / db per sample split, the embedding-table reduce's run-boundary flushes, the query
+tower's rows reduce), the column-sum kernel's row splits and the gradient-norm kernel
+combine partial sums with float atomics, whose result depends on arrival order.  With
+``set_deterministic(True)`` (or ``Configuration.deterministic``):
+
+* those kernels add int64 fixed-point values instead (resolution 2^-40, saturating at
+  +-2^23; ``csrc/kernels/common.h::fx_add``): integer addition is associative, so the total
+  does not depend on arrival order, and one ordered pass (``det.hip::fx_flush_kernel``)
+  adds it into the float gradient;
+* the column-sum kernel uses one row split (a single atomic per column and launch);
+* a training step runs on ONE HIP stream (no query-tower or dW side streams), and
+  ``Trainer`` does not capture hipGraphs (the fixed-point buffer may grow between steps).
+
+Everything else on the CDSSM step (fused conv forward, dense / L2 kernels, the loss kernels'
+fixed-order split sums, the radix sort, Adam) is order-free already.  Cost: the extra
+memset + flush per accumulating launch (the 30k x 100 table: 24 MB of int64 per reduce).
+CPU training is always deterministic (tests/test_determinism.py).
+"""
+from __future__ import annotations
+
+from .. import _native
+
+_ON = [False]
+
+
+def set_deterministic(on: bool = True) -> None:
+    _ON[0] = bool(on)
+    import torch
+
+    if not torch.cuda.is_available():  # CPU training is deterministic without the kernels' mode
+        return
+    lib = _native.hip(required=False)
+    if lib is not None:
+        lib.pv_set_deterministic(1 if on else 0)
+
+
+def enabled() -> bool:
+    return _ON[0]

@@ -28,6 +28,7 @@ import torch
 
 from ..models.base import TwoTowerModel, bump_generation
 from ..ops import dense as dops
+from ..ops import determinism
 from ..ops import grad_sink
 from ..ops import loss as lops
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
@@ -115,7 +116,12 @@ class Trainer:
         # hipGraph mode (single process on a GPU): after GRAPH_WARMUP eager steps the whole
         # step (forward, backward, Adam) is captured once and replayed — one launch per step
         # instead of hundreds (the launch-bound MLP / BERT steps)
-        self.graph_mode = bool(graph) and self.device.type == "cuda" and not self.info.enabled
+        # deterministic reduction mode (ops/determinism.py) is process-wide: it follows the
+        # latest Trainer's config; its fixed-point buffer may grow between steps, so no capture
+        self.deterministic = bool(getattr(cfg, "deterministic", False))
+        determinism.set_deterministic(self.deterministic)
+        self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
+                           and not self.deterministic)
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
         # Round 1 needed it: replays interleaved with eager allocating work faulted after ~97
         # CDSSM steps inside rocPRIM's onesweep radix sort (the dTable gradient's bucketing),

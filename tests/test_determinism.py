@@ -52,3 +52,47 @@ def test_gpu_forward_bit_identical_and_training_reproducible():
         l1, _ = a.compute_loss(q, d, seed=11)
         l2, _ = a.compute_loss(q, d, seed=11)
     assert torch.equal(l1, l2)
+
+
+def _run_det(dev, deterministic, steps=3, ld=40):
+    torch.manual_seed(0)
+    pdist.set_info(pdist.DistInfo(device=torch.device(dev)))
+    cfg = _cfg().replace(deterministic=deterministic, document_length=ld, dropout_prob=(0.25, 0.5))
+    tr = Trainer(cfg, CDSSM(cfg, 300), torch.device(dev))
+    g = torch.Generator().manual_seed(5)
+    losses = []
+    for _ in range(steps):
+        q = torch.randint(1, 300, (16, 12), generator=g, dtype=torch.int32).to(dev)
+        d = torch.randint(1, 300, (16, 4, ld), generator=g, dtype=torch.int32).to(dev)
+        losses.append(float(tr.train_step(q, d)["loss"]))
+    torch.cuda.synchronize() if dev == "cuda" else None
+    return tr, losses
+
+
+def test_deterministic_flag_cpu_is_noop():
+    """The config flag exists everywhere; on CPU the reference ops are order-free anyway."""
+    a, la = _run_det("cpu", True, steps=2)
+    b, lb = _run_det("cpu", False, steps=2)
+    assert la == lb and torch.equal(a.flat.data, b.flat.data)
+    from dnn_page_vectors_amd.ops import determinism
+    determinism.set_deterministic(False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ld", [40, 200])
+def test_gpu_deterministic_mode_bit_identical_training(ld):
+    """with the deterministic reduction mode two GPU training runs give
+    bit-identical losses AND parameters (fixed-point cross-workgroup sums, one stream);
+    the mode changes the result only at rounding level.  ld = 40 takes the query-style
+    dense-dX table backward, ld = 200 the page tower's emit / sort / reduce path."""
+    from dnn_page_vectors_amd.ops import determinism
+    try:
+        a, la = _run_det("cuda", True, ld=ld)
+        b, lb = _run_det("cuda", True, ld=ld)
+        assert la == lb
+        assert torch.equal(a.flat.data, b.flat.data)
+        assert torch.equal(a.opt.m, b.opt.m) and torch.equal(a.opt.v, b.opt.v)
+        c, lc = _run_det("cuda", False, ld=ld)
+        torch.testing.assert_close(c.flat.data, a.flat.data, rtol=1e-4, atol=1e-5)
+    finally:
+        determinism.set_deterministic(False)
