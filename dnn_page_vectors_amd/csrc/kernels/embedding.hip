@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256) void bag_bwd_sorted_kernel(const unsigned shor
                                                              const unsigned* __restrict__ svals,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ lens, float* __restrict__ dW,
-                                                             long M, int EPW, int L, int E, int V, int mean) {
+                                                             long M, int EPW, int L, int E, int V, int mean,
+                                                             long long* fx) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
   if (wbeg >= M) return;
@@ -162,7 +163,10 @@ __global__ __launch_bounds__(256) void bag_bwd_sorted_kernel(const unsigned shor
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int c = 4 * lane + 256 * j;
-          if (c < E) {
+          if (c < E && fx) {  // deterministic mode (common.h): order-free fixed-point sums
+#pragma unroll
+            for (int k = 0; k < 4; ++k) fx_add(fx, (size_t)cur * E + c + k, acc[j][k]);
+          } else if (c < E) {
             atomicAdd(&drow[c + 0], acc[j][0]);
             atomicAdd(&drow[c + 1], acc[j][1]);
             atomicAdd(&drow[c + 2], acc[j][2]);
@@ -373,17 +377,19 @@ PV_API int pv_bag_bwd_sorted(const void* skeys, const unsigned* svals, const flo
   const dim3 grid((unsigned)((waves + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
   const unsigned short* k = (const unsigned short*)skeys;
+  long long* fx = pv::det_on() ? pv::det_scratch((size_t)V * E, st) : nullptr;
+  if (pv::det_on() && !fx) return -4;
   if (E <= 256)
     hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<1>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
-                       E, V, mean);
+                       E, V, mean, fx);
   else if (E <= 512)
     hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<2>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
-                       E, V, mean);
+                       E, V, mean, fx);
   else
     hipLaunchKernelGGL(pv::embed::bag_bwd_sorted_kernel<4>, grid, dim3(256), 0, st, k, svals, g, lens, dW, M, epw, L,
-                       E, V, mean);
+                       E, V, mean, fx);
   PV_LAUNCH_CHECK();
-  return 0;
+  return fx ? pv::det_flush(fx, dW, (size_t)V * E, st) : 0;
 }
 
 // counts (N, ldc) bf16.  ldc <= HIST_MAX and ldc % 4 == 0: the LDS path writes every

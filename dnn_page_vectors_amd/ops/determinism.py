@@ -11,7 +11,10 @@ combine partial sums with float atomics, whose result depends on arrival order. 
   +-2^23; ``csrc/kernels/common.h::fx_add``): integer addition is associative, so the total
   does not depend on arrival order, and one ordered pass (``det.hip::fx_flush_kernel``)
   adds it into the float gradient;
-* the column-sum kernel uses one row split (a single atomic per column and launch);
+* the column-sum kernel uses one row split (a single atomic per column and launch), the
+  MLP embedding bag's sparse backward sends its run-boundary sums through the fixed-point
+  buffer too, and torch's own ops use their deterministic algorithms
+  (``torch.use_deterministic_algorithms``: the BERT token-embedding ``index_add_``);
 * a training step runs on ONE HIP stream (no query-tower or dW side streams), and
   ``Trainer`` does not capture hipGraphs (the fixed-point buffer may grow between steps).
 
@@ -33,6 +36,13 @@ def set_deterministic(on: bool = True) -> None:
 
     if not torch.cuda.is_available():  # CPU training is deterministic without the kernels' mode
         return
+    # the few torch ops on the training paths (the BERT token-embedding index_add_) switch to
+    # their deterministic implementations; uninitialised memory is NOT NaN-filled (every
+    # kernel output is fully written; padded operands are allocated zeroed)
+    torch.use_deterministic_algorithms(bool(on), warn_only=True)
+    import torch.utils.deterministic as _tud
+
+    _tud.fill_uninitialized_memory = False
     lib = _native.hip(required=False)
     if lib is not None:
         lib.pv_set_deterministic(1 if on else 0)

@@ -96,3 +96,34 @@ def test_gpu_deterministic_mode_bit_identical_training(ld):
         torch.testing.assert_close(c.flat.data, a.flat.data, rtol=1e-4, atol=1e-5)
     finally:
         determinism.set_deterministic(False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset", ["mlp_xgpu", "bert_dp8"])
+def test_gpu_deterministic_mode_other_models(preset):
+    """The deterministic mode covers the MLP (embedding-bag sparse backward, column sums)
+    and BERT (LayerNorm / bias partial sums, token-embedding index_add_) steps too."""
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.ops import determinism
+
+    cfg = preset_config(preset).replace(deterministic=True, loss_mode="in_batch")
+    if preset == "bert_dp8":
+        cfg = cfg.replace(bert_layers=2, batch_size=16, document_length=64, query_length=16)
+    else:
+        cfg = cfg.replace(batch_size=64, document_length=256, mlp_dims=(128, 128, 64), embedding_dim=128)
+    pdist.set_info(pdist.DistInfo(device=torch.device("cuda")))
+    try:
+        runs = []
+        for _ in range(2):
+            torch.manual_seed(0)
+            tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device("cuda"))
+            data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=256), "cuda", seed=3)
+            losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(3)]
+            torch.cuda.synchronize()
+            runs.append((losses, tr.flat.data.clone()))
+        assert runs[0][0] == runs[1][0]
+        assert torch.equal(runs[0][1], runs[1][1])
+    finally:
+        determinism.set_deterministic(False)
