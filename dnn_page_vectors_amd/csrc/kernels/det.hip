@@ -8,8 +8,9 @@
 namespace pv {
 namespace {
 int g_det = 0;
-long long* g_fx = nullptr;
-size_t g_cap = 0;
+constexpr int kMaxDev = 64;
+long long* g_fx[kMaxDev] = {};  // one buffer per device (the current device at the call)
+size_t g_cap[kMaxDev] = {};
 
 __global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restrict__ fx, float* __restrict__ dst,
                                                        long n) {
@@ -24,22 +25,24 @@ __global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restri
 bool det_on() { return g_det != 0; }
 
 long long* det_scratch(size_t n, hipStream_t st) {
-  if (n > g_cap) {
-    if (g_fx) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (n > g_cap[dev]) {
+    if (g_fx[dev]) {
       if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-      (void)hipFree(g_fx);
-      g_fx = nullptr;
-      g_cap = 0;
+      (void)hipFree(g_fx[dev]);
+      g_fx[dev] = nullptr;
+      g_cap[dev] = 0;
     }
     const size_t cap = n < ((size_t)1 << 20) ? ((size_t)1 << 20) : n;
-    if (hipMalloc(&g_fx, cap * sizeof(long long)) != hipSuccess) {
-      g_fx = nullptr;
+    if (hipMalloc(&g_fx[dev], cap * sizeof(long long)) != hipSuccess) {
+      g_fx[dev] = nullptr;
       return nullptr;
     }
-    g_cap = cap;
+    g_cap[dev] = cap;
   }
-  if (hipMemsetAsync(g_fx, 0, n * sizeof(long long), st) != hipSuccess) return nullptr;
-  return g_fx;
+  if (hipMemsetAsync(g_fx[dev], 0, n * sizeof(long long), st) != hipSuccess) return nullptr;
+  return g_fx[dev];
 }
 
 int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st) {
