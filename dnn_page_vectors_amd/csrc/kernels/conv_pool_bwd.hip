@@ -39,7 +39,7 @@ constexpr int FW = 150;
 // hashes of a sample are computed once by lanes 0..k-1 and fetched with ds_bpermute.
 // Table loads for 4 samples are issued before use.
 constexpr int PIECES_ROW = EP / 8;  // 13
-template <int K>
+template <int K, int DM>
 __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const float* __restrict__ pooled,
                                           const int* __restrict__ argmax, const int* __restrict__ ids,
                                           const unsigned short* __restrict__ table, float* __restrict__ dw,
@@ -97,7 +97,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
 #pragma unroll
         for (int j = 0; j < 4; ++j) tv[j] = __builtin_amdgcn_ds_bpermute(su * 4, tok[j]);
         tq = jq == 0 ? tv[0] : jq == 1 ? tv[1] : jq == 2 ? tv[2] : tv[3];
-        if (thr > 0) {
+        if (DM < 0 ? thr > 0 : DM != 0) {
           const int au = __builtin_amdgcn_ds_bpermute(su * 4, a);
           hq = (lane < 16 && jq < K) ? dropout_row_hash(seed, row_offset + (unsigned)((base + su) * L + au + jq)) : 0u;
         }
@@ -109,13 +109,13 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         const bool ok = pv_ && t >= 0 && t < V;
         // 32-bit element offset (V * EP < 2^31): no 64-bit multiply per piece
         raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (unsigned)(t * EP + pc * 8)) : u32x4{0u, 0u, 0u, 0u};
-        if (thr > 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
+        if (DM < 0 ? thr > 0 : DM != 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
           const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, (int)hq);
-          if (token_mode) {
+          if (DM == 3 || (DM < 0 && token_mode)) {
             const unsigned k = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
             raw[u] &= u32x4{k, k, k, k};
           } else {
-            raw[u] &= keep_piece(hr, pc, thr);
+            raw[u] &= keep_piece(hr, pc, DM == 1 ? 64 : thr);
           }
         }
       }
@@ -163,6 +163,8 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
   }
 }
 
+// DM: compile-time dropout mode (-1 runtime, 0 off, 1 element p = 0.25, 2 element any p, 3 token)
+template <int DM>
 __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, const float* pooled, const int* argmax,
                                                           const int* ids, const unsigned short* table, float* dw3,
                                                           float* dw4, float* db, int N, int L, int E, int V, int nsplit,
@@ -186,10 +188,10 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
   const int per = ((N + nsplit - 1) / nsplit + 255) / 256 * 256;
   const int n0 = split * per, n1 = min(N, n0 + per);
   if (f < FW)
-    dw_filter<3>(gpool, pooled, argmax, ids, table, dw3, db, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
+    dw_filter<3, DM>(gpool, pooled, argmax, ids, table, dw3, db, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx, fx ? fx + (size_t)7 * FW * E : nullptr);
   else
-    dw_filter<4>(gpool, pooled, argmax, ids, table, dw4, db, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
+    dw_filter<4, DM>(gpool, pooled, argmax, ids, table, dw4, db, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx ? fx + (size_t)3 * FW * E : nullptr, fx ? fx + (size_t)7 * FW * E : nullptr);
 }
 
@@ -478,6 +480,125 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
         for (int k = 0; k < 8; ++k) acc[k] += v[k];
         continue;
       }
+      bool done = false;
+      for (int it = 0; it < 5; ++it) {
+        const bool mine = !done && kg == cur;
+        if (mine) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += v[k];
+          done = true;
+        }
+        const unsigned long long left = __ballot(!done);
+        if (left == 0) break;
+        reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
+      }
+    }
+    if (n < 64) break;  // the dead (key == V) tail starts inside this sub-chunk
+    k0 = k1; s0 = s1; r0 = r1;
+    k1 = k2; s1 = s2;
+  }
+  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
+}
+
+// reduce7 = reduce5 with the dropout mode as a template parameter (DM: 0 off, 1 element
+// p = 0.25, 2 element any p, 3 token) and the common round's multiply + add as packed FMAs
+// (reduce5: a separate v = g * w pass, then 8 adds).
+template <typename KT, int DM>
+__global__ __launch_bounds__(256) void conv_bwd_reduce7_kernel(const KT* __restrict__ skeys,
+                                                               const unsigned* __restrict__ svals,
+                                                               const int2* __restrict__ rec,
+                                                               const unsigned short* __restrict__ wrow,
+                                                               float* __restrict__ dtable, long M, int EPW, int L,
+                                                               int E, int V, unsigned seed, const unsigned* seed_ptr,
+                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
+  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
+  if (seed_ptr) seed += *seed_ptr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, p = lane & 15;
+  float* slab = slabs[wave];
+  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
+  if (wbeg >= M) return;
+  const long wend = min(M, wbeg + (long)EPW);
+  const unsigned UV = (unsigned)V;
+  // pipeline: (k0, s0, r0) = current sub-chunk, (k1, s1) = next, (k2, s2) = the one after
+  unsigned k0, s0, k1, s1, k2, s2;
+  rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
+  rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
+  auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
+    if (!(key < UV && PV_OK((long)sl < M, PV_ERR_SLOT))) return int2{0, 0};
+    unsigned nn, f, j;
+    slot_decode(sl, nn, f, j);
+    return rec[nn * (2 * FW) + f];
+  };
+  int2 r0 = ld_rec(k0, s0);
+  unsigned cur = UV;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const bool act = p < RPIECES;
+  for (long b = wbeg; b < wend; b += 64) {
+    rd_meta(skeys, svals, b + 128 + lane, wend, UV, k2, s2);
+    const int2 r1 = ld_rec(k1, s1);
+    // this lane's entry of sub-chunk b
+    const unsigned key = k0;
+    unsigned fj = 0, hr = 0;
+    float gg = 0.f;
+    if (key < UV) {
+      unsigned nn, f, j;
+      slot_decode(s0, nn, f, j);
+      fj = (f << 2) | j;
+      gg = __int_as_float(r0.x);
+      if (DM != 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
+    }
+    const int n = __popcll(__ballot(key < UV));  // live entries are a prefix (sorted)
+    if (n == 0) break;
+    if (cur == UV) cur = __builtin_amdgcn_readfirstlane(key);
+    const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);
+    for (int q0 = 0; q0 < n; q0 += 4) {
+      const int e = q0 + g;
+      const bool valid = e < n;
+      const int src = (valid ? e : q0) * 4;
+      unsigned kg = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
+      const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
+      float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
+      const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
+      if (!valid) ge = 0.f;
+      float x[8];
+      {
+        // every lane loads (lanes p >= 13 re-read piece 12; their sums are never flushed):
+        // no exec-masked load
+        u32x4 w = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * (act ? p : RPIECES - 1)));
+        if constexpr (DM == 3) {
+          const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+          w &= u32x4{k, k, k, k};
+        } else if constexpr (DM == 1) {
+          w &= keep_piece(he, p, 64);  // compile-time p = 0.25 (the reference's rate)
+        } else if constexpr (DM == 2) {
+          w &= keep_piece(he, p, thr);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = __uint_as_float((k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16));
+      }
+      if (!valid) kg = klast;
+      const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
+      const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
+      if (ka == cur && kb == cur) {  // common round: packed FMAs straight into the run sums
+        const f32x2 g2 = {ge, ge};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          f32x2 a2 = {acc[2 * k], acc[2 * k + 1]};
+          a2 = __builtin_elementwise_fma(g2, f32x2{x[2 * k], x[2 * k + 1]}, a2);
+          acc[2 * k] = a2[0];
+          acc[2 * k + 1] = a2[1];
+        }
+        continue;
+      }
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ge * x[k];
       bool done = false;
       for (int it = 0; it < 5; ++it) {
         const bool mine = !done && kg == cur;
@@ -870,6 +991,10 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
+  static const bool dw_runtime_dm = [] {  // PAGEVEC_DW_DM=runtime: the runtime-mode kernel (A/B switch)
+    const char* e = getenv("PAGEVEC_DW_DM");
+    return e && e[0] == 'r';
+  }();
   static const int xcd_map = [] {  // PAGEVEC_DW_XCD=0: natural block order (A/B switch)
     const char* e = getenv("PAGEVEC_DW_XCD");
     return (e && e[0] == '0') ? 0 : 1;
@@ -879,9 +1004,17 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   const size_t nfx = (size_t)7 * FW * E + 2 * FW;
   long long* fx = det_on() ? det_scratch(nfx, st) : nullptr;
   if (det_on() && !fx) return -4;
-  hipLaunchKernelGGL(conv_bwd_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled,
-                     argmax, ids, (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr,
-                     row_offset, thr, token_mode, scale, xcd_map, fx);
+  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+#define PV_DW(DMV)                                                                                               \
+  hipLaunchKernelGGL((conv_bwd_dw_kernel<DMV>), dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled, argmax, ids, \
+                     (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr, row_offset, thr, \
+                     token_mode, scale, xcd_map, fx)
+  if (dw_runtime_dm) PV_DW(-1);
+  else if (dm == 0) PV_DW(0);
+  else if (dm == 1) PV_DW(1);
+  else if (dm == 3) PV_DW(3);
+  else PV_DW(2);
+#undef PV_DW
   PV_LAUNCH_CHECK();
   if (fx) {
     int rc = det_flush(fx, dw3, (size_t)3 * FW * E, st);
@@ -952,6 +1085,34 @@ PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals
                      token_mode, det.fx);
   PV_LAUNCH_CHECK();
   return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
+}
+
+// reduce7 (compile-time dropout mode, packed FMAs), 2-byte keys; same arguments as reduce5.
+PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                        float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
+                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                                        void* stream) {
+  using namespace pv::convbwd;
+  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
+  const long waves = (M + epw - 1) / epw;
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  const DetAcc det((size_t)V * E, st);
+  if (det.err) return det.err;
+  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+#define PV_R7(DMV)                                                                                               \
+  hipLaunchKernelGGL((conv_bwd_reduce7_kernel<unsigned short, DMV>), grid, dim3(256), 0, st,                     \
+                     (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, \
+                     epw, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx)
+  switch (dm) {
+    case 0: PV_R7(0); break;
+    case 1: PV_R7(1); break;
+    case 3: PV_R7(3); break;
+    default: PV_R7(2); break;
+  }
+#undef PV_R7
+  PV_LAUNCH_CHECK();
+  return det.finish(dtable, (size_t)V * E, st);
 }
 
 // reduce6 (RB rounds of row gathers in flight per wave); rb in {2, 4, 8, 16}, 2-byte keys.

@@ -34,6 +34,7 @@ SIGS = {
     "pv_conv_pool_bwd_emit3_u16": "pppppp" "iii" "f" "p",
     "pv_conv_pool_bwd_reduce5_u16": "ppppp" "liiii" "upuii" "p",
     "pv_conv_pool_bwd_reduce6_u16": "ppppp" "liiii" "upuii" "ip",
+    "pv_conv_pool_bwd_reduce7_u16": "ppppp" "liiii" "upuii" "p",
     "pv_sort_iota_u32": "plppp" "li" "p",
     # radix_sort.hip
     "pv_rsort_temp_bytes": "lii",

@@ -60,6 +60,9 @@ _grid_cache = {}
 REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
 # reduce6: weight-row gathers of RB 4-entry rounds in flight per wave (0 = reduce5)
 REDUCE_RB = int(os.environ.get("PAGEVEC_REDUCE_RB", "0"))
+# reduce7: compile-time dropout mode + packed FMAs (5 = reduce5); same process at the bench
+# shape 0.468 vs 0.558 ms (tools/reduce_ab.py), headline step 7.72-7.79 vs 7.79-7.83 ms
+REDUCE_V = int(os.environ.get("PAGEVEC_REDUCE_V", "7"))
 
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
 # (both halves are gather/latency-bound and leave CU slots idle when run back to back)
@@ -240,7 +243,11 @@ class _ConvPoolFn(torch.autograd.Function):
             sort_pairs_iota(keys, skeys, svals, end_bit)
             dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
             wrow = _weight_rows(w3, w4, EP)
-            if k16 and REDUCE_RB > 0:
+            if k16 and REDUCE_V == 7 and REDUCE_RB == 0:
+                check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
+                      "pv_conv_pool_bwd_reduce7_u16")
+            elif k16 and REDUCE_RB > 0:
                 check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
                                                       L, E, V, seed, P(sp), row_offset, thr, tok, REDUCE_RB, s),
                       "pv_conv_pool_bwd_reduce6_u16")

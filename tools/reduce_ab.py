@@ -76,6 +76,10 @@ def main():
         check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7,
                                               None, 0, thr, 0, rb, s), "reduce6")
 
+    def r7(out):
+        check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7,
+                                              None, 0, thr, 0, s), "reduce7")
+
     dw3, dw4, db = torch.zeros_like(w3), torch.zeros_like(w4), torch.zeros(2 * F, device=dev)
 
     def dw():
@@ -85,6 +89,12 @@ def main():
     ref = torch.zeros(V, E, device=dev)
     r5(ref)
     torch.cuda.synchronize()
+    out7 = torch.zeros(V, E, device=dev)
+    r7(out7)
+    torch.cuda.synchronize()
+    err7 = float((out7 - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    print(json.dumps({"reduce7_rel_err_vs_reduce5": err7}), flush=True)
+    assert err7 < 1e-5, err7
     rbs = [int(x) for x in a.rb.split(",") if x]
     for rb in rbs:
         out = torch.zeros(V, E, device=dev)
@@ -94,10 +104,11 @@ def main():
         print(json.dumps({"rb": rb, "rel_err_vs_reduce5": err}), flush=True)
         assert err < 1e-5, err
     scratch = torch.zeros(V, E, device=dev)
-    res = {"reduce5": [], "dw": []}
+    res = {"reduce5": [], "reduce7": [], "dw": []}
     res.update({f"reduce6_rb{rb}": [] for rb in rbs})
     for _ in range(a.rounds):
         res["reduce5"].append(ev_time(lambda: r5(scratch), a.iters))
+        res["reduce7"].append(ev_time(lambda: r7(scratch), a.iters))
         res["dw"].append(ev_time(dw, a.iters))
         for rb in rbs:
             res[f"reduce6_rb{rb}"].append(ev_time(lambda: r6(scratch, rb), a.iters))
