@@ -128,8 +128,11 @@ def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor
 # dTable of short sequences (the query towers) from per-sample dense dX rows (N*L rows sorted by
 # token) instead of N*1050 (f, j) entries through emit -> sort -> reduce.  Same-process A/B
 # (tools/qbwd_micro.py, whole conv backward incl. dW): 4096 x 45 0.445 vs 0.459 ms, but
-# 1024 x 250 0.293 vs 0.265 ms — so only up to DENSE_DX_MAXL tokens.  PAGEVEC_DENSE_DX=0: off.
-DENSE_DX = os.environ.get("PAGEVEC_DENSE_DX", "1") != "0"
+# 1024 x 250 0.293 vs 0.265 ms — so only up to DENSE_DX_MAXL tokens.  Since the faster
+# reduce7 / templated dW kernels the entry path wins for the headline query tower too
+# (same box, headline step 7.637 / 7.595 vs 7.650 / 7.638 ms), so the dense-dX path is
+# now opt-in: PAGEVEC_DENSE_DX=1.
+DENSE_DX = os.environ.get("PAGEVEC_DENSE_DX", "0") != "0"
 DENSE_DX_MAXL = 64
 
 

@@ -24,7 +24,11 @@ def test_native_hip_library_loaded():
 
 @pytest.mark.parametrize("N,L,p,mode", [(8, 37, 0.0, "element"), (5, 130, 0.25, "element"), (3, 64, 0.25, "token"),
                                         (6, 4, 0.0, "element"), (300, 45, 0.25, "element"),
-                                        (12, 5000, 0.25, "element")])  # char-level page length
+                                        (12, 5000, 0.25, "element"),  # char-level page length
+                                        # long-sequence table reduce (reduce7) and dW in every
+                                        # compile-time dropout mode: off, element p = 0.3, token
+                                        (5, 130, 0.0, "element"), (5, 130, 0.3, "element"),
+                                        (4, 130, 0.25, "token")])
 def test_conv_pool_fwd_bwd(N, L, p, mode):
     torch.manual_seed(0)
     V, E, F = 97, 100, 150
@@ -62,11 +66,13 @@ def test_conv_pool_fwd_bwd(N, L, p, mode):
         torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("variant", [5, 7])
 @pytest.mark.parametrize("epw", [64, 512, 1024])
-def test_dtable_reduce_long_runs_match_reduce4(epw):
-    """reduce5 (a wave walks epw sorted entries, runs carried across 64-entry sub-chunks)
-    equals the 64-entry reduce4 kernel on Zipf-skewed ids whose hottest rows span many
-    sub-chunks and waves (fp32 atomics: equal up to summation order)."""
+def test_dtable_reduce_long_runs_match_reduce4(epw, variant):
+    """reduce5 / reduce7 (a wave walks epw sorted entries, runs carried across 64-entry
+    sub-chunks; reduce7 with packed FMAs) equal the 64-entry reduce4 kernel on Zipf-skewed
+    ids whose hottest rows span many sub-chunks and waves (fp32 atomics and FMA vs mul + add:
+    equal up to rounding)."""
     torch.manual_seed(1)
     V, E, F, N, L = 500, 100, 150, 64, 300
     ranks = torch.arange(1, V, dtype=torch.float64)
@@ -76,7 +82,8 @@ def test_dtable_reduce_long_runs_match_reduce4(epw):
     w3, w4 = bf(torch.randn(F, 3, E, device=DEV) * 0.1), bf(torch.randn(F, 4, E, device=DEV) * 0.1)
     b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
     grads = []
-    saved = cops.REDUCE_EPW
+    saved, saved_v = cops.REDUCE_EPW, cops.REDUCE_V
+    cops.REDUCE_V = variant
     try:
         for e in (0, epw):
             cops.REDUCE_EPW = e
@@ -85,8 +92,8 @@ def test_dtable_reduce_long_runs_match_reduce4(epw):
             (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
             grads.append(t.grad)
     finally:
-        cops.REDUCE_EPW = saved
-    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-5)
+        cops.REDUCE_EPW, cops.REDUCE_V = saved, saved_v
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=3e-5)
     assert grads[0].abs().sum() > 0
 
 
