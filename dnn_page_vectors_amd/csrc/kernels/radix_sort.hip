@@ -16,6 +16,7 @@
 // Layout of the temp buffer: key ping-pong copy (n keys), value copy (n u32), hist
 // (256 x tiles u32, digit-major), totals (256 u32).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pv {
 namespace rsort {
@@ -211,7 +212,15 @@ __host__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Items per thread: 16 (4096-item tiles) for large sorts; small ones (the sparse bag
 // backward's ~200k keys) use 1024-item tiles so the grid still covers the CUs.
-__host__ inline int pick_ipt(long n) { return n <= (1L << 20) ? 4 : IPT; }
+// PAGEVEC_RSORT_IPT / pv_rsort_set_ipt: 4, 16 or 32 for every size (A/B; 0 = this rule).
+inline int g_ipt_override = [] {
+  const char* e = getenv("PAGEVEC_RSORT_IPT");
+  return e ? atoi(e) : 0;
+}();
+__host__ inline int pick_ipt(long n) {
+  if (g_ipt_override == 4 || g_ipt_override == 16 || g_ipt_override == 32) return g_ipt_override;
+  return n <= (1L << 20) ? 4 : IPT;
+}
 
 __host__ inline Layout layout(long n, int end_bit, int key_bytes) {
   Layout L{};
@@ -254,11 +263,16 @@ int sort_impl(void* temp, long temp_bytes, const KT* keys_in, KT* keys_out, cons
     unsigned* vout = to_out ? vals_out : vtmp;
     if (pick_ipt(n) == 4)
       hipLaunchKernelGGL((rs_count_kernel<KT, 4>), dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
+    else if (pick_ipt(n) == 32)
+      hipLaunchKernelGGL((rs_count_kernel<KT, 32>), dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
     else
       hipLaunchKernelGGL((rs_count_kernel<KT, IPT>), dim3(L.nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, L.nb);
     hipLaunchKernelGGL(rs_scan_kernel, dim3(RADIX), dim3(BT), 0, st, hist, L.nb, totals);
     if (pick_ipt(n) == 4)
       hipLaunchKernelGGL((rs_scatter_kernel<KT, 4>), dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift,
+                         nbits, (const unsigned*)hist, (const unsigned*)totals, L.nb);
+    else if (pick_ipt(n) == 32)
+      hipLaunchKernelGGL((rs_scatter_kernel<KT, 32>), dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift,
                          nbits, (const unsigned*)hist, (const unsigned*)totals, L.nb);
     else
       hipLaunchKernelGGL((rs_scatter_kernel<KT, IPT>), dim3(L.nb), dim3(BT), 0, st, kin, vin, kout, vout, n, shift,
@@ -274,6 +288,8 @@ int sort_impl(void* temp, long temp_bytes, const KT* keys_in, KT* keys_out, cons
 }  // namespace pv
 
 using namespace pv;
+
+PV_API void pv_rsort_set_ipt(int ipt) { pv::rsort::g_ipt_override = ipt; }
 
 PV_API long pv_rsort_temp_bytes(long n, int end_bit, int key_bytes) {
   return (long)pv::rsort::layout(n, end_bit, key_bytes).bytes;

@@ -37,6 +37,7 @@ SIGS = {
     "pv_conv_pool_bwd_reduce7_u16": "ppppp" "liiii" "upuii" "p",
     "pv_sort_iota_u32": "plppp" "li" "p",
     # radix_sort.hip
+    "pv_rsort_set_ipt": "i",
     "pv_rsort_temp_bytes": "lii",
     "pv_rsort_pairs": "plpppp" "lii" "p",
     # w2v.hip

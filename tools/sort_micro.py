@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--M", type=int, nargs="*", default=[17_203_200, 4_300_800])
     ap.add_argument("--end-bit", type=int, default=15)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--ipt", type=int, nargs="*", default=[4, 16, 32], help="forced items-per-thread arms")
     a = ap.parse_args()
     dev = torch.device("cuda")
     for M in a.M:
@@ -29,18 +30,36 @@ def main():
         skeys = torch.empty_like(keys)
         svals = torch.empty(M, dtype=torch.int32, device=dev)
         res = {}
-        for impl in ("rsort", "rocprim"):
-            cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=impl)  # warm
-        torch.cuda.synchronize()
-        times = {"rsort": [], "rocprim": []}
+        lib = cops.lib()
+        ref_k = ref_v = None
+        arms = ["rsort", "rocprim"] + [f"rsort_ipt{i}" for i in a.ipt]
+
+        def run(arm):
+            if arm.startswith("rsort_ipt"):
+                lib.pv_rsort_set_ipt(int(arm[9:]))
+                try:
+                    cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl="rsort")
+                finally:
+                    lib.pv_rsort_set_ipt(0)
+            else:
+                cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=arm)
+
+        for arm in arms:
+            run(arm)  # warm + every arm must give the same (stable) result
+            torch.cuda.synchronize()
+            if ref_k is None:
+                ref_k, ref_v = skeys.clone(), svals.clone()
+            else:
+                assert torch.equal(skeys, ref_k) and torch.equal(svals, ref_v), arm
+        times = {arm: [] for arm in arms}
         for _ in range(a.iters):
-            for impl in ("rsort", "rocprim"):
+            for arm in arms:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=impl)
+                run(arm)
                 e1.record()
                 e1.synchronize()
-                times[impl].append(e0.elapsed_time(e1))
+                times[arm].append(e0.elapsed_time(e1))
         for impl, t in times.items():
             t.sort()
             res[impl + "_ms_median"] = round(t[len(t) // 2], 4)
