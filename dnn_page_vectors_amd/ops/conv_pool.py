@@ -165,11 +165,14 @@ class _ConvPoolFn(torch.autograd.Function):
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
+        ctx.set_materialize_grads(False)  # no zero-filled (N, 300) int gradient for argmax
         ctx.params = (table, w3, w4)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return pooled, argmax
 
     @staticmethod
     def backward(ctx, gpool, _gargmax):
+        if gpool is None:
+            return (None,) * 12
         ids, pooled, argmax, tbl16, w3, w4 = ctx.saved_tensors
         V, E, seed, row_offset, thr, tok, scale, sp = ctx.meta
         N, L = ids.shape

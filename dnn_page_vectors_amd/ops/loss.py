@@ -44,10 +44,13 @@ class _ExplicitFn(torch.autograd.Function):
                                      int(clip), stream(q.device)), "pv_dssm_explicit")
         ctx.save_for_backward(dq, dd)
         ctx.mark_non_differentiable(prob)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for prob / acc
         return loss, prob
 
     @staticmethod
     def backward(ctx, gl, _gp):
+        if gl is None:
+            return None, None, None, None
         dq, dd = ctx.saved_tensors
         g = gl.contiguous().float()
         return dq * g[:, None], dd * g[:, None, None], None, None
@@ -149,6 +152,7 @@ class _InBatchFn(torch.autograd.Function):
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
         ctx.reduce = bool(reduce)
         ctx.mark_non_differentiable(prob)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for prob / acc
         if reduce:
             lm, acc = _loss_stats(loss, prob)
             ctx.mark_non_differentiable(acc)
@@ -157,6 +161,8 @@ class _InBatchFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gl, _gp, _ga=None):
+        if gl is None:  # materialize_grads is off: the loss output was not used
+            return (None,) * len(ctx.needs_input_grad)
         qb, db, pos, sumexp, U = ctx.saved_tensors
         B, M, D, DP, gamma, clip = ctx.meta
         s = stream(qb.device)
@@ -249,6 +255,7 @@ class _CrossGpuFn(torch.autograd.Function):
         pos = (pos_local + rank * n).contiguous()
         loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
         ctx.mark_non_differentiable(prob)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for prob / acc
         # the backward scores the LOCAL pages against ALL ranks' queries (dD needs no
         # cross-rank sum then): gather the bf16 queries now, in flight during the rest of
         # the forward and the tower's own backward (B*DP*2 bytes per rank)
@@ -268,6 +275,8 @@ class _CrossGpuFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gl, _gp, _ga=None):
+        if gl is None:  # materialize_grads is off: the loss output was not used
+            return (None,) * len(ctx.needs_input_grad)
         qb, db, dbl, pos_local, sumexp, U = ctx.saved_tensors
         B, M, n, D, DP, gamma, clip, group, W = ctx.meta
         s = stream(qb.device)
