@@ -861,6 +861,33 @@ PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* o
   return 0;
 }
 
+// Backward weight rows: bf16 [2*FW][4][EP] (k=3 filters' 4th row and columns >= E zero), the
+// operand of the sparse dTable kernels (conv_pool_bwd.hip) -- one launch instead of a
+// zero fill + two strided copies.
+__global__ void conv_weight_rows_kernel(const float* __restrict__ w3, const float* __restrict__ w4, int E,
+                                        unsigned short* __restrict__ out) {
+  using namespace pv::convpool;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // element of [2*FW][4][EP]
+  if (i >= 2 * FW * 4 * EP) return;
+  const int e = i % EP, j = (i / EP) % 4, f = i / (4 * EP);
+  float x = 0.f;
+  if (e < E) {
+    if (f < FW) x = j < 3 ? w3[((size_t)f * 3 + j) * E + e] : 0.f;
+    else x = w4[((size_t)(f - FW) * 4 + j) * E + e];
+  }
+  out[i] = f32_to_bf16(x);
+}
+
+PV_API int pv_conv_weight_rows(const float* w3, const float* w4, int E, void* out, void* stream) {
+  using namespace pv::convpool;
+  if (E > EP) return -1;
+  const int n = 2 * FW * 4 * EP;
+  hipLaunchKernelGGL(conv_weight_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w3, w4, E,
+                     (unsigned short*)out);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
 PV_API int pv_conv_packed_size() {
   using namespace pv::convpool;
   return (NT * S3 + NT * S4 + S4) * 64 * 8;  // bf16 elements

@@ -10,6 +10,7 @@ _T = {"p": ctypes.c_void_p, "i": ctypes.c_int, "u": ctypes.c_uint, "l": ctypes.c
 SIGS = {
     # conv_pool_fwd.hip
     "pv_conv_pack_weights": "ppipp",
+    "pv_conv_weight_rows": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
     # det.hip (deterministic reduction mode, ops/determinism.py)

@@ -139,6 +139,11 @@ DENSE_DX_MAXL = 64
 def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
     """bf16 weight rows [2*FW][4][EP] (zero padded): the operands the forward MFMAs used."""
     F, _, E = w3.shape
+    if w3.is_cuda and F == FW and ep == EP and w3.dtype == torch.float32 and w4.dtype == torch.float32:
+        wrow = torch.empty(2 * F, 4, ep, dtype=torch.bfloat16, device=w3.device)  # one launch
+        check(lib().pv_conv_weight_rows(P(w3.detach().contiguous()), P(w4.detach().contiguous()), E, P(wrow),
+                                        stream(w3.device)), "pv_conv_weight_rows")
+        return wrow
     wrow = torch.zeros(2 * F, 4, ep, dtype=torch.bfloat16, device=w3.device)
     wrow[:F, :3, :E] = w3.detach()
     wrow[F:, :, :E] = w4.detach()

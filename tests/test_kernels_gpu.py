@@ -1213,3 +1213,17 @@ def test_bert_residual_link_matches_autograd_sum(monkeypatch):
         a, b = grads[0][n].float(), grads[1][n].float()
         err = float((a - b).abs().max() / a.abs().max().clamp_min(1e-12))
         assert err < 3e-2, (n, err)
+
+
+def test_conv_weight_rows_kernel_matches_torch_layout():
+    """pv_conv_weight_rows (one launch) == the zero-filled [2F][4][EP] bf16 layout built with
+    torch ops (the backward's dTable operand)."""
+    torch.manual_seed(3)
+    F, E = 150, 100
+    w3 = torch.randn(F, 3, E, device=DEV)
+    w4 = torch.randn(F, 4, E, device=DEV)
+    got = cops._weight_rows(w3, w4, cops.EP)
+    ref_rows = torch.zeros(2 * F, 4, cops.EP, dtype=torch.bfloat16, device=DEV)
+    ref_rows[:F, :3, :E] = w3
+    ref_rows[F:, :, :E] = w4
+    assert torch.equal(got, ref_rows)
