@@ -58,6 +58,54 @@ __global__ void quant_fp8_kernel(const float* __restrict__ x, const float* __res
   }
 }
 
+// Fill-free pair (quantize() in ops/fp8.py): amax_part_kernel writes one max per block
+// (no atomics, so the scalar needs no zero fill launch first); quant_part_kernel reduces
+// the <= AMAX_PARTS partials in every block (L2-resident, 2 KB), block 0 also stores the
+// scalar amax the fp8 GEMM's dequantisation reads.
+constexpr int AMAX_PARTS = 512;
+
+__global__ __launch_bounds__(256) void amax_part_kernel(const float* __restrict__ x, long n,
+                                                        float* __restrict__ parts, int aligned) {
+  __shared__ float sh[4];
+  const long n4 = aligned ? n / 4 : 0;
+  const long stride = (long)gridDim.x * blockDim.x;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+}
+
+__global__ __launch_bounds__(256) void quant_part_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ parts, int nparts,
+                                                         float* __restrict__ amax_out, unsigned* __restrict__ out,
+                                                         long n4) {
+  __shared__ float sh[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) m = fmaxf(m, parts[i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const float amax = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *amax_out = amax;
+  const float s = 448.f / fmaxf(amax, 1e-12f);
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    unsigned w = 0;
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * s, -448.f), 448.f), fminf(fmaxf(v[1] * s, -448.f), 448.f),
+                                        w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * s, -448.f), 448.f), fminf(fmaxf(v[3] * s, -448.f), 448.f),
+                                        w, true);
+    out[i] = w;
+  }
+}
+
 __device__ __forceinline__ float act_fn(float x, int act) {
   if (act == 1) return x > 0.f ? x : 0.f;
   if (act == 3) return tanhf(x);
@@ -153,6 +201,27 @@ PV_API int pv_amax(const float* x, long n, float* amax, void* stream) {
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(pv::fp8::amax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, amax,
                      aligned);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// x (n fp32, 16-byte aligned, n % 4 == 0) -> out (n e4m3 bytes) and *amax_out; ws: at
+// least AMAX_PARTS floats of scratch (uninitialised is fine).  Two launches, no fill.
+PV_API int pv_amax_quant_fp8(const float* x, long n, float* ws, float* amax_out, void* out, void* stream) {
+  using namespace pv::fp8;
+  if (n % 4 || (reinterpret_cast<uintptr_t>(x) & 15)) return -1;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > AMAX_PARTS) blocks = AMAX_PARTS;
+  if (blocks < 1) blocks = 1;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(amax_part_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, ws, 1);
+  PV_LAUNCH_CHECK();
+  const long n4 = n / 4;
+  long qb = (n4 + 255) / 256;
+  if (qb > 4096) qb = 4096;
+  if (qb < 1) qb = 1;
+  hipLaunchKernelGGL(quant_part_kernel, dim3((unsigned)qb), dim3(256), 0, st, x, (const float*)ws, (int)blocks,
+                     amax_out, (unsigned*)out, n4);
   PV_LAUNCH_CHECK();
   return 0;
 }

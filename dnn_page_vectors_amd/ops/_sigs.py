@@ -81,6 +81,7 @@ SIGS = {
     "pv_softmax_bwd": "pp" "lif" "p",
     # fp8.hip
     "pv_amax": "plpp",
+    "pv_amax_quant_fp8": "plppp" "p",
     "pv_quant_fp8": "ppp" "l" "p",
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip

@@ -15,6 +15,7 @@ import torch
 from ._common import P, check, lib, stream, use_hip
 
 FP8_MAX = 448.0
+AMAX_PARTS = 512  # fp8.hip::AMAX_PARTS
 _ACT = {"none": 0, "relu": 1, "tanh": 3}
 
 
@@ -23,13 +24,14 @@ def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     x = x.contiguous().float()
     if x.data_ptr() % 16:  # the quantiser reads 16-byte vectors
         x = x.clone()
-    amax = torch.zeros(1, dtype=torch.float32, device=x.device)
     n = x.numel()
-    check(lib().pv_amax(P(x), n, P(amax), stream(x.device)), "pv_amax")
-    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     if n % 4:
         raise ValueError("fp8 quantisation needs numel % 4 == 0")
-    check(lib().pv_quant_fp8(P(x), P(amax), P(q), n, stream(x.device)), "pv_quant_fp8")
+    # per-block partial maxima + the scalar in one uninitialised buffer: no zero-fill launch
+    ws = torch.empty(AMAX_PARTS + 1, dtype=torch.float32, device=x.device)
+    amax = ws[AMAX_PARTS:]
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    check(lib().pv_amax_quant_fp8(P(x), n, P(ws), P(amax), P(q), stream(x.device)), "pv_amax_quant_fp8")
     return q, amax
 
 
