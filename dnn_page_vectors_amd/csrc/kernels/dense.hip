@@ -203,8 +203,9 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
 }
 
 // dz = dy * act'(y) (in place allowed); relu: y > 0 ; tanh: 1 - y^2 ; none: 1
+// dz16 (optional): also a bf16 copy of dz, the operand of the bf16 backward GEMMs
 __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy, float* __restrict__ dz,
-                               long n, int act) {
+                               long n, int act, unsigned short* __restrict__ dz16) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long stride = (long)gridDim.x * blockDim.x;
   for (; i < n; i += stride) {
@@ -212,6 +213,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ y, const float* __restr
     if (act == ACT_RELU) g = y[i] > 0.f ? g : 0.f;
     else if (act == ACT_TANH) g = g * (1.f - y[i] * y[i]);
     dz[i] = g;
+    if (dz16) dz16[i] = f32_to_bf16(g);
   }
 }
 
@@ -335,7 +337,20 @@ PV_API int pv_act_bwd(const float* y, const float* dy, float* dz, long n, int ac
   long blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, n, act);
+  hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, n, act,
+                     (unsigned short*)nullptr);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// act_bwd writing dz (fp32) AND its bf16 copy dz16 in one pass
+PV_API int pv_act_bwd2(const float* y, const float* dy, float* dz, void* dz16, long n, int act, void* stream) {
+  using namespace pv::dense;
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz, n, act,
+                     (unsigned short*)dz16);
   PV_LAUNCH_CHECK();
   return 0;
 }

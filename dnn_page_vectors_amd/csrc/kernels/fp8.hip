@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void amax_part_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void quant_part_kernel(const float* __restrict__ x,
                                                          const float* __restrict__ parts, int nparts,
                                                          float* __restrict__ amax_out, unsigned* __restrict__ out,
-                                                         long n4) {
+                                                         long n4, uint2* __restrict__ x16) {
   __shared__ float sh[4];
   float m = 0.f;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) m = fmaxf(m, parts[i]);
@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void quant_part_kernel(const float* __restrict
     w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * s, -448.f), 448.f), fminf(fmaxf(v[3] * s, -448.f), 448.f),
                                         w, true);
     out[i] = w;
+    if (x16) x16[i] = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};  // bf16 copy for the backward
   }
 }
 
@@ -207,7 +208,8 @@ PV_API int pv_amax(const float* x, long n, float* amax, void* stream) {
 
 // x (n fp32, 16-byte aligned, n % 4 == 0) -> out (n e4m3 bytes) and *amax_out; ws: at
 // least AMAX_PARTS floats of scratch (uninitialised is fine).  Two launches, no fill.
-PV_API int pv_amax_quant_fp8(const float* x, long n, float* ws, float* amax_out, void* out, void* stream) {
+PV_API int pv_amax_quant_fp8(const float* x, long n, float* ws, float* amax_out, void* out, void* out16,
+                             void* stream) {
   using namespace pv::fp8;
   if (n % 4 || (reinterpret_cast<uintptr_t>(x) & 15)) return -1;
   long blocks = (n / 4 + 255) / 256;
@@ -221,7 +223,7 @@ PV_API int pv_amax_quant_fp8(const float* x, long n, float* ws, float* amax_out,
   if (qb > 4096) qb = 4096;
   if (qb < 1) qb = 1;
   hipLaunchKernelGGL(quant_part_kernel, dim3((unsigned)qb), dim3(256), 0, st, x, (const float*)ws, (int)blocks,
-                     amax_out, (unsigned*)out, n4);
+                     amax_out, (unsigned*)out, n4, (uint2*)out16);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -47,6 +47,7 @@ SIGS = {
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
     "pv_l2norm_bwd": "ppppp" "ii" "p",
+    "pv_act_bwd2": "ppppl" "ip",
     "pv_act_bwd": "ppp" "li" "p",
     # loss.hip
     "pv_dssm_explicit": "pppppp" "iii" "ffi" "p",
@@ -81,7 +82,7 @@ SIGS = {
     "pv_softmax_bwd": "pp" "lif" "p",
     # fp8.hip
     "pv_amax": "plpp",
-    "pv_amax_quant_fp8": "plppp" "p",
+    "pv_amax_quant_fp8": "plppp" "pp",
     "pv_quant_fp8": "ppp" "l" "p",
     "pv_fp8_linear": "ppppppp" "iiii" "p",
     # optim.hip

@@ -19,8 +19,9 @@ AMAX_PARTS = 512  # fp8.hip::AMAX_PARTS
 _ACT = {"none": 0, "relu": 1, "tanh": 3}
 
 
-def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """fp32 tensor -> (uint8 e4m3 bytes, amax device scalar)."""
+def quantize(x: torch.Tensor, with_bf16: bool = False):
+    """fp32 tensor -> (uint8 e4m3 bytes, amax device scalar); with_bf16: also a bf16 copy of
+    x written by the same pass (the operand of the bf16 weight-gradient GEMM)."""
     x = x.contiguous().float()
     if x.data_ptr() % 16:  # the quantiser reads 16-byte vectors
         x = x.clone()
@@ -31,8 +32,9 @@ def quantize(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     ws = torch.empty(AMAX_PARTS + 1, dtype=torch.float32, device=x.device)
     amax = ws[AMAX_PARTS:]
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    check(lib().pv_amax_quant_fp8(P(x), n, P(ws), P(amax), P(q), stream(x.device)), "pv_amax_quant_fp8")
-    return q, amax
+    x16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if with_bf16 else None
+    check(lib().pv_amax_quant_fp8(P(x), n, P(ws), P(amax), P(q), P(x16), stream(x.device)), "pv_amax_quant_fp8")
+    return (q, amax, x16) if with_bf16 else (q, amax)
 
 
 def _emulate(x: torch.Tensor) -> torch.Tensor:
@@ -47,12 +49,12 @@ class _FP8LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).contiguous().float()
         M, K = x2.shape
         N = w.shape[0]
-        xq, ax = quantize(x2)
+        xq, ax, x16 = quantize(x2, with_bf16=True)  # x16: the wgrad operand (no fp32 copy saved)
         w8, aw = wq if wq is not None else quantize(w.detach())
         y = torch.empty(M, N, dtype=torch.float32, device=x.device)
         check(lib().pv_fp8_linear(P(xq), P(w8), P(ax), P(aw), P(b) if b is not None else None, P(y), None, M, N, K,
                                   _ACT[act], stream(x.device)), "pv_fp8_linear")
-        ctx.save_for_backward(x2, y if act != "none" else None)
+        ctx.save_for_backward(x16, y if act != "none" else None)
         ctx.act, ctx.xshape = act, x.shape
         ctx.params = (w, b)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return y.view(*x.shape[:-1], N)
@@ -63,14 +65,17 @@ class _FP8LinearFn(torch.autograd.Function):
         from . import grad_sink
         from .transformer import weight_bf16, wgrad_f32
 
-        x2, y = ctx.saved_tensors
+        x16, y = ctx.saved_tensors
         w, b = ctx.params
         dz = dy.reshape(-1, dy.shape[-1]).contiguous().float()
-        if y is not None:  # activation mask in one kernel
+        if y is not None:  # activation mask + the bf16 copy in one kernel
             dzm = torch.empty_like(dz)
-            check(lib().pv_act_bwd(P(y), P(dz), P(dzm), dz.numel(), _ACT[ctx.act], stream(dz.device)), "pv_act_bwd")
+            dzb = torch.empty(dz.shape, dtype=torch.bfloat16, device=dz.device)
+            check(lib().pv_act_bwd2(P(y), P(dz), P(dzm), P(dzb), dz.numel(), _ACT[ctx.act], stream(dz.device)),
+                  "pv_act_bwd2")
             dz = dzm
-        dzb = dz.to(torch.bfloat16)
+        else:
+            dzb = dz.to(torch.bfloat16)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             try:
@@ -80,7 +85,7 @@ class _FP8LinearFn(torch.autograd.Function):
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             tw = grad_sink.write_target(w)
-            dw = wgrad_f32(dzb, x2.to(torch.bfloat16), out=tw)  # split-K fp32, straight into the flat grad
+            dw = wgrad_f32(dzb, x16, out=tw)  # split-K fp32, straight into the flat grad
             if tw is not None:
                 grad_sink.done(w)
                 dw = None
