@@ -224,6 +224,7 @@ def main():
             "config": {"model": MODEL_DESC[a.model],
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend,
+                       "softmax_scale": (cfg.inbatch_gamma or cfg.GAMMA) if a.loss != "explicit" else cfg.GAMMA,
                        "deterministic": bool(a.deterministic)},
             "recall_at_10": None if recall is None else round(recall, 4),
             "recall_after_steps": max(done, a.quality_steps),

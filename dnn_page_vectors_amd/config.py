@@ -106,6 +106,9 @@ class Configuration:
     # ---- training (new) ------------------------------------------------------
     loss_mode: str = "explicit"          # explicit (J negatives, parity) | in_batch | cross_gpu
     cos_clip: bool = True                 # R = clip(cos, 0, 1) as RTH/RTF (cnn_dssm_th.py:76-78)
+    # softmax scale of the in-batch / cross-GPU losses (new modes: the reference's GAMMA = 10
+    # belongs to its 4-way head); 0 = GAMMA
+    inbatch_gamma: float = 0.0
     lr: float = 1e-3                      # Keras 1 Adam defaults
     beta1: float = 0.9
     beta2: float = 0.999
@@ -291,8 +294,11 @@ def preset_config(name: str) -> Configuration:
                              cos_clip=False, lr=3e-3, J=0, num_train_samples=1024, num_validation_samples=256)
     if name in ("cdssm_ngram_bf16", "config2"):
         # CDSSM 1D-conv 300d, 30k hashed tri-grams, bf16, batch 4096 on 1 MI355X
+        # inbatch_gamma 40: the reference's GAMMA = 10 is the scale of its 4-way head; over 16k
+        # in-batch negatives it caps Recall@10 near 0.15 (profiles/quality_r2_final.md:
+        # 2000 steps, gamma 10 / 20 / 40 / 80 -> Recall@10 0.15 / 0.29 / 0.35 / 0.37)
         return Configuration(model="cdssm", feature_level="ngram", vocab_hash_size=30000,
-                             batch_size=4096, dtype="bf16", loss_mode="cross_gpu")
+                             batch_size=4096, dtype="bf16", loss_mode="cross_gpu", inbatch_gamma=40.0)
     if name in ("mlp_xgpu", "config3"):
         # Two-tower MLP 512-512-128, cross-GPU in-batch negatives via all-gather
         return Configuration(model="mlp", feature_level="ngram", vocab_hash_size=30000,

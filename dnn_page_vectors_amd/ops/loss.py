@@ -308,6 +308,19 @@ def _reduce_rows(loss: torch.Tensor, prob: torch.Tensor):
     return loss.mean(), prob, (prob > 0.5).float().mean()
 
 
+# The in-batch kernels shift every logit by the largest possible one (gamma; no running max):
+# exp(gamma * (S - 1)) must stay a normal fp32 for the lowest S (0 with the clip, -1 without),
+# i.e. gamma * span <= ~87.  Larger scales would underflow whole rows to 0 (log 0 = -inf).
+MAX_LOGIT_SPAN = 80.0
+
+
+def _check_gamma(gamma: float, clip: bool) -> None:
+    span = float(gamma) * (1.0 if clip else 2.0)
+    if span > MAX_LOGIT_SPAN:
+        raise ValueError(f"in-batch softmax scale {gamma} too large (gamma * logit span {span:.0f} > "
+                         f"{MAX_LOGIT_SPAN:.0f}: exp underflows in fp32)")
+
+
 def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, gamma: float, clip: bool = True,
                    group=None, gathered: Optional[PageGather] = None, reduce: bool = False):
     """qn (B, D) and the LOCAL page vectors dn (n, D), normalised; pos_local (B,) indexes dn.
@@ -315,6 +328,7 @@ def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, 
     ``gathered``: the PageGather started on ``dn`` right after the doc tower.
     -> (per-row loss, P+); ``reduce``: (mean loss, P+, accuracy), the mean and metric
     computed in the loss kernels' epilogue (no separate reductions)."""
+    _check_gamma(gamma, clip)
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return inbatch_loss(qn, dn, pos_local, gamma, clip, reduce=reduce)
     if use_hip(qn, dn) and qn.shape[1] <= 192:
@@ -331,6 +345,7 @@ def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, ga
                  reduce: bool = False):
     """qn (B, D), dn (M, D) normalised; pos_index (B,) -> (per-row loss, P_pos);
     ``reduce``: (mean loss, P_pos, accuracy)."""
+    _check_gamma(gamma, clip)
     if use_hip(qn, dn):
         if qn.shape[1] > 192:
             out = _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip))

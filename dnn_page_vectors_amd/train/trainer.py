@@ -167,12 +167,13 @@ class Trainer:
             loss = per_row.mean()
         elif cfg.loss_mode in ("in_batch", "cross_gpu"):
             pos = self._pos_cache(B, S, q.device)
+            gamma = float(getattr(cfg, "inbatch_gamma", 0.0) or cfg.GAMMA)
             # mean loss and accuracy straight from the loss kernels (reduce=True)
             if cfg.loss_mode == "cross_gpu" and self.info.enabled:
-                loss, P, self._acc = lops.cross_gpu_loss(qn, dn, pos, cfg.GAMMA, clip, gathered=pre.get("gather"),
+                loss, P, self._acc = lops.cross_gpu_loss(qn, dn, pos, gamma, clip, gathered=pre.get("gather"),
                                                          reduce=True)
             else:
-                loss, P, self._acc = lops.inbatch_loss(qn, dn, pos, cfg.GAMMA, clip, reduce=True)
+                loss, P, self._acc = lops.inbatch_loss(qn, dn, pos, gamma, clip, reduce=True)
         else:
             raise ValueError(f"unknown loss_mode {cfg.loss_mode!r}")
         range_pop()

@@ -128,3 +128,28 @@ def test_lazy_embedding_adam_keeps_untouched_rows(tmp_path):
         assert not torch.equal(emb.detach()[1:100], after1[1:100])
         assert not torch.equal(tr.model.doc_towers[0].conv_w[0].detach(), conv1)
     assert moved[True] == 0.0 and moved[False] > 0.0, moved
+
+
+def test_inbatch_gamma_overrides_gamma_for_inbatch_losses_only():
+    """cfg.inbatch_gamma is the softmax scale of the in-batch / cross-GPU losses (new modes);
+    the reference's GAMMA keeps driving the explicit 1 + J head."""
+    pdist.set_info(pdist.DistInfo(device=torch.device("cpu")))
+    g = torch.Generator().manual_seed(2)
+    q = torch.randint(1, 300, (8, 12), generator=g, dtype=torch.int32)
+    d = torch.randint(1, 300, (8, 4, 30), generator=g, dtype=torch.int32)
+    base = dict(feature_level="ngram", vocab_hash_size=300, query_length=12, document_length=30, batch_size=8,
+                embedding_dim=24, hidden_dims=32, cos_clip=False)
+    losses = {}
+    for name, kw in {"ib_override": dict(loss_mode="in_batch", inbatch_gamma=40.0),
+                     "ib_gamma": dict(loss_mode="in_batch", GAMMA=40.0),
+                     "ib_default": dict(loss_mode="in_batch"),
+                     "ex_override": dict(loss_mode="explicit", inbatch_gamma=40.0),
+                     "ex_default": dict(loss_mode="explicit")}.items():
+        torch.manual_seed(0)
+        cfg = Configuration(**base, **kw)
+        tr = Trainer(cfg, CDSSM(cfg, 300), torch.device("cpu"))
+        with torch.no_grad():
+            losses[name] = float(tr.compute_loss(q, d, seed=3)[0])
+    assert losses["ib_override"] == losses["ib_gamma"]
+    assert losses["ib_override"] != losses["ib_default"]
+    assert losses["ex_override"] == losses["ex_default"]
