@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops import dense as dops
 from .base import TwoTowerModel
 from .mlp_dssm import MLPTower
 
@@ -54,5 +55,5 @@ class ChunkedPageEncoder(TwoTowerModel):
             ids = torch.nn.functional.pad(ids, (0, pad))
         chunks = ids.reshape(N * C, self.chunk_len)
         v = self.doc_towers[0](chunks, cache.get("doc0")).view(N, C, -1)
-        live = (chunks != 0).any(dim=1).view(N, C, 1).to(v.dtype)
-        return (v * live).sum(1) / live.sum(1).clamp(min=1.0)
+        # masked mean over the non-empty chunks (one fused HIP kernel per direction on GPU)
+        return dops.chunk_mean_pool(v, ids.reshape(N, C * self.chunk_len), self.chunk_len)

@@ -13,6 +13,9 @@ SIGS = {
     "pv_conv_weight_rows": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
+    # chunkpool.hip (chunked long-page encoder, models/chunked.py)
+    "pv_chunk_mean_fwd": "pp" "iiii" "pp" "p",
+    "pv_chunk_mean_bwd": "pp" "iii" "p" "p",
     # det.hip (deterministic reduction mode, ops/determinism.py)
     "pv_set_deterministic": "i",
     "pv_get_deterministic": "",

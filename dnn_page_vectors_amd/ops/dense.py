@@ -192,3 +192,38 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
     if use_hip(x):
         return _L2NormFn.apply(x)
     return ref.l2_normalize(x)
+
+
+class _ChunkMeanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v, ids, C, CL):
+        N, _, D = v.shape
+        vc = v.contiguous().float()
+        idc = ids.contiguous()
+        out = torch.empty(N, D, dtype=torch.float32, device=v.device)
+        scale = torch.empty(N, C, dtype=torch.float32, device=v.device)
+        check(lib().pv_chunk_mean_fwd(P(vc), P(idc), N, C, CL, D, P(out), P(scale), stream(v.device)),
+              "pv_chunk_mean_fwd")
+        ctx.save_for_backward(scale)
+        ctx.shape = (N, C, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (scale,) = ctx.saved_tensors
+        N, C, D = ctx.shape
+        dv = torch.empty(N, C, D, dtype=torch.float32, device=g.device)
+        check(lib().pv_chunk_mean_bwd(P(g.contiguous().float()), P(scale), N, C, D, P(dv), stream(g.device)),
+              "pv_chunk_mean_bwd")
+        return dv, None, None, None
+
+
+def chunk_mean_pool(v: torch.Tensor, ids: torch.Tensor, chunk_len: int) -> torch.Tensor:
+    """v (N, C, D) chunk vectors, ids (N, C * chunk_len) token ids (0 = padding) -> the mean of
+    the non-empty chunks' vectors (N, D); a page with no non-empty chunk gets zeros.  GPU: one
+    fused kernel per direction (chunkpool.hip); CPU: the torch expression."""
+    N, C, D = v.shape
+    if use_hip(v, ids) and ids.dtype == torch.int32 and C <= 64 and ids.shape[1] == C * chunk_len:
+        return _ChunkMeanFn.apply(v, ids, C, int(chunk_len))
+    live = (ids.reshape(N, C, chunk_len) != 0).any(dim=2).unsqueeze(2).to(v.dtype)
+    return (v * live).sum(1) / live.sum(1).clamp(min=1.0)

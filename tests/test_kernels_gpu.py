@@ -1227,3 +1227,27 @@ def test_conv_weight_rows_kernel_matches_torch_layout():
     ref_rows[:F, :3, :E] = w3
     ref_rows[F:, :, :E] = w4
     assert torch.equal(got, ref_rows)
+
+
+@pytest.mark.parametrize("CL", [512, 7])
+def test_chunk_mean_pool_matches_torch(CL):
+    """chunkpool.hip masked mean over non-empty chunks (fwd + bwd) == the torch expression,
+    with empty chunks and a page whose chunks are all padding."""
+    torch.manual_seed(5)
+    N, C, D = 6, 8, 128
+    ids = torch.randint(1, 1000, (N, C * CL), dtype=torch.int32, device=DEV)
+    ids.view(N, C, CL)[1, 3] = 0          # one empty chunk
+    ids.view(N, C, CL)[2, 5:] = 0         # trailing empty chunks
+    ids[4] = 0                            # an all-padding page -> zeros
+    ids.view(N, C, CL)[0, 2, :-1] = 0     # one non-pad id keeps a chunk alive
+    v = torch.randn(N, C, D, device=DEV, requires_grad=True)
+    out = dops.chunk_mean_pool(v, ids, CL)
+    live = (ids.view(N, C, CL) != 0).any(dim=2).unsqueeze(2).float()
+    v2 = v.detach().clone().requires_grad_(True)
+    ref_out = (v2 * live).sum(1) / live.sum(1).clamp(min=1.0)
+    torch.testing.assert_close(out, ref_out, rtol=1e-5, atol=1e-6)
+    g = torch.randn(N, D, device=DEV)
+    (out * g).sum().backward()
+    (ref_out * g).sum().backward()
+    torch.testing.assert_close(v.grad, v2.grad, rtol=1e-5, atol=1e-6)
+    assert torch.all(out[4] == 0)
