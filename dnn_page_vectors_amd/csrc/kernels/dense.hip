@@ -343,6 +343,38 @@ PV_API int pv_act_bwd(const float* y, const float* dy, float* dz, long n, int ac
   return 0;
 }
 
+// Bag-mean backward prologue in one pass: dz = dy * act'(y) (fp32, for the bias column sum;
+// y may be null = no activation) and dz16 = bf16(dz / max(1, lens[row])) (the per-bag 1/len
+// of the mean folded in; lens null = sum bags), rows of E columns.
+__global__ void act_bwd_rowscale_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                        float* __restrict__ dz, unsigned short* __restrict__ dz16,
+                                        const float* __restrict__ lens, long E, long n, int act) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    float g = dy[i];
+    if (y) {
+      if (act == pv::dense::ACT_RELU) g = y[i] > 0.f ? g : 0.f;
+      else if (act == pv::dense::ACT_TANH) g = g * (1.f - y[i] * y[i]);
+    }
+    if (dz) dz[i] = g;
+    const float s = lens ? 1.f / fmaxf(lens[i / E], 1.f) : 1.f;
+    dz16[i] = f32_to_bf16(g * s);
+  }
+}
+
+PV_API int pv_act_bwd_rowscale(const float* y, const float* dy, float* dz, void* dz16, const float* lens, long E,
+                               long n, int act, void* stream) {
+  using namespace pv::dense;
+  if (E < 1 || n < 1 || !dz16) return -1;
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(act_bwd_rowscale_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, dy, dz,
+                     (unsigned short*)dz16, lens, E, n, act);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
 // act_bwd writing dz (fp32) AND its bf16 copy dz16 in one pass
 PV_API int pv_act_bwd2(const float* y, const float* dy, float* dz, void* dz16, long n, int act, void* stream) {
   using namespace pv::dense;

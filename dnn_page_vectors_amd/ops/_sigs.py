@@ -50,6 +50,7 @@ SIGS = {
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
     "pv_l2norm_bwd": "ppppp" "ii" "p",
+    "pv_act_bwd_rowscale": "pppp" "p" "lli" "p",
     "pv_act_bwd2": "ppppl" "ip",
     "pv_act_bwd": "ppp" "li" "p",
     # loss.hip

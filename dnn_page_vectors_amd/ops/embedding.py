@@ -122,6 +122,8 @@ class _BagFn(torch.autograd.Function):
         W, V, bias = ctx.W, ctx.V, ctx.bias
         first, lens, y = ctx.saved_tensors
         g = g.contiguous().float()
+        if ctx.sparse is None and ctx.needs_input_grad[1]:
+            return _counts_backward(ctx, g, first, lens, y)
         if y is not None:  # activation mask: dpre = dy * act'(y)
             dz = torch.empty_like(g)
             check(lib().pv_act_bwd(P(y), P(g), P(dz), g.numel(), _BAG_ACT[ctx.act], stream(g.device)), "pv_act_bwd")
@@ -165,6 +167,39 @@ class _BagFn(torch.autograd.Function):
             grad_sink.done(W)
             return None, None, None, None, None, None, db, None
         return None, (Ct @ gs).float(), None, None, None, None, db, None
+
+
+def _counts_backward(ctx, g, C, lens, y):
+    """Backward of the counts-GEMM bag (long bags): ONE prologue kernel computes the
+    activation mask, the fp32 dz for the bias column sum and bf16(dz / len) for the C^T G
+    weight-gradient GEMM (was act_bwd + clamp + reciprocal + mul + cast)."""
+    W, V, bias = ctx.W, ctx.V, ctx.bias
+    N, E = g.shape
+    want_db = bias is not None and ctx.needs_input_grad[6]
+    dz = torch.empty_like(g) if want_db else None
+    gs = torch.empty(N, E, dtype=torch.bfloat16, device=g.device)
+    check(lib().pv_act_bwd_rowscale(P(y), P(g), P(dz), P(gs), P(lens) if ctx.mean else None, E, g.numel(),
+                                    _BAG_ACT[ctx.act] if y is not None else 0, stream(g.device)),
+          "pv_act_bwd_rowscale")
+    db = None
+    if want_db:
+        tb = grad_sink.write_target(bias)
+        db = dops.colsum(dz, out=tb, accumulate=tb is not None)
+        if tb is not None:
+            grad_sink.done(bias)
+            db = None
+        elif db.dtype != bias.dtype:
+            db = db.to(bias.dtype)
+    Ct = C[:, :V].t()
+    tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
+    if tw is not None:
+        try:
+            torch.mm(Ct, gs, out_dtype=torch.float32, out=tw)
+        except (TypeError, RuntimeError, NotImplementedError):
+            tw.copy_(Ct @ gs)
+        grad_sink.done(W)
+        return None, None, None, None, None, None, db, None
+    return None, (Ct @ gs).float(), None, None, None, None, db, None
 
 
 def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor] = None, pad: int = 0,
