@@ -273,12 +273,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, l
     for (int k = 0; k < VEC; ++k) atomicAdd(out + c + k, s4[k]);
     return;
   }
-  if (mode == 2) {
+  if (mode >= 2) {  // 3: scale holds bag lengths, the factor is 1 / max(len, 1) (bag mean)
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       const long cc = c + k;
       float y = s4[k];
-      if (scale) y *= scale[cc / E];
+      if (scale) y *= mode == 3 ? 1.f / fmaxf(scale[cc / E], 1.f) : scale[cc / E];
       if (bias) y += bias[cc % E];
       s4[k] = act_fn(y, act);
     }
@@ -394,7 +394,8 @@ PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* ou
                      const float* bias, int E, int act, void* stream) {
   using namespace pv::dense;
   if (R < 1 || C < 1) return -1;
-  if (mode == 2 && E < 1) return -2;
+  if (mode >= 2 && E < 1) return -2;
+  if (mode > 3) return -3;
   // 4 columns per thread when rows and pointers allow 16-byte (fp32) / 8-byte (bf16) loads
   const bool vec = C % 4 == 0 && ldx % 4 == 0 && !((uintptr_t)out & 15) && !((uintptr_t)x & (xdt ? 7 : 15));
   const int V = vec ? 4 : 1;

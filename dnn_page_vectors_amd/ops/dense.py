@@ -84,7 +84,7 @@ def _colsum_ok(x: torch.Tensor, C: int, ldx: int) -> bool:
 
 
 def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False, scale=None, bias=None,
-           act: str = "none") -> torch.Tensor:
+           act: str = "none", scale_is_len: bool = False) -> torch.Tensor:
     """Sum over the leading axis of x (R, ...) -> fp32 (...) on the HIP column-sum kernel
     (dense.hip::colsum_kernel): the bias gradients and split-K partial sums of the backward.
     ``accumulate``: add into ``out`` (a zeroed buffer or a flat-gradient region).
@@ -100,7 +100,7 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
     if use_hip(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.dtype == torch.float32)):
         E = int(tail[-1]) if len(tail) else 1
         if epi:
-            mode = 2
+            mode = 3 if (scale_is_len and scale is not None) else 2
         elif accumulate or R > 64:
             mode = 1
         else:
@@ -119,7 +119,8 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
     y = torch.sum(x, 0, dtype=torch.float32)
     if epi:
         if scale is not None:
-            y = y * scale.reshape(-1, *([1] * (y.dim() - 1))).float()
+            sc = (1.0 / scale.float().clamp(min=1.0)) if scale_is_len else scale.float()
+            y = y * sc.reshape(-1, *([1] * (y.dim() - 1)))
         if bias is not None:
             y = y + bias.float()
         y = _torch_act(y, act)

@@ -44,7 +44,7 @@ def _counts(ids: torch.Tensor, V: int, pad: int):
     return C, lens
 
 
-def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, scale: Optional[torch.Tensor] = None,
+def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor] = None,
                  bias: Optional[torch.Tensor] = None, act: str = "none") -> torch.Tensor:
     """C (N, V) @ W16 (V, E) in fp32.  The (N, E) output has only (N/256)(E/256) = 32 tiles for
     the MLP page bags (N 4096, E 512) over a 30000-long reduction, so the single GEMM runs on
@@ -61,11 +61,11 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, scale: Optional[torch.Tenso
             part = torch.bmm(Cb, W16.reshape(sk, V // sk, E), out_dtype=torch.float32)
         except (TypeError, RuntimeError, NotImplementedError):
             part = None
-        if part is not None:  # split-K sum fused with the bag-mean scale / bias / activation
-            return dops.colsum(part, scale=scale, bias=bias, act=act)
+        if part is not None:  # split-K sum fused with the bag-mean 1/len / bias / activation
+            return dops.colsum(part, scale=lens, bias=bias, act=act, scale_is_len=True)
     out = (C @ W16).float()
-    if scale is not None:
-        out = out * scale[:, None]
+    if lens is not None:
+        out = out / lens.clamp(min=1.0)[:, None]
     if bias is not None:
         out = out + bias.float()
     return dops._torch_act(out, act)
@@ -110,8 +110,7 @@ class _BagFn(torch.autograd.Function):
                 C, lens = _counts(ids, V, pad)
         else:
             C, lens = _counts(ids, V, pad)
-            scale = (1.0 / lens.clamp(min=1.0)) if mean else None
-            out = _counts_gemm(C[:, :V], W16, scale, bf, act)
+            out = _counts_gemm(C[:, :V], W16, lens if mean else None, bf, act)
             keys = None
         ctx.sparse = (L, E) if C is None else None
         ctx.save_for_backward(keys if C is None else C, lens, out if act != "none" else None)

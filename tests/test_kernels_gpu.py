@@ -1251,3 +1251,17 @@ def test_chunk_mean_pool_matches_torch(CL):
     (ref_out * g).sum().backward()
     torch.testing.assert_close(v.grad, v2.grad, rtol=1e-5, atol=1e-6)
     assert torch.all(out[4] == 0)
+
+
+def test_colsum_bag_mean_length_epilogue():
+    """colsum mode 3 (scale_is_len): act(sum / max(len, 1) + bias) -- the split-K bag-mean
+    epilogue of the counts GEMM, with zero-length bags."""
+    torch.manual_seed(6)
+    S, N, E = 8, 37, 512
+    x = torch.randn(S, N, E, device=DEV)
+    lens = torch.randint(0, 50, (N,), device=DEV).float()
+    lens[3] = 0.0
+    bias = torch.randn(E, device=DEV)
+    y = dops.colsum(x, scale=lens, bias=bias, act="tanh", scale_is_len=True)
+    ref_y = torch.tanh(x.sum(0) / lens.clamp(min=1.0)[:, None] + bias)
+    torch.testing.assert_close(y, ref_y, rtol=1e-5, atol=1e-5)
