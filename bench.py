@@ -16,6 +16,18 @@ of that trained model on held-out query/page pairs (`recall_at_10`, `recall_afte
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
 
+Launch: with ``--gpus N > 1`` and no torchrun environment (``WORLD_SIZE`` unset) this
+process never touches the GPU: it spawns N fresh rank processes of itself through
+``dnn_page_vectors_amd.launch`` (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+a free MASTER_PORT, ``HSA_ENABLE_IPC_MODE_LEGACY=0`` for RCCL's dmabuf IPC), waits for them
+and exits with the first non-zero rank status.  Under torchrun the ranks come from the
+environment.  Either way every rank checks ``world_size == --gpus`` and, on GPUs, that the
+process group runs on RCCL (``backend == "nccl"``; ``PAGEVEC_DIST_BACKEND=gloo`` is the
+explicit one-GPU rehearsal override), and rank 0 reports ``n_gpus`` = the world size.
+
+``--dry-run``: the same launch / process-group / timing / JSON path on the CPU (gloo,
+eager PyTorch ops, a tiny config-1-sized model) — the CPU test of the multi-rank launch.
+
 Rank 0 prints ONE JSON line (driver contract).
 """
 from __future__ import annotations
@@ -26,7 +38,10 @@ import os
 import sys
 import time
 
-import torch
+# RCCL on this driver needs dmabuf IPC: set before anything can initialise HIP
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
 
 
 MODEL_DESC = {
@@ -65,6 +80,8 @@ def parse():
     ap.add_argument("--deterministic", type=int, default=0,
                     help="deterministic reduction mode (ops/determinism.py): order-free fixed-point "
                          "gradient sums, one stream, no hipGraph")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launch / process group / JSON path (gloo, eager ops, tiny model)")
     ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "cdssm_char"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5; "
                          "cdssm_char = the reference's default run (char level, 250 / 5000 tokens), per-GPU "
@@ -105,18 +122,43 @@ def _eager_pairs_per_s(cfg, V, dev, batch=512, steps=3, warmup=2):
         return None
 
 
+def _sync(dev) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _spawn_ranks(a) -> int:
+    """--gpus N > 1 without a torchrun environment: N fresh rank processes of this script
+    (this process has not initialised HIP and never will)."""
+    from dnn_page_vectors_amd.launch import launch
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], a.gpus, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(a))
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
-    from dnn_page_vectors_amd.eval.retrieval import recall_at_k
+    from dnn_page_vectors_amd.eval.retrieval import distributed_recall_table, recall_at_k
     from dnn_page_vectors_amd.models import build_model
     from dnn_page_vectors_amd.models.cdssm import cdssm_flops_per_sample
     from dnn_page_vectors_amd.ops._common import set_backend
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
-    info = pdist.init_distributed()
+    info = pdist.init_distributed(device="cpu" if a.dry_run else None)
+    if info.world_size != a.gpus:
+        raise SystemExit(f"bench.py: world size {info.world_size} != --gpus {a.gpus} (launch N ranks with "
+                         f"`bench.py --gpus N` or torchrun --nproc-per-node N)")
+    if info.world_size > 1 and info.device.type == "cuda" and info.backend != "nccl" \
+            and os.environ.get("PAGEVEC_DIST_BACKEND") != info.backend:
+        raise SystemExit(f"bench.py: multi-GPU runs use RCCL (backend 'nccl'), got {info.backend!r}")
+    if a.dry_run:  # CPU rehearsal: eager PyTorch ops, a tiny model, no quality phase
+        a.backend, a.graph, a.eager_compare, a.quality_steps = "torch", 0, 0, 0
+        a.recall = min(a.recall, 64)
     if a.backend == "torch":
         set_backend("torch")
     preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "chunked": "longpage_fp8",
@@ -132,6 +174,9 @@ def main():
     cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode,
                       deterministic=bool(a.deterministic))
     a.batch = batch
+    if a.dry_run:
+        a.batch = min(a.batch, 16)
+        cfg = cfg.replace(batch_size=a.batch, query_length=12, document_length=32, vocab_hash_size=1000)
     V = cfg.vocab_hash_size
     dev = info.device
     model = build_model(cfg, V)
@@ -145,10 +190,10 @@ def main():
 
     # 65536 distinct synthetic pages (the quality phase draws fresh batches from them; a
     # smaller pool lets the towers memorise training pages instead of generalising)
-    spec = spec_from_config(cfg, V, num_pages=65536)
+    spec = spec_from_config(cfg, V, num_pages=512 if a.dry_run else 65536)
     data = SyntheticPairs(spec, dev, seed=1337 + info.rank)
     pool = [data.batch(a.batch) for _ in range(max(1, a.pool))]
-    torch.cuda.synchronize()
+    _sync(dev)
 
     def step(i):
         q, d = pool[i % len(pool)]
@@ -156,15 +201,15 @@ def main():
 
     for i in range(a.warmup):
         m = step(i)
-    torch.cuda.synchronize()
+    _sync(dev)
     pdist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         m = step(a.warmup + i)
-    torch.cuda.synchronize()
+    _sync(dev)
     pdist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     pdist.all_reduce_max_(t)
@@ -178,12 +223,16 @@ def main():
         m = trainer.train_step(*data.batch(a.batch))
     quality_loss = float(m["loss"])
 
-    recall = None
+    recall = recall_local = None
     if a.recall > 0:
-        qe, pe = data.eval_set(a.recall)
+        # every rank encodes its own held-out pairs (rank-specific pages, one shared vocabulary);
+        # Recall@10 ranks each query against the pages of ALL ranks (all-gathered page vectors)
+        qe, pe = data.eval_set(a.recall, seed=7 + 1000 * info.rank)
         qv = model.encode(qe, "query")
         pv = model.encode(pe, "doc")
-        recall = recall_at_k(qv, pv, torch.arange(a.recall, device=dev), k=10)
+        rel = torch.arange(a.recall, device=dev)
+        recall_local = recall_at_k(qv, pv, rel, k=10)
+        recall = distributed_recall_table(qv, pv, rel, ks=(10,))["recall@10"]
 
     W = info.world_size
     eager = None
@@ -225,16 +274,26 @@ def main():
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend,
                        "softmax_scale": (cfg.inbatch_gamma or cfg.GAMMA) if a.loss != "explicit" else cfg.GAMMA,
-                       "deterministic": bool(a.deterministic)},
+                       "deterministic": bool(a.deterministic),
+                       "dist_backend": info.backend, "grad_bucket_mb": cfg.grad_bucket_mb,
+                       "launch": "torchrun-env" if os.environ.get("TORCHELASTIC_RUN_ID") else
+                                 ("bench-spawn" if W > 1 else "single"),
+                       "rccl_env": {k: v for k, v in sorted(os.environ.items())
+                                    if k.startswith(("NCCL_", "RCCL_")) and "SOCKET" not in k}},
             "recall_at_10": None if recall is None else round(recall, 4),
+            "recall_candidates": a.recall * W if recall is not None else None,
+            "recall_at_10_rank_local": None if recall_local is None else round(recall_local, 4),
             "recall_after_steps": max(done, a.quality_steps),
             "final_loss": round(final_loss, 4),
             "loss_after_quality_steps": round(quality_loss, 4),
             "fwd_model_tflops": round(flops / 1e12, 1),
             "train_model_tflops": round(flops * train_mult / 1e12, 1) if train_mult else None,
-            "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else None,
             "hip_graph": graph_used,
         }
+        if a.dry_run:
+            out["dry_run"] = True
+            out["data"] = "synthetic (CPU dry run: gloo, eager PyTorch ops, tiny model; not a measurement)"
         if eager:
             out["eager_pytorch_pairs_per_s"] = round(eager, 1)
             out["speedup_vs_eager_pytorch"] = round(value / eager, 1)

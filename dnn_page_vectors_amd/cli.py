@@ -233,7 +233,9 @@ def cmd_serve(a) -> int:
         if batch_txt:
             index.add(engine.encode(batch_txt, "doc"), batch_ids, normalize=False)
         log.info("indexed %d pages", len(index))
-    uvicorn.run(create_app(engine, index), host=a.host, port=a.port, log_level="info")
+    if a.save_dir:
+        os.makedirs(a.save_dir, exist_ok=True)
+    uvicorn.run(create_app(engine, index, save_dir=a.save_dir, max_items=a.max_items), host=a.host, port=a.port, log_level="info")
     engine.close()
     return 0
 
@@ -287,6 +289,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--max-batch", type=int, default=4096)
     p.add_argument("--max-wait-ms", type=float, default=2.0)
+    p.add_argument("--save-dir", default=None,
+                   help="directory POST /index/save may write into (default: saving over HTTP disabled)")
+    p.add_argument("--max-items", type=int, default=4096, help="max texts / pages / queries per request")
     p.set_defaults(fn=cmd_serve)
     p = sub.add_parser("bench", help="run bench.py (headline benchmark)")
     p.add_argument("rest", nargs=argparse.REMAINDER)

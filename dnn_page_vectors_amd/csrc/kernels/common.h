@@ -179,8 +179,12 @@ enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3, PV_ERR_A
 // ordered pass.  Partial sums inside a workgroup are already formed in a fixed order.
 namespace pv {
 constexpr float PV_FX_SCALE = 1099511627776.0f;  // 2^40
+// Only each ADDEND is clamped (to +-2^61, i.e. +-2^21 in value units); the int64 SUM of many
+// addends can still pass +-2^63 and wrap.  det_flush treats any total of magnitude >= 2^62
+// (+-2^22 in value units, far beyond a sane gradient) as an overflow and writes NaN into the
+// target, so the trainer's non-finite guard skips the step instead of applying a wrapped sum.
 __device__ __forceinline__ void fx_add(long long* fx, size_t i, float v) {
-  const float x = fminf(fmaxf(v * PV_FX_SCALE, -9.0e18f), 9.0e18f);  // saturate, never wrap
+  const float x = fminf(fmaxf(v * PV_FX_SCALE, -2.3058430e18f), 2.3058430e18f);  // |addend| <= 2^61
   atomicAdd(reinterpret_cast<unsigned long long*>(fx) + i, (unsigned long long)__float2ll_rn(x));
 }
 bool det_on();

@@ -17,7 +17,11 @@ __global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restri
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const long long v = fx[i];
-    if (v != 0) dst[i] += (float)((double)v * (1.0 / 1099511627776.0));
+    // |total| >= 2^62: the sum may have wrapped (fx_add clamps addends only) -> NaN, which
+    // the non-finite gradient guard turns into a skipped step
+    const bool overflow = v >= (1LL << 62) || v <= -(1LL << 62);
+    if (overflow) dst[i] = __builtin_nanf("");
+    else if (v != 0) dst[i] += (float)((double)v * (1.0 / 1099511627776.0));
   }
 }
 }  // namespace

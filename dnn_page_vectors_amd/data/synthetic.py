@@ -36,7 +36,11 @@ class SyntheticSpec:
 
 
 class SyntheticPairs:
-    def __init__(self, spec: SyntheticSpec, device: torch.device | str = "cpu", seed: int = 1337):
+    def __init__(self, spec: SyntheticSpec, device: torch.device | str = "cpu", seed: int = 1337,
+                 vocab_seed: int = 1337):
+        """``seed`` draws the pages / queries / batches (data-parallel ranks pass rank-specific
+        seeds); ``vocab_seed`` fixes the token-frequency "language" (which id is the k-th most
+        frequent token), shared by every rank so all ranks train on one distribution."""
         self.spec = spec
         self.device = torch.device(device)
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
@@ -44,7 +48,7 @@ class SyntheticPairs:
         ranks = torch.arange(1, V, dtype=torch.float64)
         probs = ranks.pow(-spec.zipf_s)
         # random permutation of ids so frequent tokens are spread over the id space (as hashing does)
-        perm = torch.randperm(V - 1, generator=self.gen) + 1
+        perm = torch.randperm(V - 1, generator=torch.Generator(device="cpu").manual_seed(vocab_seed)) + 1
         self.cdf = torch.cumsum(probs / probs.sum(), 0).float().to(self.device)
         self.id_of_rank = perm.to(torch.int32).to(self.device)
         self.pages = self._sample_pages(spec.num_pages)

@@ -30,22 +30,41 @@ from .. import _native
 _ON = [False]
 
 
-def set_deterministic(on: bool = True) -> None:
-    _ON[0] = bool(on)
+def set_deterministic(on: bool = True):
+    """Switch the mode; returns the previous state (for ``restore``)."""
     import torch
+    import torch.utils.deterministic as _tud
 
+    prev = (_ON[0], torch.are_deterministic_algorithms_enabled(),
+            torch.is_deterministic_algorithms_warn_only_enabled(), _tud.fill_uninitialized_memory)
+    _ON[0] = bool(on)
     if not torch.cuda.is_available():  # CPU training is deterministic without the kernels' mode
-        return
+        return prev
     # the few torch ops on the training paths (the BERT token-embedding index_add_) switch to
     # their deterministic implementations; uninitialised memory is NOT NaN-filled (every
     # kernel output is fully written; padded operands are allocated zeroed)
-    torch.use_deterministic_algorithms(bool(on), warn_only=True)
-    import torch.utils.deterministic as _tud
-
-    _tud.fill_uninitialized_memory = False
+    if on:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        _tud.fill_uninitialized_memory = False
     lib = _native.hip(required=False)
     if lib is not None:
         lib.pv_set_deterministic(1 if on else 0)
+    return prev
+
+
+def restore(prev) -> None:
+    """Undo ``set_deterministic``: the native flag and torch's global flags as they were."""
+    import torch
+    import torch.utils.deterministic as _tud
+
+    on, algos, warn_only, fill = prev
+    _ON[0] = bool(on)
+    if torch.cuda.is_available():
+        torch.use_deterministic_algorithms(algos, warn_only=warn_only)
+        _tud.fill_uninitialized_memory = fill
+        lib = _native.hip(required=False)
+        if lib is not None:
+            lib.pv_set_deterministic(1 if on else 0)
 
 
 def enabled() -> bool:

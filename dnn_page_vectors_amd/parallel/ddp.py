@@ -13,6 +13,16 @@ overlapped with backward).  Buckets are also cut where the top-level module chan
 (``query_tower`` | ``doc_towers``): the query tower runs last in forward, so its gradient
 (12.6 MB for CDSSM-ngram) is complete early in backward and its all-reduce overlaps the
 doc tower's backward instead of sharing one 25 MB bucket launched after everything.
+The cut is made at EVERY such boundary, whatever the open bucket's size, so a bucket never
+mixes the two towers' parameters.
+
+Streams: the towers' backward passes run on different HIP streams (the query tower on its
+side stream, models/base.py; the page tower's dW on the conv side stream, ops/conv_pool.py),
+and a bucket's all-reduce is launched from whichever gradient hook completes it.  Every hook
+therefore records the stream that was current when its gradient was produced, and
+``_launch`` makes the launching stream wait on each of the bucket's producer streams before
+it enqueues the collective — the all-reduce can never read a gradient still being written on
+another stream, independent of how the buckets are cut.
 """
 from __future__ import annotations
 
@@ -26,7 +36,7 @@ from ..ops.optim import FlatParams
 
 
 class GradBuckets:
-    MIN_SPLIT_BYTES = 1 << 20  # module-boundary cuts only once the open bucket holds >= 1 MB
+    MIN_SPLIT_BYTES = 1 << 20  # embedding tables of at least 1 MB get a bucket of their own
     OWN_BUCKET_LEAVES = ("embedding", "word")  # >= 1 MB embedding tables: one bucket each
 
     def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg"):
@@ -60,7 +70,7 @@ class GradBuckets:
                 continue
             if cur_lo is None:
                 cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
-            elif mod != cur_mod and (cur_hi - cur_lo) >= min_split:
+            elif mod != cur_mod:  # never mix towers in one bucket
                 self._add(cur_lo, cur_hi, members)
                 cur_lo, cur_hi, members, cur_mod = o, end, [name], mod
             elif (cur_hi - o) <= cap:
@@ -72,6 +82,7 @@ class GradBuckets:
         if cur_lo is not None:
             self._add(cur_lo, cur_hi, members)
         self.pending: List[set] = [set() for _ in self.buckets]
+        self.streams: List[dict] = [{} for _ in self.buckets]  # producer streams per bucket
         self.handles: List[Optional[object]] = [None] * len(self.buckets)
         self._hooks = []
         if self.overlap:
@@ -92,6 +103,9 @@ class GradBuckets:
         def hook(p):
             seen = self.pending[bi]
             seen.add(id(p))  # a set: a parameter reached twice counts once
+            if p.is_cuda:
+                st = torch.cuda.current_stream(p.device)
+                self.streams[bi][st.cuda_stream] = st
             if len(seen) == self.buckets[bi][2] and self.handles[bi] is None:
                 self._launch(bi)
         return hook
@@ -99,6 +113,11 @@ class GradBuckets:
     def _launch(self, bi: int) -> None:
         lo, hi, _ = self.buckets[bi]
         view = self.flat.grad[lo:hi]
+        if view.is_cuda:  # order the collective after every stream that wrote into the bucket
+            cur = torch.cuda.current_stream(view.device)
+            for key, st in self.streams[bi].items():
+                if key != cur.cuda_stream:
+                    cur.wait_stream(st)
         if self.avg_op is not None:
             self.handles[bi] = dist.all_reduce(view, op=self.avg_op, async_op=True)
         else:
@@ -106,6 +125,7 @@ class GradBuckets:
 
     def start_step(self) -> None:
         self.pending = [set() for _ in self.buckets]
+        self.streams = [{} for _ in self.buckets]
         self.handles = [None] * len(self.buckets)
 
     def finish(self) -> None:

@@ -51,6 +51,9 @@ def info() -> DistInfo:
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None) -> DistInfo:
     """Initialise from the torchrun environment; a no-op single-process setup otherwise."""
     global _INFO
+    # RCCL's peer-memory IPC on this driver is dmabuf only: the HSA runtime reads this at
+    # HIP initialisation, which happens below (set_device) — never earlier in this module
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

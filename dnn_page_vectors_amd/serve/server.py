@@ -8,7 +8,14 @@ Endpoints (JSON):
   POST /encode   {"texts": [...], "tower": "doc"|"query"}      -> {"vectors": [[...]], "dim"}
   POST /index/add {"pages": [{"id": ..., "text": ...}]}        -> {"added", "pages"}
   POST /search   {"queries": [...], "k": 10}                   -> {"results": [[{"id", "score"}]]}
-  POST /index/save {"path": ...}                               -> {"saved", "pages"}
+  POST /index/save {"name": ...}                               -> {"saved", "pages"}
+       (only when the server was started with a save directory, ``--save-dir``: the name is
+       a plain file stem resolved inside that directory; anything that would escape it is
+       rejected — the HTTP client never chooses a filesystem path)
+
+Every list in a request body is capped (``max_items``, default 4096 texts / pages / queries)
+and every text is capped at ``max_chars`` characters, so one request cannot make the
+engine featurize and encode an unbounded batch.
 
 Request handlers run in FastAPI's thread pool and only wait on the engine's futures:
 all device work goes through the EncoderEngine worker (dynamic batching) and the index
@@ -16,6 +23,8 @@ search, serialised by a lock so one HIP stream sees a well-ordered launch sequen
 """
 from __future__ import annotations
 
+import os
+import re
 import threading
 from typing import Any, List, Optional, Union
 
@@ -46,14 +55,38 @@ class SearchReq(BaseModel):
 
 
 class SaveReq(BaseModel):
-    path: str
+    name: str
 
 
-def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100):
+_NAME = re.compile(r"^[A-Za-z0-9][A-Za-z0-9_.-]{0,127}$")
+
+
+def resolve_save_path(save_dir: str, name: str) -> str:
+    """``save_dir/name`` for a plain file stem; ValueError for anything else (separators,
+    ``..``, absolute paths, hidden names) or a result outside ``save_dir``."""
+    if not _NAME.match(name) or ".." in name:
+        raise ValueError(f"invalid index name {name!r}: use [A-Za-z0-9_.-], no path separators")
+    root = os.path.realpath(save_dir)
+    path = os.path.realpath(os.path.join(root, name))
+    if os.path.dirname(path) != root:
+        raise ValueError(f"index name {name!r} escapes the save directory")
+    return path
+
+
+def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100, save_dir: Optional[str] = None,
+               max_items: int = 4096, max_chars: int = 100_000):
+    """``save_dir``: directory that POST /index/save writes into (None: the endpoint is off).
+    ``max_items`` / ``max_chars``: per-request caps on list length and text length."""
     from fastapi import FastAPI, HTTPException
 
     app = FastAPI(title="dnn_page_vectors_amd", version="1")
     lock = threading.Lock()
+
+    def _cap(texts: List[str]) -> None:
+        if len(texts) > max_items:
+            raise HTTPException(413, f"at most {max_items} items per request")
+        if any(len(t) > max_chars for t in texts):
+            raise HTTPException(413, f"texts are limited to {max_chars} characters")
 
     @app.get("/health")
     def health() -> Any:
@@ -64,6 +97,7 @@ def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100):
     def encode(req: EncodeReq) -> Any:
         if req.tower not in ("doc", "query"):
             raise HTTPException(400, "tower must be 'doc' or 'query'")
+        _cap(req.texts)
         v = engine.encode(req.texts, req.tower)
         return {"vectors": v.tolist(), "dim": int(v.shape[1]) if v.dim() == 2 else 0}
 
@@ -71,6 +105,7 @@ def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100):
     def add(req: AddReq) -> Any:
         if not req.pages:
             return {"added": 0, "pages": len(index)}
+        _cap([p.text for p in req.pages])
         v = engine.encode([p.text for p in req.pages], "doc")
         with lock:
             index.add(v, [p.id for p in req.pages], normalize=False)
@@ -83,6 +118,7 @@ def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100):
             raise HTTPException(400, f"k must be <= {max_k}")
         if not req.queries:
             return {"results": []}
+        _cap(req.queries)
         q = engine.encode(req.queries, "query")
         with lock:
             hits = index.search(q, req.k)
@@ -90,10 +126,16 @@ def create_app(engine: EncoderEngine, index: PageIndex, max_k: int = 100):
 
     @app.post("/index/save")
     def save(req: SaveReq) -> Any:
+        if save_dir is None:
+            raise HTTPException(403, "index saving is disabled (start the server with --save-dir)")
+        try:
+            path = resolve_save_path(save_dir, req.name)
+        except ValueError as e:
+            raise HTTPException(400, str(e))
         with lock:
-            index.save(req.path)
+            index.save(path)
             n = len(index)
-        return {"saved": req.path, "pages": n}
+        return {"saved": os.path.basename(path), "pages": n}
 
     return app
 

@@ -119,7 +119,11 @@ class Trainer:
         # deterministic reduction mode (ops/determinism.py) is process-wide: it follows the
         # latest Trainer's config; its fixed-point buffer may grow between steps, so no capture
         self.deterministic = bool(getattr(cfg, "deterministic", False))
-        determinism.set_deterministic(self.deterministic)
+        # only a deterministic config touches the process-wide mode (torch's deterministic-
+        # algorithm flags are left as the user set them otherwise); Trainer.close() restores it
+        self._det_prev = None
+        if self.deterministic:
+            self._det_prev = determinism.set_deterministic(True)
         self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
                            and not self.deterministic)
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
@@ -134,6 +138,12 @@ class Trainer:
         self._graph = None
         self._graph_key = None
         self._graph_warm = 0
+
+    def close(self) -> None:
+        """Restore the process-wide deterministic mode this trainer switched on (if any)."""
+        if self._det_prev is not None:
+            determinism.restore(self._det_prev)
+            self._det_prev = None
 
     # ------------------------------------------------------------------ core step
     def _base_seed(self) -> int:
@@ -274,7 +284,10 @@ class Trainer:
         loss, P = self.compute_loss(q_ids, d_ids, seed)
         if timer:
             timer.mark()
-        if self.buckets is not None and self.buckets.overlap:
+        # parameters with several gradient producers keep autograd's accumulation: needed for
+        # bucket hooks (DDP) and, on GPU, for towers that share weights across the query side
+        # stream and the main stream (a direct write on one stream would race the other's add)
+        if (self.buckets is not None and self.buckets.overlap) or self.device.type == "cuda":
             key = (tuple(q_ids.shape), tuple(d_ids.shape))
             if key not in self._sink_scanned:  # once per input shape (ops/grad_sink.py)
                 grad_sink.mark_multi_use(loss, self.flat)

@@ -218,3 +218,69 @@ def test_cli_train_tower_placement_two_ranks(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     hist = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])["history"]
     assert len(hist["loss"]) == 1 and hist["loss"][0] == hist["loss"][0]
+
+
+def _recall_worker(rank, world, port, q):
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.eval.retrieval import distributed_recall_table
+    from dnn_page_vectors_amd.parallel import dist as pdist
+
+    pdist.init_distributed(device="cpu")
+    Q, P, n = _recall_data(world)
+    sl = slice(rank * n, (rank + 1) * n)
+    r = distributed_recall_table(Q[sl], P[sl], torch.arange(n), ks=(1, 5, 10))
+    q.put((rank, r))
+    pdist.destroy()
+
+
+def _recall_data(world, n=24, D=8):
+    g = torch.Generator().manual_seed(3)
+    P = torch.nn.functional.normalize(torch.randn(world * n, D, generator=g), dim=1)
+    Q = torch.nn.functional.normalize(P + 0.9 * torch.randn(world * n, D, generator=g), dim=1)
+    return Q, P, n
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_recall_matches_single_process(world):
+    """W ranks, each with its own queries and pages: Recall@k over the all-gathered pages
+    equals the single-process Recall@k on the concatenated collection."""
+    from dnn_page_vectors_amd.eval.retrieval import recall_table
+
+    Q, P, n = _recall_data(world)
+    want = recall_table(Q, P, torch.arange(world * n), ks=(1, 5, 10))
+    assert 0.0 < want["recall@1"] < 1.0  # a non-trivial case
+    port = _port()
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    ps = [ctx.Process(target=_recall_worker, args=(r, world, port, qq)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(qq.get(timeout=120) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    for r in range(world):
+        assert res[r] == pytest.approx(want), (r, res[r], want)
+
+
+def test_buckets_never_mix_towers():
+    """A bucket holds one top-level module's parameters only (query tower vs doc towers),
+    even when the open bucket is tiny: its all-reduce waits on one tower's streams."""
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.ops.optim import FlatParams
+    from dnn_page_vectors_amd.parallel.ddp import GradBuckets
+
+    cfg = _cfg("explicit", 4)
+    flat = FlatParams(CDSSM(cfg, 150).named_parameters())
+
+    b = GradBuckets.__new__(GradBuckets)  # constructed without a process group (world size 1)
+    import dnn_page_vectors_amd.parallel.ddp as ddp
+    orig = ddp.dist
+    try:
+        ddp.dist = type("D", (), {"is_initialized": staticmethod(lambda: False),
+                                  "get_world_size": staticmethod(lambda: 1)})
+        b.__init__(flat, bucket_mb=64.0)
+    finally:
+        ddp.dist = orig
+    owner = {}
+    for name, bi in b.param_bucket.items():
+        owner.setdefault(bi, set()).add(name.split(".", 1)[0])
+    assert len(b.buckets) >= 2
+    assert all(len(mods) == 1 for mods in owner.values()), owner

@@ -38,3 +38,31 @@ def test_launch_propagates_failure(tmp_path):
         time.sleep(60)  # peers would hang; the launcher must terminate them
     """)
     assert r.returncode == 7
+
+
+def test_bench_spawns_ranks_for_gpus_n():
+    """`python bench.py --gpus 2` without torchrun: the bench itself spawns 2 rank processes
+    (the driver's multi-GPU invocation); CPU dry run over gloo — one JSON line, n_gpus 2."""
+    import json
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                        "--warmup", "1"], env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["dist_backend"] == "gloo" and out["config"]["launch"] == "bench-spawn"
+    assert out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
+    assert out["recall_candidates"] == 2 * 64 and out["dry_run"] is True
+
+
+def test_bench_rejects_world_size_mismatch():
+    """Under a torchrun-style environment a --gpus that differs from WORLD_SIZE is an error,
+    never a silent single-GPU measurement."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1",
+                        "--warmup", "0"], env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "world size 1 != --gpus 2" in (r.stderr + r.stdout)

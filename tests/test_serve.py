@@ -152,6 +152,36 @@ def test_http_endpoints():
     assert len(s) == 2 and len(s[0]) == 4 and all("score" in h for h in s[0])
     assert c.post("/search", json={"queries": ["a"], "k": 1000}).status_code == 400
     assert c.post("/encode", json={"texts": ["a"], "tower": "nope"}).status_code == 400
+    # saving is off unless a save directory was configured
+    assert c.post("/index/save", json={"name": "idx"}).status_code == 403
+    eng.close()
+
+
+def test_http_save_confined_and_request_caps(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from dnn_page_vectors_amd.serve.engine import EncoderEngine
+    from dnn_page_vectors_amd.serve.server import create_app, resolve_save_path
+
+    m = _ToyModel()
+    eng = EncoderEngine(m, _ToyFz(), 8, 16, device=torch.device("cpu"), max_batch=64, max_wait_ms=1)
+    idx = PageIndex(m.out_dim, device="cpu")
+    save_dir = tmp_path / "indexes"
+    save_dir.mkdir()
+    c = TestClient(create_app(eng, idx, save_dir=str(save_dir), max_items=8, max_chars=64))
+    c.post("/index/add", json={"pages": [{"id": i, "text": f"{i} p"} for i in range(4)]})
+    r = c.post("/index/save", json={"name": "snap1"})
+    assert r.status_code == 200 and r.json() == {"saved": "snap1", "pages": 4}
+    assert (save_dir / "snap1.json").exists()
+    for bad in ("../evil", "/etc/passwd", "a/b", "..", ".hidden", ""):
+        assert c.post("/index/save", json={"name": bad}).status_code == 400, bad
+        with pytest.raises(ValueError):
+            resolve_save_path(str(save_dir), bad)
+    assert not any(p.name.startswith("evil") for p in tmp_path.rglob("*"))
+    assert c.post("/encode", json={"texts": ["a"] * 9}).status_code == 413
+    assert c.post("/encode", json={"texts": ["a" * 65]}).status_code == 413
+    assert c.post("/search", json={"queries": ["q"] * 9, "k": 1}).status_code == 413
+    assert c.post("/index/add", json={"pages": [{"id": i, "text": "t"} for i in range(9)]}).status_code == 413
     eng.close()
 
 
