@@ -72,6 +72,8 @@ def _declare_rt(lib: ctypes.CDLL) -> None:
     lib.pv_featurize.restype = c.c_int
     lib.pv_clean_str.argtypes = [c.c_char_p, c.c_char_p, c.c_int64]
     lib.pv_clean_str.restype = c.c_int64
+    lib.pv_normalize_html.argtypes = [c.c_char_p, c.c_char_p, c.c_int64]
+    lib.pv_normalize_html.restype = c.c_int64
     lib.pv_dataset_open.argtypes = [c.c_char_p, c.c_int, c.c_int]
     lib.pv_dataset_open.restype = c.c_void_p
     lib.pv_dataset_size.argtypes = [c.c_void_p]

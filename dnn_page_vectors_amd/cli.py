@@ -59,10 +59,11 @@ def _featurizer(cfg):
     from .data.featurize import Featurizer
 
     if cfg.vocab_hash_size > 1:
-        return Featurizer(cfg.feature_level, hash_size=cfg.vocab_hash_size)
+        return Featurizer(cfg.feature_level, hash_size=cfg.vocab_hash_size, html=cfg.html_normalize,
+                          nthreads=cfg.num_workers)
     from .io.vocab import load_vocab
 
-    return Featurizer(cfg.feature_level, vocab=load_vocab(cfg))
+    return Featurizer(cfg.feature_level, vocab=load_vocab(cfg), html=cfg.html_normalize, nthreads=cfg.num_workers)
 
 
 def cmd_train(a) -> int:
@@ -181,27 +182,52 @@ def cmd_encode(a) -> int:
 
 
 def cmd_eval(a) -> int:
+    """Recall@1/10/100.  ``--data FILE`` (or ``--data validation``: the experiment's
+    model_validation_data): real {'q', 'doc_corr', 'doc_incorr'} rows, every query ranked
+    against all distinct pages of the file; without --data: held-out synthetic pairs.
+    Under a multi-rank launch (launch.py / torchrun) the rows are sharded and the page
+    vectors all-gathered (eval/retrieval.py::distributed_recall_table)."""
     import torch
 
-    from .data.synthetic import SyntheticPairs, spec_from_config
-    from .eval.retrieval import recall_table
+    from .eval.retrieval import evaluate_pairs_dataset, recall_table
     from .io import checkpoint as ck
     from .models import build_model
+    from .parallel import dist as pdist
 
     cfg = _config(a)
-    dev = torch.device("cuda" if torch.cuda.device_count() > 0 else "cpu")
-    V = cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000
-    model = build_model(cfg, V).to(dev)
-    if a.weights:
-        ck.load_weights(model, a.weights)
-    gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=1024), dev, seed=cfg.seed)
-    q, p = gen.eval_set(a.pages)
-    r = recall_table(model.encode(q, "query"), model.encode(p, "doc"), torch.arange(a.pages, device=dev))
-    if a.metrics:
-        from .utils.metrics import MetricsLogger
+    info = pdist.init_distributed()
+    dev = info.device
+    if a.data:
+        from .data.dataset import JsonlPairDataset
 
-        MetricsLogger(a.metrics).log(eval="synthetic_retrieval", pages=a.pages, weights=a.weights, **r)
-    print(json.dumps(r))
+        path = cfg.model_validation_data if a.data == "validation" else a.data
+        fz = _featurizer(cfg)
+        model = build_model(cfg, fz.num_ids).to(dev)
+        weights = a.weights or os.path.join(cfg.trained_model_dir, ck.FINAL_WEIGHTS)
+        if os.path.exists(weights) or a.weights:
+            ck.load_weights(model, weights)
+        ds = JsonlPairDataset(path, fz, cfg.query_length, cfg.document_length, cfg.num_negative_examples)
+        r = evaluate_pairs_dataset(model, ds, dev, max_rows=a.max_rows, include_negatives=not a.no_negatives)
+        r.update(data=path, skipped_rows=ds.skipped)
+        kind = "jsonl_retrieval"
+    else:
+        from .data.synthetic import SyntheticPairs, spec_from_config
+
+        V = cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000
+        model = build_model(cfg, V).to(dev)
+        if a.weights:
+            ck.load_weights(model, a.weights)
+        gen = SyntheticPairs(spec_from_config(cfg, V, num_pages=1024), dev, seed=cfg.seed)
+        q, p = gen.eval_set(a.pages)
+        r = recall_table(model.encode(q, "query"), model.encode(p, "doc"), torch.arange(a.pages, device=dev))
+        kind = "synthetic_retrieval"
+    if info.is_main:
+        if a.metrics:
+            from .utils.metrics import MetricsLogger
+
+            MetricsLogger(a.metrics).log(eval=kind, pages=a.pages, weights=a.weights, **r)
+        print(json.dumps(r))
+    pdist.destroy()
     return 0
 
 
@@ -277,7 +303,12 @@ def main(argv: Optional[List[str]] = None) -> int:
     p = sub.add_parser("eval")
     _common(p)
     p.add_argument("--weights", default=None)
-    p.add_argument("--pages", type=int, default=2048)
+    p.add_argument("--pages", type=int, default=2048, help="synthetic pairs (without --data)")
+    p.add_argument("--data", default=None,
+                   help="JSONL {'q','doc_corr','doc_incorr'} file to evaluate on, or 'validation' for the "
+                        "experiment's model_validation_data")
+    p.add_argument("--max-rows", type=int, default=0, help="evaluate the first N rows only (0 = all)")
+    p.add_argument("--no-negatives", action="store_true", help="rank against the positive pages only")
     p.add_argument("--metrics", default=None, help="append the eval record to this metrics JSONL")
     p.set_defaults(fn=cmd_eval)
     p = sub.add_parser("serve", help="HTTP page-vector service: /encode, /index/add, /search")

@@ -115,7 +115,10 @@ class Configuration:
     adam_eps: float = 1e-8
     lazy_embedding_adam: bool = False    # Adam skips embedding rows with an all-zero gradient (large vocabularies)
     optimizer_bf16_mirror: bool = True   # the Adam kernel also writes the bf16 compute copies of big weights
-    dtype: str = "fp32"                   # fp32 | bf16 (compute dtype of hot kernels)
+    # compute precision (ops/_common.py::precision_scope): bf16 = the HIP kernels (bf16 MFMA
+    # operands, fp32 accumulation / master weights); fp32 = the reference's precision through
+    # PyTorch's fp32 ops (no bf16 anywhere).  CPU runs compute fp32 either way.
+    dtype: str = "bf16"
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
     grad_bucket_mb: float = 32.0
@@ -124,8 +127,8 @@ class Configuration:
     placement: str = "dp"                # dp (data parallel) | tower (slots over ranks, cnn_dssm_tf.py:139-158)
     log_every: int = 10
     skip_nonfinite: bool = True
-    prefetch: int = 2
-    num_workers: int = 4
+    prefetch: int = 2                     # featurized batches the loader thread keeps ahead (pinned)
+    num_workers: int = 0                  # featurizer threads per batch (C++ pool); 0 = min(16, CPUs)
 
     # --------------------------------------------------------------------------
     def __post_init__(self) -> None:
@@ -139,6 +142,14 @@ class Configuration:
             self.query_length = ql
         if self.document_length is None:
             self.document_length = dl
+        if self.dtype not in ("bf16", "fp32"):
+            raise ValueError(f"dtype must be 'bf16' (HIP kernels) or 'fp32' (reference precision), got {self.dtype!r}")
+        if self.use_fp8 and self.dtype != "bf16":
+            raise ValueError("use_fp8 (fp8 chunk GEMMs) runs on the HIP path: it needs dtype='bf16'")
+        if self.chunk_encoder not in ("mlp", "cdssm"):
+            raise ValueError(f"chunk_encoder must be 'mlp' or 'cdssm', got {self.chunk_encoder!r}")
+        if self.num_workers < 0 or self.prefetch < 1:
+            raise ValueError("num_workers must be >= 0 (0 = auto) and prefetch >= 1")
 
     # ---- derived paths (config.py:41-75) --------------------------------------
     @property
@@ -281,11 +292,11 @@ class Configuration:
 def preset_config(name: str) -> Configuration:
     name = name.lower()
     if name in ("reference", "reference_char", "cdssm_v2"):
-        # exact dssm_cnn_v2/cnn_dssm_th.py run configuration
-        return Configuration()
+        # exact dssm_cnn_v2/cnn_dssm_th.py run configuration, in its fp32 precision
+        return Configuration(dtype="fp32")
     if name in ("reference_v1", "cdssm_v1"):
         return Configuration(feature_level="word", batch_size=1024, nb_epoch=3,
-                             share_doc_tower=False, final_dropout=True)
+                             share_doc_tower=False, final_dropout=True, dtype="fp32")
     if name in ("tiny_dssm_cpu", "config1"):
         # Tiny 3-layer DSSM, 1k tri-gram hash, batch 32 on CPU
         return Configuration(model="mlp", feature_level="ngram", vocab_hash_size=1024,

@@ -104,6 +104,262 @@ inline void encode_cp(uint32_t cp, std::string& o) {
   }
 }
 
+// ------------------------------------------------------- HTML normaliser --
+// utils/word2vec_normalizer.py:116-146 (Word2VecTextNormalizer.preprocess_line) as restated
+// in data/text.py::normalize_html_line: strip, drop ';lt;'-style fragments, html.unescape,
+// strip tags (HTMLParser data only, charrefs converted again), drop \n \r \t, collapse dot
+// runs and pad them with spaces, per-word [^\wäöüß€\n.$] -> ' ' + lower-case, collapse
+// whitespace runs.  Entity names come from Python's own table (html_entities.inc).
+struct HtmlEntity { const char* name; const char* utf8; };
+struct NumericFix { uint32_t cp; const char* utf8; };
+#include "html_entities.inc"
+
+using U32 = std::u32string;
+
+inline bool py_space(uint32_t c) {  // str.isspace / re \s for str patterns
+  return (c >= 9 && c <= 13) || (c >= 0x1C && c <= 0x20) || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+         (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+
+void append_utf8(const char* s, U32& o) {
+  std::vector<uint32_t> cps;
+  decode_utf8(s, strlen(s), cps);
+  o.append(cps.begin(), cps.end());
+}
+
+const HtmlEntity* find_entity(const std::string& name) {
+  size_t lo = 0, hi = sizeof(kHtmlEntities) / sizeof(kHtmlEntities[0]);
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    int c = strcmp(kHtmlEntities[mid].name, name.c_str());
+    if (c == 0) return &kHtmlEntities[mid];
+    if (c < 0) lo = mid + 1; else hi = mid;
+  }
+  return nullptr;
+}
+
+std::string to_utf8(const U32& s, size_t b, size_t e) {
+  std::string o;
+  for (size_t i = b; i < e; ++i) encode_cp(s[i], o);
+  return o;
+}
+
+// html.unescape: &(#[0-9]+;?|#[xX][0-9a-fA-F]+;?|[^\t\n\f <&#;]{1,32};?)
+U32 html_unescape(const U32& s) {
+  if (s.find(U'&') == U32::npos) return s;
+  U32 o;
+  o.reserve(s.size());
+  const size_t n = s.size();
+  size_t i = 0;
+  while (i < n) {
+    if (s[i] != U'&') { o.push_back(s[i++]); continue; }
+    size_t j = i + 1;
+    if (j < n && s[j] == U'#') {
+      bool hex = j + 1 < n && (s[j + 1] == U'x' || s[j + 1] == U'X');
+      size_t d = j + (hex ? 2 : 1), k = d;
+      uint64_t num = 0;
+      auto digit = [&](uint32_t c, int& v) {
+        if (c >= '0' && c <= '9') { v = (int)(c - '0'); return true; }
+        if (hex && c >= 'a' && c <= 'f') { v = (int)(c - 'a' + 10); return true; }
+        if (hex && c >= 'A' && c <= 'F') { v = (int)(c - 'A' + 10); return true; }
+        return false;
+      };
+      int v;
+      while (k < n && digit(s[k], v)) {
+        num = num * (hex ? 16 : 10) + (uint64_t)v;
+        if (num > 0x110000) num = 0x110000;  // anything past 0x10FFFF is U+FFFD
+        ++k;
+      }
+      if (k == d) { o.push_back(s[i++]); continue; }  // "&#" without digits: literal
+      if (k < n && s[k] == U';') ++k;
+      bool done = false;
+      for (const auto& f : kInvalidCharrefs)
+        if (f.cp == num) { append_utf8(f.utf8, o); done = true; break; }
+      if (!done) {
+        if ((num >= 0xD800 && num <= 0xDFFF) || num > 0x10FFFF) o.push_back(0xFFFD);
+        else {
+          bool invalid = false;
+          for (uint32_t c : kInvalidCodepoints) if (c == num) { invalid = true; break; }
+          if (!invalid) o.push_back((uint32_t)num);
+        }
+      }
+      i = k;
+      continue;
+    }
+    size_t k = j;
+    while (k < n && k - j < 32) {
+      uint32_t c = s[k];
+      if (c == U'\t' || c == U'\n' || c == U'\f' || c == U' ' || c == U'<' || c == U'&' || c == U'#' || c == U';')
+        break;
+      ++k;
+    }
+    if (k == j) { o.push_back(s[i++]); continue; }
+    if (k < n && s[k] == U';') ++k;
+    std::string name = to_utf8(s, j, k);
+    if (const HtmlEntity* e = find_entity(name)) {
+      append_utf8(e->utf8, o);
+    } else {
+      bool hit = false;
+      for (size_t x = k - j - 1; x >= 2; --x) {  // longest known prefix (legacy names without ';')
+        if (const HtmlEntity* e2 = find_entity(to_utf8(s, j, j + x))) {
+          append_utf8(e2->utf8, o);
+          o.append(s, j + x, k - (j + x));
+          hit = true;
+          break;
+        }
+      }
+      if (!hit) { o.push_back(U'&'); o.append(s, j, k - j); }
+    }
+    i = k;
+  }
+  return o;
+}
+
+inline bool ascii_alpha(uint32_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+inline uint32_t ascii_lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+
+bool ieq_at(const U32& s, size_t i, const char* lit) {  // ASCII case-insensitive prefix match
+  for (size_t k = 0; lit[k]; ++k)
+    if (i + k >= s.size() || ascii_lower(s[i + k]) != (uint32_t)lit[k]) return false;
+  return true;
+}
+
+// html.parser.HTMLParser(convert_charrefs=True) fed one line and closed: the concatenation of
+// its handle_data() calls.  Start / end tags, comments, declarations and processing
+// instructions produce no data; script / style content is raw data (no unescape); an
+// unterminated construct at the end of the line swallows the rest, as the parser's close() does.
+U32 html_strip_tags(const U32& s) {
+  U32 o;
+  const size_t n = s.size();
+  size_t i = 0;
+  std::string cdata;  // "script" / "style" while inside one
+  while (i < n) {
+    if (!cdata.empty()) {  // raw text up to </cdata\s*>
+      size_t k = i;
+      for (; k < n; ++k) {
+        if (s[k] != U'<' || k + 1 >= n || s[k + 1] != U'/') continue;
+        size_t m = k + 2;
+        while (m < n && py_space(s[m])) ++m;
+        if (!ieq_at(s, m, cdata.c_str())) continue;
+        m += cdata.size();
+        while (m < n && py_space(s[m])) ++m;
+        if (m < n && s[m] == U'>') { o.append(s, i, k - i); i = m + 1; cdata.clear(); break; }
+      }
+      if (k >= n) return o;  // unterminated script/style: dropped
+      continue;
+    }
+    size_t j = s.find(U'<', i);
+    if (j == U32::npos) j = n;
+    if (j > i) o += html_unescape(s.substr(i, j - i));
+    i = j;
+    if (i >= n) break;
+    if (i + 1 < n && ascii_alpha(s[i + 1])) {  // start tag: name, attributes (quoted values may hold '>')
+      size_t k = i + 1, nb = k;
+      while (k < n && s[k] != U'\t' && s[k] != U'\n' && s[k] != U'\r' && s[k] != U'\f' && s[k] != U' ' &&
+             s[k] != U'/' && s[k] != U'>' && s[k] != 0)
+        ++k;
+      std::string name;
+      for (size_t t = nb; t < k; ++t) name.push_back((char)ascii_lower(s[t] < 128 ? s[t] : '?'));
+      uint32_t q = 0;
+      for (; k < n; ++k) {
+        if (q) { if (s[k] == q) q = 0; continue; }
+        if (s[k] == U'"' || s[k] == U'\'') {
+          if (k > 0 && (s[k - 1] == U'=' || py_space(s[k - 1]))) q = s[k];
+          continue;
+        }
+        if (s[k] == U'>') break;
+      }
+      if (k >= n) return o;  // unterminated start tag: the rest is dropped
+      bool selfclose = k > 0 && s[k - 1] == U'/';
+      if (!selfclose && (name == "script" || name == "style")) cdata = name;
+      i = k + 1;
+    } else if (i + 1 < n && s[i + 1] == U'/') {
+      size_t k = s.find(U'>', i + 1);
+      if (k == U32::npos) {
+        if (i + 2 == n) o += U"</";
+        return o;
+      }
+      i = k + 1;
+    } else if (ieq_at(s, i, "<!--")) {
+      size_t k = i + 4;
+      for (; k < n; ++k) {  // --\s*>
+        if (s[k] != U'-' || k + 1 >= n || s[k + 1] != U'-') continue;
+        size_t m = k + 2;
+        while (m < n && py_space(s[m])) ++m;
+        if (m < n && s[m] == U'>') { k = m; break; }
+      }
+      if (k >= n) return o;
+      i = k + 1;
+    } else if (i + 1 < n && (s[i + 1] == U'!' || s[i + 1] == U'?')) {
+      size_t k = s.find(U'>', i + 2);
+      if (k == U32::npos) return o;
+      i = k + 1;
+    } else {
+      o.push_back(U'<');
+      ++i;
+    }
+  }
+  return o;
+}
+
+inline bool w2v_keep(uint32_t c) {  // [\wäöüß€\n.$]
+  switch (c) {
+    case 0xE4: case 0xF6: case 0xFC: case 0xDF: case 0x20AC: case '\n': case '.': case '$':
+      return true;
+    default:
+      return is_word_cp(c);
+  }
+}
+
+// normalize_html_line on code points (in place in `cps`)
+void html_normalize(std::vector<uint32_t>& cps) {
+  size_t b = 0, e = cps.size();
+  while (b < e && py_space(cps[b])) ++b;
+  while (e > b && py_space(cps[e - 1])) --e;
+  if (b == e) return;  // blank line: returned unchanged
+  U32 s(cps.begin() + b, cps.begin() + e);
+  for (const char32_t* frag : {U";lt;", U";gt;", U";amp;", U";apos;", U";quot;"}) {
+    const U32 f(frag);
+    for (size_t p = s.find(f); p != U32::npos; p = s.find(f, p)) s.erase(p, f.size());
+  }
+  s = html_strip_tags(html_unescape(s));
+  U32 t;  // drop \n \r \t; dot runs -> " . "
+  for (size_t i = 0; i < s.size(); ++i) {
+    uint32_t c = s[i];
+    if (c == U'\n' || c == U'\r' || c == U'\t') continue;
+    if (c == U'.') {
+      while (i + 1 < s.size() && (s[i + 1] == U'.' || s[i + 1] == U'\n' || s[i + 1] == U'\r' || s[i + 1] == U'\t'))
+        ++i;
+      t += U" . ";
+      continue;
+    }
+    t.push_back(c);
+  }
+  // " ".join(RGX.sub(" ", w.strip().lower()) for w in t.split(" ")), then \s+ -> " "
+  U32 u;
+  size_t start = 0;
+  for (size_t i = 0; i <= t.size(); ++i) {
+    if (i < t.size() && t[i] != U' ') continue;
+    size_t wb = start, we = i;
+    while (wb < we && py_space(t[wb])) ++wb;
+    while (we > wb && py_space(t[we - 1])) --we;
+    if (start > 0) u.push_back(U' ');
+    for (size_t k = wb; k < we; ++k) {
+      uint32_t c = lower_cp(t[k]);
+      u.push_back(w2v_keep(c) ? c : U' ');
+    }
+    start = i + 1;
+  }
+  cps.clear();
+  bool prev_space = false;
+  for (uint32_t c : u) {
+    bool sp = py_space(c);
+    if (sp && prev_space) continue;
+    cps.push_back(sp ? (uint32_t)' ' : c);
+    prev_space = sp;
+  }
+}
+
 inline uint32_t fnv1a(const char* p, size_t n) {
   uint32_t h = 0x811C9DC5u;
   for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 0x01000193u; }
@@ -139,6 +395,7 @@ struct Vocab {
 
 struct Spec {
   int mode;        // 0 word, 1 ngram, 2 char
+  bool html;       // HTML / word2vec normalisation before clean_str (cfg.html_normalize)
   int length;      // cutoff == pad length
   const Vocab* vocab;
   int hash_size;   // > 0 => hashing
@@ -162,9 +419,11 @@ inline int32_t token_id(const Spec& sp, const char* p, size_t n, Scratch& sc) {
   return it == sp.vocab->map.end() ? sp.unk_id : it->second;
 }
 
-// clean_str: replace non-kept code points by ' ', strip ' '/'\n', lower-case.
-void clean(const char* s, size_t n, Scratch& sc) {
+// clean_str: replace non-kept code points by ' ', strip ' '/'\n', lower-case (after the
+// optional HTML normalisation of the raw text).
+void clean(const char* s, size_t n, Scratch& sc, bool html = false) {
   decode_utf8(s, n, sc.cps);
+  if (html) html_normalize(sc.cps);
   for (auto& c : sc.cps) c = keep_cp(c) ? c : (uint32_t)' ';
   size_t b = 0, e = sc.cps.size();
   auto ws = [](uint32_t c) { return c == ' ' || c == '\n'; };
@@ -181,7 +440,7 @@ void clean(const char* s, size_t n, Scratch& sc) {
 }
 
 void featurize_one(const char* s, size_t n, const Spec& sp, int32_t* out, Scratch& sc) {
-  clean(s, n, sc);
+  clean(s, n, sc, sp.html);
   const size_t ncp = sc.off.size() - 1;
   const char* u = sc.utf8.data();
   int t = 0;
@@ -402,9 +661,11 @@ int64_t pv_vocab_size(void* v) { return (int64_t)((Vocab*)v)->map.size(); }
 // texts: n NUL-terminated UTF-8 strings. out: n x length int32.
 int pv_featurize(const char** texts, int n, int mode, int length, void* vocab, int hash_size, int unk_id,
                  int pad_id, int32_t* out, int nthreads) {
-  if (mode < 0 || mode > 2 || length <= 0) return -1;
+  const bool html = (mode & 4) != 0;  // bit 2: HTML normalisation
+  mode &= 3;
+  if (mode > 2 || length <= 0) return -1;
   if (hash_size <= 1 && !vocab) return -2;
-  Spec sp{mode, length, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
+  Spec sp{mode, html, length, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
   if (mode == 2 && sp.hash_size == 0) ((Vocab*)vocab)->build_cp_table(unk_id);
   parallel_for(n, nthreads, [&](int i, Scratch& sc) {
     featurize_one(texts[i], strlen(texts[i]), sp, out + (int64_t)i * length, sc);
@@ -420,6 +681,22 @@ int64_t pv_clean_str(const char* s, char* out, int64_t cap) {
   if (cap > 0) {
     int64_t m = n < cap - 1 ? n : cap - 1;
     memcpy(out, sc.utf8.data(), (size_t)m);
+    out[m] = 0;
+  }
+  return n;
+}
+
+// HTML / word2vec normalisation of one line (tests: parity with data/text.py)
+int64_t pv_normalize_html(const char* s, char* out, int64_t cap) {
+  std::vector<uint32_t> cps;
+  decode_utf8(s, strlen(s), cps);
+  html_normalize(cps);
+  std::string o;
+  for (uint32_t c : cps) encode_cp(c, o);
+  int64_t n = (int64_t)o.size();
+  if (cap > 0) {
+    int64_t m = n < cap - 1 ? n : cap - 1;
+    memcpy(out, o.data(), (size_t)m);
     out[m] = 0;
   }
   return n;
@@ -479,8 +756,12 @@ int pv_dataset_batch(void* h, const int64_t* rows, int n, int mode, int qlen, in
                      int hash_size, int unk_id, int pad_id, int32_t* q_out, int32_t* d_out, int nthreads) {
   auto* ds = (Dataset*)h;
   const int J = ds->num_neg;
-  Spec sq{mode, qlen, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
-  Spec sd{mode, dlen, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
+  const bool html = (mode & 4) != 0;
+  mode &= 3;
+  if (mode > 2) return -3;
+  if (mode == 2 && hash_size <= 1 && vocab) ((Vocab*)vocab)->build_cp_table(unk_id);
+  Spec sq{mode, html, qlen, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
+  Spec sd{mode, html, dlen, (const Vocab*)vocab, hash_size > 1 ? hash_size : 0, unk_id, pad_id};
   std::atomic<int> err{0};
   parallel_for(n, nthreads, [&](int i, Scratch& sc) {
     int64_t r = rows[i];

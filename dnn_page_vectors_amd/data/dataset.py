@@ -67,7 +67,7 @@ class JsonlPairDataset:
             q_out = np.empty((n, self.qlen), dtype=np.int32)
         if d_out is None:
             d_out = np.empty((n, 1 + self.J, self.dlen), dtype=np.int32)
-        rc = self._lib.pv_dataset_batch(self._h, rows.ctypes.data, n, MODES[self.fz.mode], self.qlen, self.dlen,
+        rc = self._lib.pv_dataset_batch(self._h, rows.ctypes.data, n, self.fz.native_mode, self.qlen, self.dlen,
                                         self.fz.handle(), self.fz.hash_size, self.fz.unk_id, self.fz.pad_id,
                                         q_out.ctypes.data, d_out.ctypes.data, self.nthreads)
         if rc != 0:

@@ -15,19 +15,26 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 from .. import _native
-from .text import MODES, PAD, Vocab, build_vocab_counts, split_features
+from .text import MODES, PAD, Vocab, build_vocab_counts, normalize_html_line, split_features
+
+HTML_FLAG = 4  # mode bit of the native calls: HTML / word2vec normalisation first
 
 
 class Featurizer:
-    """text -> int32 ids of fixed length (clean, split, cutoff, pad, lookup/hash)."""
+    """text -> int32 ids of fixed length ([HTML-normalise,] clean, split, cutoff, pad, lookup/hash).
+
+    ``html=True`` (``Configuration.html_normalize``) runs the reference's page-text normaliser
+    (utils/word2vec_normalizer.py:116-146: unescape, strip tags, dot / punctuation rules) on
+    every text before ``clean_str`` — natively, inside the same multithreaded call."""
 
     def __init__(self, mode: str = "char", vocab: Optional[Vocab] = None, hash_size: int = 0,
-                 nthreads: int = 0):
+                 nthreads: int = 0, html: bool = False):
         if mode not in MODES:
             raise ValueError(f"mode must be one of {list(MODES)}")
         if hash_size <= 1 and vocab is None:
             raise ValueError("Featurizer needs a vocab or hash_size > 1")
         self.mode = mode
+        self.html = bool(html)
         self.vocab = vocab
         self.hash_size = hash_size if hash_size > 1 else 0
         self.nthreads = nthreads or min(16, os.cpu_count() or 4)
@@ -66,7 +73,7 @@ class Featurizer:
             return out
         enc = [t.encode("utf-8") for t in texts]
         arr = (ctypes.c_char_p * n)(*enc)
-        rc = self._lib.pv_featurize(arr, n, MODES[self.mode], length, self._vh, self.hash_size,
+        rc = self._lib.pv_featurize(arr, n, self.native_mode, length, self._vh, self.hash_size,
                                     self.unk_id, self.pad_id, out.ctypes.data, self.nthreads)
         if rc != 0:
             raise RuntimeError(f"pv_featurize failed: {rc}")
@@ -75,6 +82,10 @@ class Featurizer:
     def handle(self):
         return self._vh
 
+    @property
+    def native_mode(self) -> int:
+        return MODES[self.mode] | (HTML_FLAG if self.html else 0)
+
 
 def clean_str_native(s: str) -> str:
     lib = _native.runtime()
@@ -82,6 +93,16 @@ def clean_str_native(s: str) -> str:
     cap = 4 * len(b) + 16
     buf = ctypes.create_string_buffer(cap)
     n = lib.pv_clean_str(b, buf, cap)
+    return buf.raw[:n].decode("utf-8")
+
+
+def normalize_html_native(s: str) -> str:
+    """data/text.py::normalize_html_line through the C++ featurizer (parity tests)."""
+    lib = _native.runtime()
+    b = s.encode("utf-8")
+    n = lib.pv_normalize_html(b, None, 0)
+    buf = ctypes.create_string_buffer(int(n) + 1)
+    lib.pv_normalize_html(b, buf, int(n) + 1)
     return buf.raw[:n].decode("utf-8")
 
 
@@ -98,10 +119,11 @@ def iter_jsonl_texts(path: str, num_neg: int) -> Iterable[List[str]]:
             yield [d["q"], d["doc_corr"]] + list(d["doc_incorr"])
 
 
-def generate_vocabulary(files: Sequence[str], mode: str, num_neg: int) -> Vocab:
+def generate_vocabulary(files: Sequence[str], mode: str, num_neg: int, html: bool = False) -> Vocab:
     """Vocabulary over train+val files (dssm_cnn_v2/data_helpers.py:77-124), no cutoff.
 
     Deterministic: reserved tokens first, then by descending count, ties lexicographic.
+    ``html``: tokens of the HTML-normalised text (the featurizer's ``html=True`` input).
     """
     from collections import Counter
 
@@ -109,9 +131,9 @@ def generate_vocabulary(files: Sequence[str], mode: str, num_neg: int) -> Vocab:
     for fn in files:
         for texts in iter_jsonl_texts(fn, num_neg):
             for t in texts:
-                c.update(split_features(t, mode))
+                c.update(split_features(normalize_html_line(t) if html else t, mode))
     toks = [w for w, _ in sorted(c.items(), key=lambda kv: (-kv[1], kv[0])) if w != PAD]
     return Vocab(toks)
 
 
-__all__ = ["Featurizer", "clean_str_native", "generate_vocabulary", "iter_jsonl_texts", "build_vocab_counts"]
+__all__ = ["Featurizer", "clean_str_native", "normalize_html_native", "generate_vocabulary", "iter_jsonl_texts", "build_vocab_counts"]

@@ -134,10 +134,12 @@ class Vocab:
 
 
 def featurize_py(texts: Sequence[str], mode: str, length: int, vocab: Optional[Vocab] = None,
-                 hash_size: int = 0) -> List[List[int]]:
-    """Reference (slow) featurizer: clean -> split -> cutoff -> pad -> ids."""
+                 hash_size: int = 0, html: bool = False) -> List[List[int]]:
+    """Reference (slow) featurizer: [normalise HTML ->] clean -> split -> cutoff -> pad -> ids."""
     out = []
     for t in texts:
+        if html:
+            t = normalize_html_line(t)
         toks = pad_tokens(split_features(t, mode, cutoff=length), length)
         if hash_size > 0:
             out.append([hash_token(x, hash_size) for x in toks])

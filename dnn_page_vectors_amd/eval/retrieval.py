@@ -78,3 +78,81 @@ def distributed_recall_table(qn: torch.Tensor, pn: torch.Tensor, relevant: torch
     dist.all_reduce(hits)
     total = float(hits[-1])
     return {f"recall@{k}": float(hits[i]) / max(1.0, total) for i, k in enumerate(ks)}
+
+
+def _hits(qn: torch.Tensor, pages: torch.Tensor, relevant: torch.Tensor, ks: Sequence[int]) -> list:
+    kmax = min(max(ks), pages.shape[0])
+    _, idx = topk_cosine(qn, pages, kmax)
+    rel = relevant.view(-1, 1).to(idx.dtype)
+    return [float((idx[:, :min(k, kmax)] == rel).any(dim=1).sum()) for k in ks]
+
+
+@torch.no_grad()
+def evaluate_pairs_dataset(model, dataset, device: torch.device, ks: Sequence[int] = (1, 10, 100),
+                           max_rows: int = 0, include_negatives: bool = True, batch: int = 1024) -> Dict[str, float]:
+    """Recall@k on a real {'q', 'doc_corr', 'doc_incorr'} JSONL file (``data.dataset.JsonlPairDataset``):
+    the reference's per-epoch validation pass over ``model_validation_data``
+    (dssm_cnn_v2/cnn_dssm_th.py:189-194), measured as retrieval instead of Keras accuracy.
+
+    Every row's query is ranked against the collection of all distinct pages of the file
+    (the positives, plus the rows' negatives as distractors when ``include_negatives``);
+    a query hits when its own positive page is in the top k.  Pages are de-duplicated by
+    their featurized ids (the same page text in several rows is ONE page).
+
+    Under a process group (collective: every rank calls it) every rank featurizes the rows
+    (host work) so all ranks agree on the distinct-page numbering, encodes its contiguous
+    shard of the queries and of the distinct pages, all-gathers the page vectors
+     and the hit counts are summed: the result equals the single-process one."""
+    distributed = dist.is_initialized() and dist.get_world_size() > 1
+    rank, W = (dist.get_rank(), dist.get_world_size()) if distributed else (0, 1)
+    n = len(dataset)
+    if max_rows:
+        n = min(n, int(max_rows))
+    if n == 0:
+        raise ValueError("no rows to evaluate")
+    qs, pages, rel, index = [], [], [], {}
+
+    def page_id(ids_row) -> int:
+        key = ids_row.tobytes()
+        j = index.get(key)
+        if j is None:
+            j = index[key] = len(pages)
+            pages.append(ids_row.copy())
+        return j
+
+    import numpy as np
+
+    for s in range(0, n, batch):
+        q, d = dataset.batch(np.arange(s, min(n, s + batch)))
+        for i in range(q.shape[0]):
+            rel.append(page_id(d[i, 0]))
+            if include_negatives:
+                for j in range(1, d.shape[1]):
+                    page_id(d[i, j])
+        qs.append(q)
+    q_all = np.concatenate(qs)
+    P = len(pages)
+
+    def shard(m: int):
+        per = -(-m // W)
+        return min(m, rank * per), min(m, (rank + 1) * per)
+
+    q0, q1 = shard(n)
+    p0, p1 = shard(P)
+    enc_q = model.encode(torch.from_numpy(q_all[q0:q1]).to(device), "query", batch_size=batch) if q1 > q0 else None
+    p_local = torch.from_numpy(np.stack(pages[p0:p1])).to(device) if p1 > p0 else None
+    pv = model.encode(p_local, "doc", batch_size=batch) if p_local is not None else None
+    D = model.out_dim
+    if pv is None:
+        pv = torch.empty(0, D, device=device)
+    allp = _gather_rows(pv.float())[0] if distributed else pv
+    relevant = torch.tensor(rel[q0:q1], device=device)
+    hits = _hits(enc_q, allp, relevant, ks) if enc_q is not None else [0.0] * len(ks)
+    comm = device if (distributed and dist.get_backend() == "nccl") else torch.device("cpu")
+    h = torch.tensor(hits + [float(q1 - q0)], dtype=torch.float64, device=comm)
+    if distributed:
+        dist.all_reduce(h)
+    out = {f"recall@{k}": float(h[i]) / max(1.0, float(h[-1])) for i, k in enumerate(ks)}
+    out["queries"] = int(n)
+    out["pages"] = int(P)
+    return out

@@ -70,6 +70,7 @@ class SetupExperiment:
         from .data.featurize import generate_vocabulary
         from .io.vocab import save_vocab
 
-        v = generate_vocabulary(self.conf.input_file_list, self.conf.feature_level, self.conf.num_negative_examples)
+        v = generate_vocabulary(self.conf.input_file_list, self.conf.feature_level, self.conf.num_negative_examples,
+                                html=self.conf.html_normalize)
         save_vocab(v, self.conf)
         return v

@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from ..ops import dense as dops
 from ..ops import determinism
+from ..ops._common import precision_scope
 
 _GENERATION = [0]
 
@@ -70,6 +71,10 @@ class TwoTowerModel(nn.Module):
         ``doc_hook(d)`` is called before the query tower, so a cross-GPU page gather can be
         in flight while the query tower computes.
         """
+        with precision_scope(self.cfg):
+            return self._forward(q_ids, d_ids, seed, doc_hook)
+
+    def _forward(self, q_ids, d_ids, seed, doc_hook):
         B, S, Ld = d_ids.shape
         training = self.training
         if getattr(self.cfg, "share_doc_tower", True):
@@ -121,7 +126,7 @@ class TwoTowerModel(nn.Module):
         self.eval()
         outs = []
         try:
-            with torch.no_grad():  # no autograd graph: nothing saved for a backward
+            with torch.no_grad(), precision_scope(self.cfg):  # no autograd graph: nothing saved
                 for i in range(0, ids.shape[0], batch_size):
                     v = self.tower_forward(tower, ids[i:i + batch_size], False, 0)
                     outs.append(dops.l2_normalize(v) if normalize else v)

@@ -1,6 +1,8 @@
 """Shared helpers for the op wrappers: backend selection, pointers, streams, checks."""
 from __future__ import annotations
 
+import contextlib
+import logging
 import os
 from typing import Optional
 
@@ -21,6 +23,32 @@ def set_backend(name: str) -> None:
 
 def get_backend() -> str:
     return _FORCE or "auto"
+
+
+_FP32_NOTED = [False]
+
+
+@contextlib.contextmanager
+def precision_scope(cfg):
+    """Compute precision of a model's forward ops (``Configuration.dtype``).
+
+    ``bf16`` (default): the HIP kernels — bf16 MFMA operands, fp32 accumulation, fp32 master
+    weights and optimizer state.  ``fp32``: the reference's precision (Keras/Theano trains in
+    fp32, dssm_cnn_v2/cnn_dssm_th.py:182) — inside this scope every op runs its fp32 PyTorch
+    implementation (rocBLAS / MIOpen on the GPU), none of the bf16 HIP kernels; the fused
+    Adam kernel is fp32 already.  CPU runs are fp32 either way."""
+    global _FORCE
+    if getattr(cfg, "dtype", "bf16") != "fp32" or _FORCE == "torch":
+        yield
+        return
+    if not _FP32_NOTED[0]:
+        logging.getLogger(__name__).info("dtype=fp32: reference-precision PyTorch ops (no bf16 HIP kernels)")
+        _FP32_NOTED[0] = True
+    prev, _FORCE = _FORCE, "torch"
+    try:
+        yield
+    finally:
+        _FORCE = prev
 
 
 def use_hip(*tensors: torch.Tensor) -> bool:

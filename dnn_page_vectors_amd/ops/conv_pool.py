@@ -303,6 +303,13 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
             tbl16, wpack = compute_cache
         return _ConvPoolFn.apply(ids, table, w3, w4, bias, tbl16, wpack, float(p), int(seed), int(row_offset),
                                  bool(training), mode)
+    if ids.is_cuda and use_hip(ids, table):
+        # no silent eager fallback on the GPU: the fused kernel is built for this geometry only
+        raise NotImplementedError(
+            f"fused CDSSM conv kernel supports filter_sizes={WIDTHS}, num_filters={FW}, embedding_dim<={EP}; got "
+            f"filter_sizes={tuple(w.shape[1] for w in weights)}, num_filters={weights[0].shape[0]}, "
+            f"embedding_dim={table.shape[1]}. Use dtype='fp32' (reference-precision PyTorch ops, any geometry) "
+            f"or the supported geometry.")
     x = ref.embed_dropout(ids, table, p, seed, training, mode) if row_offset == 0 else \
         _embed_dropout_offset(ids, table, p, seed, training, mode, row_offset)
     return ref.conv_relu_maxpool(x, weights, biases)

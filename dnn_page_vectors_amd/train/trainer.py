@@ -31,6 +31,7 @@ from ..ops import dense as dops
 from ..ops import determinism
 from ..ops import grad_sink
 from ..ops import loss as lops
+from ..ops._common import precision_scope
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
 from ..parallel import placement
@@ -93,6 +94,7 @@ class Trainer:
         # bf16 compute copies written by the optimizer kernel itself (no per-step casts)
         mirror = [n for n in self.model.bf16_mirror_params() if n in self.flat.offsets] \
             if (hasattr(self.model, "bf16_mirror_params") and getattr(cfg, "optimizer_bf16_mirror", True)
+                and getattr(cfg, "dtype", "bf16") != "fp32"
                 and os.environ.get("PAGEVEC_NO_MIRROR", "0") != "1") else None
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
                             torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror)
@@ -152,6 +154,10 @@ class Trainer:
     def compute_loss(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed: int
                      ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Mean loss over the local batch and per-row P(D+|Q)."""
+        with precision_scope(self.cfg):
+            return self._compute_loss(q_ids, d_ids, seed)
+
+    def _compute_loss(self, q_ids, d_ids, seed):
         cfg = self.cfg
         B, S, _ = d_ids.shape
         range_push("forward")

@@ -34,3 +34,46 @@ def test_cli_setup_train_encode(tmp_path):
     texts.write_text("topic 3 page text\nother 1 text\n")
     out = _run(["encode", "--input", str(texts), "--output", str(tmp_path / "v.npy")] + common, tmp_path)
     assert json.loads(out.strip().splitlines()[-1])["shape"] == [2, 8]
+
+    # Recall@k on the real validation file (reference: validation pass, cnn_dssm_th.py:189-194)
+    r = json.loads(_run(["eval", "--data", "validation"] + common, tmp_path).strip().splitlines()[-1])
+    assert set(r) >= {"recall@1", "recall@10", "recall@100", "queries", "pages"} and r["queries"] > 0
+    assert 0.0 <= r["recall@1"] <= r["recall@10"] <= r["recall@100"] == 1.0  # fewer pages than 100
+    # the same numbers from 2 ranks (rows / pages sharded, page vectors all-gathered over gloo)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "-m", "dnn_page_vectors_amd.launch", "--nproc", "2", "-m",
+                        "dnn_page_vectors_amd", "eval", "--data", "validation"] + common, cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r2 = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    for k in ("recall@1", "recall@10", "recall@100", "queries", "pages"):
+        assert r2[k] == r[k], (k, r2, r)
+
+
+def test_evaluate_pairs_dataset_dedup_and_oracle(tmp_path):
+    """A model whose query vector is its page's vector finds every page at rank 1; pages that
+    repeat across rows count once."""
+    import numpy as np
+    import torch
+
+    from dnn_page_vectors_amd.data.dataset import JsonlPairDataset
+    from dnn_page_vectors_amd.data.featurize import Featurizer
+    from dnn_page_vectors_amd.eval.retrieval import evaluate_pairs_dataset
+
+    rows = [{"q": f"p{i % 5}", "doc_corr": f"p{i % 5}", "doc_incorr": ["n1", "n2", f"p{(i + 1) % 5}"]}
+            for i in range(12)]
+    f = tmp_path / "v.jsonl"
+    f.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    ds = JsonlPairDataset(str(f), Featurizer("word", hash_size=997), 1, 1, 3)
+
+    class Oracle(torch.nn.Module):
+        out_dim = 997
+
+        def encode(self, ids, tower, batch_size=0):
+            return torch.nn.functional.one_hot(ids[:, 0].long(), 997).float()
+
+    r = evaluate_pairs_dataset(Oracle(), ds, torch.device("cpu"), ks=(1, 2))
+    assert r["queries"] == 12 and r["pages"] == 7  # p0..p4 + n1 + n2
+    assert r["recall@1"] == 1.0
+    r = evaluate_pairs_dataset(Oracle(), ds, torch.device("cpu"), ks=(1,), include_negatives=False)
+    assert r["pages"] == 5

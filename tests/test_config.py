@@ -52,3 +52,24 @@ def test_json_roundtrip(tmp_path):
     p = tmp_path / "c.json"
     c.save_json(str(p))
     assert Configuration.load_json(str(p)) == c
+
+
+def test_config_validation_and_precision_scope():
+    from dnn_page_vectors_amd.ops._common import get_backend, precision_scope
+
+    with pytest.raises(ValueError):
+        Configuration(dtype="fp16")
+    with pytest.raises(ValueError):
+        Configuration(dtype="fp32", use_fp8=True)
+    with pytest.raises(ValueError):
+        Configuration(chunk_encoder="bert")
+    with pytest.raises(ValueError):
+        Configuration(num_workers=-1)
+    assert preset_config("reference_char").dtype == "fp32"      # the reference trains in fp32
+    assert preset_config("cdssm_ngram_bf16").dtype == "bf16"
+    before = get_backend()
+    with precision_scope(Configuration(dtype="fp32")):
+        assert get_backend() == "torch"                         # no bf16 HIP kernel inside
+    assert get_backend() == before
+    with precision_scope(Configuration(dtype="bf16")):
+        assert get_backend() == before

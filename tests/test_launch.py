@@ -66,3 +66,20 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1",
                         "--warmup", "0"], env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "world size 1 != --gpus 2" in (r.stderr + r.stdout)
+
+
+def test_comm_micro_gloo_and_channel_sweep():
+    """tools/comm_micro.py (the RCCL tuning table for the 8-GPU node) runs its collectives
+    over gloo at W = 2, and --sweep-channels relaunches once per NCCL_MIN_NCHANNELS value."""
+    import json
+
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "comm_micro.py"), "--sweep-channels", "2", "4",
+                        "--nproc", "2", "--device", "cpu", "--scale", "0.002", "--iters", "1", "--warmup", "0",
+                        "--models", "cdssm", "--bucket-mb", "1"], env=env, cwd=REPO, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 2 * 3  # per channel setting: 1 all-reduce + 2 all-gathers
+    assert {x["env"].get("NCCL_MIN_NCHANNELS") for x in recs} == {"2", "4"}
+    assert all(x["world"] == 2 and x["ms"] > 0 for x in recs)

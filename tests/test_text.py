@@ -111,3 +111,79 @@ def test_native_char_vocab_fuzz(texts, L):
     fz._lib.pv_vocab_add(fz.handle(), "ü".encode(), 77)  # edit after the table was built
     got2 = fz(["über"], 4)
     assert got2[0, 0] == 77
+
+
+# ---- HTML normalisation in the native featurizer (cfg.html_normalize) -----------------------
+HTML_GOLD = [
+    ("Hello &amp; <b>World</b>... Foo", "hello world . foo"),
+    ("<p>Caf&eacute; &lt;b&gt;x&lt;/b&gt; &#39;q&#39; &#x41;</p>", "café x q a"),
+    ("<script>var a = 1 < 2;</script>text", "var a 1 2 text"),
+    ("a;lt;b ;amp; c", "ab c"),
+    ("<!-- c -->x<?pi?>y<!DOCTYPE html>z", "xyz"),
+    ("Ünïcödé   Straße  €5.00!!! ...", "ünïcödé straße €5 . 00 . "),
+    ("&notit; &amp &ampx &#0; &#x110000; &#128;", " it x €"),
+    ("<a href='x>y'>link</a> rest", "link rest"),
+    ("5 < 6 and 7 > 3", "5 6 and 7 3"),
+]
+
+
+def test_html_normalize_native_golden():
+    from dnn_page_vectors_amd.data.featurize import normalize_html_native
+
+    for src, want in HTML_GOLD:
+        assert T.normalize_html_line(src) == want, src
+        assert normalize_html_native(src) == want, src
+
+
+_WORDS = st.sampled_from(["page", "Straße", "NYC", "$25.00", "a-b_c", "x...y", "über", "Ω", "#1", "é", "12", "."])
+_ENTS = st.sampled_from(["&amp;", "&lt;", "&gt;", "&quot;", "&#39;", "&nbsp;", "&eacute;", "&#x41;", "&#8364;",
+                         "&copy", "&notin;", "&bogus;", "&", ";lt;", ";amp;"])
+_TAGS = st.sampled_from(["<b>", "</b>", "<p class=\"x\">", "<br/>", "<a href='u?a=1&b=2'>", "</a>", "<!-- note -->",
+                         "<img src=x.png alt=\"a > b\">", "</ p>", "<?php x ?>", "<!DOCTYPE html>", " < ", " > "])
+_SEPS = st.sampled_from([" ", "  ", "\t", "\n", "", ", ", "!", "..."])
+
+
+@st.composite
+def _html_line(draw):
+    parts = draw(st.lists(st.one_of(_WORDS, _ENTS, _TAGS, _SEPS), min_size=0, max_size=24))
+    if draw(st.booleans()):
+        parts.insert(draw(st.integers(0, len(parts))), "<script>if (a < b) { x = '&amp;'; }</script>")
+    return "".join(parts)
+
+
+@settings(max_examples=300, deadline=None)
+@given(_html_line())
+def test_html_normalize_native_fuzz(line):
+    """The C++ normaliser equals data/text.py::normalize_html_line (Python's html.unescape +
+    HTMLParser) on generated HTML fragments: tags with quoted / unquoted attributes, end tags,
+    comments, declarations, processing instructions, named / numeric / legacy / unknown
+    entities, script content, dot runs, tabs and newlines."""
+    from dnn_page_vectors_amd.data.featurize import normalize_html_native
+
+    assert normalize_html_native(line) == T.normalize_html_line(line)
+
+
+@pytest.mark.parametrize("mode", ["word", "ngram", "char"])
+def test_featurizer_html_mode_matches_python(mode):
+    texts = [src for src, _ in HTML_GOLD] + ["plain text", ""]
+    fz = Featurizer(mode, hash_size=1000, html=True)
+    got = fz(texts, 24)
+    want = np.array(T.featurize_py(texts, mode, 24, hash_size=1000, html=True), dtype=np.int32)
+    np.testing.assert_array_equal(got, want)
+    # and the flag matters: without it the markup is tokenised
+    assert not np.array_equal(Featurizer(mode, hash_size=1000)(texts, 24), got)
+
+
+def test_dataset_html_mode(tmp_path):
+    from dnn_page_vectors_amd.data.dataset import JsonlPairDataset
+
+    p = tmp_path / "d.jsonl"
+    rows = [{"q": "caf&eacute; <b>menu</b>", "doc_corr": "<p>The Caf&eacute; &amp; bar...</p>",
+             "doc_incorr": ["<i>x</i>", "y &lt; z", "<!-- c -->w"]}]
+    p.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    fz = Featurizer("word", hash_size=500, html=True)
+    ds = JsonlPairDataset(str(p), fz, 6, 10, 3)
+    q, d = ds.batch(np.array([0]))
+    np.testing.assert_array_equal(q[0], T.featurize_py([rows[0]["q"]], "word", 6, hash_size=500, html=True)[0])
+    want = T.featurize_py([rows[0]["doc_corr"]] + rows[0]["doc_incorr"], "word", 10, hash_size=500, html=True)
+    np.testing.assert_array_equal(d[0], np.array(want, dtype=np.int32))
