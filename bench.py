@@ -51,6 +51,8 @@ MODEL_DESC = {
     "cdssm_char": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), char level (reference default), ~100-symbol "
                   "vocab, Lq=250, Ld=5000, J=3",
     "chunked": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, MLP 512-512-128 fp8 e4m3, mean-pool",
+    "chunked_cdssm": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, CDSSM conv tower per chunk (fused "
+                     "conv kernel), mean-pool",
 }
 
 
@@ -76,13 +78,14 @@ def parse():
     ap.add_argument("--quality-steps", type=int, default=-1,
                     help="after the timed steps, keep training (untimed, fresh synthetic batches, eager) until "
                          "this many optimizer steps in total, then measure Recall@10 on held-out pairs; "
-                         "-1 = auto (1000 for cdssm / mlp, 0 = none for bert / chunked)")
+                         "-1 = auto (1000 for cdssm / mlp, 500 for chunked / cdssm_char, 200 for bert)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="deterministic reduction mode (ops/determinism.py): order-free fixed-point "
                          "gradient sums, one stream, no hipGraph")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launch / process group / JSON path (gloo, eager ops, tiny model)")
-    ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "cdssm_char"],
+    ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "chunked_cdssm",
+                                                         "cdssm_char"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5; "
                          "cdssm_char = the reference's default run (char level, 250 / 5000 tokens), per-GPU "
                          "batch --batch (default 1024 here)")
@@ -162,7 +165,7 @@ def main():
     if a.backend == "torch":
         set_backend("torch")
     preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "chunked": "longpage_fp8",
-              "cdssm_char": "reference_char"}[a.model]
+              "chunked_cdssm": "longpage_cdssm", "cdssm_char": "reference_char"}[a.model]
     cfg = preset_config(preset)
     if a.loss is None:
         a.loss = "explicit" if a.model == "cdssm_char" else "cross_gpu"
@@ -182,9 +185,10 @@ def main():
     model = build_model(cfg, V)
     # the capture happens after 2 eager steps: only inside the untimed warmup
     if a.graph < 0:
-        a.graph = 0 if a.model in ("cdssm", "cdssm_char") else 1
+        a.graph = 0 if a.model in ("cdssm", "cdssm_char", "chunked_cdssm") else 1
     if a.quality_steps < 0:
-        a.quality_steps = 1000 if a.model in ("cdssm", "mlp") else 0
+        a.quality_steps = {"cdssm": 1000, "mlp": 1000, "chunked": 500, "chunked_cdssm": 500, "cdssm_char": 500,
+                           "bert": 200}[a.model]
     # pre-built device-resident batches and nothing eager between replays: no per-replay fence
     trainer = Trainer(cfg, model, dev, graph=bool(a.graph) and a.warmup > Trainer.GRAPH_WARMUP, graph_fence=False)
 
@@ -245,6 +249,10 @@ def main():
     # argmax windows — so a dense "3 x forward" count would overstate the work done)
     if a.model in ("cdssm", "cdssm_char"):
         per_pair = cdssm_flops_per_sample(cfg)
+        train_mult = None
+    elif a.model == "chunked_cdssm":  # query tower + (1+J) pages x num_chunks conv towers of chunk_len
+        C = -(-cfg.document_length // cfg.chunk_len)
+        per_pair = cdssm_flops_per_sample(cfg.replace(document_length=cfg.chunk_len, J=(1 + cfg.J) * C - 1))
         train_mult = None
     elif a.model == "bert":
         from dnn_page_vectors_amd.models.bert_dual import bert_flops_per_token

@@ -324,10 +324,17 @@ def preset_config(name: str) -> Configuration:
                              embedding_dim=512, mlp_dims=(512, 512, 128), chunk_len=512,
                              num_chunks=8, query_length=45, document_length=4096,
                              batch_size=512, dtype="bf16", use_fp8=True, loss_mode="cross_gpu", J=0)
+    if name in ("longpage_cdssm", "config5_cdssm"):
+        # config 5 with the reference's conv tower as the chunk encoder (8 x 512-trigram chunks
+        # through the fused conv kernel, chunk vectors mean-pooled)
+        return Configuration(model="chunked", chunk_encoder="cdssm", feature_level="ngram",
+                             vocab_hash_size=30000, chunk_len=512, num_chunks=8, query_length=45,
+                             document_length=4096, batch_size=512, dtype="bf16", loss_mode="cross_gpu",
+                             J=0, inbatch_gamma=40.0)
     if name in ("lstm", "legacy_lstm"):
         return Configuration(model="lstm", feature_level="word", batch_size=64, nb_epoch=2)
     raise KeyError(f"unknown preset {name!r}")
 
 
 PRESETS = ["reference_char", "reference_v1", "tiny_dssm_cpu", "cdssm_ngram_bf16",
-           "mlp_xgpu", "bert_dp8", "longpage_fp8", "lstm"]
+           "mlp_xgpu", "bert_dp8", "longpage_fp8", "longpage_cdssm", "lstm"]

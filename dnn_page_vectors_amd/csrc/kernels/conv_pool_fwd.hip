@@ -51,8 +51,11 @@ constexpr int R = PV_CONV_R;       // window rows per chunk (7 blocks; 3 staged 
 static_assert(R % 16 == 0, "chunk = whole 16-window blocks");
 constexpr int CROWS = R + 3;       // LDS rows per chunk
 constexpr int NTHREADS = 512;
-constexpr int PPT = (CROWS * PIECES + NTHREADS - 1) / NTHREADS;  // pieces per thread (4)
-constexpr int IDS_PT = (CROWS + NTHREADS - 1) / NTHREADS;        // ids per thread (1)
+// staging work per thread for a workgroup of NTH threads (v5: 256 threads, one wave per SIMD)
+template <int NTH> constexpr int ppt_of() { return (CROWS * PIECES + NTH - 1) / NTH; }  // 16-byte pieces
+template <int NTH> constexpr int ids_of() { return (CROWS + NTH - 1) / NTH; }           // token ids
+constexpr int PPT = ppt_of<NTHREADS>();     // pieces per thread (4)
+constexpr int IDS_PT = ids_of<NTHREADS>();  // ids per thread (1)
 
 struct Params {
   const int* ids;              // (N, L)
@@ -105,10 +108,11 @@ __device__ __forceinline__ void advance(Cursor& cu) {
 }
 
 // Load the token ids of chunk (n,c) row `r` for this thread.
-__device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int (&tok)[IDS_PT]) {
+template <int NTH = NTHREADS>
+__device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int (&tok)[ids_of<NTH>()]) {
 #pragma unroll
-  for (int i = 0; i < IDS_PT; ++i) {
-    int r = threadIdx.x + i * NTHREADS;
+  for (int i = 0; i < ids_of<NTH>(); ++i) {
+    int r = threadIdx.x + i * NTH;
     int t = cu.c * R + r;
     tok[i] = (cu.n < p.N && r < CROWS && t < p.L) ? p.ids[(size_t)cu.n * p.L + t] : -1;
     PV_CHECK(tok[i] < p.V && (tok[i] >= 0 || !(cu.n < p.N && r < CROWS && t < p.L)), PV_ERR_ID);
@@ -117,11 +121,11 @@ __device__ __forceinline__ void load_ids(const Params& p, const Cursor& cu, int 
 
 // Issue the 16-byte table loads for this thread's pieces of chunk (n,c).
 // tok_of_row(r) reads another thread's id through LDS scratch (ids_lds).
-template <int DBG>
-__device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u32x4 (&v)[PPT]) {
+template <int DBG, int NTH = NTHREADS>
+__device__ __forceinline__ void load_rows(const Params& p, const int* ids_lds, u32x4 (&v)[ppt_of<NTH>()]) {
 #pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    int q = threadIdx.x + i * NTHREADS;
+  for (int i = 0; i < ppt_of<NTH>(); ++i) {
+    int q = threadIdx.x + i * NTH;
     int r = q / PIECES, pc = q - r * PIECES;
     int tok = (q < CROWS * PIECES) ? ids_lds[r] : -1;
     if constexpr ((DBG & 128) != 0) {  // ablation: synthetic non-zero rows, no table gather
@@ -148,11 +152,12 @@ __device__ __forceinline__ bool dm_on(const Params& p) {
   return DM < 0 ? p.thr > 0 : DM != 0;
 }
 
-template <int DBG, int DM = -1>
-__device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsigned* hrow, u32x4 (&v)[PPT]) {
+template <int DBG, int DM = -1, int NTH = NTHREADS>
+__device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsigned* hrow,
+                                           u32x4 (&v)[ppt_of<NTH>()]) {
 #pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    int q = threadIdx.x + i * NTHREADS;
+  for (int i = 0; i < ppt_of<NTH>(); ++i) {
+    int q = threadIdx.x + i * NTH;
     if (q < CROWS * PIECES) {
       int r = q / PIECES, pc = q - r * PIECES;
       u32x4 x = v[i];
@@ -426,8 +431,9 @@ __device__ __forceinline__ float max_tagged(float m, float x, unsigned keep, uns
   return r;
 }
 
-template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1, bool MIX = false>
+template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1, bool MIX = false, int NTH = NTHREADS>
 __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4base, char* xl0, int* ids_lds) {
+  constexpr int IDS_PT = ids_of<NTH>(), PPT = ppt_of<NTH>();
   const int lane = threadIdx.x & 63;
   constexpr int A3 = N3 > 0 ? N3 : 1, A4 = N4 > 0 ? N4 : 1;
   bf16x8 w3[A3][S3];
@@ -456,32 +462,32 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
   unsigned hrw[IDS_PT];
   u32x4 stage[PPT];
   // prologue: chunk 0 -> xl[0]; chunk 1 rows -> regs; chunk 2 ids + hashes -> LDS slot 0; chunk 3 ids -> regs
-  load_ids(p, cur, tok);
+  load_ids<NTH>(p, cur, tok);
 #pragma unroll
   for (int i = 0; i < IDS_PT; ++i) {
-    const int r = threadIdx.x + i * NTHREADS;
+    const int r = threadIdx.x + i * NTH;
     if (r < CROWS) {
       ids_lds[r] = tok[i];
       hs[r] = row_hash<DM>(p, cur, r);
     }
   }
   __syncthreads();
-  load_rows<DBG>(p, ids_lds, stage);
-  store_rows<DBG, DM>(p, xl0, hs, stage);
-  load_ids(p, c1, tok);
+  load_rows<DBG, NTH>(p, ids_lds, stage);
+  store_rows<DBG, DM, NTH>(p, xl0, hs, stage);
+  load_ids<NTH>(p, c1, tok);
 #pragma unroll
   for (int i = 0; i < IDS_PT; ++i) {
-    const int r = threadIdx.x + i * NTHREADS;
+    const int r = threadIdx.x + i * NTH;
     if (r < CROWS) {
       ids_lds[CROWS + r] = tok[i];
       hs[CROWS + r] = row_hash<DM>(p, c1, r);
     }
   }
-  load_ids(p, c2, tok);
+  load_ids<NTH>(p, c2, tok);
 #pragma unroll
-  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c2, threadIdx.x + i * NTHREADS);
+  for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c2, threadIdx.x + i * NTH);
   __syncthreads();
-  load_rows<DBG>(p, ids_lds + CROWS, stage);  // rows of c1
+  load_rows<DBG, NTH>(p, ids_lds + CROWS, stage);  // rows of c1
   // slot bookkeeping: ids/hashes of chunk c live in slot (c parity); the stage regs hold c1
   int par = 0;  // parity of `cur` (xl buffer and id/hash slot of cur)
   const int nw3 = p.L - 2, nw4 = p.L - 3;
@@ -718,20 +724,20 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
       reset_state();
     }
     // stage chunk c1 into the idle buffer (its hashes are in slot par^1), publish c2's ids/hashes
-    store_rows<DBG, DM>(p, xl0 + (par ^ 1) * (CROWS * ROWB), hs + (par ^ 1) * CROWS, stage);
+    store_rows<DBG, DM, NTH>(p, xl0 + (par ^ 1) * (CROWS * ROWB), hs + (par ^ 1) * CROWS, stage);
 #pragma unroll
     for (int i = 0; i < IDS_PT; ++i) {
-      const int r = threadIdx.x + i * NTHREADS;
+      const int r = threadIdx.x + i * NTH;
       if (r < CROWS) {
         ids_lds[par * CROWS + r] = tok[i];  // c2 has the parity of cur
         hs[par * CROWS + r] = hrw[i];
       }
     }
     if constexpr ((DBG & 64) == 0) __syncthreads();
-    load_rows<DBG>(p, ids_lds + par * CROWS, stage);  // rows of c2
-    load_ids(p, c3, tok);
+    load_rows<DBG, NTH>(p, ids_lds + par * CROWS, stage);  // rows of c2
+    load_ids<NTH>(p, c3, tok);
 #pragma unroll
-    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c3, threadIdx.x + i * NTHREADS);
+    for (int i = 0; i < IDS_PT; ++i) hrw[i] = row_hash<DM>(p, c3, threadIdx.x + i * NTH);
     cur = c1;
     c1 = c2;
     c2 = c3;
@@ -812,6 +818,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd4_kernel(Params p) {
     run_wave2<0, 2, PF, DBG, OPT, DM, true>(p, 0, 8, xl, ids_lds);
   } else {
     run_wave2<0, 2, PF, DBG, OPT, DM>(p, 0, wave == 3 ? 6 : 2 * (wave - 4), xl, ids_lds);
+  }
+}
+
+// v5 = v4's tile sets with ONE wave per SIMD: a 256-thread workgroup whose wave s runs the
+// union of v4's waves s and s+4 (SIMD s's whole tile set, ~224 weight VGPRs of a 512-entry
+// budget).  The A fragments of a 16-window block are read from LDS once per SIMD instead of
+// twice (52 instead of 104 ds_read_b128 per block and CU), barriers join 4 waves instead of 8;
+// latency is hidden by the wave's own independent accumulator chains (5 tiles) and the
+// prefetched A fragments.
+template <int PF, int DBG, int OPT, int DM>
+__global__ __launch_bounds__(256, 1) void conv_pool_fwd5_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
+  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < 3) {
+    run_wave2<3, 2, PF, DBG, OPT, DM, false, 256>(p, 3 * wave, 2 * wave, xl, ids_lds);  // k3 3w..3w+2, k4 2w..2w+1
+  } else {
+    run_wave2<0, 4, PF, DBG, OPT, DM, true, 256>(p, 0, 6, xl, ids_lds);               // k4 6-8 + mixed
   }
 }
 
@@ -948,6 +974,23 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
         case 1: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
         case 2: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 2>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
         default: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 3>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+      }
+      break;
+    }
+    case 8192:      // v5: one wave per SIMD (256-thread workgroups), OPT 13
+    case 8192 + 2:  // v5 + software-pipelined epilogue (OPT 15)
+    case 8192 + 3: {  // v5 + PIPE, A prefetch depth 3
+      const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+      if (dm != 1 && dm != 0) return -3;  // A/B variant: the bench's dropout modes only
+      if (dbg == 8192) {
+        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 13, 1>), dim3(grid), dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 13, 0>), dim3(grid), dim3(256), 0, st, p);
+      } else if (dbg == 8192 + 2) {
+        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 15, 1>), dim3(grid), dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 15, 0>), dim3(grid), dim3(256), 0, st, p);
+      } else {
+        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<3, 0, 15, 1>), dim3(grid), dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<3, 0, 15, 0>), dim3(grid), dim3(256), 0, st, p);
       }
       break;
     }

@@ -10,6 +10,17 @@ non-empty chunk vectors (empty = all padding; masked out).  Chunks are independe
 a page could be split over CUs or GPUs with one all-reduce of partial sums (the
 "context parallel" of this workload) — at 288 GB per MI355X it is not
 needed.  Queries use the same tower type without chunking.
+
+``chunk_encoder`` selects the per-chunk encoder ("encode each chunk (CDSSM or
+MLP or BERT)"):
+* ``"mlp"``   — the DSSM MLP tower above (config 5 as benchmarked; fp8 e4m3 dense layers
+  with ``use_fp8``);
+* ``"cdssm"`` — the reference's conv tower (cnn_dssm_th.py:83-139) on every chunk through
+  the fused gather -> dropout -> conv -> max-pool HIP kernel (the N x C chunks are the
+  kernel's samples; each chunk max-pools over its own windows, like the reference's global
+  max-pool over a page, cnn_dssm_th.py:94), then Dense + ReLU; chunk vectors mean-pooled
+  as above.  Needs the CDSSM geometry (embedding_dim <= 104, filters (3, 4) x 150):
+  preset ``longpage_cdssm``.
 """
 from __future__ import annotations
 
@@ -18,6 +29,7 @@ import torch.nn as nn
 
 from ..ops import dense as dops
 from .base import TwoTowerModel
+from .cdssm import CDSSMTower
 from .mlp_dssm import MLPTower
 
 
@@ -29,14 +41,23 @@ class ChunkedPageEncoder(TwoTowerModel):
         self.vocab_size = vocab_size
         self.chunk_len = int(cfg.chunk_len)
         self.num_chunks = int(cfg.num_chunks)
-        self.query_tower = MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)
-        self.doc_towers = nn.ModuleList([MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)])
+        self.encoder = getattr(cfg, "chunk_encoder", "mlp")
+        if self.encoder == "cdssm":
+            if cfg.use_fp8:
+                raise ValueError("chunk_encoder='cdssm' runs the bf16 conv kernel: set use_fp8=False")
+            self.query_tower = CDSSMTower(vocab_size, cfg, gen)
+            self.doc_towers = nn.ModuleList([CDSSMTower(vocab_size, cfg, gen)])
+        else:
+            self.query_tower = MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)
+            self.doc_towers = nn.ModuleList([MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)])
 
     @property
     def out_dim(self) -> int:
-        return self.cfg.mlp_dims[-1]
+        return self.cfg.hidden_dims if self.encoder == "cdssm" else self.cfg.mlp_dims[-1]
 
     def bf16_mirror_params(self):
+        if self.encoder == "cdssm":
+            return []  # the conv tower casts its bf16 table copy in build_cache
         return [n for n, _ in self.named_parameters() if n.endswith(".embedding")]
 
     def build_cache(self):
@@ -44,16 +65,21 @@ class ChunkedPageEncoder(TwoTowerModel):
             return {}
         return {"query": self.query_tower.build_cache(), "doc0": self.doc_towers[0].build_cache()}
 
+    def _tower(self, t, ids, training, seed, cache):
+        if self.encoder == "cdssm":
+            return t(ids, training, seed, cache)
+        return t(ids, cache)
+
     def tower_forward(self, tower: str, ids: torch.Tensor, training: bool, seed: int, slot: int = 0) -> torch.Tensor:
         cache = self.compute_cache()
         if tower == "query":
-            return self.query_tower(ids, cache.get("query"))
+            return self._tower(self.query_tower, ids, training, seed, cache.get("query"))
         N, L = ids.shape
         C = max(1, -(-L // self.chunk_len))
         pad = C * self.chunk_len - L
         if pad:
             ids = torch.nn.functional.pad(ids, (0, pad))
         chunks = ids.reshape(N * C, self.chunk_len)
-        v = self.doc_towers[0](chunks, cache.get("doc0")).view(N, C, -1)
+        v = self._tower(self.doc_towers[0], chunks, training, seed, cache.get("doc0")).view(N, C, -1)
         # masked mean over the non-empty chunks (one fused HIP kernel per direction on GPU)
         return dops.chunk_mean_pool(v, ids.reshape(N, C * self.chunk_len), self.chunk_len)

@@ -95,21 +95,32 @@ def _grid(device: torch.device) -> int:
     return _grid_cache[idx]
 
 
-# dTable sort: the in-tree LSD radix sort (radix_sort.hip: graph-safe, no memsets / atomics);
-# PAGEVEC_SORT=rocprim selects rocPRIM's onesweep sort (A/B and reference only: its
-# hipMemsetAsync-reset state faulted under long hipGraph replays, docs/PERF.md)
-SORT_IMPL = os.environ.get("PAGEVEC_SORT", "rsort")
+# dTable sort: the one-pass counting sort for keys < 2^15 (count_sort.hip: 4 launches, one
+# 2^15-bin LDS histogram per block; not stable) by default, the stable in-tree LSD radix
+# sort (radix_sort.hip) for wider keys and in deterministic mode; both graph-safe (no
+# memsets / global atomics).  PAGEVEC_SORT=rsort forces the LSD sort, =rocprim rocPRIM's
+# onesweep sort (A/B and reference only: its hipMemsetAsync-reset state faulted under long
+# hipGraph replays, docs/PERF.md)
+SORT_IMPL = os.environ.get("PAGEVEC_SORT", "csort")
 
 
 def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor, end_bit: int,
                     impl: Optional[str] = None) -> None:
-    """Stable sort of ``keys`` (int16 / int32, read as unsigned) by bits [0, end_bit): sorted
-    keys -> ``skeys``, their input positions -> ``svals`` (int32)."""
+    """Sort of ``keys`` (int16 / int32, read as unsigned) by bits [0, end_bit): sorted keys ->
+    ``skeys``, their input positions -> ``svals`` (int32).  Stable except for the counting
+    sort (``csort``: equal keys in arbitrary order; the dTable reduce sums them either way)."""
     L_ = lib()
     M = keys.numel()
     s = stream(keys.device)
     kb = keys.element_size()
     impl = impl or SORT_IMPL
+    if impl == "csort" and (end_bit > 15 or determinism.enabled() or keys.data_ptr() % 16):
+        impl = "rsort"  # stable order needed / keys too wide for one LDS histogram
+    if impl == "csort":
+        tb = int(L_.pv_csort_temp_bytes(M, end_bit))
+        temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
+        check(L_.pv_csort_pairs(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, kb, s), "pv_csort_pairs")
+        return
     if impl == "rocprim":
         if kb == 2:
             tb = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))

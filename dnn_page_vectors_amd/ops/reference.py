@@ -103,6 +103,32 @@ def conv_relu_maxpool(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: 
     return torch.cat(outs, dim=1), torch.cat(args, dim=1)
 
 
+def conv_maxpool_grads_at(x: torch.Tensor, weights: Sequence[torch.Tensor], pooled: torch.Tensor,
+                          argmax: torch.Tensor, gpool: torch.Tensor):
+    """fp32 backward of ``conv_relu_maxpool`` through GIVEN argmax windows (e.g. the fused
+    kernel's own, so near-ties in the forward cannot make the comparison skip): with
+    g = gpool * [pooled > 0],  dW[f, j] = sum_n g[n, f] x[n, a + j],  db[f] = sum_n g[n, f],
+    dx[n, a + j] += g[n, f] W[f, j].  Returns ([dW_i], [db_i], dx)."""
+    N, L, E = x.shape
+    g = gpool * (pooled > 0).to(gpool.dtype)
+    dx = torch.zeros_like(x)
+    dws, dbs = [], []
+    c = 0
+    for w in weights:
+        Fk, k, _ = w.shape
+        gi = g[:, c:c + Fk]
+        a = argmax[:, c:c + Fk].long()
+        pos = a.unsqueeze(2) + torch.arange(k, device=x.device)           # (N, F, k)
+        win = x[torch.arange(N, device=x.device)[:, None, None], pos]     # (N, F, k, E)
+        dws.append(torch.einsum("nf,nfke->fke", gi, win))
+        dbs.append(gi.sum(0))
+        contrib = gi[:, :, None, None] * w.unsqueeze(0)                   # (N, F, k, E)
+        dx.index_put_((torch.arange(N, device=x.device)[:, None, None].expand_as(pos), pos), contrib,
+                      accumulate=True)
+        c += Fk
+    return dws, dbs, dx
+
+
 def cdssm_tower_features(ids, table, weights, biases, p, seed, training, mode="element"):
     x = embed_dropout(ids, table, p, seed, training, mode)
     pooled, _ = conv_relu_maxpool(x, weights, biases)

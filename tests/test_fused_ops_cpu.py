@@ -48,3 +48,21 @@ def test_inbatch_loss_reduce_cpu():
     torch.testing.assert_close(lm, per_row.mean())
     torch.testing.assert_close(P2, P)
     torch.testing.assert_close(acc, (P > 0.5).float().mean())
+
+
+def test_conv_grads_at_given_argmax_match_autograd():
+    """ops/reference.py::conv_maxpool_grads_at (the GPU tests' reference backward through the
+    kernel's argmax) == autograd of the reference conv when given the reference's argmax."""
+    torch.manual_seed(0)
+    N, L, E, F = 4, 20, 6, 5
+    x = torch.randn(N, L, E, requires_grad=True)
+    w3 = torch.randn(F, 3, E, requires_grad=True)
+    w4 = torch.randn(F, 4, E, requires_grad=True)
+    b3 = torch.randn(F, requires_grad=True)
+    b4 = torch.randn(F, requires_grad=True)
+    p, a = ref.conv_relu_maxpool(x, [w3, w4], [b3, b4])
+    g = torch.randn_like(p)
+    (p * g).sum().backward()
+    dws, dbs, dx = ref.conv_maxpool_grads_at(x.detach(), [w3.detach(), w4.detach()], p.detach(), a, g)
+    for got, want in ((dws[0], w3.grad), (dws[1], w4.grad), (dbs[0], b3.grad), (dbs[1], b4.grad), (dx, x.grad)):
+        torch.testing.assert_close(got, want)

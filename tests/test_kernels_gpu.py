@@ -55,15 +55,18 @@ def test_conv_pool_fwd_bwd(N, L, p, mode):
     agree = (argmax == ar) | ~live
     assert agree.float().mean() > 0.97
     g = torch.randn_like(pooled)
-    # backward consistency: use the kernel's argmax in both to avoid tie-breaking noise
     (pooled * g).sum().backward()
-    (pr * g).sum().backward()
-    torch.testing.assert_close(b3.grad, b3r.grad, rtol=2e-3, atol=2e-3)
-    torch.testing.assert_close(b4.grad, b4r.grad, rtol=2e-3, atol=2e-3)
-    if agree.all():
-        torch.testing.assert_close(w3.grad, w3r.grad, rtol=1e-3, atol=2e-3)
-        torch.testing.assert_close(w4.grad, w4r.grad, rtol=1e-3, atol=2e-3)
-        torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
+    # the fp32 reference backward scatters through the KERNEL's argmax windows, so every
+    # gradient is compared on every shape (near-ties in the forward cannot skip the check)
+    xr = ref.embed_dropout(ids, tr, p, seed, True, mode)
+    dws, dbs, dx = ref.conv_maxpool_grads_at(xr.detach(), [w3r.detach(), w4r.detach()], pooled.detach(), argmax,
+                                             g)
+    xr.backward(dx)
+    torch.testing.assert_close(b3.grad, dbs[0], rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(b4.grad, dbs[1], rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(w3.grad, dws[0], rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(w4.grad, dws[1], rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
 
 
 @pytest.mark.parametrize("variant", [5, 7])
@@ -429,22 +432,46 @@ def test_fp8_linear():
 
 @pytest.mark.parametrize("preset", ["bert_dp8", "longpage_fp8"])
 def test_big_model_train_steps_gpu(preset):
+    """Configs 4 / 5 on the HIP path: (1) the full-model parameter gradient of one step
+    matches the fp32 PyTorch implementation of the same model, loss and weights (dtype
+    fp32 precision scope: rocBLAS / MIOpen ops, no bf16 / fp8 kernel); (2) training on one
+    fixed (memorisable) batch drives the loss down — the optimizer sees useful gradients."""
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
     from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.ops._common import precision_scope
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
     pdist.init_distributed()
     cfg = preset_config(preset)
     if preset == "bert_dp8":
-        cfg = cfg.replace(bert_layers=2, batch_size=16, document_length=128)
+        cfg = cfg.replace(bert_layers=2, batch_size=16, document_length=128, bert_dropout=0.0, lr=3e-4)
     else:
         cfg = cfg.replace(batch_size=64, document_length=2048)
+    torch.manual_seed(5)
     tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device(DEV))
     data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=256), DEV)
-    losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(6)]
+    q, d = data.batch(cfg.batch_size)
+
+    def grad(fp32: bool) -> torch.Tensor:
+        tr.flat.zero_grad()
+        with precision_scope(cfg.replace(dtype="fp32", use_fp8=False) if fp32 else cfg):
+            loss, _ = tr.compute_loss(q, d, 0)
+            loss.backward()
+        torch.cuda.synchronize()
+        return tr.flat.grad.detach().clone()
+
+    g_hip, g_ref = grad(False), grad(True)
+    rel = float((g_hip - g_ref).norm() / g_ref.norm())
+    cos = float(torch.nn.functional.cosine_similarity(g_hip, g_ref, dim=0))
+    print(f"{preset}: grad rel err {rel:.4f} cos {cos:.5f}")
+    assert torch.isfinite(g_hip).all()
+    assert rel < (0.15 if cfg.use_fp8 else 0.05) and cos > (0.99 if cfg.use_fp8 else 0.999), (rel, cos)
+    losses = [float(tr.train_step(q, d)["loss"]) for _ in range(25)]
+    print(f"{preset}: loss {losses[0]:.4f} -> {losses[-1]:.4f}")
     assert all(l == l for l in losses)
+    assert losses[-1] < 0.7 * losses[0], losses
 
 
 def test_inbatch_loss_wide_rows_path():
@@ -757,11 +784,11 @@ def test_embedding_bag_counts_split_k():
 
 def test_cdssm_recall_quality_guard():
     """Training-quality guard for the headline config: 1000 steps of CDSSM-300d (B 4096,
-    cross-GPU loss on one rank) on fresh synthetic batches must reach Recall@10 >= 0.175 on
-    held-out pairs.  The float-atomic gradient sums make runs differ: 0.183-0.240 over 7
-    round-2 runs (tools/gpu_runs/recall_ab.sh, with and without the query side stream).  A
-    weaker dropout group hash that still passed the mask rate / correlation tests reached
-    0.15-0.18 (round 1)."""
+    cross-GPU loss on one rank, in-batch softmax scale 40) on fresh synthetic batches must
+    reach Recall@10 >= 0.35 on held-out pairs.  The float-atomic gradient sums make runs
+    differ: 0.41-0.44 over the round-2/3 driver and builder benches (BENCH_r02.json 0.413,
+    round-3 first run 0.443).  A kernel regression that halves the learning signal lands
+    near the reference-head plateau (~0.15-0.2, profiles/quality_r2_final.md) and fails."""
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
     from dnn_page_vectors_amd.eval.retrieval import recall_at_k
@@ -788,7 +815,7 @@ def test_cdssm_recall_quality_guard():
     assert float(m["loss"]) == float(m["loss"])
     print(f"recall@10 after 1000 steps: {r:.4f} (exact top-k {r_ref:.4f})")
     assert abs(r - r_ref) <= 2.0 / 2048, (r, r_ref)
-    assert r >= 0.175, r
+    assert r >= 0.35, r
 
 
 def test_resume_restores_device_adam_step(tmp_path):
@@ -862,6 +889,29 @@ def test_radix_sort_matches_stable_sort(n, kbytes, end_bit, impl):
     assert torch.equal(svals.cpu().to(torch.int64), ref_i)
 
 
+@pytest.mark.parametrize("n,kbytes,end_bit", [(1, 2, 15), (100, 2, 15), (16_385, 2, 15), (4097, 2, 8),
+                                              (1_000_003, 2, 15), (17_203_200, 2, 15), (300_001, 4, 15),
+                                              (4_300_800, 2, 15), (70_000, 4, 12)])
+def test_count_sort_matches_sort(n, kbytes, end_bit):
+    """The one-pass counting sort (count_sort.hip): keys sorted exactly as torch.sort, and the
+    positions a permutation whose keys match (order within a key is free: not stable)."""
+    g = torch.Generator().manual_seed(n + 1)
+    hi = 1 << end_bit
+    k = (torch.rand(n, generator=g) ** 3 * (hi - 1)).long()
+    k[::7] = hi - 1
+    kin = k.to(torch.int16 if kbytes == 2 else torch.int32).to(DEV)
+    skeys = torch.empty_like(kin)
+    svals = torch.empty(n, dtype=torch.int32, device=DEV)
+    cops.sort_pairs_iota(kin, skeys, svals, end_bit, impl="csort")
+    torch.cuda.synchronize()
+    ref_k, _ = torch.sort(k, stable=True)
+    got_k = skeys.cpu().to(torch.int64)
+    assert torch.equal(got_k, ref_k)
+    sv = svals.cpu().to(torch.int64)
+    assert torch.equal(torch.sort(sv).values, torch.arange(n))
+    assert torch.equal(k[sv], got_k)
+
+
 def test_hipgraph_cdssm_unfenced_fresh_batches():
     """CDSSM steps replayed from a hipGraph with NO per-replay sync while eager work (a fresh
     synthetic batch, i.e. new allocations) runs between replays: the pattern that faulted in
@@ -873,7 +923,7 @@ def test_hipgraph_cdssm_unfenced_fresh_batches():
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
-    assert cops.SORT_IMPL == "rsort"
+    assert cops.SORT_IMPL in ("rsort", "csort")  # both graph-safe (no memsets / global atomics)
     pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
     cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=128, document_length=512)
     data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=8192), DEV, seed=3)
@@ -1265,3 +1315,46 @@ def test_colsum_bag_mean_length_epilogue():
     y = dops.colsum(x, scale=lens, bias=bias, act="tanh", scale_is_len=True)
     ref_y = torch.tanh(x.sum(0) / lens.clamp(min=1.0)[:, None] + bias)
     torch.testing.assert_close(y, ref_y, rtol=1e-5, atol=1e-5)
+
+
+def test_cdssm_training_curve_hip_matches_torch():
+    """Training-curve parity: CDSSM (B 512, pages 256 tokens, cross-GPU loss on one rank)
+    trained 300 steps from the same initial weights on the same batches with the same
+    dropout masks, once through the HIP kernels (bf16 MFMA, sparse argmax backward, counting
+    sort, fused Adam) and once through eager fp32 PyTorch ops.  Loss curves and the final
+    Recall@10 must agree within run-to-run noise: the HIP backward learns exactly what the
+    framework-reference model learns (the CDSSM-vs-MLP quality gap is the model, not the
+    kernels)."""
+    import copy
+
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.eval.retrieval import recall_at_k
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    base = preset_config("cdssm_ngram_bf16").replace(batch_size=512, document_length=256)
+    V = base.vocab_hash_size
+    torch.manual_seed(21)
+    m0 = build_model(base, V)
+    out = {}
+    for dtype in ("bf16", "fp32"):
+        cfg = base.replace(dtype=dtype)
+        model = copy.deepcopy(m0)
+        model.cfg = cfg
+        tr = Trainer(cfg, model, torch.device(DEV))
+        data = SyntheticPairs(spec_from_config(cfg, V, num_pages=8192), DEV, seed=77)
+        losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(300)]
+        qe, pe = data.eval_set(1024)
+        r = recall_at_k(model.encode(qe, "query"), model.encode(pe, "doc"), torch.arange(1024, device=DEV), k=10)
+        out[dtype] = (losses, r)
+    (lh, rh), (lt, rt) = out["bf16"], out["fp32"]
+    tail_h, tail_t = sum(lh[-50:]) / 50, sum(lt[-50:]) / 50
+    print(f"HIP bf16: loss {lh[0]:.3f} -> {tail_h:.3f}, R@10 {rh:.3f} | torch fp32: loss {lt[0]:.3f} -> "
+          f"{tail_t:.3f}, R@10 {rt:.3f}")
+    assert abs(lh[0] - lt[0]) < 0.02 * lt[0]
+    assert tail_h < 0.9 * lh[0] and tail_t < 0.9 * lt[0]  # both learn
+    assert abs(tail_h - tail_t) < 0.05 * tail_t, (tail_h, tail_t)
+    assert abs(rh - rt) < 0.05, (rh, rt)

@@ -33,6 +33,8 @@ def test_tiny_dssm_config1_learns_recall():
                       query_length=8, document_length=24, batch_size=8)),
     ("longpage_fp8", dict(vocab_hash_size=300, mlp_dims=(32, 32, 16), chunk_len=16, num_chunks=4,
                           document_length=64, query_length=12, batch_size=8)),
+    ("longpage_cdssm", dict(vocab_hash_size=300, chunk_len=16, num_chunks=4, document_length=64, query_length=12,
+                            batch_size=8)),
     ("lstm", dict(query_length=8, document_length=20, batch_size=8, loss_mode="explicit")),
     ("lstm", dict(query_length=8, document_length=20, batch_size=8, loss_mode="explicit", lstm_conv=True)),
 ])

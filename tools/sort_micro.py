@@ -32,7 +32,7 @@ def main():
         res = {}
         lib = cops.lib()
         ref_k = ref_v = None
-        arms = ["rsort", "rocprim"] + [f"rsort_ipt{i}" for i in a.ipt]
+        arms = ["rsort", "rocprim", "csort"] + [f"rsort_ipt{i}" for i in a.ipt]
 
         def run(arm):
             if arm.startswith("rsort_ipt"):
@@ -49,6 +49,8 @@ def main():
             torch.cuda.synchronize()
             if ref_k is None:
                 ref_k, ref_v = skeys.clone(), svals.clone()
+            elif arm == "csort":  # not stable: same keys, positions a key-preserving permutation
+                assert torch.equal(skeys, ref_k) and torch.equal(keys[svals.long()], skeys), arm
             else:
                 assert torch.equal(skeys, ref_k) and torch.equal(svals, ref_v), arm
         times = {arm: [] for arm in arms}
