@@ -821,25 +821,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd4_kernel(Params p) {
   }
 }
 
-// v5 = v4's tile sets with ONE wave per SIMD: a 256-thread workgroup whose wave s runs the
-// union of v4's waves s and s+4 (SIMD s's whole tile set, ~224 weight VGPRs of a 512-entry
-// budget).  The A fragments of a 16-window block are read from LDS once per SIMD instead of
-// twice (52 instead of 104 ds_read_b128 per block and CU), barriers join 4 waves instead of 8;
-// latency is hidden by the wave's own independent accumulator chains (5 tiles) and the
-// prefetched A fragments.
-template <int PF, int DBG, int OPT, int DM>
-__global__ __launch_bounds__(256, 1) void conv_pool_fwd5_kernel(Params p) {
-  if (p.seed_ptr) p.seed += *p.seed_ptr;
-  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
-  char* xl = smem;
-  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave < 3) {
-    run_wave2<3, 2, PF, DBG, OPT, DM, false, 256>(p, 3 * wave, 2 * wave, xl, ids_lds);  // k3 3w..3w+2, k4 2w..2w+1
-  } else {
-    run_wave2<0, 4, PF, DBG, OPT, DM, true, 256>(p, 0, 6, xl, ids_lds);               // k4 6-8 + mixed
-  }
-}
+// (v5, measured and removed: v4's tile sets with ONE wave per SIMD in a 256-thread
+// workgroup — A fragments read once per SIMD instead of twice — ran 7.23-7.31 ms against
+// v4's 5.53 ms at the bench shape, bit-identical outputs: without a partner wave nothing
+// covers the LDS / staging latencies between the MFMA bursts; docs/PERF.md round 3.)
 
 PV_DEBUG_EXPORT(convfwd)
 }  // namespace convpool
@@ -974,23 +959,6 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
         case 1: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
         case 2: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 2>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
         default: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 13, 3>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
-      }
-      break;
-    }
-    case 8192:      // v5: one wave per SIMD (256-thread workgroups), OPT 13
-    case 8192 + 2:  // v5 + software-pipelined epilogue (OPT 15)
-    case 8192 + 3: {  // v5 + PIPE, A prefetch depth 3
-      const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
-      if (dm != 1 && dm != 0) return -3;  // A/B variant: the bench's dropout modes only
-      if (dbg == 8192) {
-        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 13, 1>), dim3(grid), dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 13, 0>), dim3(grid), dim3(256), 0, st, p);
-      } else if (dbg == 8192 + 2) {
-        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 15, 1>), dim3(grid), dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<2, 0, 15, 0>), dim3(grid), dim3(256), 0, st, p);
-      } else {
-        if (dm == 1) hipLaunchKernelGGL((conv_pool_fwd5_kernel<3, 0, 15, 1>), dim3(grid), dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_pool_fwd5_kernel<3, 0, 15, 0>), dim3(grid), dim3(256), 0, st, p);
       }
       break;
     }

@@ -95,13 +95,13 @@ def _grid(device: torch.device) -> int:
     return _grid_cache[idx]
 
 
-# dTable sort: the one-pass counting sort for keys < 2^15 (count_sort.hip: 4 launches, one
-# 2^15-bin LDS histogram per block; not stable) by default, the stable in-tree LSD radix
-# sort (radix_sort.hip) for wider keys and in deterministic mode; both graph-safe (no
-# memsets / global atomics).  PAGEVEC_SORT=rsort forces the LSD sort, =rocprim rocPRIM's
-# onesweep sort (A/B and reference only: its hipMemsetAsync-reset state faulted under long
-# hipGraph replays, docs/PERF.md)
-SORT_IMPL = os.environ.get("PAGEVEC_SORT", "csort")
+# dTable sort: the in-tree stable LSD radix sort (radix_sort.hip: graph-safe, no memsets /
+# atomics).  PAGEVEC_SORT=csort selects the one-pass 15-bit counting sort (count_sort.hip;
+# measured SLOWER: 0.435 vs 0.291 ms at 17.2 M keys — its scattered 2-/4-byte writes into
+# 30k buckets combine far worse than the LSD passes' 256 buckets — kept as an A/B arm),
+# =rocprim rocPRIM's onesweep sort (A/B and reference only: its hipMemsetAsync-reset state
+# faulted under long hipGraph replays, docs/PERF.md)
+SORT_IMPL = os.environ.get("PAGEVEC_SORT", "rsort")
 
 
 def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor, end_bit: int,

@@ -38,9 +38,15 @@ def quantize(x: torch.Tensor, with_bf16: bool = False):
 
 
 def _emulate(x: torch.Tensor) -> torch.Tensor:
-    a = x.abs().max().clamp(min=1e-12)
-    s = FP8_MAX / a
-    return (x * s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float() / s
+    """e4m3 round trip with per-tensor current scaling, as the HIP quantiser.  The backward
+    is straight-through (identity), like the HIP path's bf16 backward GEMMs on the
+    unquantised operands: a float8 cast has no autograd edge, so without the detach trick
+    no gradient would reach x or w at all."""
+    with torch.no_grad():
+        a = x.abs().max().clamp(min=1e-12)
+        s = FP8_MAX / a
+        q = (x * s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float() / s
+    return x + (q - x).detach() if x.requires_grad else q
 
 
 class _FP8LinearFn(torch.autograd.Function):

@@ -70,3 +70,21 @@ def test_bert_shared_tower_is_siamese():
     assert m.doc_towers[0] is m.query_tower
     n_params = sum(p.numel() for p in m.parameters())
     assert n_params == sum(p.numel() for p in m.query_tower.parameters())
+
+
+def test_fp8_emulation_backward_is_straight_through():
+    """CPU fp8 linear (e4m3 round trip of x and w): the gradient reaches x and w (straight-
+    through, like the HIP path's bf16 backward GEMMs) — a float8 cast alone cuts autograd and
+    trained only the last bias of the chunked fp8 encoder on the CPU path."""
+    from dnn_page_vectors_amd.ops import fp8 as fops
+
+    torch.manual_seed(0)
+    x = torch.randn(16, 32, requires_grad=True)
+    w = (torch.randn(8, 32) * 0.1).requires_grad_(True)
+    b = torch.zeros(8, requires_grad=True)
+    g = torch.randn(16, 8)
+    (fops.fp8_linear(x, w, b, "tanh") * g).sum().backward()
+    x2, w2, b2 = x.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True), torch.zeros(8, requires_grad=True)
+    (torch.tanh(torch.nn.functional.linear(x2, w2, b2)) * g).sum().backward()
+    for got, want in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        assert float((got - want).norm() / want.norm()) < 0.1
