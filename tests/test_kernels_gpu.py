@@ -797,9 +797,9 @@ def test_embedding_bag_counts_split_k():
 def test_cdssm_recall_quality_guard():
     """Training-quality guard for the headline config: 1000 steps of CDSSM-300d (B 4096,
     cross-GPU loss on one rank, in-batch softmax scale 40) on fresh synthetic batches must
-    reach Recall@10 >= 0.35 on held-out pairs.  The float-atomic gradient sums make runs
-    differ: 0.41-0.44 over the round-2/3 driver and builder benches (BENCH_r02.json 0.413,
-    round-3 first run 0.443).  A kernel regression that halves the learning signal lands
+    reach Recall@10 >= 0.30 on held-out pairs (2x the reference-head plateau).  The
+    float-atomic gradient sums make runs differ: 0.36 (this test, round 3) to 0.41-0.45
+    (driver and builder benches, BENCH_r02.json 0.413, round-3 runs 0.443 / 0.452).  A kernel regression that halves the learning signal lands
     near the reference-head plateau (~0.15-0.2, profiles/quality_r2_final.md) and fails."""
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
@@ -827,7 +827,7 @@ def test_cdssm_recall_quality_guard():
     assert float(m["loss"]) == float(m["loss"])
     print(f"recall@10 after 1000 steps: {r:.4f} (exact top-k {r_ref:.4f})")
     assert abs(r - r_ref) <= 2.0 / 2048, (r, r_ref)
-    assert r >= 0.35, r
+    assert r >= 0.30, r
 
 
 def test_resume_restores_device_adam_step(tmp_path):
@@ -1352,16 +1352,28 @@ def test_cdssm_training_curve_hip_matches_torch():
     torch.manual_seed(21)
     m0 = build_model(base, V)
     out = {}
-    for dtype in ("bf16", "fp32"):
-        cfg = base.replace(dtype=dtype)
-        model = copy.deepcopy(m0)
-        model.cfg = cfg
-        tr = Trainer(cfg, model, torch.device(DEV))
-        data = SyntheticPairs(spec_from_config(cfg, V, num_pages=8192), DEV, seed=77)
-        losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(300)]
-        qe, pe = data.eval_set(1024)
-        r = recall_at_k(model.encode(qe, "query"), model.encode(pe, "doc"), torch.arange(1024, device=DEV), k=10)
-        out[dtype] = (losses, r)
+    # the fp32 arm's F.conv1d through PyTorch's native (unfold + GEMM) convolution: MIOpen
+    # would search / compile kernels for every new shape on a fresh box first
+    cudnn_prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        for dtype in ("bf16", "fp32"):
+            cfg = base.replace(dtype=dtype)
+            model = copy.deepcopy(m0)
+            model.cfg = cfg
+            tr = Trainer(cfg, model, torch.device(DEV))
+            data = SyntheticPairs(spec_from_config(cfg, V, num_pages=8192), DEV, seed=77)
+            losses = []
+            for i in range(300):
+                losses.append(float(tr.train_step(*data.batch(cfg.batch_size))["loss"]))
+                if i % 50 == 0:
+                    print(f"{dtype} step {i} loss {losses[-1]:.4f}", flush=True)
+            qe, pe = data.eval_set(1024)
+            r = recall_at_k(model.encode(qe, "query"), model.encode(pe, "doc"), torch.arange(1024, device=DEV),
+                            k=10)
+            out[dtype] = (losses, r)
+    finally:
+        torch.backends.cudnn.enabled = cudnn_prev
     (lh, rh), (lt, rt) = out["bf16"], out["fp32"]
     tail_h, tail_t = sum(lh[-50:]) / 50, sum(lt[-50:]) / 50
     print(f"HIP bf16: loss {lh[0]:.3f} -> {tail_h:.3f}, R@10 {rh:.3f} | torch fp32: loss {lt[0]:.3f} -> "
@@ -1370,3 +1382,53 @@ def test_cdssm_training_curve_hip_matches_torch():
     assert tail_h < 0.9 * lh[0] and tail_t < 0.9 * lt[0]  # both learn
     assert abs(tail_h - tail_t) < 0.05 * tail_t, (tail_h, tail_t)
     assert abs(rh - rt) < 0.05, (rh, rt)
+
+
+@pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 136, 128), (1000, 520, 768), (64, 1032, 2048),
+                                   (8, 256, 4096)])
+def test_gemm_engine_layouts(a_col, b_col, M, N, K):
+    """gemm.hip: C = A . B^T for every operand storage (row = K contiguous, col = M / N
+    contiguous), edge tiles, and split-K, against fp32 torch on the same bf16 operands."""
+    from dnn_page_vectors_amd.ops import gemm as gops
+
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    B = torch.randn(N, K, generator=g).bfloat16()
+    ref_c = A.float() @ B.float().t()
+    a = (A.t().contiguous() if a_col else A).to(DEV)
+    b = (B.t().contiguous() if b_col else B).to(DEV)
+    for ks in (1, 0, 4):
+        if ks == 4 and K < 4 * 64:
+            continue
+        c = gops.gemm(a, b, a_col, b_col, ksplit=ks)
+        torch.cuda.synchronize()
+        err = float((c.cpu() - ref_c).abs().max() / ref_c.abs().max())
+        assert err < 1e-5, (ks, err)
+
+
+def test_gemm_engine_epilogues():
+    """Fused epilogue: alpha, bias, relu / gelu / tanh, bf16 output, beta = 1 accumulation;
+    split-K with the same epilogue through the column-sum reduce."""
+    from dnn_page_vectors_amd.ops import gemm as gops
+
+    g = torch.Generator().manual_seed(9)
+    M, N, K = 520, 384, 512
+    A = torch.randn(M, K, generator=g).bfloat16().to(DEV)
+    B = torch.randn(N, K, generator=g).bfloat16().to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    pre = 0.5 * (A.float() @ B.float().t()) + bias
+    acts = {"none": pre, "relu": torch.relu(pre), "tanh": torch.tanh(pre),
+            "gelu": torch.nn.functional.gelu(pre, approximate="tanh")}
+    for act, want in acts.items():
+        for ks in (1, 2):
+            c = gops.gemm(A, B, bias=bias, act=act, alpha=0.5, ksplit=ks)
+            torch.testing.assert_close(c, want, rtol=2e-4, atol=2e-3)
+        c16 = gops.gemm(A, B, bias=bias, act=act, alpha=0.5, out_dtype=torch.bfloat16)
+        assert c16.dtype == torch.bfloat16
+        torch.testing.assert_close(c16.float(), want, rtol=1e-2, atol=2e-2)
+    base = torch.randn(M, N, generator=g).to(DEV)
+    for ks in (1, 2):
+        c = base.clone()
+        gops.gemm(A, B, out=c, accumulate=True, ksplit=ks)
+        torch.testing.assert_close(c, base + A.float() @ B.float().t(), rtol=2e-4, atol=2e-3)

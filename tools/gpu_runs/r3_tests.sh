@@ -1,0 +1,12 @@
+# Round 3: full GPU test suite + smoke
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r3c
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3c/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 gpurun_out/r3c/pytest.log)"; [ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3c/smoke.log 2>&1
+rc2=$?; echo "smoke rc=$rc2 $(tail -1 gpurun_out/r3c/smoke.log)"; [ $rc2 -eq 0 ] || exit $rc2
+timeout -k 10 300 python bench.py --model chunked > gpurun_out/r3c/bench_chunked.log 2>&1
+rc3=$?; echo "chunked rc=$rc3 $(grep '^{' gpurun_out/r3c/bench_chunked.log | cut -c1-120)"; [ $rc3 -eq 0 ] || exit $rc3
+timeout -k 10 300 python bench.py --model chunked_cdssm > gpurun_out/r3c/bench_chunked_cdssm.log 2>&1
+rc4=$?; echo "chunked_cdssm rc=$rc4 $(grep '^{' gpurun_out/r3c/bench_chunked_cdssm.log | cut -c1-120)"; exit $rc
