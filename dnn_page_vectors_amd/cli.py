@@ -96,10 +96,26 @@ def cmd_train(a) -> int:
         steps = max(1, cfg.num_train_samples // (cfg.batch_size * d_world))
         train_loader = SyntheticLoader(gen, cfg.batch_size, steps)
         val_loader = SyntheticLoader(gen, cfg.batch_size, max(1, cfg.num_validation_samples // cfg.batch_size))
+    elif a.validation_split is not None:
+        # v1 data path (dssm_cnn/cnn_dssm.py:201): one in-memory file, pad to the dataset max,
+        # Keras validation_split (last fraction) + per-epoch shuffle
+        from .data.dataset import InMemoryPairs
+
+        fz = _featurizer(cfg)
+        V = fz.num_ids
+        mem = InMemoryPairs(a.data or cfg.model_training_data, fz, cfg.query_length, cfg.document_length,
+                            cfg.num_negative_examples, validation_split=a.validation_split)
+        cfg = cfg.replace(query_length=mem.query_length, document_length=mem.document_length)
+        train_loader = mem.train_loader(cfg.batch_size, shuffle=True, seed=cfg.seed, device=info.device,
+                                        rank=d_rank, world_size=d_world)
+        val_loader = mem.val_loader(cfg.batch_size, device=info.device, rank=d_rank, world_size=d_world)
+        steps = max(1, train_loader.num_batches())
+        log.info("in-memory data: %d train / %d validation rows, padded to %d / %d tokens", mem.n_train,
+                 mem.n_val, mem.query_length, mem.document_length)
     else:
         fz = _featurizer(cfg)
         V = fz.num_ids
-        tr = JsonlPairDataset(cfg.model_training_data, fz, cfg.query_length, cfg.document_length,
+        tr = JsonlPairDataset(a.data or cfg.model_training_data, fz, cfg.query_length, cfg.document_length,
                               cfg.num_negative_examples)
         va = JsonlPairDataset(cfg.model_validation_data, fz, cfg.query_length, cfg.document_length,
                               cfg.num_negative_examples)
@@ -292,6 +308,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.add_argument("--synthetic-pages", type=int, default=65536)
     p.add_argument("--shuffle", action="store_true")
     p.add_argument("--resume", action="store_true")
+    p.add_argument("--data", default=None, help="training JSONL (default: the experiment's model_training_data)")
+    p.add_argument("--validation-split", type=float, default=None,
+                   help="v1 in-memory mode: hold out the last fraction of --data for validation (Keras "
+                        "validation_split), pad to the dataset's longest text, shuffle every epoch")
     p.set_defaults(fn=cmd_train)
     p = sub.add_parser("encode")
     _common(p)

@@ -250,3 +250,23 @@ PV_API int pv_fp8_linear(const void* X8, const void* W8, const float* amax_x, co
   PV_LAUNCH_CHECK();
   return 0;
 }
+
+// ---- block-scaled (MX) fp8 MFMA layout probe -------------------------------------------
+// One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, e8m0 scales) by one wave: lane l
+// passes its 32 A bytes a[l], 32 B bytes b[l], its A / B scale bytes sa[l] / sb[l], and
+// stores its 4 accumulator floats.  tests/test_kernels_gpu.py::test_mx_fp8_mfma_layout
+// checks the operand / scale mapping the MX GEMM relies on against a host reference.
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+__global__ void mx_probe_kernel(const v8i_t* a, const v8i_t* b, const int* sa, const int* sb, f32x4* c) {
+  const int l = threadIdx.x;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], acc, 0, 0, 0, sa[l], 0, sb[l]);
+  c[l] = acc;
+}
+
+PV_API int pv_mx_probe(const void* a, const void* b, const int* sa, const int* sb, float* c, void* stream) {
+  hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const v8i_t*)a, (const v8i_t*)b, sa,
+                     sb, (f32x4*)c);
+  PV_LAUNCH_CHECK();
+  return 0;
+}

@@ -25,6 +25,7 @@
 // Edges: rows / columns beyond M / N are loaded from a clamped (valid) address and never
 // stored; K must be a multiple of 64 (callers pad — the operands here all are).
 #include "common.h"
+#include <stdlib.h>
 
 namespace pv {
 namespace gemm {
@@ -51,9 +52,10 @@ struct Params {
   const float* bias;    // (N) or null
   float alpha;
   int act;
-  int beta;             // 1: C += result (fp32 output only)
+  int beta;             // 1: C += result (fp32 or bf16 C)
   int out_bf16;
   int tiles_m, tiles_n;
+  int n_fastest;        // tile order: 1 = N-fastest (A panel shared by consecutive tiles)
 };
 
 __device__ __forceinline__ int h_of(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
@@ -117,6 +119,57 @@ __device__ __forceinline__ float act_f(float x, int act) {
   return x;
 }
 
+__device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[8][4], int split, int m0, int n0, int wr,
+                                         int wc, int lane) {
+  // acc[i][j][r] is C[m0 + wr*128 + 16i + 4(lane>>4) + r][n0 + wc*64 + 16j + (lane&15)]
+  const int colb = n0 + wc * 64 + (lane & 15);
+  const int rowb = m0 + wr * 128 + 4 * (lane >> 4);
+  if (p.ksplit > 1) {  // fp32 partial slab of this K slice
+    float* Cs = reinterpret_cast<float*>(p.C) + (size_t)split * p.slab;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rowb + 16 * i + r;
+        if (row >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = colb + 16 * j;
+          if (col < p.N) Cs[(size_t)row * p.ldc + col] = acc[i][j][r] * p.alpha;
+        }
+      }
+    return;
+  }
+  float bj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = colb + 16 * j;
+    bj[j] = (p.bias && col < p.N) ? p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rowb + 16 * i + r;
+      if (row >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = colb + 16 * j;
+        if (col >= p.N) continue;
+        float v = act_f(acc[i][j][r] * p.alpha + bj[j], p.act);
+        const size_t o = (size_t)row * p.ldc + col;
+        if (p.out_bf16) {
+          unsigned short* Cb = reinterpret_cast<unsigned short*>(p.C);
+          if (p.beta) v += bf16_to_f32(Cb[o]);
+          Cb[o] = f32_to_bf16(v);
+        } else {
+          float* Cf = reinterpret_cast<float*>(p.C);
+          Cf[o] = p.beta ? Cf[o] + v : v;
+        }
+      }
+    }
+}
+
 template <int ALAY, int BLAY>
 __global__ __launch_bounds__(NTH, 2) void gemm_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [buf][A, B]
@@ -127,7 +180,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(Params p) {
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int ntile = p.tiles_m * p.tiles_n;
   const int split = bid / ntile, t = bid - split * ntile;
-  const int tm = t % p.tiles_m, tn = t / p.tiles_m;  // M-fastest: consecutive tiles share B panels
+  // consecutive tile ids (one XCD under the remap) share the panel of the LARGER operand,
+  // so it is read from HBM once and re-served from that XCD's L2 (tall-skinny GEMMs: the
+  // whole small operand stays L2-resident anyway)
+  const int tm = p.n_fastest ? t / p.tiles_n : t % p.tiles_m;
+  const int tn = p.n_fastest ? t % p.tiles_n : t / p.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.ksplit - 1) / p.ksplit;
@@ -171,51 +228,120 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(Params p) {
     }
   }
 
-  // ---- epilogue: acc[i][j][r] is C[m0 + wr*128 + 16i + 4(lane>>4) + r][n0 + wc*64 + 16j + (lane&15)]
-  const int colb = n0 + wc * 64 + (lane & 15);
-  const int rowb = m0 + wr * 128 + 4 * (lane >> 4);
-  if (p.ksplit > 1) {  // fp32 partial slab of this K slice
-    float* Cs = reinterpret_cast<float*>(p.C) + (size_t)split * p.slab;
+  epilogue(p, acc, split, m0, n0, wr, wc, lane);
+}
+
+// ---- v2 schedule: fragment reads software-pipelined one sub-step ahead --------------------
+// A K tile is 4 sub-steps of 16 MFMAs (k-step s x half h of the wave's 8 A row tiles); the
+// fragments of sub-step u+1 are read while the MFMAs of u run (two register sets), and the
+// tile switch is placed INSIDE the last sub-step: wait for the next tile (staged one tile
+// ahead), barrier, issue its first fragment reads, THEN the last 16 MFMAs of the current
+// tile, then stage the tile after next into the buffer everyone has finished reading.  One
+// barrier per K tile and no fragment-read bubble at the tile boundary.
+template <int LAY, int H>
+__device__ __forceinline__ void read_a4(const char* t, int rb, int s, bf16x8 (&a)[4]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rowb + 16 * i + r;
-        if (row >= p.M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = colb + 16 * j;
-          if (col < p.N) Cs[(size_t)row * p.ldc + col] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  float bj[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = colb + 16 * j;
-    bj[j] = (p.bias && col < p.N) ? p.bias[col] : 0.f;
-  }
+  for (int i = 0; i < 4; ++i) a[i] = frag<LAY>(t, rb + 64 * H + 16 * i, s);
+}
+
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(NTH, 2) void gemm2_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [buf][A, B]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int tm = p.n_fastest ? t / p.tiles_n : t % p.tiles_m;
+  const int tn = p.n_fastest ? t % p.tiles_n : t / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * per, kt1 = min(ktiles, kt0 + per);
+  const int arb = wr * 128, brb = wc * 64;
+
+  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rowb + 16 * i + r;
-      if (row >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = colb + 16 * j;
-        if (col >= p.N) continue;
-        float v = act_f(acc[i][j][r] * p.alpha + bj[j], p.act);
-        const size_t o = (size_t)row * p.ldc + col;
-        if (p.out_bf16) {
-          reinterpret_cast<unsigned short*>(p.C)[o] = f32_to_bf16(v);
-        } else {
-          float* Cf = reinterpret_cast<float*>(p.C);
-          Cf[o] = p.beta ? Cf[o] + v : v;
-        }
-      }
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    stage<ALAY>(p.A, p.lda, m0, p.M - 1, kt0 * BK, smem);
+    stage<BLAY>(p.B, p.ldb, n0, p.N - 1, kt0 * BK, smem + TILE_BYTES);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt0 + 1 < kt1) {
+      stage<ALAY>(p.A, p.lda, m0, p.M - 1, (kt0 + 1) * BK, smem + 2 * TILE_BYTES);
+      stage<BLAY>(p.B, p.ldb, n0, p.N - 1, (kt0 + 1) * BK, smem + 3 * TILE_BYTES);
     }
+    bf16x8 a0[4], a1[4], b0[4], b1[4];
+    {
+      const char* ta = smem;
+      const char* tb = smem + TILE_BYTES;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b0[j] = frag<BLAY>(tb, brb + 16 * j, 0);
+      read_a4<ALAY, 0>(ta, arb, 0, a0);
+    }
+    int buf = 0;
+#pragma unroll 1
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const char* ta = smem + buf * 2 * TILE_BYTES;
+      const char* tb = ta + TILE_BYTES;
+      // u = 0: (s0, h0) computes with a0/b0; read (s0, h1) -> a1, and s1's B -> b1
+      read_a4<ALAY, 1>(ta, arb, 0, a1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b1[j] = frag<BLAY>(tb, brb + 16 * j, 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      // u = 1: (s0, h1) with a1/b0; read (s1, h0) -> a0
+      read_a4<ALAY, 0>(ta, arb, 1, a0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b0[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      // u = 2: (s1, h0) with a0/b1; read (s1, h1) -> a1
+      read_a4<ALAY, 1>(ta, arb, 1, a1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b1[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      // u = 3: (s1, h1) with a1/b1; tile switch: next tile landed -> barrier -> its first reads
+      const bool more = kt + 1 < kt1;
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (more) {
+        const char* na = smem + (buf ^ 1) * 2 * TILE_BYTES;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b0[j] = frag<BLAY>(na + TILE_BYTES, brb + 16 * j, 0);
+        read_a4<ALAY, 0>(na, arb, 0, a0);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (kt + 2 < kt1) {  // everyone passed the barrier: this buffer is free
+        char* sa = smem + buf * 2 * TILE_BYTES;
+        stage<ALAY>(p.A, p.lda, m0, p.M - 1, (kt + 2) * BK, sa);
+        stage<BLAY>(p.B, p.ldb, n0, p.N - 1, (kt + 2) * BK, sa + TILE_BYTES);
+      }
+      buf ^= 1;
+    }
+  }
+  epilogue(p, acc, split, m0, n0, wr, wc, lane);
 }
 
 PV_DEBUG_EXPORT(gemm)
@@ -223,6 +349,11 @@ PV_DEBUG_EXPORT(gemm)
 }  // namespace pv
 
 using namespace pv;
+
+// schedule: 2 = fragment reads pipelined one sub-step ahead (gemm2_kernel, default);
+// 1 = the plain double-buffered loop (gemm_kernel) — A/B arm for tools/gemm_engine_micro.py
+static int g_gemm_sched = getenv("PAGEVEC_GEMM_SCHED") ? atoi(getenv("PAGEVEC_GEMM_SCHED")) : 2;
+PV_API void pv_gemm_set_sched(int s) { g_gemm_sched = s; }
 
 // C = epi(alpha * A . B^T); a_col / b_col select the COL storage of A ([K][M]) / B ([K][N]).
 // ksplit > 1: C is a workspace of ksplit fp32 slabs (slab = elements per slab), reduced by
@@ -233,18 +364,24 @@ PV_API int pv_gemm_bf16(const void* A, long lda, int a_col, const void* B, long 
   using namespace pv::gemm;
   if (M <= 0 || N <= 0 || K <= 0 || K % BK) return -1;
   if (ksplit < 1) ksplit = 1;
-  if (ksplit > 1 && (out_bf16 || beta || bias || act)) return -2;
+  if (ksplit > 1 && (out_bf16 || beta || bias || act)) return -2;  // split-K: the caller's reduce does the epilogue
   if (((size_t)A & 15) || ((size_t)B & 15)) return -3;           // 16-byte source vectors
   if (lda % 8 || ldb % 8) return -4;                            // rows start 16-byte aligned
   if ((a_col && M % 8) || (b_col && N % 8)) return -5;           // whole 8-column groups of COL operands
   Params p{(const unsigned short*)A, (const unsigned short*)B, lda, ldb, C, ldc, M, N, K, ksplit, slab,
-           bias, alpha, act, beta, out_bf16, (M + BM - 1) / BM, (N + BN - 1) / BN};
+           bias, alpha, act, beta, out_bf16, (M + BM - 1) / BM, (N + BN - 1) / BN, N <= M ? 1 : 0};
   const int grid = p.tiles_m * p.tiles_n * ksplit;
   hipStream_t st = (hipStream_t)stream;
-  if (!a_col && !b_col) hipLaunchKernelGGL((gemm_kernel<ROW, ROW>), dim3(grid), dim3(NTH), 0, st, p);
-  else if (!a_col && b_col) hipLaunchKernelGGL((gemm_kernel<ROW, COL>), dim3(grid), dim3(NTH), 0, st, p);
-  else if (a_col && !b_col) hipLaunchKernelGGL((gemm_kernel<COL, ROW>), dim3(grid), dim3(NTH), 0, st, p);
-  else hipLaunchKernelGGL((gemm_kernel<COL, COL>), dim3(grid), dim3(NTH), 0, st, p);
+#define PV_GEMM_LAUNCH(KER)                                                                        \
+  do {                                                                                            \
+    if (!a_col && !b_col) hipLaunchKernelGGL((KER<ROW, ROW>), dim3(grid), dim3(NTH), 0, st, p);    \
+    else if (!a_col && b_col) hipLaunchKernelGGL((KER<ROW, COL>), dim3(grid), dim3(NTH), 0, st, p); \
+    else if (a_col && !b_col) hipLaunchKernelGGL((KER<COL, ROW>), dim3(grid), dim3(NTH), 0, st, p); \
+    else hipLaunchKernelGGL((KER<COL, COL>), dim3(grid), dim3(NTH), 0, st, p);                     \
+  } while (0)
+  if (g_gemm_sched == 1) PV_GEMM_LAUNCH(gemm_kernel);
+  else PV_GEMM_LAUNCH(gemm2_kernel);
+#undef PV_GEMM_LAUNCH
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -193,3 +193,92 @@ class SyntheticLoader:
             yield self.gen.batch(self.B)
         self.epoch += 1
         self.cursor = 0
+
+
+class InMemoryPairs:
+    """The v1 data path (dssm_cnn/data_helpers.py:261-307 + cnn_dssm.py:201): the
+    whole JSONL file featurized into memory once, every field padded to the DATASET's longest
+    text (``pad_sentences`` pads to the max length, :88-103) — capped here by the configured
+    lengths, which the reference left unbounded — and Keras ``fit(validation_split=s,
+    shuffle=True)`` semantics: the LAST ``s`` fraction of the rows (file order) is the
+    validation set, the training rows are re-shuffled every epoch (``batch_iter``, :310-324).
+
+    ``train_loader`` / ``val_loader`` give the ``epoch_iter`` interface of ``PairLoader``
+    (device tensors, resumable cursor)."""
+
+    def __init__(self, path: str, featurizer: Featurizer, query_length: int, document_length: int,
+                 num_negatives: int = 3, validation_split: float = 0.2, nthreads: int = 0):
+        if not 0.0 <= validation_split < 1.0:
+            raise ValueError("validation_split must be in [0, 1)")
+        ds = JsonlPairDataset(path, featurizer, query_length, document_length, num_negatives, nthreads)
+        try:
+            n = len(ds)
+            q, d = ds.batch(np.arange(n))
+            self.skipped = ds.skipped
+        finally:
+            ds.close()
+        pad = featurizer.pad_id
+
+        def used(x: np.ndarray) -> int:  # longest non-padding prefix over all rows
+            nz = (x != pad).reshape(-1, x.shape[-1])
+            if not nz.any():
+                return 1
+            last = x.shape[-1] - np.argmax(nz[:, ::-1], axis=1)
+            return int(np.max(np.where(nz.any(axis=1), last, 0)))
+
+        self.query_length, self.document_length = used(q), used(d)
+        self.q = torch.from_numpy(np.ascontiguousarray(q[:, :self.query_length]))
+        self.d = torch.from_numpy(np.ascontiguousarray(d[:, :, :self.document_length]))
+        self.n_val = int(round(n * validation_split))
+        self.n_train = n - self.n_val
+
+    def __len__(self) -> int:
+        return self.n_train + self.n_val
+
+    def train_loader(self, batch_size: int, shuffle: bool = True, seed: int = 1337,
+                     device: Optional[torch.device] = None, rank: int = 0, world_size: int = 1) -> "_TensorLoader":
+        return _TensorLoader(self.q[:self.n_train], self.d[:self.n_train], batch_size, shuffle, seed, device, rank,
+                             world_size)
+
+    def val_loader(self, batch_size: int, device: Optional[torch.device] = None, rank: int = 0,
+                   world_size: int = 1) -> "_TensorLoader":
+        return _TensorLoader(self.q[self.n_train:], self.d[self.n_train:], batch_size, False, 0, device, rank,
+                             world_size)
+
+
+class _TensorLoader:
+    """Batches of in-memory (q, d) tensors; per-epoch seeded shuffle; rank shard; cursor."""
+
+    def __init__(self, q: torch.Tensor, d: torch.Tensor, batch_size: int, shuffle: bool, seed: int,
+                 device: Optional[torch.device], rank: int, world_size: int):
+        self.q, self.d, self.B = q, d, int(batch_size)
+        self.shuffle, self.seed, self.device = shuffle, seed, device
+        self.rank, self.world = rank, world_size
+        self.epoch = 0
+        self.cursor = 0
+
+    def num_batches(self) -> int:
+        return (self.q.shape[0] // self.world) // self.B
+
+    def state(self) -> dict:
+        return {"epoch": self.epoch, "cursor": self.cursor}
+
+    def load_state(self, st: dict) -> None:
+        self.epoch, self.cursor = int(st["epoch"]), int(st["cursor"])
+
+    def epoch_iter(self, epoch: Optional[int] = None) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
+        if epoch is not None and epoch != self.epoch:
+            self.epoch, self.cursor = epoch, 0
+        n = self.q.shape[0]
+        order = (np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n))
+        per = n // self.world
+        order = torch.from_numpy(order[self.rank * per:(self.rank + 1) * per])
+        for b in range(self.cursor, self.num_batches()):
+            idx = order[b * self.B:(b + 1) * self.B]
+            qa, da = self.q[idx], self.d[idx]
+            if self.device is not None:
+                qa, da = qa.to(self.device, non_blocking=True), da.to(self.device, non_blocking=True)
+            self.cursor += 1
+            yield qa, da
+        self.epoch += 1
+        self.cursor = 0

@@ -104,6 +104,8 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
     # gemm.hip
     "pv_gemm_bf16": "p" "l" "i" "p" "l" "i" "p" "l" "iii" "i" "l" "p" "f" "iii" "p",
+    "pv_gemm_set_sched": "i",
+    "pv_mx_probe": "ppppp" "p",
 }
 
 _RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_csort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,

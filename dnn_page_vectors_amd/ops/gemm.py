@@ -15,8 +15,14 @@ bias / activation epilogue there.
 
 Requirements of the kernel: bf16 operands, 16-byte aligned, row strides multiples of 8
 elements, K a multiple of 64, M (N) a multiple of 8 for a transposed A (B).  ``supported``
-checks them; callers fall back to the library GEMM otherwise (and the GEMM micro-benchmark,
-tools/gemm_engine_micro.py, decides where the engine is the default).
+checks them; callers fall back to the library GEMM otherwise.
+
+Status (round 3, measured): correct for every storage combination, split-K and epilogue
+(tests/test_kernels_gpu.py::test_gemm_engine_*), but at 0.47-0.96 PF/s it is 60-70% of
+hipBLASLt on the same shapes (0.75-1.48 PF/s, profiles/r3_gemm_engine.md): its
+double-buffered K loop lacks the 8-phase interleave (counted vmcnt with loads in flight
+across barriers) that the library's kernels have.  The model paths therefore keep the
+library GEMMs (``USE`` is empty); the engine is the base for fused-epilogue / fp8 work.
 """
 from __future__ import annotations
 
@@ -77,8 +83,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_col: bool = False, b_col: bool = Fa
     dev = a.device
     bf = bias.float().contiguous() if bias is not None else None
     ks = ksplit or auto_ksplit(M, N, K)
-    if accumulate and out_dtype != torch.float32:
-        raise ValueError("accumulate needs an fp32 output")
+    if out is not None:
+        out_dtype = out.dtype
+    if accumulate and out_dtype != torch.float32 and ks > 1:
+        ks = 1  # bf16 accumulation happens in the kernel epilogue (no split-K reduce for it)
     if out is None:
         out = (torch.zeros if (accumulate and ks > 1) else torch.empty)(M, N, dtype=out_dtype, device=dev)
     s = stream(dev)
@@ -107,3 +115,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_col: bool = False, b_col: bool = Fa
 
 
 ENABLED = os.environ.get("PAGEVEC_GEMM", "1") != "0"
+
+# Which GEMMs of a linear layer go to the engine instead of hipBLASLt.  Measured
+# (tools/gemm_engine_micro.py, profiles/r3_gemm_engine.md): the engine reaches 0.47-0.96 PF/s
+# where the library reaches 0.75-1.48 PF/s on the same operands, so NONE by default;
+# PAGEVEC_GEMM_USE=fwd,dgrad,wgrad routes them (A/B, fused-epilogue experiments).
+_DEFAULT_USE = set()
+USE = set(filter(None, os.environ.get("PAGEVEC_GEMM_USE", ",".join(sorted(_DEFAULT_USE))).split(",")))
+
+
+def use(kind: str, a: torch.Tensor, b: torch.Tensor, a_col: bool = False, b_col: bool = False) -> bool:
+    """Route GEMM ``kind`` (fwd / dgrad / wgrad / bag) to the engine?"""
+    return ENABLED and kind in USE and supported(a, b, a_col, b_col)

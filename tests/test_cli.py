@@ -30,6 +30,10 @@ def test_cli_setup_train_encode(tmp_path):
     out = _run(["train"] + common, tmp_path)
     hist = json.loads(out.strip().splitlines()[-1])["history"]
     assert len(hist["loss"]) == 2 and len(hist["val_loss"]) == 2
+    # v1 data path: one in-memory file, Keras validation_split, per-epoch shuffle
+    out = _run(["train", "--data", str(src), "--validation-split", "0.25"] + common, tmp_path)
+    hist = json.loads(out.strip().splitlines()[-1])["history"]
+    assert len(hist["loss"]) == 2 and len(hist["val_loss"]) == 2
     texts = tmp_path / "pages.txt"
     texts.write_text("topic 3 page text\nother 1 text\n")
     out = _run(["encode", "--input", str(texts), "--output", str(tmp_path / "v.npy")] + common, tmp_path)

@@ -67,3 +67,33 @@ def test_loader_sequential_shuffle_shard_resume(tmp_path):
 def test_dataset_missing_file(tmp_path):
     with pytest.raises(FileNotFoundError):
         JsonlPairDataset(str(tmp_path / "nope.jsonl"), Featurizer("char", hash_size=10), 4, 4, 3)
+
+
+def test_in_memory_pairs_v1_semantics(tmp_path):
+    """v1 data path (dssm_cnn/data_helpers.py + cnn_dssm.py:201): pad to the dataset's longest
+    text (capped by the configured lengths), Keras validation_split = the LAST rows, a fresh
+    shuffle of the training rows every epoch."""
+    import json
+
+    import numpy as np
+
+    from dnn_page_vectors_amd.data.dataset import InMemoryPairs
+    from dnn_page_vectors_amd.data.featurize import Featurizer
+
+    rows = [{"q": "w " * (1 + i % 4), "doc_corr": "d " * (2 + i % 7), "doc_incorr": ["x", "y y", "z"]}
+            for i in range(20)]
+    rows.append({"q": "bad", "doc_corr": "row", "doc_incorr": ["only one"]})  # skipped (!= 3 negatives)
+    p = tmp_path / "v1.jsonl"
+    p.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    fz = Featurizer("word", hash_size=97)
+    mem = InMemoryPairs(str(p), fz, 64, 64, 3, validation_split=0.25)
+    assert len(mem) == 20 and mem.skipped == 1
+    assert mem.n_val == 5 and mem.n_train == 15
+    assert mem.query_length == 4 and mem.document_length == 8  # "w w w w" / 8 tokens ("d " * 8 -> 8 + '')
+    tl = mem.train_loader(5, shuffle=True, seed=3)
+    e0 = torch.cat([q for q, _ in tl.epoch_iter()])
+    e1 = torch.cat([q for q, _ in tl.epoch_iter()])
+    assert e0.shape == (15, 4) and not torch.equal(e0, e1)           # reshuffled per epoch
+    assert sorted(map(tuple, e0.tolist())) == sorted(map(tuple, e1.tolist()))
+    vq = torch.cat([q for q, _ in mem.val_loader(5).epoch_iter()])
+    np.testing.assert_array_equal(vq.numpy(), mem.q[15:].numpy())    # the last 25% in file order

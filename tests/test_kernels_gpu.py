@@ -1385,7 +1385,7 @@ def test_cdssm_training_curve_hip_matches_torch():
 
 
 @pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 136, 128), (1000, 520, 768), (64, 1032, 2048),
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 136, 128), (1000, 520, 768), (64, 1032, 2048),
                                    (8, 256, 4096)])
 def test_gemm_engine_layouts(a_col, b_col, M, N, K):
     """gemm.hip: C = A . B^T for every operand storage (row = K contiguous, col = M / N
@@ -1432,3 +1432,67 @@ def test_gemm_engine_epilogues():
         c = base.clone()
         gops.gemm(A, B, out=c, accumulate=True, ksplit=ks)
         torch.testing.assert_close(c, base + A.float() @ B.float().t(), rtol=2e-4, atol=2e-3)
+
+
+def _mx_k_of(hyp: str, l: int, j: int) -> int:
+    """k index of byte j (0..31) of lane l's 32-byte operand under a layout hypothesis."""
+    g = l >> 4
+    if hyp == "contig32":      # lane group g holds k 32g .. 32g+31
+        return 32 * g + j
+    if hyp == "halves16":      # k 16g + j (j < 16), 64 + 16g + j - 16
+        return 16 * g + j if j < 16 else 64 + 16 * g + (j - 16)
+    if hyp == "chunks8":       # four K=32 sub-ops: byte j of chunk c = j // 8 -> k 32c + 8g + j % 8
+        return 32 * (j // 8) + 8 * g + (j % 8)
+    raise ValueError(hyp)
+
+
+def test_mx_fp8_mfma_layout():
+    """v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, e8m0 scales): which byte of which lane
+    is which k (the MX GEMM's operand packing) and which 32-k block a lane's scale byte
+    scales.  Exact check with small-integer e4m3 data against host references of the
+    candidate layouts; C in the standard 16x16 layout (row 4 (l >> 4) + r, col l & 15)."""
+    from dnn_page_vectors_amd.ops._common import P, check, lib, stream
+
+    g = torch.Generator().manual_seed(0)
+    a = torch.randint(-4, 5, (64, 32), generator=g).float()   # lane-major raw operand values
+    b = torch.randint(-4, 5, (64, 32), generator=g).float()
+    ea = torch.randint(-2, 3, (64,), generator=g)
+    eb = torch.randint(-2, 3, (64,), generator=g)
+
+    def run(sa_exp, sb_exp):
+        ad = a.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
+        bd = b.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
+        sad = (127 + sa_exp).to(torch.int32).to(DEV)
+        sbd = (127 + sb_exp).to(torch.int32).to(DEV)
+        c = torch.empty(64, 4, device=DEV)
+        check(lib().pv_mx_probe(P(ad), P(bd), P(sad), P(sbd), P(c), stream(c.device)), "pv_mx_probe")
+        torch.cuda.synchronize()
+        got = torch.empty(16, 16)
+        cc = c.cpu()
+        for l in range(64):
+            for r in range(4):
+                got[4 * (l >> 4) + r, l & 15] = cc[l, r]
+        return got
+
+    def ref(hyp, sa_exp, sb_exp, scale_block):
+        A = torch.zeros(16, 128)
+        B = torch.zeros(128, 16)
+        for l in range(64):
+            for j in range(32):
+                k = _mx_k_of(hyp, l, j)
+                A[l & 15, k] = a[l, j] * 2.0 ** float(sa_exp[scale_block(l, k)])
+                B[k, l & 15] = b[l, j] * 2.0 ** float(sb_exp[scale_block(l, k)])
+        return A @ B
+
+    zero = torch.zeros(64, dtype=torch.long)
+    got1 = run(zero, zero)
+    layouts = [h for h in ("contig32", "halves16", "chunks8") if torch.equal(got1, ref(h, zero, zero, lambda l, k: 0))]
+    print("MX layouts matching unit-scale data:", layouts)
+    assert layouts, "no candidate layout matches"
+    got2 = run(ea, eb)
+    # candidate scale owners: the lane holding (row l & 15, k-block k // 32)
+    def owner(l, k):
+        return (l & 15) + 16 * (k // 32)
+    scaled = [h for h in layouts if torch.equal(got2, ref(h, ea, eb, owner))]
+    print("MX layouts matching per-(row, 32-k block) scales owned by lane row + 16 * block:", scaled)
+    assert scaled, (got2, [ref(h, ea, eb, owner) for h in layouts])

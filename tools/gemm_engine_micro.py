@@ -14,6 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from dnn_page_vectors_amd.ops import gemm as gops  # noqa: E402
+from dnn_page_vectors_amd.ops._common import lib as _lib  # noqa: E402
+
+L = _lib()
 
 # (name, M, N, K, a_col, b_col): BERT-base at 73728 tokens (B 256 x (32 + 256)), MLP / bag
 SHAPES = [
@@ -60,21 +63,31 @@ def main():
         def ours():
             return gops.gemm(a_, b_, a_col, b_col)
 
+        def ours1():  # the plain double-buffered schedule (A/B arm)
+            L.pv_gemm_set_sched(1)
+            try:
+                return gops.gemm(a_, b_, a_col, b_col)
+            finally:
+                L.pv_gemm_set_sched(2)
+
         def lib():
             return torch.mm(lib_a, lib_b, out_dtype=torch.float32)
 
         c1, c2 = ours(), lib()
         err = float((c1 - c2).abs().max() / c2.abs().max())
-        t1, t2 = [], []
+        err1 = float((ours1() - c2).abs().max() / c2.abs().max())
+        t1, t2, t3 = [], [], []
         for _ in range(a.rounds):
             t1.append(timeit(ours, a.iters))
+            t3.append(timeit(ours1, a.iters))
             t2.append(timeit(lib, a.iters))
-        m1, m2 = statistics.median(t1), statistics.median(t2)
+        m1, m2, m3 = statistics.median(t1), statistics.median(t2), statistics.median(t3)
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "a_col": a_col, "b_col": b_col,
-                          "ksplit": gops.auto_ksplit(M, N, K), "engine_ms": round(m1, 4), "library_ms": round(m2, 4),
-                          "engine_tflops": round(fl / m1 / 1e9, 1), "library_tflops": round(fl / m2 / 1e9, 1),
-                          "max_rel_err": err}), flush=True)
+                          "ksplit": gops.auto_ksplit(M, N, K), "engine_ms": round(m1, 4), "engine_v1_ms": round(m3, 4),
+                          "library_ms": round(m2, 4), "engine_tflops": round(fl / m1 / 1e9, 1),
+                          "engine_v1_tflops": round(fl / m3 / 1e9, 1), "library_tflops": round(fl / m2 / 1e9, 1),
+                          "max_rel_err": err, "v1_max_rel_err": err1}), flush=True)
         del A, B, a_, b_, c1, c2
         torch.cuda.empty_cache()
 
