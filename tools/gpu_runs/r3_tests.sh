@@ -2,7 +2,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r3c
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3c/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 250 --timeout-method thread -p no:cacheprovider > gpurun_out/r3c/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc $(tail -1 gpurun_out/r3c/pytest.log)"; [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3c/smoke.log 2>&1
 rc2=$?; echo "smoke rc=$rc2 $(tail -1 gpurun_out/r3c/smoke.log)"; [ $rc2 -eq 0 ] || exit $rc2
