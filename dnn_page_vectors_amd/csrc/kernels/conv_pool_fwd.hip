@@ -431,15 +431,6 @@ __device__ __forceinline__ float max_tagged(float m, float x, unsigned keep, uns
   return r;
 }
 
-// m = max(m, tag(x, bx), tag(y, by)) with ONE v_max3_f32 (OPT & 16: blocks merged in pairs)
-__device__ __forceinline__ float max2_tagged(float m, float x, unsigned bx, float y, unsigned by, unsigned keep) {
-  const float tx = __uint_as_float((__float_as_uint(x) & keep) | bx);
-  const float ty = __uint_as_float((__float_as_uint(y) & keep) | by);
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(tx), "v"(ty));
-  return r;
-}
-
 template <int N3, int N4, int PF, int DBG, int OPT = 0, int DM = -1, bool MIX = false, int NTH = NTHREADS>
 __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4base, char* xl0, int* ids_lds) {
   constexpr int IDS_PT = ids_of<NTH>(), PPT = ppt_of<NTH>();
@@ -531,12 +522,8 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
     if (i < N3) m3[i][r] = max_tagged(m3[i][r], q3[i][r], keep, qtag);
     else m4[i - N3][r] = max_tagged(m4[i - N3][r], q4[i - N3][r], keep, qtag);
   };
-  // OPT & 16 (PAIR): a FULL block's accumulators wait in q3/q4 for the next FULL block, and
-  // the two merge into the running max with one v_max3 per element (3 VALU per element per
-  // two blocks instead of 4); a partial block / the sample end flushes a lone pending one.
-  constexpr bool PAIR = (OPT & 16) != 0 && !PIPE && (DBG & 2) == 0;
   auto flush_pending = [&]() {
-    if ((PIPE || PAIR) && qpend) {
+    if (PIPE && qpend) {
 #pragma unroll
       for (int e = 0; e < NPEND; ++e) pend_elem(e);
       qpend = false;
@@ -588,25 +575,6 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
         for (int i = 0; i < N3; ++i) m3[i] += c3[i];
 #pragma unroll
         for (int i = 0; i < N4; ++i) m4[i] += c4[i];
-      } else if constexpr (FULL && PAIR) {
-        if (!qpend) {  // hold this block for the next one
-#pragma unroll
-          for (int i = 0; i < N3; ++i) q3[i] = c3[i];
-#pragma unroll
-          for (int i = 0; i < N4; ++i) q4[i] = c4[i];
-          qtag = btag;
-          qpend = true;
-        } else {
-#pragma unroll
-          for (int i = 0; i < N3; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) m3[i][r] = max2_tagged(m3[i][r], q3[i][r], qtag, c3[i][r], btag, keep);
-#pragma unroll
-          for (int i = 0; i < N4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) m4[i][r] = max2_tagged(m4[i][r], q4[i][r], qtag, c4[i][r], btag, keep);
-          qpend = false;
-        }
       } else if constexpr (FULL) {
 #pragma unroll
         for (int i = 0; i < N3; ++i)
@@ -617,7 +585,6 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
 #pragma unroll
           for (int r = 0; r < 4; ++r) m4[i][r] = max_tagged(m4[i][r], c4[i][r], keep, btag);
       } else {
-        if constexpr (PAIR) flush_pending();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = t0 + win_of_row(4 * kq + r);
@@ -979,8 +946,6 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
     case 4096 + 3: hipLaunchKernelGGL((conv_pool_fwd4_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 4: hipLaunchKernelGGL((conv_pool_fwd4_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 12: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 12, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
-    case 4096 + 29: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 29, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
-    case 4096 + 25: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 25, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 9: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 9, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 1: hipLaunchKernelGGL((conv_pool_fwd3_kernel<1, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 3: hipLaunchKernelGGL((conv_pool_fwd3_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
