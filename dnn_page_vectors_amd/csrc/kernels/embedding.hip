@@ -343,6 +343,56 @@ __global__ __launch_bounds__(1024) void bag_counts_lds16_kernel(const int* __res
   }
 }
 
+// counts for the MX fp8 bag GEMM: the same 16-bit LDS histogram, the row written as e4m3
+// bytes (c8, ldc8 % 4 == 0: counts <= 16 exact, larger ones rounded to the nearest e4m3
+// value, saturated at 448) and, when the weight gradient is needed, ALSO as bf16 (c16,
+// exact, the operand of the backward's C^T G); columns V..ldc are zeros in both.
+__global__ __launch_bounds__(1024) void bag_counts8_kernel(const int* __restrict__ ids,
+                                                           unsigned short* __restrict__ c16, int ldc16,
+                                                           unsigned char* __restrict__ c8, int ldc8,
+                                                           float* __restrict__ lens, int N, int L, int V, int pad) {
+  extern __shared__ unsigned hist2[];
+  __shared__ int part[16];
+  const int n = blockIdx.x;
+  const int ldh = ldc8 > ldc16 ? ldc8 : ldc16;
+  for (int c = threadIdx.x; c < ldh / 2; c += blockDim.x) hist2[c] = 0u;
+  __syncthreads();
+  const int* row = ids + (size_t)n * L;
+  int local = 0;
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    const int v = row[t];
+    PV_CHECK(v == pad || (v >= 0 && v < V), PV_ERR_ID);
+    if (v != pad && v >= 0 && v < V) {
+      ++local;
+      atomicAdd(&hist2[v >> 1], 1u << ((v & 1) * 16));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
+  __syncthreads();
+  unsigned* r8 = reinterpret_cast<unsigned*>(c8 + (size_t)n * ldc8);
+  for (int c4 = threadIdx.x; c4 < ldc8 / 4; c4 += blockDim.x) {
+    const unsigned a = hist2[2 * c4], b = hist2[2 * c4 + 1];
+    unsigned w = 0;
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf((float)(a & 0xFFFFu), 448.f), fminf((float)(a >> 16), 448.f), w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf((float)(b & 0xFFFFu), 448.f), fminf((float)(b >> 16), 448.f), w, true);
+    r8[c4] = w;
+  }
+  if (c16) {
+    uint2* r16 = reinterpret_cast<uint2*>(c16 + (size_t)n * ldc16);
+    for (int c4 = threadIdx.x; c4 < ldc16 / 4; c4 += blockDim.x) {
+      const unsigned a = hist2[2 * c4], b = hist2[2 * c4 + 1];
+      r16[c4] = uint2{pack_bf16x2((float)(a & 0xFFFFu), (float)(a >> 16)),
+                      pack_bf16x2((float)(b & 0xFFFFu), (float)(b >> 16))};
+    }
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    lens[n] = (float)s;
+  }
+}
+
 PV_DEBUG_EXPORT(embed)
 }  // namespace embed
 }  // namespace pv
@@ -432,6 +482,26 @@ PV_API int pv_bag_counts(const int* ids, void* counts, float* lens, int N, int L
   if (!zeroed) return -2;
   hipLaunchKernelGGL(pv::embed::bag_counts_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, ids,
                      (unsigned short*)counts, lens, N, L, V, ldc, pad);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// counts8 (N, ldc8) e4m3 (+ counts16 (N, ldc16) bf16 when non-null), every element written.
+PV_API int pv_bag_counts8(const int* ids, void* counts16, int ldc16, void* counts8, int ldc8, float* lens, int N,
+                          int L, int V, int pad, void* stream) {
+  if (ldc8 < V || ldc8 % 4 || (counts16 && (ldc16 < V || ldc16 % 4)) || L >= 65536) return -1;
+  const int ldh = counts16 && ldc16 > ldc8 ? ldc16 : ldc8;
+  if (ldh > 40960) return -2;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&pv::embed::bag_counts8_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 40960 * 2) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  hipLaunchKernelGGL(pv::embed::bag_counts8_kernel, dim3(N), dim3(1024), (ldh / 2) * sizeof(unsigned),
+                     (hipStream_t)stream, ids, (unsigned short*)counts16, counts16 ? ldc16 : 0,
+                     (unsigned char*)counts8, ldc8, lens, N, L, V, pad);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -251,6 +251,53 @@ PV_API int pv_fp8_linear(const void* X8, const void* W8, const float* amax_x, co
   return 0;
 }
 
+// ---- transposed quantisation for the MX fp8 GEMM's K-contiguous operands ------------------
+// W (V, E) fp32 row-major -> out (E, ldo) e4m3 bytes, out[e][v] = e4m3(W[v][e] * 448 / amax)
+// for v < V and 0 for V <= v < ldo (the GEMM's K padding); amax from the amax_part_kernel
+// partials (reduced again by every block, 2 KB L2-resident), block 0 stores it.  64 x 64
+// tiles through LDS: coalesced 16-byte reads along E, 4-byte (4 x e4m3) writes along V.
+__global__ __launch_bounds__(256) void quant_t_kernel(const float* __restrict__ W, int V, int E,
+                                                      const float* __restrict__ parts, int nparts,
+                                                      float* __restrict__ amax_out, unsigned char* __restrict__ out,
+                                                      int ldo) {
+  __shared__ float sh[4];
+  __shared__ float tile[64][65];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) m = fmaxf(m, parts[i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const float amax = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *amax_out = amax;
+  const float s = 448.f / fmaxf(amax, 1e-12f);
+  const int v0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+  // load: 64 rows (v) x 64 cols (e) = 1024 float4, 4 per thread
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    const int r = q >> 4, c4 = (q & 15) * 4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (v0 + r < V && e0 + c4 < E) x = *reinterpret_cast<const f32x4*>(W + (size_t)(v0 + r) * E + e0 + c4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[r][c4 + k] = x[k];
+  }
+  __syncthreads();
+  // store: out row e (64 of them) x 64 v bytes = 16 dwords per row, 4 per thread
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    const int e = q >> 4, v4 = (q & 15) * 4;
+    if (e0 + e >= E || v0 + v4 >= ldo) continue;
+    float f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = fminf(fmaxf(tile[v4 + k][e] * s, -448.f), 448.f);
+    unsigned w = 0;
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+    *reinterpret_cast<unsigned*>(out + (size_t)(e0 + e) * ldo + v0 + v4) = w;
+  }
+}
+
 // ---- block-scaled (MX) fp8 MFMA layout probe -------------------------------------------
 // One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, e8m0 scales) by one wave: lane l
 // passes its 32 A bytes a[l], 32 B bytes b[l], its A / B scale bytes sa[l] / sb[l], and
@@ -267,6 +314,25 @@ __global__ void mx_probe_kernel(const v8i_t* a, const v8i_t* b, const int* sa, c
 PV_API int pv_mx_probe(const void* a, const void* b, const int* sa, const int* sb, float* c, void* stream) {
   hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const v8i_t*)a, (const v8i_t*)b, sa,
                      sb, (f32x4*)c);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// W (V, E) fp32 (16-byte aligned, E % 4 == 0) -> out (E, ldo) e4m3, transposed and zero-padded
+// to ldo (ldo % 64 == 0, ldo >= V), *amax_out = max |W|; ws >= AMAX_PARTS floats of scratch.
+PV_API int pv_amax_quant_fp8_t(const float* W, int V, int E, float* ws, float* amax_out, void* out, int ldo,
+                               void* stream) {
+  using namespace pv::fp8;
+  if (E % 4 || ldo % 64 || ldo < V || (reinterpret_cast<uintptr_t>(W) & 15)) return -1;
+  const long n = (long)V * E;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > AMAX_PARTS) blocks = AMAX_PARTS;
+  if (blocks < 1) blocks = 1;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(amax_part_kernel, dim3((unsigned)blocks), dim3(256), 0, st, W, n, ws, 1);
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(quant_t_kernel, dim3(ldo / 64, (E + 63) / 64), dim3(256), 0, st, W, V, E, (const float*)ws,
+                     (int)blocks, amax_out, (unsigned char*)out, ldo);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -5,7 +5,8 @@ The reference scales to long pages only by truncation + a global max-pool
 (data_utils.py:29-68, cnn_dssm_th.py:94).  Here a page of up to
 ``num_chunks * chunk_len`` (8 x 512 = 4096) hashed trigram ids is cut into chunks,
 every chunk is encoded independently by the DSSM MLP tower (bag-of-trigrams via the
-counts GEMM, then fp8 e4m3 MFMA dense layers), and the page vector is the MEAN of its
+counts GEMM — with ``use_fp8`` e4m3 counts x e4m3 table on the block-scaled fp8 MFMA,
+csrc/kernels/gemm_mx8.hip — then fp8 e4m3 MFMA dense layers), and the page vector is the MEAN of its
 non-empty chunk vectors (empty = all padding; masked out).  Chunks are independent, so
 a page could be split over CUs or GPUs with one all-reduce of partial sums (the
 "context parallel" of this workload) — at 288 GB per MI355X it is not
@@ -50,6 +51,7 @@ class ChunkedPageEncoder(TwoTowerModel):
         else:
             self.query_tower = MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)
             self.doc_towers = nn.ModuleList([MLPTower(vocab_size, cfg.mlp_dims, act, gen, use_fp8=cfg.use_fp8)])
+            self.doc_towers[0].long_bags = True  # chunk bags: the counts plan (fp8 MFMA with use_fp8)
 
     @property
     def out_dim(self) -> int:

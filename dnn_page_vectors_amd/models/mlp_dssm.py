@@ -33,6 +33,9 @@ class MLPTower(nn.Module):
     def __init__(self, vocab_size: int, dims, act: str, gen: torch.Generator, use_fp8: bool = False):
         super().__init__()
         self.use_fp8 = use_fp8
+        # set by the owner for towers that see long bags (the chunked encoder's doc tower): with
+        # use_fp8 their bag runs the counts plan on the block-scaled fp8 MFMA (ops/embedding.py)
+        self.long_bags = False
         d1 = dims[0]
         self.embedding = nn.Parameter(torch.empty(vocab_size, d1))
         lim = math.sqrt(6.0 / (vocab_size + d1)) * math.sqrt(vocab_size / 64.0)  # bag mean of ~64 tokens
@@ -54,6 +57,9 @@ class MLPTower(nn.Module):
         c = {"emb16": m if m is not None else self.embedding.detach().to(torch.bfloat16).contiguous()}
         if self.use_fp8:
             c["w8"] = [fops.quantize(w.detach()) for w in self.ws]
+            if self.long_bags:
+                V = self.embedding.shape[0]
+                c["emb8"] = fops.quantize_t(self.embedding, -(-V // fops.MX_BK) * fops.MX_BK)
         return c
 
     def forward(self, ids: torch.Tensor, cache=None) -> torch.Tensor:
@@ -62,9 +68,10 @@ class MLPTower(nn.Module):
         cache = cache or {}
         if self.act in ("none", "relu", "tanh"):  # first bias + activation fused into the bag kernel
             h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True, bias=self.b1,
-                                   act=self.act)
+                                   act=self.act, fp8=self.use_fp8, w8=cache.get("emb8"))
             return self.dense_stack(h, cache, first_done=True)
-        h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True)
+        h = eops.embedding_bag(ids, self.embedding, cache.get("emb16"), pad=0, mean=True, fp8=self.use_fp8,
+                               w8=cache.get("emb8"))
         return self.dense_stack(h, cache)
 
     def dense_stack(self, h: torch.Tensor, cache=None, first_done: bool = False) -> torch.Tensor:

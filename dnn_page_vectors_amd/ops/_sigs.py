@@ -106,6 +106,9 @@ SIGS = {
     "pv_gemm_bf16": "p" "l" "i" "p" "l" "i" "p" "l" "iii" "i" "l" "p" "f" "iii" "p",
     "pv_gemm_set_sched": "i",
     "pv_mx_probe": "ppppp" "p",
+    "pv_gemm_mx8": "p" "l" "p" "l" "p" "l" "iii" "i" "l" "p" "f" "p" "ii" "p",
+    "pv_amax_quant_fp8_t": "p" "ii" "ppp" "i" "p",
+    "pv_bag_counts8": "p" "p" "i" "p" "i" "p" "iiii" "p",
 }
 
 _RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_csort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,

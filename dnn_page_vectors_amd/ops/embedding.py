@@ -44,6 +44,22 @@ def _counts(ids: torch.Tensor, V: int, pad: int):
     return C, lens
 
 
+def _counts8(ids: torch.Tensor, V: int, pad: int, want16: bool):
+    """-> (e4m3 counts (N, ldc8), bf16 counts (N, ldc16) or None, lens): one histogram kernel
+    (embedding.hip::bag_counts8_kernel); ldc8 is the MX GEMM's K padding (multiple of 128)."""
+    from .fp8 import MX_BK
+
+    N, L = ids.shape
+    ldc8 = -(-V // MX_BK) * MX_BK
+    ldc16 = (V + 63) // 64 * 64
+    C8 = torch.empty(N, ldc8, dtype=torch.uint8, device=ids.device)
+    C16 = torch.empty(N, ldc16, dtype=torch.bfloat16, device=ids.device) if want16 else None
+    lens = torch.empty(N, dtype=torch.float32, device=ids.device)
+    check(lib().pv_bag_counts8(P(ids), P(C16), ldc16, P(C8), ldc8, P(lens), N, L, V, pad, stream(ids.device)),
+          "pv_bag_counts8")
+    return C8, C16, lens
+
+
 def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor] = None,
                  bias: Optional[torch.Tensor] = None, act: str = "none") -> torch.Tensor:
     """C (N, V) @ W16 (V, E) in fp32.  The (N, E) output has only (N/256)(E/256) = 32 tiles for
@@ -85,7 +101,7 @@ class _BagFn(torch.autograd.Function):
     epilogue); the backward runs the activation mask, the bias column sum and dW."""
 
     @staticmethod
-    def forward(ctx, ids, W, W16, pad, mean, plan, bias, act):
+    def forward(ctx, ids, W, W16, pad, mean, plan, bias, act, w8=None):
         ids = ids.to(torch.int32).contiguous()
         N, L = ids.shape
         V, E = W.shape
@@ -108,6 +124,19 @@ class _BagFn(torch.autograd.Function):
                                          pad, int(mean), stream(ids.device)), "pv_embedding_bag")
             if not want_keys and ctx.needs_input_grad[1]:
                 C, lens = _counts(ids, V, pad)
+        elif w8 is not None:
+            # fp8 bag (use_fp8 towers): e4m3 counts x the step's e4m3 W^T on the block-scaled
+            # MFMA, split-K partials reduced with the mean / bias / activation epilogue; the
+            # exact bf16 counts are kept only for the weight gradient (C^T G, bf16)
+            from . import fp8 as fops
+
+            W8t, amax = w8
+            C8, C, lens = _counts8(ids, V, pad, ctx.needs_input_grad[1])
+            part = fops.gemm_mx8(C8, W8t, 1.0 / fops.FP8_MAX, amax)
+            if part.dim() == 2:
+                part = part.unsqueeze(0)
+            out = dops.colsum(part, scale=lens if mean else None, bias=bf, act=act, scale_is_len=True)
+            keys = None
         else:
             C, lens = _counts(ids, V, pad)
             out = _counts_gemm(C[:, :V], W16, lens if mean else None, bf, act)
@@ -137,7 +166,7 @@ class _BagFn(torch.autograd.Function):
             elif db.dtype != bias.dtype:
                 db = db.to(bias.dtype)
         if not ctx.needs_input_grad[1]:
-            return None, None, None, None, None, None, db, None
+            return None, None, None, None, None, None, db, None, None
         if ctx.sparse is not None:
             keys = first
             L, E = ctx.sparse
@@ -152,7 +181,7 @@ class _BagFn(torch.autograd.Function):
             if tw is not None:
                 grad_sink.done(W)
                 dW = None
-            return None, dW, None, None, None, None, db, None
+            return None, dW, None, None, None, None, db, None, None
         C = first
         scale = (1.0 / lens.clamp(min=1.0)) if ctx.mean else torch.ones_like(lens)
         gs = (g * scale[:, None]).to(torch.bfloat16)
@@ -164,8 +193,8 @@ class _BagFn(torch.autograd.Function):
             except (TypeError, RuntimeError, NotImplementedError):
                 tw.copy_(Ct @ gs)
             grad_sink.done(W)
-            return None, None, None, None, None, None, db, None
-        return None, (Ct @ gs).float(), None, None, None, None, db, None
+            return None, None, None, None, None, None, db, None, None
+        return None, (Ct @ gs).float(), None, None, None, None, db, None, None
 
 
 def _counts_backward(ctx, g, C, lens, y):
@@ -197,15 +226,18 @@ def _counts_backward(ctx, g, C, lens, y):
         except (TypeError, RuntimeError, NotImplementedError):
             tw.copy_(Ct @ gs)
         grad_sink.done(W)
-        return None, None, None, None, None, None, db, None
-    return None, (Ct @ gs).float(), None, None, None, None, db, None
+        return None, None, None, None, None, None, db, None, None
+    return None, (Ct @ gs).float(), None, None, None, None, db, None, None
 
 
 def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor] = None, pad: int = 0,
                   mean: bool = True, plan: str = "auto", bias: Optional[torch.Tensor] = None,
-                  act: str = "none") -> torch.Tensor:
+                  act: str = "none", fp8: bool = False, w8=None) -> torch.Tensor:
     """(N, L) ids -> (N, E): act(sum (or mean) of the rows of W over non-pad tokens + bias).
-    ``act`` in {none, relu, tanh}; bias / act are fused into the producing kernel on the GPU."""
+    ``act`` in {none, relu, tanh}; bias / act are fused into the producing kernel on the GPU.
+    ``fp8``: long bags (the counts plan) multiply e4m3 counts by the per-tensor-scaled e4m3
+    table on the block-scaled fp8 MFMA (``w8`` = ops.fp8.quantize_t(W) of this step, else
+    quantised here); the weight gradient stays the exact bf16 C^T G (straight-through)."""
     if use_hip(ids, W) and act in _BAG_ACT:
         if W16 is None:
             W16 = W.detach().to(torch.bfloat16).contiguous()
@@ -213,10 +245,37 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
             plan = "gather" if ids.shape[1] <= 256 else "counts"
         if W.shape[1] % 8:
             plan = "counts"
+        if fp8 and plan == "counts" and W.shape[1] % 4 == 0 and W.shape[0] <= 40960:
+            if w8 is None:
+                from . import fp8 as fops
+
+                w8 = fops.quantize_t(W, -(-W.shape[0] // fops.MX_BK) * fops.MX_BK)
+            return _BagFn.apply(ids, W, W16, pad, mean, plan, bias, act, w8)
         return _BagFn.apply(ids, W, W16, pad, mean, plan, bias, act)
+    if fp8 and ids.shape[1] > 256:  # CPU reference of the fp8 bag: e4m3 counts x e4m3 W (STE)
+        return _bag_fp8_reference(ids, W, pad, mean, bias, act)
     out = ref.embedding_bag_sum(ids, W, pad)
     if mean:
         out = out / (ids != pad).sum(dim=1, keepdim=True).clamp(min=1).to(out.dtype)
+    if bias is not None:
+        out = out + bias
+    return dops._torch_act(out, act)
+
+
+def _bag_fp8_reference(ids, W, pad, mean, bias, act):
+    from . import fp8 as fops
+
+    V = W.shape[0]
+    valid = (ids != pad) & (ids >= 0) & (ids < V)
+    C = torch.zeros(ids.shape[0], V, dtype=torch.float32, device=ids.device)
+    C.scatter_add_(1, torch.where(valid, ids, torch.zeros_like(ids)).long(), valid.float())
+    lens = valid.sum(dim=1).float()
+    exact = C @ W  # the GPU backward's exact C^T G: straight-through for counts AND table
+    with torch.no_grad():
+        q = fops.emulate_e4m3(C) @ fops._emulate(W.detach())
+    out = exact + (q - exact).detach() if exact.requires_grad else q
+    if mean:
+        out = out / lens.clamp(min=1.0)[:, None]
     if bias is not None:
         out = out + bias
     return dops._torch_act(out, act)

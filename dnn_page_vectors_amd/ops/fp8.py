@@ -37,6 +37,49 @@ def quantize(x: torch.Tensor, with_bf16: bool = False):
     return (q, amax, x16) if with_bf16 else (q, amax)
 
 
+def quantize_t(w: torch.Tensor, ldo: int):
+    """fp32 (V, E) -> (e4m3 bytes (E, ldo): W^T zero-padded along V to ldo, amax device scalar):
+    the K-contiguous B operand of the MX fp8 GEMM (gemm_mx8), per-tensor scale 448 / amax."""
+    w = w.detach().contiguous().float()
+    V, E = w.shape
+    ws = torch.empty(AMAX_PARTS + 1, dtype=torch.float32, device=w.device)
+    amax = ws[AMAX_PARTS:]
+    out = torch.empty(E, ldo, dtype=torch.uint8, device=w.device)
+    check(lib().pv_amax_quant_fp8_t(P(w), V, E, P(ws), P(amax), P(out), ldo, stream(w.device)), "pv_amax_quant_fp8_t")
+    return out, amax
+
+
+MX_BK = 128  # gemm_mx8.hip BK (bytes of K per tile): K operands are padded to a multiple of it
+
+
+def mx8_ksplit(M: int, N: int, K: int) -> int:
+    """K slices so that the 256 x 128 output tiles x slices cover the 256 CUs (one 96 KB-LDS
+    workgroup per CU), with >= 8 K tiles per slice."""
+    tiles = -(-M // 256) * -(-N // 128)
+    ks = max(1, 256 // tiles)
+    return max(1, min(ks, (K // MX_BK) // 8))
+
+
+def gemm_mx8(a8: torch.Tensor, b8: torch.Tensor, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
+             ksplit: Optional[int] = None) -> torch.Tensor:
+    """fp32 alpha * (*alpha_ptr) * a8 (M, K) . b8 (N, K)^T on the block-scaled fp8 MFMA
+    (csrc/kernels/gemm_mx8.hip); e4m3 bytes, K % 128 == 0.  ksplit > 1 returns the (ksplit,
+    M, N) fp32 partials (the caller's column-sum reduces them with its epilogue)."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    ks = mx8_ksplit(M, N, K) if ksplit is None else int(ksplit)
+    out = torch.empty((ks, M, N) if ks > 1 else (M, N), dtype=torch.float32, device=a8.device)
+    check(lib().pv_gemm_mx8(P(a8), a8.stride(0), P(b8), b8.stride(0), P(out), N, M, N, K, ks, M * N, None,
+                            float(alpha), P(alpha_ptr) if alpha_ptr is not None else None, 0, 0,
+                            stream(a8.device)), "pv_gemm_mx8")
+    return out
+
+
+def emulate_e4m3(x: torch.Tensor) -> torch.Tensor:
+    """Round to the nearest OCP e4m3 value (saturating at +-448), as the GPU conversion."""
+    return x.float().clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float()
+
+
 def _emulate(x: torch.Tensor) -> torch.Tensor:
     """e4m3 round trip with per-tensor current scaling, as the HIP quantiser.  The backward
     is straight-through (identity), like the HIP path's bf16 backward GEMMs on the

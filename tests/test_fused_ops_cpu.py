@@ -6,6 +6,7 @@ import torch
 from dnn_page_vectors_amd.ops import dense as dops
 from dnn_page_vectors_amd.ops import embedding as eops
 from dnn_page_vectors_amd.ops import loss as lops
+from dnn_page_vectors_amd.ops import reference as ref
 
 
 def test_colsum_cpu_modes():

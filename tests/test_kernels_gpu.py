@@ -1496,3 +1496,88 @@ def test_mx_fp8_mfma_layout():
     scaled = [h for h in layouts if torch.equal(got2, ref(h, ea, eb, owner))]
     print("MX layouts matching per-(row, 32-k block) scales owned by lane row + 16 * block:", scaled)
     assert scaled, (got2, [ref(h, ea, eb, owner) for h in layouts])
+
+
+@pytest.mark.parametrize("M,N,K,ks", [(256, 128, 128, 1), (300, 136, 1024, 1), (1000, 520, 768, None),
+                                      (4096, 512, 30080, None), (64, 1000, 2048, 2)])
+def test_gemm_mx8(M, N, K, ks):
+    """gemm_mx8.hip (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 x e4m3, unit block scales):
+    C = alpha * (*alpha_ptr) * A8 . B8^T, edge tiles and split-K partials, against fp32 torch
+    on the dequantised operands (products exact in fp32; only the summation order differs)."""
+    from dnn_page_vectors_amd.ops import fp8 as fops
+
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = fops.emulate_e4m3(torch.randn(M, K, generator=g) * 8)
+    B = fops.emulate_e4m3(torch.randn(N, K, generator=g) * 8)
+    a8 = A.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
+    b8 = B.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
+    amax = torch.tensor([3.0], device=DEV)
+    out = fops.gemm_mx8(a8, b8, 0.25, amax, ksplit=ks)
+    torch.cuda.synchronize()
+    c = out.sum(0) if out.dim() == 3 else out
+    want = 0.75 * (A.double() @ B.double().t())
+    err = float((c.cpu().double() - want).abs().max() / want.abs().max())
+    assert err < 1e-5, err
+
+
+def test_quant_fp8_t_and_counts8():
+    """The MX bag's operands: W^T in e4m3 (per-tensor 448 / amax, zero K padding) and the
+    e4m3 + bf16 count rows of one histogram kernel (exact <= 16, e4m3 rounding above)."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+    from dnn_page_vectors_amd.ops import fp8 as fops
+
+    g = torch.Generator().manual_seed(1)
+    V, E = 1000, 96
+    W = torch.randn(V, E, generator=g) * 0.05
+    w8, amax = fops.quantize_t(W.to(DEV), 1024)
+    torch.cuda.synchronize()
+    a = float(W.abs().max())
+    assert abs(float(amax) - a) < 1e-7
+    want = fops.emulate_e4m3(W.t() * (448.0 / a))
+    got = w8.cpu().view(torch.float8_e4m3fn).float()
+    assert torch.equal(got[:, :V], want) and not got[:, V:].any()
+    ids = torch.randint(1, 40, (16, 700), generator=g, dtype=torch.int32)
+    ids[:, :300] = 5          # one token 300 times: e4m3 rounds 300 -> 288
+    ids[3] = 0                # an all-padding bag
+    C8, C16, lens = eops._counts8(ids.to(DEV), V, 0, True)
+    torch.cuda.synchronize()
+    C = torch.zeros(16, V)
+    C.scatter_add_(1, ids.long(), (ids != 0).float())
+    C[:, 0] = 0
+    assert torch.equal(C16.cpu().float()[:, :V], C) and not C16.cpu()[:, V:].float().any()
+    assert torch.equal(C8.cpu().view(torch.float8_e4m3fn).float()[:, :V], fops.emulate_e4m3(C))
+    assert torch.equal(lens.cpu(), C.sum(1))
+
+
+def test_fp8_bag_matches_reference():
+    """embedding_bag(fp8=True) on the GPU (e4m3 counts x e4m3 W^T on the MX MFMA + split-K
+    column-sum epilogue: mean, bias, tanh) against the CPU reference with the same
+    quantisation; the weight gradient is the exact bf16 C^T G on both (straight-through)."""
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    g = torch.Generator().manual_seed(2)
+    N, L, V, E = 512, 512, 30000, 512
+    # Zipf-like ids: frequent tokens repeat > 16 times per bag (the rounded counts)
+    ranks = torch.arange(1, V, dtype=torch.float64)
+    p = (1.0 / ranks) / (1.0 / ranks).sum()
+    ids = (torch.multinomial(p, N * L, replacement=True, generator=g) + 1).view(N, L).to(torch.int32)
+    ids[:, 400:] = 0
+    W = (torch.randn(V, E, generator=g) * 0.05).requires_grad_(True)
+    b = (torch.randn(E, generator=g) * 0.1).requires_grad_(True)
+    out_ref = eops.embedding_bag(ids, W, pad=0, mean=True, bias=b, act="tanh", fp8=True)
+    gy = torch.randn(N, E, generator=g)
+    (out_ref * gy).sum().backward()
+    Wd = W.detach().to(DEV).requires_grad_(True)
+    bd = b.detach().to(DEV).requires_grad_(True)
+    out = eops.embedding_bag(ids.to(DEV), Wd, pad=0, mean=True, bias=bd, act="tanh", fp8=True)
+    (out * gy.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    err = float((out.detach().cpu() - out_ref.detach()).abs().max())
+    assert err < 2e-4, err
+    exact = eops.embedding_bag(ids, W.detach(), pad=0, mean=True, bias=b.detach(), act="tanh")
+    qerr = float((out.detach().cpu() - exact).abs().max() / exact.abs().max())
+    print(f"fp8 bag vs reference-quantised {err:.2e}, vs exact fp32 (quantisation) {qerr:.3f}")
+    assert qerr < 0.08
+    gw = float((Wd.grad.cpu() - W.grad).abs().max() / W.grad.abs().max())
+    assert gw < 1e-2, gw  # bf16 dz on the GPU
+    torch.testing.assert_close(bd.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
