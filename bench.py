@@ -225,6 +225,8 @@ def main():
     graph_used = trainer._graph is not None
     for i in range(max(0, a.quality_steps - done)):
         m = trainer.train_step(*data.batch(a.batch))
+        if info.rank == 0 and (i + 1) % 100 == 0:
+            print(f"quality step {done + i + 1}: loss {float(m['loss']):.4f}", file=sys.stderr, flush=True)
     quality_loss = float(m["loss"])
 
     recall = recall_local = None

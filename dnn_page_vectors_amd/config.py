@@ -323,7 +323,11 @@ def preset_config(name: str) -> Configuration:
         return Configuration(model="chunked", feature_level="ngram", vocab_hash_size=30000,
                              embedding_dim=512, mlp_dims=(512, 512, 128), chunk_len=512,
                              num_chunks=8, query_length=45, document_length=4096,
-                             batch_size=512, dtype="bf16", use_fp8=True, loss_mode="cross_gpu", J=0)
+                             batch_size=512, dtype="bf16", use_fp8=True, loss_mode="cross_gpu", J=0,
+                             # the MLP tower's in-batch training setting (mlp_xgpu): with the
+                             # reference's [0, 1] cosine clip a fresh batch whose cosines all sit
+                             # <= 0 has zero gradient (loss stuck at ln B, measured round 3)
+                             cos_clip=False, lr=3e-3)
     if name in ("longpage_cdssm", "config5_cdssm"):
         # config 5 with the reference's conv tower as the chunk encoder (8 x 512-trigram chunks
         # through the fused conv kernel, chunk vectors mean-pooled)

@@ -90,6 +90,7 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor
 SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
 _BAG_SPLITK = int(os.environ.get("PAGEVEC_BAG_SPLITK", "0"))  # override of the vocabulary split (A/B)
 BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
+FP8_BAG = os.environ.get("PAGEVEC_FP8_BAG", "1") != "0"  # 0: fp8 towers keep the bf16 counts GEMM (A/B)
 
 
 _BAG_ACT = {"none": 0, "relu": 1, "tanh": 3}
@@ -245,7 +246,7 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
             plan = "gather" if ids.shape[1] <= 256 else "counts"
         if W.shape[1] % 8:
             plan = "counts"
-        if fp8 and plan == "counts" and W.shape[1] % 4 == 0 and W.shape[0] <= 40960:
+        if fp8 and FP8_BAG and plan == "counts" and W.shape[1] % 4 == 0 and W.shape[0] <= 40960:
             if w8 is None:
                 from . import fp8 as fops
 

@@ -1517,7 +1517,8 @@ def test_gemm_mx8(M, N, K, ks):
     c = out.sum(0) if out.dim() == 3 else out
     want = 0.75 * (A.double() @ B.double().t())
     err = float((c.cpu().double() - want).abs().max() / want.abs().max())
-    assert err < 1e-5, err
+    print(f"mx8 {M}x{N}x{K} ks={ks}: max rel err {err:.2e}")
+    assert err < 2e-4, err  # the MFMA's internal sum of a 128-k block is not a plain fp32 chain
 
 
 def test_quant_fp8_t_and_counts8():
@@ -1544,7 +1545,8 @@ def test_quant_fp8_t_and_counts8():
     C = torch.zeros(16, V)
     C.scatter_add_(1, ids.long(), (ids != 0).float())
     C[:, 0] = 0
-    assert torch.equal(C16.cpu().float()[:, :V], C) and not C16.cpu()[:, V:].float().any()
+    # bf16 counts: exact up to 256 (the 300+ repeats round like torch's bf16 cast)
+    assert torch.equal(C16.cpu().float()[:, :V], C.bfloat16().float()) and not C16.cpu()[:, V:].float().any()
     assert torch.equal(C8.cpu().view(torch.float8_e4m3fn).float()[:, :V], fops.emulate_e4m3(C))
     assert torch.equal(lens.cpu(), C.sum(1))
 
