@@ -59,6 +59,8 @@ MODEL_DESC = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="Configuration overrides for A/B runs (recorded in the JSON config)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (queries)")
@@ -177,6 +179,8 @@ def main():
     cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode,
                       deterministic=bool(a.deterministic))
     a.batch = batch
+    if a.set:
+        cfg = cfg.override(a.set)
     if a.dry_run:
         a.batch = min(a.batch, 16)
         cfg = cfg.replace(batch_size=a.batch, query_length=12, document_length=32, vocab_hash_size=1000)
@@ -289,7 +293,8 @@ def main():
                        "launch": "torchrun-env" if os.environ.get("TORCHELASTIC_RUN_ID") else
                                  ("bench-spawn" if W > 1 else "single"),
                        "rccl_env": {k: v for k, v in sorted(os.environ.items())
-                                    if k.startswith(("NCCL_", "RCCL_")) and "SOCKET" not in k}},
+                                    if k.startswith(("NCCL_", "RCCL_")) and "SOCKET" not in k},
+                       **({"overrides": list(a.set)} if a.set else {})},
             "recall_at_10": None if recall is None else round(recall, 4),
             "recall_candidates": a.recall * W if recall is not None else None,
             "recall_at_10_rank_local": None if recall_local is None else round(recall_local, 4),

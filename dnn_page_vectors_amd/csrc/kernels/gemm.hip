@@ -344,6 +344,173 @@ __global__ __launch_bounds__(NTH, 2) void gemm2_kernel(Params p) {
   epilogue(p, acc, split, m0, n0, wr, wc, lane);
 }
 
+
+// v3 accumulator map: acc[i][j][r] = C[m0 + 128 (i >> 2) + 64 wr + 16 (i & 3) + 4 (lane >> 4) + r]
+//                                       [n0 + 128 (j >> 1) + 32 wc + 16 (j & 1) + (lane & 15)]
+__device__ __forceinline__ void epilogue3(const Params& p, f32x4 (&acc)[8][4], int split, int m0, int n0, int wr,
+                                          int wc, int lane) {
+  const bool part = p.ksplit > 1;
+  float* Cs = reinterpret_cast<float*>(p.C) + (part ? (size_t)split * p.slab : 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + 128 * (j >> 1) + 32 * wc + 16 * (j & 1) + (lane & 15);
+    if (col >= p.N) continue;
+    const float bj = (!part && p.bias) ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 128 * (i >> 2) + 64 * wr + 16 * (i & 3) + 4 * (lane >> 4) + r;
+        if (row >= p.M) continue;
+        const size_t o = (size_t)row * p.ldc + col;
+        if (part) {
+          Cs[o] = acc[i][j][r] * p.alpha;
+          continue;
+        }
+        float v = act_f(acc[i][j][r] * p.alpha + bj, p.act);
+        if (p.out_bf16) {
+          unsigned short* Cb = reinterpret_cast<unsigned short*>(p.C);
+          if (p.beta) v += bf16_to_f32(Cb[o]);
+          Cb[o] = f32_to_bf16(v);
+        } else {
+          float* Cf = reinterpret_cast<float*>(p.C);
+          Cf[o] = p.beta ? Cf[o] + v : v;
+        }
+      }
+  }
+}
+
+// ---- v3 schedule: 8 waves in two staggered groups, 4 phases per K tile ------------------
+// (cdna_hip_programming.md §5 "The 256² 8-phase template" / MI355X_MICROARCH "two waves per
+// SIMD": waves w and w + 4 share a SIMD; group 1 (waves 4-7) runs one barrier behind group 0,
+// so on every SIMD one wave's MFMA segment coincides with its partner's load segment.)
+// Each operand tile is staged as two 128-row HALVES; a wave owns rows {64 wr + [0, 64)} of
+// BOTH A halves and columns {32 wc + [0, 32)} of BOTH B halves, so its 128 x 64 output is 4
+// quadrants and the K tile's phases run (A0, B0) (A0, B1) (A1, B0) (A1, B1), B fragments
+// of both halves kept in registers: the LDS of a tile is read only in phases 0 (A0, B0),
+// 1 (B1) and 2 (A1).  Its buffer is therefore free from phase 3 on, and the halves of tile
+// T are staged 4-5 phases before their first read: A0 in phase 3 of tile T - 2, B0 / B1 / A1
+// in phases 0 / 1 / 2 of tile T - 1 (2 glds per thread each).  WAR: every half is re-staged
+// >= 2 phases after its last read (reads retire by lgkmcnt(0) at the start of the MFMA
+// segment).  RAW: each load segment ends with vmcnt(6) (the 3 newest phases' glds may fly),
+// and the next load segment (2 barriers later) reads only halves staged >= 4 phases ago.
+// Raw s_barrier only: __syncthreads() would drain the in-flight glds (vmcnt(0)).
+// Segment = ds_reads + glds + vmcnt | barrier | lgkmcnt(0) setprio(1) 16 MFMAs setprio(0) | barrier.
+constexpr int HALF_BYTES = 128 * 64 * 2;  // 16 KB: 128 rows x 64 k bf16
+
+template <int LAY>
+__device__ __forceinline__ void stage_half(const unsigned short* __restrict__ X, long ld, int r0, int rmax, int k0,
+                                           char* dst) {
+  static_assert(LAY == ROW, "v3: row-major operands");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int piece = wave * 2 + u;                  // 0..15, 1 KB each
+    const int r = piece * 8 + (lane >> 3);           // half row 0..127
+    const int c = (lane & 7) ^ (r & 7);
+    const int gr = min(r0 + r, rmax);
+    glds16(X + (size_t)gr * ld + k0 + c * 8, dst + piece * 1024);
+  }
+}
+
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(NTH, 1) void gemm3_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 4 * HALF_BYTES];  // [buf][A0 B0 B1 A1]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int grp = wave >> 2, wr = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int tm = p.n_fastest ? t / p.tiles_n : t % p.tiles_m;
+  const int tn = p.n_fastest ? t % p.tiles_n : t / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * per, kt1 = min(ktiles, kt0 + per);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    // half q (0 A0, 1 B0, 2 B1, 3 A1) of tile kt into its buffer ((kt - kt0) & 1); past the
+    // split's end a clamped reload (same timing as a real one, so WAR-safe; never read)
+    auto stage_q = [&](int q, int kt) {
+      char* dst = smem + ((kt - kt0) & 1) * 4 * HALF_BYTES + q * HALF_BYTES;
+      const int kk = min(kt, kt1 - 1) * BK;
+      if (q == 0) stage_half<ALAY>(p.A, p.lda, m0, p.M - 1, kk, dst);
+      else if (q == 3) stage_half<ALAY>(p.A, p.lda, m0 + 128, p.M - 1, kk, dst);
+      else stage_half<BLAY>(p.B, p.ldb, n0 + 128 * (q - 1), p.N - 1, kk, dst);
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stage_q(q, kt0);
+    stage_q(0, kt0 + 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // tile kt0 landed; kt0 + 1's A0 may fly
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 one barrier behind
+    bf16x8 a[4][2], b0[2][2], b1[2][2];
+    const int arow = wr * 64, bcol = wc * 32;
+#pragma unroll 1
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const char* cur = smem + ((kt - kt0) & 1) * 4 * HALF_BYTES;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int ah = ph >> 1;  // A half (0: phases 0, 1; 1: phases 2, 3)
+        // ---- load segment
+        if (ph == 0) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) b0[j][s2] = frag<BLAY>(cur + 1 * HALF_BYTES, bcol + 16 * j, s2);
+        }
+        if (ph == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) b1[j][s2] = frag<BLAY>(cur + 2 * HALF_BYTES, bcol + 16 * j, s2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (ph == 0 || ph == 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              a[i][s2] = frag<ALAY>(cur + (ah ? 3 : 0) * HALF_BYTES, arow + 16 * i, s2);
+        }
+        if (ph < 3) stage_q(ph + 1, kt + 1);
+        else stage_q(0, kt + 2);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMA segment: quadrant (ah, bh = ph & 1), K = 64
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16x8 bb = (ph & 1) ? b1[j][s2] : b0[j][s2];
+              acc[4 * ah + i][2 * (ph & 1) + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb, acc[4 * ah + i][2 * (ph & 1) + j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  epilogue3(p, acc, split, m0, n0, wr, wc, lane);
+}
+
 PV_DEBUG_EXPORT(gemm)
 }  // namespace gemm
 }  // namespace pv
@@ -379,7 +546,9 @@ PV_API int pv_gemm_bf16(const void* A, long lda, int a_col, const void* B, long 
     else if (a_col && !b_col) hipLaunchKernelGGL((KER<COL, ROW>), dim3(grid), dim3(NTH), 0, st, p); \
     else hipLaunchKernelGGL((KER<COL, COL>), dim3(grid), dim3(NTH), 0, st, p);                     \
   } while (0)
-  if (g_gemm_sched == 1) PV_GEMM_LAUNCH(gemm_kernel);
+  if (g_gemm_sched == 3 && !a_col && !b_col)
+    hipLaunchKernelGGL((gemm3_kernel<ROW, ROW>), dim3(grid), dim3(NTH), 0, st, p);
+  else if (g_gemm_sched == 1) PV_GEMM_LAUNCH(gemm_kernel);
   else PV_GEMM_LAUNCH(gemm2_kernel);
 #undef PV_GEMM_LAUNCH
   PV_LAUNCH_CHECK();

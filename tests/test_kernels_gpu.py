@@ -1398,13 +1398,19 @@ def test_gemm_engine_layouts(a_col, b_col, M, N, K):
     ref_c = A.float() @ B.float().t()
     a = (A.t().contiguous() if a_col else A).to(DEV)
     b = (B.t().contiguous() if b_col else B).to(DEV)
-    for ks in (1, 0, 4):
-        if ks == 4 and K < 4 * 64:
-            continue
-        c = gops.gemm(a, b, a_col, b_col, ksplit=ks)
-        torch.cuda.synchronize()
-        err = float((c.cpu() - ref_c).abs().max() / ref_c.abs().max())
-        assert err < 1e-5, (ks, err)
+    L = _native.hip()
+    for sched in ((2, 3) if not a_col and not b_col else (2,)):  # v3: staggered 4-phase, row/row
+        L.pv_gemm_set_sched(sched)
+        try:
+            for ks in (1, 0, 4):
+                if ks == 4 and K < 4 * 64:
+                    continue
+                c = gops.gemm(a, b, a_col, b_col, ksplit=ks)
+                torch.cuda.synchronize()
+                err = float((c.cpu() - ref_c).abs().max() / ref_c.abs().max())
+                assert err < 1e-5, (sched, ks, err)
+        finally:
+            L.pv_gemm_set_sched(2)
 
 
 def test_gemm_engine_epilogues():
