@@ -28,7 +28,11 @@ PV_DEBUG_FLAG
 
 constexpr float BCE_EPS = 1e-7f;
 
-// q: (B, D) normalised, d: (B, 1+J, D) normalised (positive first).
+// q: (B, D) normalised, d: (B, 1+J, D) normalised (positive first).  One wave per row; the
+// query row lives in registers (MAXD floats per lane: D <= 64 MAXD), the 1+J raw cosines in
+// wave-uniform registers (J1 <= MAXJ); compile-time (MAXD, MAXJ) in {2, 4, 8, 16} x {16, 64}
+// (BERT towers without projection: D = 768).
+template <int MAXD, int MAXJ>
 __global__ __launch_bounds__(256) void dssm_explicit_kernel(const float* __restrict__ q, const float* __restrict__ d,
                                                             float* __restrict__ loss, float* __restrict__ prob,
                                                             float* __restrict__ dq, float* __restrict__ dd, int B,
@@ -36,7 +40,6 @@ __global__ __launch_bounds__(256) void dssm_explicit_kernel(const float* __restr
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B) return;
-  constexpr int MAXJ = 16, MAXD = 8;  // J+1 <= 16, D <= 512
   float qv[MAXD];
   const float* qr = q + (size_t)row * D;
 #pragma unroll
@@ -44,9 +47,11 @@ __global__ __launch_bounds__(256) void dssm_explicit_kernel(const float* __restr
     int c = lane + 64 * i;
     qv[i] = c < D ? qr[c] : 0.f;
   }
-  float R[MAXJ], S[MAXJ];
+  float cs[MAXJ];  // raw cosines (the clip pass-through needs them in the backward)
   float mx = -INFINITY;
-  for (int j = 0; j < J1; ++j) {
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j >= J1) break;
     const float* dr = d + ((size_t)row * J1 + j) * D;
     float s = 0.f;
 #pragma unroll
@@ -54,14 +59,18 @@ __global__ __launch_bounds__(256) void dssm_explicit_kernel(const float* __restr
       int c = lane + 64 * i;
       if (c < D) s += qv[i] * dr[c];
     }
-    s = wave_sum(s);
-    R[j] = clip ? fminf(fmaxf(s, 0.f), 1.f) : s;
-    S[j] = gamma * R[j];
-    mx = fmaxf(mx, S[j]);
+    cs[j] = wave_sum(s);
+    const float R = clip ? fminf(fmaxf(cs[j], 0.f), 1.f) : cs[j];
+    mx = fmaxf(mx, gamma * R);
   }
+  auto S_of = [&](int j) { return gamma * (clip ? fminf(fmaxf(cs[j], 0.f), 1.f) : cs[j]); };
   float den = 0.f;
-  for (int j = 0; j < J1; ++j) den += __expf(S[j] - mx);
-  const float P0 = __expf(S[0] - mx) / den;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j >= J1) break;
+    den += __expf(S_of(j) - mx);
+  }
+  const float P0 = __expf(S_of(0) - mx) / den;
   const float Pc = fminf(fmaxf(P0, BCE_EPS), 1.f - BCE_EPS);
   if (lane == 0) {
     loss[row] = -__logf(Pc);
@@ -72,24 +81,13 @@ __global__ __launch_bounds__(256) void dssm_explicit_kernel(const float* __restr
   float gq[MAXD];
 #pragma unroll
   for (int i = 0; i < MAXD; ++i) gq[i] = 0.f;
-  for (int j = 0; j < J1; ++j) {
-    const float Pj = __expf(S[j] - mx) / den;
-    float dS = live ? (Pj - (j == 0 ? 1.f : 0.f)) * gscale : 0.f;
-    float r = R[j];
-    float dR = dS * gamma;
-    if (clip) {
-      // recompute the raw cosine to decide the clip pass-through (inclusive bounds, as T.clip)
-      const float* dr = d + ((size_t)row * J1 + j) * D;
-      float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < MAXD; ++i) {
-        int c = lane + 64 * i;
-        if (c < D) s += qv[i] * dr[c];
-      }
-      s = wave_sum(s);
-      (void)r;
-      if (s < 0.f || s > 1.f) dR = 0.f;
-    }
+  for (int j = 0; j < MAXJ; ++j) {
+    if (j >= J1) break;
+    const float Pj = __expf(S_of(j) - mx) / den;
+    const float dS = live ? (Pj - (j == 0 ? 1.f : 0.f)) * gscale : 0.f;
+    // clip pass-through with inclusive bounds, as T.clip
+    const float dR = (clip && (cs[j] < 0.f || cs[j] > 1.f)) ? 0.f : dS * gamma;
     const float* dr = d + ((size_t)row * J1 + j) * D;
     float* ddr = dd + ((size_t)row * J1 + j) * D;
 #pragma unroll
@@ -543,9 +541,19 @@ using namespace pv;
 
 PV_API int pv_dssm_explicit(const float* q, const float* d, float* loss, float* prob, float* dq, float* dd, int B,
                             int J1, int D, float gamma, float gscale, int clip, void* stream) {
-  if (J1 > 16 || D > 512) return -1;
-  hipLaunchKernelGGL(pv::loss::dssm_explicit_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, q, d, loss,
-                     prob, dq, dd, B, J1, D, gamma, gscale, clip);
+  if (J1 < 1 || J1 > 64 || D < 1 || D > 1024) return -1;
+  const dim3 grid((B + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define PV_EXPL(MD, MJ)                                                                                  \
+  hipLaunchKernelGGL((pv::loss::dssm_explicit_kernel<MD, MJ>), grid, dim3(256), 0, st, q, d, loss, prob, dq, dd, \
+                     B, J1, D, gamma, gscale, clip)
+  const int md = D <= 128 ? 2 : D <= 256 ? 4 : D <= 512 ? 8 : 16;
+  if (J1 <= 16) {
+    if (md == 2) PV_EXPL(2, 16); else if (md == 4) PV_EXPL(4, 16); else if (md == 8) PV_EXPL(8, 16); else PV_EXPL(16, 16);
+  } else {
+    if (md == 2) PV_EXPL(2, 64); else if (md == 4) PV_EXPL(4, 64); else if (md == 8) PV_EXPL(8, 64); else PV_EXPL(16, 64);
+  }
+#undef PV_EXPL
   PV_LAUNCH_CHECK();
   return 0;
 }

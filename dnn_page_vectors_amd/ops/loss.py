@@ -56,19 +56,22 @@ class _ExplicitFn(torch.autograd.Function):
         return dq * g[:, None], dd * g[:, None, None], None, None
 
 
-# limits of the fused explicit-loss kernel (pv_dssm_explicit: one wave per row, the 1+J
-# document vectors of a row staged in registers)
-EXPLICIT_MAX_J1 = 16
-EXPLICIT_MAX_D = 512
+# limits of the fused explicit-loss kernel (pv_dssm_explicit: one wave per row, the query row
+# and the 1+J raw cosines in registers; compile-time variants up to these)
+EXPLICIT_MAX_J1 = 64
+EXPLICIT_MAX_D = 1024
 
 
 def dssm_explicit_loss(qn: torch.Tensor, dn: torch.Tensor, gamma: float, clip: bool = True
                        ) -> Tuple[torch.Tensor, torch.Tensor]:
     """qn (B, D), dn (B, 1+J, D) normalised -> (per-row loss (B,), P(D+|Q) (B,)).
 
-    GPU: the fused HIP kernel when 1+J <= 16 and D <= 512; wider heads (e.g. a BERT
-    tower without projection, D = 768) take the torch expression below on the device."""
-    if use_hip(qn, dn) and dn.shape[1] <= EXPLICIT_MAX_J1 and qn.shape[1] <= EXPLICIT_MAX_D:
+    GPU: the fused HIP kernel (1+J <= 64, D <= 1024: covers the BERT tower's D = 768); beyond
+    that the loss is rejected on the GPU rather than silently run as eager torch."""
+    if use_hip(qn, dn):
+        if dn.shape[1] > EXPLICIT_MAX_J1 or qn.shape[1] > EXPLICIT_MAX_D:
+            raise NotImplementedError(f"explicit loss kernel supports 1+J <= {EXPLICIT_MAX_J1} and D <= "
+                                      f"{EXPLICIT_MAX_D}; got 1+J = {dn.shape[1]}, D = {qn.shape[1]}")
         return _ExplicitFn.apply(qn, dn, float(gamma), bool(clip))
     R = torch.clamp((qn.unsqueeze(1) * dn).sum(-1), 0.0, 1.0) if clip else (qn.unsqueeze(1) * dn).sum(-1)
     e = torch.exp(gamma * R - gamma * R.max(dim=1, keepdim=True).values.detach())

@@ -141,10 +141,14 @@ def test_l2norm():
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("clip,J1,D", [(True, 4, 150), (False, 4, 150), (True, 4, 768), (True, 20, 128)])
+@pytest.mark.parametrize("clip,J1,D", [(True, 4, 150), (False, 4, 150), (True, 4, 768), (True, 20, 128),
+                                      (False, 64, 1024), (True, 1, 32)])
 def test_explicit_loss(clip, J1, D):
-    """Fused kernel (1+J <= 16, D <= 512) and the on-device torch route beyond its limits
-    (D = 768: BERT without projection; 1+J = 20) against the fp32 expression."""
+    """The fused kernel's compile-time variants (D up to 1024 — BERT without projection is
+    768 — and 1+J up to 64) against the fp32 expression; beyond them a loud error."""
+    if J1 == 64:
+        with pytest.raises(NotImplementedError):
+            lops.dssm_explicit_loss(torch.zeros(2, 8, device=DEV), torch.zeros(2, 65, 8, device=DEV), 10.0)
     B = 40
     q = torch.relu(torch.randn(B, D, device=DEV))
     d = torch.relu(torch.randn(B, J1, D, device=DEV))

@@ -6,7 +6,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 250 --timeout
 rc=$?; echo "pytest rc=$rc $(tail -1 gpurun_out/r3c/pytest.log)"; [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3c/smoke.log 2>&1
 rc2=$?; echo "smoke rc=$rc2 $(tail -1 gpurun_out/r3c/smoke.log)"; [ $rc2 -eq 0 ] || exit $rc2
+timeout -k 10 300 python bench.py > gpurun_out/r3c/bench_headline.log 2>&1
+rc3=$?; echo "headline rc=$rc3 $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"recall_at_10": [0-9.]*' gpurun_out/r3c/bench_headline.log | tr '\n' ' ')"; [ $rc3 -eq 0 ] || exit $rc3
 timeout -k 10 300 python bench.py --model chunked > gpurun_out/r3c/bench_chunked.log 2>&1
-rc3=$?; echo "chunked rc=$rc3 $(grep '^{' gpurun_out/r3c/bench_chunked.log | cut -c1-120)"; [ $rc3 -eq 0 ] || exit $rc3
-timeout -k 10 300 python bench.py --model chunked_cdssm > gpurun_out/r3c/bench_chunked_cdssm.log 2>&1
-rc4=$?; echo "chunked_cdssm rc=$rc4 $(grep '^{' gpurun_out/r3c/bench_chunked_cdssm.log | cut -c1-120)"; exit $rc
+rc4=$?; echo "chunked rc=$rc4 $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"recall_at_10": [0-9.]*' gpurun_out/r3c/bench_chunked.log | tr '\n' ' ')"; exit $rc
