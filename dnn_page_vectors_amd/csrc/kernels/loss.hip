@@ -20,6 +20,7 @@
 //       ib_pos      : the positive logit (same bf16 inputs) and the one-hot term of
 //                     the gradient, -gscale*g*clip' * {d_pos, q}.
 #include "common.h"
+#include <stdlib.h>
 #include <type_traits>
 
 namespace pv {
@@ -157,17 +158,16 @@ template <int KS>
 __device__ __forceinline__ void st_tile(const bf16x8 (&xb)[2][KS], const unsigned short* yt, f32x4 (&acc)[4][2]) {
   using T = IbTile<KS>;
   const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // k-step 0 takes the inline-constant 0 as its C operand (no per-tile zeroing moves)
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(yt + (c * 16 + (lane & 15)) * T::LDY + s * 32 + (lane >> 4) * 8);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[i][s], acc[c][i], 0, 0, 0);
+      for (int i = 0; i < 2; ++i)
+        acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[i][s], s == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[c][i],
+                                                            0, 0, 0);
     }
 }
 
@@ -407,6 +407,407 @@ __global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __
   }
 }
 
+// ---- ib3: 512-thread workgroups, Y tiles by LDS-DMA into a 3-slot ring --------------------
+// Same per-tile math as ib_bwd_kernel (S^T tile -> G^T in registers -> out^T += Y^T G^T), with
+// the three costs that kept that kernel at ~0.75 PF/s at the W = 8 shape removed:
+//  * 8 waves x 32 X rows = 256 rows per workgroup (one per CU, 2 waves per SIMD): each
+//    staged Y tile feeds twice the MFMAs, half the Y bytes per FLOP;
+//  * Y tiles land in LDS by global_load_lds_dwordx4 (no staging VGPRs: the old kernel sat at
+//    256 VGPRs and spilled), issued two tiles ahead into a 3-slot ring, one barrier per tile,
+//    each wave waiting only for its own pieces of the next tile (counted vmcnt);
+//  * the workgroups of one Y split are consecutive after the XCD remap, so they share an
+//    XCD's L2 (the split's Y tiles come from the Infinity Cache / HBM once per XCD).
+// The LDS image keeps the old row stride (DP + 16 elements, 4 KS + 2 chunks of 16 B): the
+// two pad chunks per row take part in the DMA (each re-reads chunk 0 of its row) so every
+// wave-instruction writes 1 KB of consecutive LDS, and the conflict-free read patterns of
+// st_tile / the transposed reads are unchanged.  !ROW: the 64 per-row scales of a tile ride
+// along as one 4-byte-per-lane DMA (wave 7).
+constexpr int TQ3 = 256;
+
+template <int KS>
+struct Ib3 {
+  static constexpr int DP = KS * 32, LDY = DP + 16;
+  static constexpr int CPR = LDY / 8;           // 16-byte chunks per LDS row
+  static constexpr int PIECES = TD * CPR / 64;  // 1 KB wave-instructions per tile (= CPR)
+  static constexpr int TILE_B = TD * LDY * 2;
+};
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+// wave-uniform n: wait until at most n of this wave's vector-memory operations are in flight
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
+
+// DMA instructions one wave issues per staged tile
+template <int KS, bool ROW>
+__device__ __forceinline__ int ib3_pieces(int wave) {
+  constexpr int P = Ib3<KS>::PIECES;
+  const int n = wave < P ? (P - wave + 7) / 8 : 0;
+  return n + ((!ROW && wave == 7) ? 1 : 0);
+}
+
+template <int KS, bool ROW>
+__device__ __forceinline__ void ib3_stage(const unsigned short* __restrict__ Y, const float* __restrict__ scale,
+                                          int c0, int c_end, char* dst, float* sdst) {
+  using T = Ib3<KS>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < (T::PIECES + 7) / 8; ++u) {
+    const int p = wave + 8 * u;
+    if (p < T::PIECES) {
+      const int q = p * 64 + lane;
+      const int r = q / T::CPR, c = q - r * T::CPR;
+      const int row = min(c0 + r, c_end - 1);  // rows past the split: valid bytes, masked by the epilogue
+      const int cc = c < 4 * KS ? c : 0;
+      glds16(Y + (size_t)row * T::DP + cc * 8, dst + p * 1024);
+    }
+  }
+  if (!ROW && wave == 7) glds4(scale + min(c0 + lane, c_end - 1), sdst);
+}
+
+template <int KS, bool ROW, bool CLIP, bool FWD = false>
+__global__ __launch_bounds__(512, 2) void ib3_kernel(const unsigned short* __restrict__ X,
+                                                      const unsigned short* __restrict__ Y,
+                                                      const float* __restrict__ scale, float* __restrict__ out,
+                                                      float* __restrict__ ws, int nx, int ny, int per_split,
+                                                      int nrb, float gamma, float* __restrict__ part = nullptr) {
+  static_assert(!FWD || ROW, "the fused forward runs over query rows");
+  using T = Ib3<KS>;
+  constexpr int NC = T::DP / 16;
+  constexpr int NB = 3;  // ring slots
+  __shared__ __attribute__((aligned(1024))) char ring[NB * T::TILE_B];
+  __shared__ __attribute__((aligned(16))) float ysc[NB][TD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  // XCD remap: the consecutive ids of one XCD cover the row blocks of one split first
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / nrb, rb = bid - split * nrb;
+  const int r0 = rb * TQ3 + wave * 32;
+  const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
+  const int ntiles = (c_end - c_begin + TD - 1) / TD;
+  const float gl = gamma * 1.4426950408889634f;
+  const int np = ib3_pieces<KS, ROW>(wave);
+  bf16x8 xb[2][KS];
+  load_xb<KS>(X, r0, nx, xb);
+  float rsc[2] = {0.f, 0.f};
+  float rs[2] = {0.f, 0.f};
+  if (ROW && !FWD) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = r0 + i * 16 + (lane & 15);
+      rsc[i] = r < nx ? scale[r] : 0.f;
+    }
+  }
+  f32x4 o[NC][2];
+#pragma unroll
+  for (int n = 0; n < NC; ++n)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) o[n][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ib3_stage<KS, ROW>(Y, scale, c_begin, c_end, ring, ysc[0]);
+  if (ntiles > 1) ib3_stage<KS, ROW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
+  wait_vm(ntiles > 1 ? np : 0);
+  __builtin_amdgcn_s_barrier();
+  const int trow = 4 * g + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
+  f32x4 acc[4][2];
+  // epilogue of the S tile in `acc` (tile slot sb, first Y row c0) + out^T += Y^T . G^T
+  auto epi_out = [&](int sb, int c0) {
+    const unsigned short* yb = reinterpret_cast<const unsigned short*>(ring + sb * T::TILE_B);
+    u32x4 gp[2][2];
+    auto epi = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        f32x4 ysv;
+        if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[sb][c * 16 + 4 * g]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          float gv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int yr = c * 16 + 4 * g + r;
+            const float v = acc[c][i][r];
+            float x;
+            if constexpr (FWD) {
+              const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
+              x = __builtin_fmaf(vc, gl, -gl);
+              if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
+              const float e = __builtin_amdgcn_exp2f(x);
+              rs[i] += e;
+              gv[r] = (!CLIP || vc == v) ? e : 0.f;
+              continue;
+            }
+            if constexpr (CLIP) {
+              const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+              x = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
+            } else {
+              x = __builtin_fmaf(v, gl, -gl);
+            }
+            if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
+            gv[r] = (ROW ? rsc[i] : ysv[r]) * __builtin_amdgcn_exp2f(x);
+          }
+          gp[c >> 1][i][(c & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
+          gp[c >> 1][i][(c & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
+        }
+      }
+    };
+    if (c0 + TD <= c_end) epi(std::true_type{});
+    else epi(std::false_type{});
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int n = 0; n < NC; ++n) {
+        typedef __attribute__((address_space(3))) v4s lds_v4s;
+        const unsigned short* p0 = yb + (s2 * 32 + trow) * T::LDY + n * 16 + tcol;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0 + 16 * T::LDY));
+        const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          o[n][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, gp[s2][i]), o[n][i], 0, 0, 0);
+      }
+  };
+  int buf = 0;
+#pragma unroll 1
+  for (int t = 0; t < ntiles; ++t) {
+    const int c0 = c_begin + t * TD;
+    const bool ahead = t + 2 < ntiles;
+    if (ahead) {  // slot (t + 2) % 3 = (t - 1) % 3: every wave left it at the last barrier
+      const int sb = buf + 2 >= NB ? buf + 2 - NB : buf + 2;
+      ib3_stage<KS, ROW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
+    }
+    st_tile<KS>(xb, reinterpret_cast<const unsigned short*>(ring + buf * T::TILE_B), acc);
+    epi_out(buf, c0);
+    // tile t + 1 must have landed (this wave's pieces; the barrier covers the others');
+    // tile t + 2's pieces may stay in flight
+    wait_vm(ahead ? np : 0);
+    __builtin_amdgcn_s_barrier();
+    buf = buf + 1 == NB ? 0 : buf + 1;
+  }
+  if constexpr (FWD) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int r = r0 + i * 16 + (lane & 15);
+      if (g == 0 && r < nx) part[(size_t)split * nx + r] = v;
+    }
+  }
+  float* dst = (gridDim.x == (unsigned)nrb) ? out : ws + (size_t)split * nx * T::DP;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int x = r0 + i * 16 + (lane & 15);
+    if (x >= nx) continue;
+    float* orow = dst + (size_t)x * T::DP;
+#pragma unroll
+    for (int n = 0; n < NC; ++n) *reinterpret_cast<f32x4*>(orow + n * 16 + 4 * g) = o[n][i];
+  }
+}
+
+// ---- ib5: the ib3 pipeline on v_mfma_f32_32x32x16_bf16 --------------------------------------
+// The epilogue (clip, exp, mask, row sums: ~6 VALU per S element) is as long as the matrix
+// work, and a 16x16x32 MFMA holds its SIMD's vector issue for 8 of its 16 cycles; a
+// 32x32x16 MFMA holds it for 8 of 32, so the partner wave's exp epilogue fits beside the
+// matrix phases (MI355X_MICROARCH.md, per-instruction constants).  Per wave: 32 X rows = the
+// N side of every product; per 64-row Y tile:
+//   S^T[y][x] (two 32x32 tiles, 10 k-steps of 16 over DP)   A = Y rows (ds_read_b128), B = X (registers)
+//   G^T = epilogue(S^T) in registers, and as 32x32 accumulators its rows (y) are exactly the
+//   k index of the next product's B operand (cdna_hip_programming.md "An accumulator tile as
+//   the next MFMA's operand": element j of lane half h is row 16s + 8(j>>2) + 4h + (j&3));
+//   out^T[feat][x] += Y^T[feat][y] G^T[y][x]  (5 feature tiles x 4 k-steps), A = two
+//   ds_read_b64_tr_b16 per fragment (rows 16s + 4h + 0..3 and + 8..11 of the y tile).
+// LDS image: unpadded 320-byte rows (DP = 160), 16-byte chunk c of row y stored at
+// c ^ ((y >> 2) & 3): conflict-free for the b128 reads (16 rows of one chunk per lane group)
+// and the transposed reads (4 consecutive rows x 64 bytes per half-wave).  Y tiles by LDS-DMA
+// into a 3-slot ring as in ib3 (pieces = whole 1 KB wave-instructions: TD * DP * 2 / 1024).
+template <int KS>
+struct Ib5 {
+  static constexpr int DP = KS * 32, ROWB = DP * 2, CPR = DP / 8;
+  static constexpr int PIECES = TD * CPR / 64;  // 20 at DP = 160
+  static constexpr int TILE_B = TD * ROWB;
+  static constexpr int K16 = DP / 16;           // k-steps of the S product
+  static constexpr int FT = DP / 32;            // feature tiles of the out product
+};
+
+__device__ __forceinline__ int ib5_swz(int y) { return (y >> 2) & 3; }
+
+template <int KS, bool ROW>
+__device__ __forceinline__ int ib5_pieces(int wave) {
+  constexpr int P = Ib5<KS>::PIECES;
+  const int n = wave < P ? (P - wave + 7) / 8 : 0;
+  return n + ((!ROW && wave == 7) ? 1 : 0);
+}
+
+template <int KS, bool ROW>
+__device__ __forceinline__ void ib5_stage(const unsigned short* __restrict__ Y, const float* __restrict__ scale,
+                                          int c0, int c_end, char* dst, float* sdst) {
+  using T = Ib5<KS>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < (T::PIECES + 7) / 8; ++u) {
+    const int p = wave + 8 * u;
+    if (p < T::PIECES) {
+      const int q = p * 64 + lane;
+      const int r = q / T::CPR, pc = q - r * T::CPR;
+      const int c = pc ^ ib5_swz(r);           // logical chunk stored at physical chunk pc
+      const int row = min(c0 + r, c_end - 1);  // rows past the split: valid bytes, masked by the epilogue
+      glds16(Y + (size_t)row * T::DP + c * 8, dst + p * 1024);
+    }
+  }
+  if (!ROW && wave == 7) glds4(scale + min(c0 + lane, c_end - 1), sdst);
+}
+
+template <int KS, bool ROW, bool CLIP, bool FWD = false>
+__global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __restrict__ X,
+                                                      const unsigned short* __restrict__ Y,
+                                                      const float* __restrict__ scale, float* __restrict__ out,
+                                                      float* __restrict__ ws, int nx, int ny, int per_split,
+                                                      int nrb, float gamma, float* __restrict__ part = nullptr) {
+  static_assert(!FWD || ROW, "the fused forward runs over query rows");
+  using T = Ib5<KS>;
+  constexpr int NB = 3;
+  __shared__ __attribute__((aligned(1024))) char ring[NB * T::TILE_B];
+  __shared__ __attribute__((aligned(16))) float ysc[NB][TD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / nrb, rb = bid - split * nrb;
+  const int r0 = rb * TQ3 + wave * 32;
+  const int x = r0 + l32;  // this lane's X row
+  const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
+  const int ntiles = (c_end - c_begin + TD - 1) / TD;
+  const float gl = gamma * 1.4426950408889634f;
+  const int np = ib5_pieces<KS, ROW>(wave);
+  // B operand of the S product: X[x][16 ks + 8 h .. + 7]
+  bf16x8 xb[T::K16];
+#pragma unroll
+  for (int ks = 0; ks < T::K16; ++ks)
+    xb[ks] = x < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)x * T::DP + 16 * ks + 8 * h)
+                    : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const float rsc = (ROW && !FWD && x < nx) ? scale[x] : 0.f;
+  float rs = 0.f;
+  f32x16 o[T::FT];
+#pragma unroll
+  for (int f = 0; f < T::FT; ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[f][r] = 0.f;
+  ib5_stage<KS, ROW>(Y, scale, c_begin, c_end, ring, ysc[0]);
+  if (ntiles > 1) ib5_stage<KS, ROW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
+  wait_vm(ntiles > 1 ? np : 0);
+  __builtin_amdgcn_s_barrier();
+  // transposed-read lane address inside a (4-row x 16-feature) block: row q = (lane & 15) >> 2,
+  // features 4p .. 4p+3 (p = lane & 3); lane group g = lane >> 4 -> half h = g >> 1 (rows + 4h),
+  // feature half (g & 1) (+16)
+  const int tq = (lane & 15) >> 2, tf = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  int buf = 0;
+#pragma unroll 1
+  for (int t = 0; t < ntiles; ++t) {
+    const int c0 = c_begin + t * TD;
+    const bool ahead = t + 2 < ntiles;
+    if (ahead) {
+      const int sb = buf + 2 >= NB ? buf + 2 - NB : buf + 2;
+      ib5_stage<KS, ROW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
+    }
+    const char* yb = ring + buf * T::TILE_B;
+    // S^T tiles: acc[yt][r] = S^T[y = 32 yt + 8 (r >> 2) + 4 h + (r & 3)][x]
+    f32x16 acc[2];
+#pragma unroll
+    for (int ks = 0; ks < T::K16; ++ks)
+#pragma unroll
+      for (int yt = 0; yt < 2; ++yt) {
+        const int y = 32 * yt + l32, c = 2 * ks + h;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(yb + y * T::ROWB + ((c ^ ib5_swz(y)) << 4));
+        acc[yt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, xb[ks], ks == 0 ? f32x16{} : acc[yt], 0, 0, 0);
+      }
+    // epilogue -> G^T as bf16 B fragments gp[yt][s] (registers 8s .. 8s+7 of acc[yt])
+    u32x4 gp[2][2];
+    auto epi = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
+#pragma unroll
+      for (int yt = 0; yt < 2; ++yt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // rows y = 32 yt + 8 j + 4 h + (0..3)
+          f32x4 ysv;
+          if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[buf][32 * yt + 8 * j + 4 * h]);
+          float gv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int yr = 32 * yt + 8 * j + 4 * h + r;
+            const float v = acc[yt][4 * j + r];
+            float xx;
+            if constexpr (FWD) {
+              const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
+              xx = __builtin_fmaf(vc, gl, -gl);
+              if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
+              const float e = __builtin_amdgcn_exp2f(xx);
+              rs += e;
+              gv[r] = (!CLIP || vc == v) ? e : 0.f;
+              continue;
+            }
+            if constexpr (CLIP) {
+              const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+              xx = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
+            } else {
+              xx = __builtin_fmaf(v, gl, -gl);
+            }
+            if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
+            gv[r] = (ROW ? rsc : ysv[r]) * __builtin_amdgcn_exp2f(xx);
+          }
+          gp[yt][j >> 1][(j & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
+          gp[yt][j >> 1][(j & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
+        }
+    };
+    if (c0 + TD <= c_end) epi(std::true_type{});
+    else epi(std::false_type{});
+    // out^T[feat][x] += Y^T[feat][y] . G^T[y][x]; k-step (yt, s) = rows 32 yt + 16 s + {4h + 0..3, 8 + 4h + 0..3}
+#pragma unroll
+    for (int yt = 0; yt < 2; ++yt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int f = 0; f < T::FT; ++f) {
+          typedef __attribute__((address_space(3))) v4s lds_v4s;
+          const int ylo = 32 * yt + 16 * s2 + 4 * h + tq, yhi = ylo + 8;
+          const int fe = 32 * f + tf;  // feature of this lane's 8-byte piece (chunk fe >> 3, half (fe & 7))
+          const char* plo = yb + ylo * T::ROWB + ((((fe >> 3) ^ ib5_swz(ylo))) << 4) + (fe & 7) * 2;
+          const char* phi = yb + yhi * T::ROWB + ((((fe >> 3) ^ ib5_swz(yhi))) << 4) + (fe & 7) * 2;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plo));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(phi));
+          const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf16x8, gp[yt][s2]), o[f], 0, 0, 0);
+        }
+    wait_vm(ahead ? np : 0);
+    __builtin_amdgcn_s_barrier();
+    buf = buf + 1 == NB ? 0 : buf + 1;
+  }
+  if constexpr (FWD) {
+    rs += __shfl_xor(rs, 32, 64);
+    if (h == 0 && x < nx) part[(size_t)split * nx + x] = rs;
+  }
+  float* dst = (gridDim.x == (unsigned)nrb) ? out : ws + (size_t)split * nx * T::DP;
+  if (x < nx) {
+    float* orow = dst + (size_t)x * T::DP;
+#pragma unroll
+    for (int f = 0; f < T::FT; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(orow + 32 * f + 8 * j + 4 * h) =
+            f32x4{o[f][4 * j], o[f][4 * j + 1], o[f][4 * j + 2], o[f][4 * j + 3]};
+  }
+}
+
 // out[i] = sum_s ws[s][i], n4 = nx*DP/4
 __global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                               long n4, int ns) {
@@ -622,9 +1023,49 @@ static int ib2_splits(int nx, int ny) {
   return ns < 1 ? 1 : ns;
 }
 
+// Kernel generation (PAGEVEC_IB / pv_ib_set_version), read once per process so the
+// workspace queries and the launches always agree:
+//   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160, ib3 for
+//                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
+//   3: ib3 everywhere;  2: the round-2 256-thread kernels (ib_bwd_kernel)
+static int g_ib_version = -1;
+static int ib_version() {
+  if (g_ib_version < 0) {
+    const char* e = getenv("PAGEVEC_IB");
+    const int v = e ? atoi(e) : 5;
+    g_ib_version = (v == 2 || v == 3) ? v : 5;
+  }
+  return g_ib_version;
+}
+
+PV_API int pv_ib_version() { return ib_version(); }
+// A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)
+PV_API int pv_ib_set_version(int v) {
+  if (v != 2 && v != 3 && v != 5) return -1;
+  g_ib_version = v;
+  return 0;
+}
+
+static int ib3_splits(int nx, int ny) {
+  // one 512-thread workgroup per CU: ~256 fill the chip; keep >= 16 tiles per split
+  const int rb = (nx + pv::loss::TQ3 - 1) / pv::loss::TQ3;
+  int ns = (256 + rb - 1) / rb;
+  const int maxs = (ny + 16 * pv::loss::TD - 1) / (16 * pv::loss::TD);
+  if (ns > maxs) ns = maxs;
+  return ns < 1 ? 1 : ns;
+}
+
+// (splits, Y rows per split) of the current kernel version, every split non-empty
+static void ib_split_plan(int nx, int ny, int& ns, int& per) {
+  ns = ib_version() >= 3 ? ib3_splits(nx, ny) : ib2_splits(nx, ny);
+  per = ((ny + ns - 1) / ns + pv::loss::TD - 1) / pv::loss::TD * pv::loss::TD;
+  ns = (ny + per - 1) / per;
+}
+
 // floats of workspace pv_ib_bwd needs for (nx, ny, DP) (0 = writes out directly)
 PV_API long pv_ib_bwd_ws(int nx, int ny, int DP) {
-  const int ns = ib2_splits(nx, ny);
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
   return ns > 1 ? (long)ns * nx * DP : 0;
 }
 
@@ -633,16 +1074,25 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
                       float gamma, int clip, int row_scale, void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
-  int ns = ib2_splits(nx, ny);
-  int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
-  ns = (ny + per - 1) / per;
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws) return -3;
-  dim3 grid((nx + TQ - 1) / TQ, ns);
   hipStream_t s = (hipStream_t)stream;
-#define PV_IB_BWD(ROWV, CLIPV)                                                                              \
-  IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, ROWV, CLIPV>), grid, dim3(256), 0, s,           \
-                                          (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, \
-                                          ny, per, gamma))
+  const int nrb = (nx + TQ3 - 1) / TQ3;
+  const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
+#define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
+  if (ib_version() == 5 && ROWV && DP == 160) {                                                                 \
+    hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else if (ib_version() >= 3) {                                                                               \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV>), grid3, dim3(512), 0, s,              \
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
+                                            nx, ny, per, nrb, gamma));                                          \
+  } else {                                                                                                      \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, ROWV, CLIPV>), grid, dim3(256), 0, s,            \
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
+                                            nx, ny, per, gamma));                                               \
+  }
   if (row_scale) {
     if (clip) { PV_IB_BWD(true, true); } else { PV_IB_BWD(true, false); }
   } else {
@@ -663,10 +1113,9 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
 // Fused forward + dQ part (see ib_bwd_kernel FWD): sumexp (nx), U (nx, DP) fp32 fully
 // written; ws_u = pv_ib_bwd_ws(nx, ny, DP) floats, part = pv_ib_fwd_dq_parts(nx, ny) floats.
 PV_API long pv_ib_fwd_dq_parts(int nx, int ny) {
-  using namespace pv::loss;
-  int ns = ib2_splits(nx, ny);
-  const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
-  return (long)((ny + per - 1) / per) * nx;
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
+  return (long)ns * nx;
 }
 
 PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, float* ws_u, float* part, int nx,
@@ -674,16 +1123,25 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
                         void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192) return -2;
-  int ns = ib2_splits(nx, ny);
-  const int per = ((ny + ns - 1) / ns + TD - 1) / TD * TD;
-  ns = (ny + per - 1) / per;
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws_u) return -3;
-  dim3 grid((nx + TQ - 1) / TQ, ns);
   hipStream_t s = (hipStream_t)stream;
-#define PV_IB_FWDDQ(CLIPV)                                                                                    \
-  IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true, CLIPV, true>), grid, dim3(256), 0, s,       \
-                                          (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u,  \
-                                          nx, ny, per, gamma, part))
+  const int nrb = (nx + TQ3 - 1) / TQ3;
+  const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
+#define PV_IB_FWDDQ(CLIPV)                                                                                      \
+  if (ib_version() == 5 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() >= 3) {                                                                               \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true>), grid3, dim3(512), 0, s,        \
+                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
+                                            ws_u, nx, ny, per, nrb, gamma, part));                              \
+  } else {                                                                                                      \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true, CLIPV, true>), grid, dim3(256), 0, s,      \
+                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
+                                            ws_u, nx, ny, per, gamma, part));                                   \
+  }
   if (clip) { PV_IB_FWDDQ(true); } else { PV_IB_FWDDQ(false); }
 #undef PV_IB_FWDDQ
   PV_LAUNCH_CHECK();

@@ -67,6 +67,8 @@ SIGS = {
     "pv_ib_fwd_dq": "pppppp" "iiif" "i" "ppp" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
     "pv_ib_rows": "pppp" "ii" "fi" "p",
+    "pv_ib_version": "",
+    "pv_ib_set_version": "i",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",
     "pv_embedding_bag": "ppppp" "pi" "iiiiii" "p",

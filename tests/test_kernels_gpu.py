@@ -193,6 +193,46 @@ def test_inbatch_loss(B, M, D, clip):
     torch.testing.assert_close(dn.grad, dn2.grad, rtol=3e-2, atol=3e-3)
 
 
+@pytest.mark.parametrize("ver", [5, 3, 2])
+@pytest.mark.parametrize("B,M,clip", [(700, 5000, True), (4096, 16384, False), (300, 20000, True)])
+def test_inbatch_loss_split_shapes(ver, B, M, clip):
+    """Shapes with several Y splits, >= 3 tiles per split (the ib3 LDS ring wraps), a
+    partial last tile and row blocks past nx, for both kernel generations (ib3: 512-thread
+    workgroups + LDS-DMA ring; PAGEVEC_IB=2: the 256-thread kernel) vs the fp32 reference."""
+    from dnn_page_vectors_amd.ops._common import lib as _lib
+
+    L_ = _lib()
+    old = L_.pv_ib_version()
+    assert L_.pv_ib_set_version(ver) == 0
+    try:
+        torch.manual_seed(3)
+        D = 150
+        q = torch.randn(B, D, device=DEV)
+        dd = torch.randn(M, D, device=DEV)
+        # weakly correlated positives: with P+ ~ 1 the bf16-rounded positive term of dQ
+        # cancels against the one-hot term (an O(1) relative error on a ~0 gradient row)
+        dd[:B] = q + 2.0 * dd[:B]
+        if clip:
+            q, dd = q.abs(), dd.abs()
+        qn = bf(ref.l2_normalize(q)).requires_grad_(True)
+        dn = bf(ref.l2_normalize(dd)).requires_grad_(True)
+        pos = torch.arange(B, device=DEV, dtype=torch.int32)
+        loss, P = lops.inbatch_loss(qn, dn, pos, 10.0, clip)
+        qn2 = qn.detach().clone().requires_grad_(True)
+        dn2 = dn.detach().clone().requires_grad_(True)
+        lr, _ = ref.inbatch_softmax_loss(qn2, dn2, pos, 10.0, clip)
+        torch.testing.assert_close(loss, lr, rtol=2e-3, atol=2e-3)
+        w = torch.rand(B, device=DEV)
+        (loss * w).sum().backward()
+        (lr * w).sum().backward()
+        for a, b in ((qn.grad, qn2.grad), (dn.grad, dn2.grad)):
+            rel = float((a - b).norm() / b.norm())
+            assert rel < 3e-2, rel
+            torch.testing.assert_close(a, b, rtol=5e-2, atol=float(b.abs().max()) * 2e-2)
+    finally:
+        L_.pv_ib_set_version(old)
+
+
 def test_adam_matches_reference():
     from dnn_page_vectors_amd.ops.optim import FlatAdam, FlatParams
 

@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--M", default="16384,131072")
     ap.add_argument("--D", type=int, default=150)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ib", default="5,3,2", help="kernel generations to time (loss.hip pv_ib_set_version)")
     a = ap.parse_args()
+    from dnn_page_vectors_amd.ops._common import lib
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
     for M in [int(x) for x in a.M.split(",")]:
@@ -45,7 +47,8 @@ def main():
         d = dn.clone().requires_grad_(True)
         lr, _ = ref.inbatch_softmax_loss(q, d, pos, 10.0, True)
         lr.sum().backward()
-        if True:
+        for ver in [int(v) for v in a.ib.split(",")]:
+            assert lib().pv_ib_set_version(ver) == 0
             l, gq, gd = run(qn, dn, pos)
             e = [float((l - lr.detach()).abs().max()), float((gq - q.grad).abs().max() / q.grad.abs().max()),
                  float((gd - d.grad).abs().max() / d.grad.abs().max())]
@@ -58,7 +61,7 @@ def main():
                 ts.append(time.perf_counter() - t0)
             t = sorted(ts[2:])[len(ts[2:]) // 2]
             fl = 2.0 * a.B * M * 160 * 5
-            print(f"M={M}: fwd+bwd {t*1e3:.3f} ms ({fl / t / 1e12:.0f} TF/s incl. glue) "
+            print(f"ib{ver} M={M}: fwd+bwd {t*1e3:.3f} ms ({fl / t / 1e12:.0f} TF/s incl. glue) "
                   f"err loss {e[0]:.2e} dq {e[1]:.2e} dd {e[2]:.2e}", flush=True)
 
 
