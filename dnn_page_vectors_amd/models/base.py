@@ -110,6 +110,11 @@ class TwoTowerModel(nn.Module):
             return None
         if determinism.enabled():  # deterministic mode: one stream (ops/determinism.py)
             return None
+        if self._towers_share_params():
+            # a tied parameter would get the query tower's gradient written on the side
+            # stream (grad sink) and the page tower's added by autograd on the main stream:
+            # nothing orders the two, so shared towers keep one stream
+            return None
         st = getattr(self, "_qstreams", None)
         if st is None:
             st = self._qstreams = {}
@@ -117,6 +122,18 @@ class TwoTowerModel(nn.Module):
         if dev not in st:
             st[dev] = torch.cuda.Stream(device=q_ids.device)
         return st[dev]
+
+    def _towers_share_params(self) -> bool:
+        """True when the query tower and a page tower hold the same parameter object
+        (siamese BERT on the unpacked path, any tied weight); computed once."""
+        v = getattr(self, "_towers_shared", None)
+        if v is None:
+            q = getattr(self, "query_tower", None)
+            docs = list(getattr(self, "doc_towers", []) or [])
+            qp = {id(p) for p in q.parameters()} if q is not None else set()
+            v = any(id(p) in qp for d in docs for p in d.parameters())
+            self._towers_shared = v
+        return v
 
     @torch.no_grad()
     def encode(self, ids: torch.Tensor, tower: str = "doc", batch_size: int = 4096,

@@ -98,3 +98,17 @@ def test_flops_estimate_matches_survey():
     cfg = Configuration(feature_level="char")
     # char sample fwd ~4.25 GFLOP
     assert abs(cdssm_flops_per_sample(cfg) / 1e9 - 4.25) < 0.05
+
+
+def test_query_stream_off_for_shared_towers():
+    """tied query / page tower parameters must not take the side-stream path."""
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.models import build_model
+
+    cfg = Configuration(model="bert", bert_layers=1, bert_hidden=32, bert_intermediate=64, bert_heads=2,
+                        bert_max_len=16, bert_out_dim=0, share_doc_tower=True)
+    m = build_model(cfg, 50)
+    assert m._towers_share_params()
+    cfg2 = Configuration(model="bert", bert_layers=1, bert_hidden=32, bert_intermediate=64, bert_heads=2,
+                         bert_max_len=16, bert_out_dim=0, share_doc_tower=False)
+    assert not build_model(cfg2, 50)._towers_share_params()
