@@ -71,11 +71,32 @@ __device__ __forceinline__ void load16(const T* __restrict__ P, int rows, int co
   }
 }
 
+// The same 16 elements for an operand stored TRANSPOSED: element (row, k + j) of the
+// logical operand is P[(k + j) * ld + row] (the dgrad's W^T read straight from W: strided
+// scalar loads of a small, L2-resident matrix instead of a transposed copy per step).
+template <typename T>
+__device__ __forceinline__ void load16t(const T* __restrict__ P, int rows, int cols, int ld, int row, int k,
+                                        u32x4 (&out)[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    unsigned w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = k + 8 * h + 2 * e;
+      const float x0 = (row < rows && c < cols) ? ldf<T>(P, (size_t)c * ld + row) : 0.f;
+      const float x1 = (row < rows && c + 1 < cols) ? ldf<T>(P, (size_t)(c + 1) * ld + row) : 0.f;
+      w[e] = pack_bf16x2(x0, x1);
+    }
+    out[h] = u32x4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 // Y^T tile = W . X^T: A operand = W rows (n), B operand = X rows (m), so the C layout
 // puts one m per lane and 4 CONSECUTIVE n per lane -> 16-byte fp32 / 8-byte bf16 stores.
 // BK = 64 (2 MFMA k-steps per tile, 8 MFMAs per wave), tile t+1 is fetched into
 // registers while tile t's MFMAs run and written to the other LDS buffer (1 barrier/tile).
-template <typename TX, typename TW>
+// WT: W is stored as [K][N] (the dgrad dx = dz W of a layer whose weight is [N_out][K_in]).
+template <typename TX, typename TW, bool WT = false>
 __global__ __launch_bounds__(256) void linear_act_kernel(const TX* __restrict__ X, const TW* __restrict__ W,
                                                          const float* __restrict__ bias, float* __restrict__ Y,
                                                          unsigned short* __restrict__ Ybf, int M, int N, int K,
@@ -95,7 +116,8 @@ __global__ __launch_bounds__(256) void linear_act_kernel(const TX* __restrict__ 
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   u32x4 ra[2], rb[2];
   load16<TX>(X, M, K, ldx, m0 + sr, sc, xvec, ra);
-  load16<TW>(W, N, K, K, n0 + sr, sc, wvec, rb);
+  if constexpr (WT) load16t<TW>(W, N, K, N, n0 + sr, sc, rb);
+  else load16<TW>(W, N, K, K, n0 + sr, sc, wvec, rb);
   *reinterpret_cast<u32x4*>(&As[0][sr * LDA + sc]) = ra[0];
   *reinterpret_cast<u32x4*>(&As[0][sr * LDA + sc + 8]) = ra[1];
   *reinterpret_cast<u32x4*>(&Bs[0][sr * LDA + sc]) = rb[0];
@@ -106,7 +128,8 @@ __global__ __launch_bounds__(256) void linear_act_kernel(const TX* __restrict__ 
     const bool more = k0 + BK < K;
     if (more) {
       load16<TX>(X, M, K, ldx, m0 + sr, k0 + BK + sc, xvec, ra);
-      load16<TW>(W, N, K, K, n0 + sr, k0 + BK + sc, wvec, rb);
+      if constexpr (WT) load16t<TW>(W, N, K, N, n0 + sr, k0 + BK + sc, rb);
+      else load16<TW>(W, N, K, K, n0 + sr, k0 + BK + sc, wvec, rb);
     }
 #pragma unroll
     for (int s2 = 0; s2 < BK / 32; ++s2) {
@@ -153,6 +176,96 @@ __global__ __launch_bounds__(256) void linear_act_kernel(const TX* __restrict__ 
             if (Y) Y[(size_t)m * ldy + n + r] = y[r];
             if (Ybf) Ybf[(size_t)m * ldy + n + r] = f32_to_bf16(y[r]);
           }
+      }
+    }
+  }
+}
+
+// Weight gradient of linear_act: dW[n][k] = sum_m dz[m][n] x[m][k] (dz fp32 or bf16 (M, N),
+// x fp32 or bf16 (M, K), both row-major as the forward left them: no transposed copies).
+// The reduction runs over the ROWS of both operands, so each 64-row step is staged into LDS
+// transposed ([n][m] and [k][m], bf16; one ds_write_b32 per lane and column writes a row
+// pair, a half-wave covers 64 consecutive m of one LDS row: conflict-free), so the MFMA
+// fragments are the same ds_read_b128 rows as linear_act's.  64 x 64 or 128 x 128 output
+// tile per workgroup (4 waves, 2 x 2; the larger tile halves the operand re-reads of wide
+// layers), rows split over gridDim.z: each slice writes its fp32 partial
+// tile into slab z of a workspace that the column-sum kernel reduces in a fixed order
+// (deterministic, no atomics).
+template <typename TZ, typename TX, int T>
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const TZ* __restrict__ dz, const TX* __restrict__ X,
+                                                           float* __restrict__ ws, int M, int N, int K, int rows_per) {
+  // T x T output tile (T = 64 or 128), 4 waves in 2 x 2, each (T/2) x (T/2)
+  constexpr int SUB = T / 32;  // 16x16 accumulator tiles per wave side
+  __shared__ __attribute__((aligned(16))) unsigned short As[T * LDA];  // dz^T tile [n][m]
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[T * LDA];  // x^T tile  [k][m]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * T, k0 = blockIdx.y * T;
+  const int m_begin = blockIdx.z * rows_per, m_end = min(M, m_begin + rows_per);
+  f32x4 acc[SUB][SUB];  // [k-subtile][n-subtile]
+#pragma unroll
+  for (int i = 0; i < SUB; ++i)
+#pragma unroll
+    for (int j = 0; j < SUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging: waves 0-1 stage dz, waves 2-3 x; lane = a row PAIR (2 * (lane & 31), + 1) and
+  // column groups of 16 (group q = 4u + 2 (wave & 1) + (lane >> 5), u < T / 64): one
+  // ds_write_b32 per lane and column puts the pair side by side in the transposed row
+  const bool zw = wave < 2;
+  const int mp = 2 * (lane & 31);
+  const bool zvec = (N % (16 / (int)sizeof(TZ))) == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0;
+  const bool xvec = (K % (16 / (int)sizeof(TX))) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  unsigned short* dst = zw ? As : Bs;
+  for (int m0 = m_begin; m0 < m_end; m0 += BK) {
+#pragma unroll
+    for (int u = 0; u < T / 64; ++u) {
+      const int c0 = 16 * (4 * u + 2 * (wave & 1) + (lane >> 5));
+      u32x4 r0[2], r1[2];  // rows m0 + mp, m0 + mp + 1: 16 columns as bf16 (zeros past the edges)
+      if (zw) {
+        load16<TZ>(dz, m_end, N, N, m0 + mp, n0 + c0, zvec, r0);
+        load16<TZ>(dz, m_end, N, N, m0 + mp + 1, n0 + c0, zvec, r1);
+      } else {
+        load16<TX>(X, m_end, K, K, m0 + mp, k0 + c0, xvec, r0);
+        load16<TX>(X, m_end, K, K, m0 + mp + 1, k0 + c0, xvec, r1);
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned lo = (r0[c >> 3][(c >> 1) & 3] >> (16 * (c & 1))) & 0xFFFFu;
+        const unsigned hi = (r1[c >> 3][(c >> 1) & 3] >> (16 * (c & 1))) & 0xFFFFu;
+        *reinterpret_cast<unsigned*>(&dst[(c0 + c) * LDA + mp]) = lo | (hi << 16);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < BK / 32; ++s2) {
+      bf16x8 a[SUB], b[SUB];
+#pragma unroll
+      for (int i = 0; i < SUB; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&Bs[(wk * (T / 2) + i * 16 + (lane & 15)) * LDA + s2 * 32 + g * 8]);
+#pragma unroll
+      for (int j = 0; j < SUB; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&As[(wn * (T / 2) + j * 16 + (lane & 15)) * LDA + s2 * 32 + g * 8]);
+#pragma unroll
+      for (int i = 0; i < SUB; ++i)
+#pragma unroll
+        for (int j = 0; j < SUB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // acc[i][j][r] = dW[n = n0 + wn*T/2 + j*16 + (lane&15)][k = k0 + wk*T/2 + i*16 + 4g + r]
+  float* slab = ws + (size_t)blockIdx.z * N * K;
+#pragma unroll
+  for (int j = 0; j < SUB; ++j) {
+    const int n = n0 + wn * (T / 2) + j * 16 + (lane & 15);
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < SUB; ++i) {
+      const int k = k0 + wk * (T / 2) + i * 16 + 4 * g;
+      if (k + 4 <= K && (K & 3) == 0) {
+        *reinterpret_cast<f32x4*>(slab + (size_t)n * K + k) = acc[i][j];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (k + r < K) slab[(size_t)n * K + k + r] = acc[i][j][r];
       }
     }
   }
@@ -311,6 +424,50 @@ PV_API int pv_linear_act(const void* X, int xdt, const void* W, int wdt, const f
   else
     hipLaunchKernelGGL((linear_act_kernel<unsigned short, unsigned short>), grid, dim3(256), 0, s,
                        (const unsigned short*)X, (const unsigned short*)W, bias, Y, yb, M, N, K, ldx, ldy, act);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// dW (N, K) partial slabs: rows [z * rows_per, (z + 1) * rows_per) of dz / x go to slab z,
+// ws holds ceil(M / rows_per) * N * K floats; rows_per a multiple of 64; tile 64 or 128.
+// zdt / xdt: 0 = fp32, 1 = bf16.
+PV_API int pv_linear_wgrad(const void* dz, int zdt, const void* X, int xdt, float* ws, int M, int N, int K, int rows_per,
+                           int tile, void* stream) {
+  using namespace pv::dense;
+  if (M < 1 || N < 1 || K < 1 || rows_per < BK || rows_per % BK || (tile != 64 && tile != 128)) return -1;
+  dim3 grid((N + tile - 1) / tile, (K + tile - 1) / tile, (M + rows_per - 1) / rows_per);
+  hipStream_t s = (hipStream_t)stream;
+#define PV_WG(TZ, TXX)                                                                                           \
+  if (tile == 64)                                                                                                \
+    hipLaunchKernelGGL((linear_wgrad_kernel<TZ, TXX, 64>), grid, dim3(256), 0, s, (const TZ*)dz, (const TXX*)X, ws, \
+                       M, N, K, rows_per);                                                                       \
+  else                                                                                                           \
+    hipLaunchKernelGGL((linear_wgrad_kernel<TZ, TXX, 128>), grid, dim3(256), 0, s, (const TZ*)dz, (const TXX*)X,    \
+                       ws, M, N, K, rows_per)
+  if (zdt == 0 && xdt == 0) { PV_WG(float, float); }
+  else if (zdt == 0) { PV_WG(float, unsigned short); }
+  else if (xdt == 0) { PV_WG(unsigned short, float); }
+  else { PV_WG(unsigned short, unsigned short); }
+#undef PV_WG
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// dx (M, K) fp32 = dz (M, N) . W (N, K): linear_act with W read transposed in its staging.
+PV_API int pv_linear_dgrad(const void* dz, int zdt, const void* W, int wdt, float* dx, int M, int N, int K,
+                           void* stream) {
+  using namespace pv::dense;
+  // GEMM view: rows M, out columns K (= the layer input width), reduction N
+  dim3 grid((M + BM - 1) / BM, (K + BN - 1) / BN);
+  hipStream_t s = (hipStream_t)stream;
+#define PV_DG(TZ, TWW)                                                                                           \
+  hipLaunchKernelGGL((linear_act_kernel<TZ, TWW, true>), grid, dim3(256), 0, s, (const TZ*)dz, (const TWW*)W, \
+                     nullptr, dx, nullptr, M, K, N, N, K, 0)
+  if (zdt == 0 && wdt == 0) PV_DG(float, float);
+  else if (zdt == 0) PV_DG(float, unsigned short);
+  else if (wdt == 0) PV_DG(unsigned short, float);
+  else PV_DG(unsigned short, unsigned short);
+#undef PV_DG
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -50,6 +50,8 @@ SIGS = {
     "pv_w2v_train": "pppppp" "ll" "iiii" "u" "f" "i" "p",
     # dense.hip
     "pv_linear_act": "pipippp" "iiiiii" "p",
+    "pv_linear_wgrad": "pipip" "iiiii" "p",
+    "pv_linear_dgrad": "pipip" "iii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
     "pv_l2norm_bwd": "ppppp" "ii" "p",
     "pv_act_bwd_rowscale": "pppp" "p" "lli" "p",

@@ -1,9 +1,12 @@
 """Fused linear + bias + activation (K4) and L2 normalisation (K5).
 
 GPU forward: ``csrc/kernels/dense.hip`` (MFMA bf16, fp32 accumulate, fused epilogue).
-Backward: the activation mask is a HIP elementwise kernel; dW = dz^T x and dx = dz W
-are plain GEMMs and go to hipBLASLt through torch.mm (per the design rule: library
-GEMMs for plain GEMMs, hand-written kernels for the fused hot ops).
+Backward: the activation mask is a HIP elementwise kernel; dx = dz W runs on the same
+linear_act kernel with W^T as its weight, dW = dz^T x on linear_wgrad_kernel (rows split
+into partial slabs, reduced by the column-sum kernel).  On the model shapes both are at or
+below hipBLASLt's time (tools/dense_bwd_micro.py, host-timed: MLP 512x512 dgrad 45 vs
+74 us, wgrad 51 vs 72 us; CDSSM page tower 26 / 39 vs 33 / 35-42 us, query tower 12 / 21 vs
+24 / 41 us).  ``PAGEVEC_DENSE_BWD=lib`` keeps the library GEMMs.
 """
 from __future__ import annotations
 
@@ -55,17 +58,20 @@ class _LinearActFn(torch.autograd.Function):
                 pre.requires_grad_(True)
                 g = torch.autograd.grad(torch.nn.functional.gelu(pre, approximate="tanh"), pre, dy2)[0]
             dz = g
-        xf = x2.float()
+        hipb = _HIP_BWD and dz.is_cuda
+        xf = x2 if hipb else x2.float()  # the in-tree kernels stage fp32 or bf16 x directly
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dz @ w.float()).view(ctx.xshape).to(x2.dtype)
+            dxf = dgrad_hip(dz, w) if hipb else dz @ w.float()
+            dx = dxf.view(ctx.xshape).to(x2.dtype)
+        wg = wgrad_hip if hipb else _wgrad
         if ctx.needs_input_grad[1]:
             tw = grad_sink.write_target(ctx.params[0])  # straight into the flat gradient (ops/grad_sink.py)
             if tw is not None:
-                _wgrad(dz, xf, out=tw)
+                wg(dz, xf, out=tw)
                 grad_sink.done(ctx.params[0])
             else:
-                dw = _wgrad(dz, xf).to(w.dtype)
+                dw = wg(dz, xf).to(w.dtype)
         if b is not None and ctx.needs_input_grad[2]:
             tb = grad_sink.write_target(ctx.params[1])
             if tb is not None:
@@ -77,6 +83,10 @@ class _LinearActFn(torch.autograd.Function):
 
 
 _COLSUM_HIP = os.environ.get("PAGEVEC_COLSUM", "1") != "0"  # 0: torch reductions (A/B)
+# dense backward GEMMs on the in-tree kernels (dgrad on linear_act with W^T, wgrad on
+# linear_wgrad_kernel); "lib": hipBLASLt through torch (A/B, tools/dense_bwd_micro.py)
+_HIP_BWD = os.environ.get("PAGEVEC_DENSE_BWD", "hip") != "lib"
+_WG_TARGET = int(os.environ.get("PAGEVEC_WGRAD_WG", "512"))  # wgrad workgroups (row slices x tiles)
 
 
 def _colsum_ok(x: torch.Tensor, C: int, ldx: int) -> bool:
@@ -151,6 +161,48 @@ def _wgrad(dz: torch.Tensor, xf: torch.Tensor, out: Optional[torch.Tensor] = Non
         return torch.mm(dz.t(), xf, out=out)
     part = torch.bmm(dz.view(sk, T // sk, -1).transpose(1, 2), xf.view(sk, T // sk, -1))
     return colsum(part, out=out)
+
+
+def wgrad_hip(dz: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
+    """dW (N, K) = dz^T x on the in-tree kernel (dense.hip::linear_wgrad_kernel): dz (M, N) and
+    x (M, K) fp32 or bf16, row-major; rows split over workgroups into fp32 partial slabs that
+    the column-sum kernel reduces in a fixed order.  ``out``: fp32 destination (overwritten)."""
+    M, N = dz.shape
+    K = x.shape[1]
+    dzc, xc = dz.contiguous(), x.contiguous()
+    tile = tile or (128 if min(N, K) >= 256 else 64)
+    tiles = -(-N // tile) * -(-K // tile)
+    want = max(1, min(-(-_WG_TARGET // tiles), M // 256, 64))  # ~_WG_TARGET workgroups, >= 256 rows each
+    rows = -(-(-(-M // want)) // 64) * 64
+    ns = -(-M // rows)
+    ws = torch.empty(ns, N, K, dtype=torch.float32, device=dz.device)
+    check(lib().pv_linear_wgrad(P(dzc), 1 if dzc.dtype == torch.bfloat16 else 0, P(xc),
+                                1 if xc.dtype == torch.bfloat16 else 0, P(ws), M, N, K, rows, tile, stream(dz.device)),
+          "pv_linear_wgrad")
+    if ns == 1:
+        return ws[0] if out is None else out.copy_(ws[0])
+    return colsum(ws, out=out)
+
+
+def dgrad_hip(dz: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx (M, K) = dz W on the forward kernel, fp32.  Small weights (<= 64k elements: the
+    CDSSM head) are read transposed straight from W in the kernel's staging
+    (pv_linear_dgrad); larger ones (the MLP's 512 x 512) go through one W^T copy, whose
+    vector loads beat the strided ones (tools/dense_bwd_micro.py: 39 + 6 vs 56 us)."""
+    M, N = dz.shape
+    K = w.shape[1]
+    dzc = dz.contiguous()
+    zdt = 1 if dzc.dtype == torch.bfloat16 else 0
+    dx = torch.empty(M, K, dtype=torch.float32, device=dz.device)
+    if w.numel() <= 65536:
+        wc = w.detach().contiguous()
+        check(lib().pv_linear_dgrad(P(dzc), zdt, P(wc), 1 if wc.dtype == torch.bfloat16 else 0, P(dx), M, N, K,
+                                    stream(dz.device)), "pv_linear_dgrad")
+    else:
+        wt = w.detach().t().contiguous()
+        check(lib().pv_linear_act(P(dzc), zdt, P(wt), 1 if wt.dtype == torch.bfloat16 else 0, None, P(dx), None,
+                                  M, K, N, N, K, 0, stream(dz.device)), "pv_linear_act(dgrad)")
+    return dx
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "relu") -> torch.Tensor:
