@@ -642,7 +642,15 @@ struct Ib5 {
   static constexpr int FT = DP / 32;            // feature tiles of the out product
 };
 
-__device__ __forceinline__ int ib5_swz(int y) { return (y >> 2) & 3; }
+// chunk swizzle of row y: DP = 160 (80-dword rows, 16 mod 64): (y >> 2) & 3 within aligned
+// groups of 4 chunks; DP = 128 (64-dword rows, every row on bank 0): a bijection of y mod 16
+// whose high two bits are y & 3 (16 rows of one chunk -> 16 slots for the b128 reads, the
+// 4 rows of a transposed read -> 4 different 64-byte groups)
+template <int KS>
+__device__ __forceinline__ int ib5_swz(int y) {
+  if constexpr (KS == 4) return ((y & 3) << 2) | ((y >> 2) & 3);
+  else return (y >> 2) & 3;
+}
 
 template <int KS, bool ROW>
 __device__ __forceinline__ int ib5_pieces(int wave) {
@@ -662,7 +670,7 @@ __device__ __forceinline__ void ib5_stage(const unsigned short* __restrict__ Y, 
     if (p < T::PIECES) {
       const int q = p * 64 + lane;
       const int r = q / T::CPR, pc = q - r * T::CPR;
-      const int c = pc ^ ib5_swz(r);           // logical chunk stored at physical chunk pc
+      const int c = pc ^ ib5_swz<KS>(r);           // logical chunk stored at physical chunk pc
       const int row = min(c0 + r, c_end - 1);  // rows past the split: valid bytes, masked by the epilogue
       glds16(Y + (size_t)row * T::DP + c * 8, dst + p * 1024);
     }
@@ -677,6 +685,7 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
                                                       float* __restrict__ ws, int nx, int ny, int per_split,
                                                       int nrb, float gamma, float* __restrict__ part = nullptr) {
   static_assert(!FWD || ROW, "the fused forward runs over query rows");
+  static_assert(KS == 4 || KS == 5, "ib5: chunk swizzles exist for DP = 128 and 160");
   using T = Ib5<KS>;
   constexpr int NB = 3;
   __shared__ __attribute__((aligned(1024))) char ring[NB * T::TILE_B];
@@ -728,7 +737,7 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
 #pragma unroll
       for (int yt = 0; yt < 2; ++yt) {
         const int y = 32 * yt + l32, c = 2 * ks + h;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(yb + y * T::ROWB + ((c ^ ib5_swz(y)) << 4));
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(yb + y * T::ROWB + ((c ^ ib5_swz<KS>(y)) << 4));
         acc[yt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, xb[ks], ks == 0 ? f32x16{} : acc[yt], 0, 0, 0);
       }
     // epilogue -> G^T as bf16 B fragments gp[yt][s] (registers 8s .. 8s+7 of acc[yt])
@@ -781,8 +790,8 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
           typedef __attribute__((address_space(3))) v4s lds_v4s;
           const int ylo = 32 * yt + 16 * s2 + 4 * h + tq, yhi = ylo + 8;
           const int fe = 32 * f + tf;  // feature of this lane's 8-byte piece (chunk fe >> 3, half (fe & 7))
-          const char* plo = yb + ylo * T::ROWB + ((((fe >> 3) ^ ib5_swz(ylo))) << 4) + (fe & 7) * 2;
-          const char* phi = yb + yhi * T::ROWB + ((((fe >> 3) ^ ib5_swz(yhi))) << 4) + (fe & 7) * 2;
+          const char* plo = yb + ylo * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(ylo))) << 4) + (fe & 7) * 2;
+          const char* phi = yb + yhi * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(yhi))) << 4) + (fe & 7) * 2;
           const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plo));
           const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(phi));
           const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -1025,7 +1034,7 @@ static int ib2_splits(int nx, int ny) {
 
 // Kernel generation (PAGEVEC_IB / pv_ib_set_version), read once per process so the
 // workspace queries and the launches always agree:
-//   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160, ib3 for
+//   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for
 //                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
 //   3: ib3 everywhere;  2: the round-2 256-thread kernels (ib_bwd_kernel)
 static int g_ib_version = -1;
@@ -1081,9 +1090,13 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   const int nrb = (nx + TQ3 - 1) / TQ3;
   const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
 #define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
-  if (ib_version() == 5 && ROWV && DP == 160) {                                                                 \
-    hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
-                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  if (ib_version() == 5 && ROWV && (DP == 160 || DP == 128)) {                                                 \
+    if (DP == 160)                                                                                              \
+      hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
+                         (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
+                         (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
   } else if (ib_version() >= 3) {                                                                               \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV>), grid3, dim3(512), 0, s,              \
                                             (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
@@ -1130,9 +1143,13 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   const int nrb = (nx + TQ3 - 1) / TQ3;
   const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
 #define PV_IB_FWDDQ(CLIPV)                                                                                      \
-  if (ib_version() == 5 && DP == 160) {                                                                         \
-    hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
-                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  if (ib_version() == 5 && (DP == 160 || DP == 128)) {                                                          \
+    if (DP == 160)                                                                                              \
+      hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
+                         (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
+    else                                                                                                        \
+      hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
+                         (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
   } else if (ib_version() >= 3) {                                                                               \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true>), grid3, dim3(512), 0, s,        \
                                             (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \

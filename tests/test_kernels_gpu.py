@@ -218,8 +218,9 @@ def test_inbatch_loss(B, M, D, clip):
 
 
 @pytest.mark.parametrize("ver", [5, 3, 2])
-@pytest.mark.parametrize("B,M,clip", [(700, 5000, True), (4096, 16384, False), (300, 20000, True)])
-def test_inbatch_loss_split_shapes(ver, B, M, clip):
+@pytest.mark.parametrize("B,M,clip,D", [(700, 5000, True, 150), (4096, 16384, False, 150), (300, 20000, True, 150),
+                                        (700, 5000, True, 128), (2048, 9000, False, 128)])
+def test_inbatch_loss_split_shapes(ver, B, M, clip, D):
     """Shapes with several Y splits, >= 3 tiles per split (the ib3 LDS ring wraps), a
     partial last tile and row blocks past nx, for both kernel generations (ib3: 512-thread
     workgroups + LDS-DMA ring; PAGEVEC_IB=2: the 256-thread kernel) vs the fp32 reference."""
@@ -230,7 +231,6 @@ def test_inbatch_loss_split_shapes(ver, B, M, clip):
     assert L_.pv_ib_set_version(ver) == 0
     try:
         torch.manual_seed(3)
-        D = 150
         q = torch.randn(B, D, device=DEV)
         dd = torch.randn(M, D, device=DEV)
         # weakly correlated positives: with P+ ~ 1 the bf16-rounded positive term of dQ
