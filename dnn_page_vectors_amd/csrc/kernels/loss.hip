@@ -453,21 +453,21 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 
 // DMA instructions one wave issues per staged tile
-template <int KS, bool ROW>
+template <int KS, bool ROW, int NW = 8>
 __device__ __forceinline__ int ib3_pieces(int wave) {
   constexpr int P = Ib3<KS>::PIECES;
-  const int n = wave < P ? (P - wave + 7) / 8 : 0;
-  return n + ((!ROW && wave == 7) ? 1 : 0);
+  const int n = wave < P ? (P - wave + NW - 1) / NW : 0;
+  return n + ((!ROW && wave == NW - 1) ? 1 : 0);
 }
 
-template <int KS, bool ROW>
+template <int KS, bool ROW, int NW = 8>
 __device__ __forceinline__ void ib3_stage(const unsigned short* __restrict__ Y, const float* __restrict__ scale,
                                           int c0, int c_end, char* dst, float* sdst) {
   using T = Ib3<KS>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int u = 0; u < (T::PIECES + 7) / 8; ++u) {
-    const int p = wave + 8 * u;
+  for (int u = 0; u < (T::PIECES + NW - 1) / NW; ++u) {
+    const int p = wave + NW * u;
     if (p < T::PIECES) {
       const int q = p * 64 + lane;
       const int r = q / T::CPR, c = q - r * T::CPR;
@@ -476,11 +476,11 @@ __device__ __forceinline__ void ib3_stage(const unsigned short* __restrict__ Y, 
       glds16(Y + (size_t)row * T::DP + cc * 8, dst + p * 1024);
     }
   }
-  if (!ROW && wave == 7) glds4(scale + min(c0 + lane, c_end - 1), sdst);
+  if (!ROW && wave == NW - 1) glds4(scale + min(c0 + lane, c_end - 1), sdst);
 }
 
-template <int KS, bool ROW, bool CLIP, bool FWD = false>
-__global__ __launch_bounds__(512, 2) void ib3_kernel(const unsigned short* __restrict__ X,
+template <int KS, bool ROW, bool CLIP, bool FWD = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 2) void ib3_kernel(const unsigned short* __restrict__ X,
                                                       const unsigned short* __restrict__ Y,
                                                       const float* __restrict__ scale, float* __restrict__ out,
                                                       float* __restrict__ ws, int nx, int ny, int per_split,
@@ -495,11 +495,11 @@ __global__ __launch_bounds__(512, 2) void ib3_kernel(const unsigned short* __res
   // XCD remap: the consecutive ids of one XCD cover the row blocks of one split first
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / nrb, rb = bid - split * nrb;
-  const int r0 = rb * TQ3 + wave * 32;
+  const int r0 = rb * (NW * 32) + wave * 32;
   const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
   const int ntiles = (c_end - c_begin + TD - 1) / TD;
   const float gl = gamma * 1.4426950408889634f;
-  const int np = ib3_pieces<KS, ROW>(wave);
+  const int np = ib3_pieces<KS, ROW, NW>(wave);
   bf16x8 xb[2][KS];
   load_xb<KS>(X, r0, nx, xb);
   float rsc[2] = {0.f, 0.f};
@@ -516,8 +516,8 @@ __global__ __launch_bounds__(512, 2) void ib3_kernel(const unsigned short* __res
   for (int n = 0; n < NC; ++n)
 #pragma unroll
     for (int i = 0; i < 2; ++i) o[n][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  ib3_stage<KS, ROW>(Y, scale, c_begin, c_end, ring, ysc[0]);
-  if (ntiles > 1) ib3_stage<KS, ROW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
+  ib3_stage<KS, ROW, NW>(Y, scale, c_begin, c_end, ring, ysc[0]);
+  if (ntiles > 1) ib3_stage<KS, ROW, NW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
   wait_vm(ntiles > 1 ? np : 0);
   __builtin_amdgcn_s_barrier();
   const int trow = 4 * g + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(512, 2) void ib3_kernel(const unsigned short* __res
     const bool ahead = t + 2 < ntiles;
     if (ahead) {  // slot (t + 2) % 3 = (t - 1) % 3: every wave left it at the last barrier
       const int sb = buf + 2 >= NB ? buf + 2 - NB : buf + 2;
-      ib3_stage<KS, ROW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
+      ib3_stage<KS, ROW, NW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
     }
     st_tile<KS>(xb, reinterpret_cast<const unsigned short*>(ring + buf * T::TILE_B), acc);
     epi_out(buf, c0);
@@ -652,21 +652,21 @@ __device__ __forceinline__ int ib5_swz(int y) {
   else return (y >> 2) & 3;
 }
 
-template <int KS, bool ROW>
+template <int KS, bool ROW, int NW = 8>
 __device__ __forceinline__ int ib5_pieces(int wave) {
   constexpr int P = Ib5<KS>::PIECES;
-  const int n = wave < P ? (P - wave + 7) / 8 : 0;
-  return n + ((!ROW && wave == 7) ? 1 : 0);
+  const int n = wave < P ? (P - wave + NW - 1) / NW : 0;
+  return n + ((!ROW && wave == NW - 1) ? 1 : 0);
 }
 
-template <int KS, bool ROW>
+template <int KS, bool ROW, int NW = 8>
 __device__ __forceinline__ void ib5_stage(const unsigned short* __restrict__ Y, const float* __restrict__ scale,
                                           int c0, int c_end, char* dst, float* sdst) {
   using T = Ib5<KS>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int u = 0; u < (T::PIECES + 7) / 8; ++u) {
-    const int p = wave + 8 * u;
+  for (int u = 0; u < (T::PIECES + NW - 1) / NW; ++u) {
+    const int p = wave + NW * u;
     if (p < T::PIECES) {
       const int q = p * 64 + lane;
       const int r = q / T::CPR, pc = q - r * T::CPR;
@@ -675,11 +675,11 @@ __device__ __forceinline__ void ib5_stage(const unsigned short* __restrict__ Y, 
       glds16(Y + (size_t)row * T::DP + c * 8, dst + p * 1024);
     }
   }
-  if (!ROW && wave == 7) glds4(scale + min(c0 + lane, c_end - 1), sdst);
+  if (!ROW && wave == NW - 1) glds4(scale + min(c0 + lane, c_end - 1), sdst);
 }
 
-template <int KS, bool ROW, bool CLIP, bool FWD = false>
-__global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __restrict__ X,
+template <int KS, bool ROW, bool CLIP, bool FWD = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 2) void ib5_kernel(const unsigned short* __restrict__ X,
                                                       const unsigned short* __restrict__ Y,
                                                       const float* __restrict__ scale, float* __restrict__ out,
                                                       float* __restrict__ ws, int nx, int ny, int per_split,
@@ -693,12 +693,12 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / nrb, rb = bid - split * nrb;
-  const int r0 = rb * TQ3 + wave * 32;
+  const int r0 = rb * (NW * 32) + wave * 32;
   const int x = r0 + l32;  // this lane's X row
   const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
   const int ntiles = (c_end - c_begin + TD - 1) / TD;
   const float gl = gamma * 1.4426950408889634f;
-  const int np = ib5_pieces<KS, ROW>(wave);
+  const int np = ib5_pieces<KS, ROW, NW>(wave);
   // B operand of the S product: X[x][16 ks + 8 h .. + 7]
   bf16x8 xb[T::K16];
 #pragma unroll
@@ -712,8 +712,8 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
   for (int f = 0; f < T::FT; ++f)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[f][r] = 0.f;
-  ib5_stage<KS, ROW>(Y, scale, c_begin, c_end, ring, ysc[0]);
-  if (ntiles > 1) ib5_stage<KS, ROW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
+  ib5_stage<KS, ROW, NW>(Y, scale, c_begin, c_end, ring, ysc[0]);
+  if (ntiles > 1) ib5_stage<KS, ROW, NW>(Y, scale, c_begin + TD, c_end, ring + T::TILE_B, ysc[1]);
   wait_vm(ntiles > 1 ? np : 0);
   __builtin_amdgcn_s_barrier();
   // transposed-read lane address inside a (4-row x 16-feature) block: row q = (lane & 15) >> 2,
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(512, 2) void ib5_kernel(const unsigned short* __res
     const bool ahead = t + 2 < ntiles;
     if (ahead) {
       const int sb = buf + 2 >= NB ? buf + 2 - NB : buf + 2;
-      ib5_stage<KS, ROW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
+      ib5_stage<KS, ROW, NW>(Y, scale, c0 + 2 * TD, c_end, ring + sb * T::TILE_B, ysc[sb]);
     }
     const char* yb = ring + buf * T::TILE_B;
     // S^T tiles: acc[yt][r] = S^T[y = 32 yt + 8 (r >> 2) + 4 h + (r & 3)][x]
@@ -1036,13 +1036,14 @@ static int ib2_splits(int nx, int ny) {
 // workspace queries and the launches always agree:
 //   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for
 //                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
+//   6: as 5 with 4-wave workgroups (two independent workgroups per CU; A/B)
 //   3: ib3 everywhere;  2: the round-2 256-thread kernels (ib_bwd_kernel)
 static int g_ib_version = -1;
 static int ib_version() {
   if (g_ib_version < 0) {
     const char* e = getenv("PAGEVEC_IB");
     const int v = e ? atoi(e) : 5;
-    g_ib_version = (v == 2 || v == 3) ? v : 5;
+    g_ib_version = (v == 2 || v == 3 || v == 6) ? v : 5;
   }
   return g_ib_version;
 }
@@ -1050,15 +1051,21 @@ static int ib_version() {
 PV_API int pv_ib_version() { return ib_version(); }
 // A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)
 PV_API int pv_ib_set_version(int v) {
-  if (v != 2 && v != 3 && v != 5) return -1;
+  if (v != 2 && v != 3 && v != 5 && v != 6) return -1;
   g_ib_version = v;
   return 0;
 }
 
+// waves per workgroup of the ib3 / ib5 kernels: 8 (one 512-thread workgroup per CU, the two
+// waves of a SIMD in lockstep) or 4 (version 6: two independent 256-thread workgroups per CU)
+static int ib_nw() { return ib_version() == 6 ? 4 : 8; }
+
 static int ib3_splits(int nx, int ny) {
-  // one 512-thread workgroup per CU: ~256 fill the chip; keep >= 16 tiles per split
-  const int rb = (nx + pv::loss::TQ3 - 1) / pv::loss::TQ3;
-  int ns = (256 + rb - 1) / rb;
+  // 2048 / NW resident waves' worth of workgroups fill the chip (256 at NW = 8); keep >= 16
+  // tiles per split
+  const int tq = 32 * ib_nw();
+  const int rb = (nx + tq - 1) / tq;
+  int ns = (256 * 8 / ib_nw() + rb - 1) / rb;
   const int maxs = (ny + 16 * pv::loss::TD - 1) / (16 * pv::loss::TD);
   if (ns > maxs) ns = maxs;
   return ns < 1 ? 1 : ns;
@@ -1087,16 +1094,29 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws) return -3;
   hipStream_t s = (hipStream_t)stream;
-  const int nrb = (nx + TQ3 - 1) / TQ3;
+  const int NWV = ib_nw();
+  const int nrb = (nx + 32 * NWV - 1) / (32 * NWV);
   const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
 #define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
-  if (ib_version() == 5 && ROWV && (DP == 160 || DP == 128)) {                                                 \
-    if (DP == 160)                                                                                              \
+  if (ib_version() >= 5 && ROWV && (DP == 160 || DP == 128)) {                                                  \
+    if (NWV == 4) {                                                                                             \
+      if (DP == 160) hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,         \
+                                        (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, \
+                                        ny, per, nrb, gamma);                                                   \
+      else hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,                   \
+                              (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, ny, per,  \
+                              nrb, gamma);                                                                      \
+    } else if (DP == 160) {                                                                                     \
       hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
                          (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
-    else                                                                                                        \
+    } else {                                                                                                    \
       hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
                          (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
+    }                                                                                                           \
+  } else if (ib_version() >= 3 && NWV == 4) {                                                                   \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,    \
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
+                                            nx, ny, per, nrb, gamma));                                          \
   } else if (ib_version() >= 3) {                                                                               \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV>), grid3, dim3(512), 0, s,              \
                                             (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
@@ -1140,16 +1160,29 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws_u) return -3;
   hipStream_t s = (hipStream_t)stream;
-  const int nrb = (nx + TQ3 - 1) / TQ3;
+  const int NWV = ib_nw();
+  const int nrb = (nx + 32 * NWV - 1) / (32 * NWV);
   const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
 #define PV_IB_FWDDQ(CLIPV)                                                                                      \
-  if (ib_version() == 5 && (DP == 160 || DP == 128)) {                                                          \
-    if (DP == 160)                                                                                              \
+  if (ib_version() >= 5 && (DP == 160 || DP == 128)) {                                                          \
+    if (NWV == 4) {                                                                                             \
+      if (DP == 160) hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,          \
+                                        (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u,   \
+                                        nx, ny, per, nrb, gamma, part);                                         \
+      else hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,                    \
+                              (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, \
+                              nrb, gamma, part);                                                                \
+    } else if (DP == 160) {                                                                                     \
       hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
                          (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
-    else                                                                                                        \
+    } else {                                                                                                    \
       hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
                          (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
+    }                                                                                                           \
+  } else if (ib_version() >= 3 && NWV == 4) {                                                                   \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,     \
+                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
+                                            ws_u, nx, ny, per, nrb, gamma, part));                              \
   } else if (ib_version() >= 3) {                                                                               \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true>), grid3, dim3(512), 0, s,        \
                                             (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \

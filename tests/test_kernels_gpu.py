@@ -217,7 +217,7 @@ def test_inbatch_loss(B, M, D, clip):
     torch.testing.assert_close(dn.grad, dn2.grad, rtol=3e-2, atol=3e-3)
 
 
-@pytest.mark.parametrize("ver", [5, 3, 2])
+@pytest.mark.parametrize("ver", [5, 6, 3, 2])
 @pytest.mark.parametrize("B,M,clip,D", [(700, 5000, True, 150), (4096, 16384, False, 150), (300, 20000, True, 150),
                                         (700, 5000, True, 128), (2048, 9000, False, 128)])
 def test_inbatch_loss_split_shapes(ver, B, M, clip, D):
