@@ -223,7 +223,7 @@ template <typename KT>
 __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool, const float* pooled,
                                                              const int* argmax, const int* ids, KT* keys,
                                                              unsigned* vals, int2* rec, int N, int L, int V,
-                                                             float scale, unsigned dead) {
+                                                             float scale) {
   const long pair = (long)blockIdx.x * 256 + threadIdx.x;
   if (pair >= (long)N * 2 * FW) return;
   const int n = (int)(pair / (2 * FW)), f = (int)(pair % (2 * FW));
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool,
       const bool ok = live && t < L;
       const int v = ok ? ids[(size_t)n * L + t] : V;
       PV_CHECK(v >= 0 && v <= V, PV_ERR_ID);
-      keys[s0 + j] = (KT)((unsigned)v < (unsigned)V ? (unsigned)v : dead);
+      keys[s0 + j] = (KT)((unsigned)v < (unsigned)V ? (unsigned)v : (unsigned)V);
       if (vals) vals[s0 + j] = s0 + j;  // null: the sort generates the positions itself
     }
   }
@@ -620,148 +620,6 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce7_kernel(const KT* __restr
     k1 = k2; s1 = s2;
   }
   if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-}
-
-// ---- dTable reduce over row buckets (reduce8): one radix pass + LDS accumulation ---------
-// The emit keys go through ONE 8-bit radix pass on bits [7, 15) (radix_sort.hip
-// pv_rsort_bucket): entries land grouped by bucket = 128 consecutive table rows, in no
-// particular order inside a bucket.  A persistent workgroup takes (bucket, part) items of
-// at most `seg` entries; the bucket's 128 x EP float rows live in LDS (53 KB), every entry
-// adds its contribution s*g*W[f,j,:]*m with ds_add_f32 (no runs, no run flushes, no second
-// sort pass), and the item ends with one float atomic per touched (row, column) into dTable.
-// A 16-lane group owns one entry per round as in reduce7 (lane p: columns 8p..8p+7, one
-// 16-byte weight-row load, the dropout keep bits of the piece).  Dead entries carry the key
-// 0xFFFF (emit `dead`), i.e. bucket 255, which holds no table row for V <= 32640.
-// Not deterministic (LDS / global float atomics): deterministic mode keeps sort + reduce7.
-constexpr int BROWS = 128;  // table rows per bucket (radix shift 7)
-constexpr int R8T = 512;    // threads per workgroup (8 waves; 2 workgroups per CU by LDS)
-
-template <int DM>
-__global__ __launch_bounds__(R8T) void conv_bwd_reduce8_kernel(const unsigned short* __restrict__ bkeys,
-                                                               const unsigned* __restrict__ bvals,
-                                                               const unsigned* __restrict__ totals,
-                                                               const int2* __restrict__ rec,
-                                                               const unsigned short* __restrict__ wrow,
-                                                               float* __restrict__ dtable, int seg, int L, int E,
-                                                               int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr) {
-  __shared__ __attribute__((aligned(16))) float acc[BROWS * EP];
-  __shared__ unsigned boff[256], bcnt[256], bpart[257];
-  __shared__ unsigned ws[R8T / 64];
-  if (seed_ptr) seed += *seed_ptr;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int g = lane >> 4, p = lane & 15;
-  const int nbk = (V + BROWS - 1) / BROWS;  // buckets holding table rows
-  // bucket offsets (all 256 digits) and the part prefix over the row buckets: exclusive
-  // scans of (count, parts) over threads 0..255 (waves 0-3)
-  unsigned c = 0u, parts = 0u;
-  if (t < 256) {
-    c = totals[t];
-    bcnt[t] = c;
-    parts = t < nbk ? (c + (unsigned)seg - 1u) / (unsigned)seg : 0u;
-  }
-  unsigned xc = c, xp = parts;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned yc = __shfl_up(xc, o, 64), yp = __shfl_up(xp, o, 64);
-    if (lane >= o) {
-      xc += yc;
-      xp += yp;
-    }
-  }
-  if (lane == 63 && wave < 4) {
-    ws[wave] = xc;
-    ws[4 + wave] = xp;
-  }
-  __syncthreads();
-  if (t < 256) {
-    unsigned bc = 0u, bp = 0u;
-    for (int i = 0; i < wave; ++i) {
-      bc += ws[i];
-      bp += ws[4 + i];
-    }
-    boff[t] = bc + xc - c;
-    bpart[t] = bp + xp - parts;
-    if (t == 255) bpart[256] = bp + xp;
-  }
-  __syncthreads();
-  const unsigned nitems = bpart[256];
-  const bool act = p < RPIECES;
-  const unsigned ms = mix32(seed);
-  for (unsigned item = blockIdx.x; item < nitems; item += gridDim.x) {
-    // bucket of this item: the last b with bpart[b] <= item (uniform binary search)
-    int lo = 0, hi = 255;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (bpart[mid] <= item) lo = mid; else hi = mid - 1;
-    }
-    const int b = lo;
-    const unsigned part = item - bpart[b];
-    const long beg = (long)boff[b] + (long)part * seg;
-    const long end = min((long)boff[b] + (long)bcnt[b], beg + seg);
-    for (int i = t; i < BROWS * EP / 4; i += R8T) reinterpret_cast<f32x4*>(acc)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();
-    for (long sc = beg + 64L * wave; sc < end; sc += 64L * (R8T / 64)) {
-      // lane metadata of entry sc + lane
-      const long e = sc + lane;
-      const bool valid = e < end;
-      unsigned roff = 0, fj = 0, hr = 0;
-      float gg = 0.f;
-      if (valid) {
-        const unsigned key = bkeys[e];
-        PV_CHECK(key < (unsigned)V && (int)(key / BROWS) == b, PV_ERR_KEY);
-        const unsigned sl = bvals[e];
-        unsigned nn, f, j;
-        slot_decode(sl, nn, f, j);
-        const int2 rc = rec[nn * (2 * FW) + f];
-        roff = (key & (BROWS - 1)) * EP;
-        fj = (f << 2) | j;
-        gg = __int_as_float(rc.x);
-        if (DM != 0) hr = (unsigned)mix32((row_offset + nn * (unsigned)L + (unsigned)rc.y + j) ^ ms);
-      }
-      const int n = __popcll(__ballot(valid));  // valid entries are a prefix
-      auto round = [&](int q0) {
-        const int src = (q0 + g) * 4;
-        const unsigned ro = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)roff);
-        const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
-        float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
-        const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
-        if (q0 + g >= n) ge = 0.f;
-        u32x4 w = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * (act ? p : RPIECES - 1)));
-        if constexpr (DM == 3) {
-          const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
-          w &= u32x4{k, k, k, k};
-        } else if constexpr (DM == 1) {
-          w &= keep_piece(he, p, 64);
-        } else if constexpr (DM == 2) {
-          w &= keep_piece(he, p, thr);
-        }
-        if (act && ge != 0.f) {
-          float* dst = acc + ro + 8 * p;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float x = __uint_as_float((k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16));
-            __hip_atomic_fetch_add(dst + k, ge * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-        }
-      };
-      if (n == 64) {
-#pragma unroll
-        for (int q0 = 0; q0 < 64; q0 += 4) round(q0);
-      } else {
-        for (int q0 = 0; q0 < n; q0 += 4) round(q0);
-      }
-    }
-    __syncthreads();
-    // flush: one float atomic per non-zero (row, column) of the bucket
-    const int rows = min(BROWS, V - b * BROWS);
-    for (int i = t; i < rows * E; i += R8T) {
-      const int r = i / E, c = i - r * E;
-      const float v = acc[r * EP + c];
-      if (v != 0.f) atomicAdd(&dtable[(size_t)(b * BROWS + r) * E + c], v);
-    }
-    __syncthreads();
-  }
 }
 
 // reduce6 = reduce5 with the weight-row gathers of RB rounds (4 entries each) issued
@@ -1176,7 +1034,7 @@ PV_API int pv_conv_pool_bwd_emit3(const float* gpool, const float* pooled, const
   using namespace pv::convbwd;
   const long pairs = (long)N * 2 * FW;
   hipLaunchKernelGGL(conv_bwd_emit3_kernel<unsigned>, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale, (unsigned)V);
+                     (hipStream_t)stream, gpool, pooled, argmax, ids, keys, vals, (int2*)rec, N, L, V, scale);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -1207,7 +1065,7 @@ PV_API int pv_conv_pool_bwd_emit3_u16(const float* gpool, const float* pooled, c
   const long pairs = (long)N * 2 * FW;
   hipLaunchKernelGGL(conv_bwd_emit3_kernel<unsigned short>, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, gpool, pooled, argmax, ids, (unsigned short*)keys, (unsigned*)nullptr,
-                     (int2*)rec, N, L, V, scale, (unsigned)V);
+                     (int2*)rec, N, L, V, scale);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -1230,45 +1088,6 @@ PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals
 }
 
 // reduce7 (compile-time dropout mode, packed FMAs), 2-byte keys; same arguments as reduce5.
-// emit with dead entries keyed `dead` (0xFFFF: the empty last bucket of the reduce8 path)
-PV_API int pv_conv_pool_bwd_emit3_u16d(const float* gpool, const float* pooled, const int* argmax, const int* ids,
-                                       void* keys, void* rec, int N, int L, int V, float scale, int dead,
-                                       void* stream) {
-  using namespace pv::convbwd;
-  if (V >= 65535 || dead < V || dead > 65535) return -1;
-  const long pairs = (long)N * 2 * FW;
-  hipLaunchKernelGGL(conv_bwd_emit3_kernel<unsigned short>, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, gpool, pooled, argmax, ids, (unsigned short*)keys, (unsigned*)nullptr,
-                     (int2*)rec, N, L, V, scale, (unsigned)dead);
-  PV_LAUNCH_CHECK();
-  return 0;
-}
-
-// bkeys / bvals: the emit keys after ONE radix pass on bits [7, 15) (pv_rsort_bucket),
-// totals: that pass's 256 digit counts.  grid: persistent workgroups (2 per CU).
-PV_API int pv_conv_pool_bwd_reduce8(const void* bkeys, const unsigned* bvals, const unsigned* totals, const void* rec,
-                                    const void* wrow, float* dtable, int seg, int grid, int L, int E, int V,
-                                    unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr,
-                                    int token_mode, void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || V > 255 * BROWS || seg < 64 || grid <= 0) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
-#define PV_R8(DMV)                                                                                                  \
-  hipLaunchKernelGGL((conv_bwd_reduce8_kernel<DMV>), dim3(grid), dim3(R8T), 0, st, (const unsigned short*)bkeys,     \
-                     bvals, totals, (const int2*)rec, (const unsigned short*)wrow, dtable, seg, L, E, V, seed,       \
-                     seed_ptr, row_offset, thr)
-  switch (dm) {
-    case 0: PV_R8(0); break;
-    case 1: PV_R8(1); break;
-    case 3: PV_R8(3); break;
-    default: PV_R8(2); break;
-  }
-#undef PV_R8
-  PV_LAUNCH_CHECK();
-  return 0;
-}
-
 PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
                                         float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
                                         const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,

@@ -309,43 +309,3 @@ PV_API int pv_rsort_pairs(void* temp, long temp_bytes, const void* keys_in, void
                                end_bit, st);
   return -3;
 }
-
-// ONE 8-bit counting pass (digit = bits [shift, shift + nbits) of the 16-bit key): entries
-// grouped by digit, stable inside a digit, values = input positions; totals (256 u32) gets
-// each digit's count — the bucketing step of the reduce8 dTable path (conv_pool_bwd.hip).
-PV_API long pv_rsort_bucket_temp_bytes(long n) {
-  using namespace pv::rsort;
-  const long tile = (long)BT * pick_ipt(n);
-  const long nb = (n + tile - 1) / tile;
-  return (long)align256((size_t)RADIX * nb * 4);
-}
-
-PV_API int pv_rsort_bucket_u16(void* temp, long temp_bytes, const void* keys_in, void* keys_out, unsigned* vals_out,
-                               unsigned* totals, long n, int shift, int nbits, void* stream) {
-  using namespace pv::rsort;
-  hipStream_t st = (hipStream_t)stream;
-  if (n <= 0) return 0;
-  if (nbits < 1 || nbits > 8 || shift < 0 || shift + nbits > 16 || n >= (1L << 32) - TILE) return -1;
-  if (temp == nullptr || temp_bytes < pv_rsort_bucket_temp_bytes(n)) return -2;
-  const int ipt = pick_ipt(n);
-  const int nb = (int)((n + (long)BT * ipt - 1) / ((long)BT * ipt));
-  unsigned* hist = (unsigned*)temp;
-  const unsigned short* kin = (const unsigned short*)keys_in;
-  unsigned short* kout = (unsigned short*)keys_out;
-#define PV_BK(IPTV)                                                                                                  \
-  hipLaunchKernelGGL((rs_count_kernel<unsigned short, IPTV>), dim3(nb), dim3(BT), 0, st, kin, n, shift, nbits, hist, \
-                     nb);                                                                                            \
-  hipLaunchKernelGGL(rs_scan_kernel, dim3(RADIX), dim3(BT), 0, st, hist, nb, totals);                                \
-  hipLaunchKernelGGL((rs_scatter_kernel<unsigned short, IPTV>), dim3(nb), dim3(BT), 0, st, kin, (const unsigned*)nullptr, \
-                     kout, vals_out, n, shift, nbits, (const unsigned*)hist, (const unsigned*)totals, nb)
-  if (ipt == 4) {
-    PV_BK(4);
-  } else if (ipt == 32) {
-    PV_BK(32);
-  } else {
-    PV_BK(IPT);
-  }
-#undef PV_BK
-  PV_LAUNCH_CHECK();
-  return 0;
-}

@@ -44,10 +44,6 @@ SIGS = {
     "pv_rsort_set_ipt": "i",
     "pv_rsort_temp_bytes": "lii",
     "pv_rsort_pairs": "plpppp" "lii" "p",
-    "pv_rsort_bucket_temp_bytes": "l",
-    "pv_rsort_bucket_u16": "plppp" "p" "lii" "p",
-    "pv_conv_pool_bwd_emit3_u16d": "pppppp" "iii" "f" "i" "p",
-    "pv_conv_pool_bwd_reduce8": "pppppp" "iiiii" "u" "p" "u" "ii" "p",
     "pv_csort_temp_bytes": "li",
     "pv_csort_pairs": "plppp" "lii" "p",
     # w2v.hip
@@ -119,7 +115,7 @@ SIGS = {
     "pv_bag_counts8": "p" "p" "i" "p" "i" "p" "iiii" "p",
 }
 
-_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_rsort_bucket_temp_bytes": ctypes.c_long, "pv_csort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_csort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

@@ -63,20 +63,12 @@ REDUCE_RB = int(os.environ.get("PAGEVEC_REDUCE_RB", "0"))
 # reduce7: compile-time dropout mode + packed FMAs (5 = reduce5); same process at the bench
 # shape 0.468 vs 0.558 ms (tools/reduce_ab.py), headline step 7.72-7.79 vs 7.79-7.83 ms
 REDUCE_V = int(os.environ.get("PAGEVEC_REDUCE_V", "7"))
-# reduce8 (REDUCE_V = 8): ONE radix pass into 128-row buckets + LDS accumulation per bucket
-# part of at most REDUCE_SEG entries (conv_bwd_reduce8_kernel; not in deterministic mode)
-REDUCE_SEG = int(os.environ.get("PAGEVEC_REDUCE_SEG", "16384"))
-BUCKET_ROWS = 128
 
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
 # (both halves are gather/latency-bound and leave CU slots idle when run back to back)
 # (round 1: no gain, 9.30 vs 9.30 ms; with the round-2 backward, same box: 7.535 / 7.555 vs
 # 7.596 / 7.624 ms per headline step, so on by default for long sequences)
 DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "1") != "0"
-# where the side-stream dW is enqueued relative to the table chain: "first" (before the emit),
-# "sort" (after the sort), "reduce" (after the reduce).  A dW grid dispatched first holds the
-# CUs until its workgroups drain, so the chain's small sort kernels queue behind it.
-DW_AT = os.environ.get("PAGEVEC_DW_AT", "first")
 _side = {}
 
 
@@ -169,28 +161,6 @@ def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
     return wrow
 
 
-def _table_reduce(L_, skeys, svals, rec, wrow, dtable, M, k16, L, E, V, seed, sp, row_offset, thr, tok, s) -> None:
-    """dTable from the fully sorted (key, slot) entries: reduce7 (default) / 6 / 5 / 4."""
-    if k16 and REDUCE_V == 7 and REDUCE_RB == 0:
-        check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                              L, E, V, seed, P(sp), row_offset, thr, tok, s),
-              "pv_conv_pool_bwd_reduce7_u16")
-    elif k16 and REDUCE_RB > 0:
-        check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                              L, E, V, seed, P(sp), row_offset, thr, tok, REDUCE_RB, s),
-              "pv_conv_pool_bwd_reduce6_u16")
-    elif k16:
-        check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                              L, E, V, seed, P(sp), row_offset, thr, tok, s),
-              "pv_conv_pool_bwd_reduce5_u16")
-    elif REDUCE_EPW > 0:
-        check(L_.pv_conv_pool_bwd_reduce5(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E,
-                                          V, seed, P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce5")
-    else:
-        check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
-                                          P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
-
-
 class _ConvPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, table, w3, w4, bias, tbl16, wpack, p, seed, row_offset, training, mode):
@@ -256,10 +226,8 @@ class _ConvPoolFn(torch.autograd.Function):
         # bucket (a bucket of its own, parallel/ddp.py) is released as soon as its reduce is
         # enqueued on this stream, so its all-reduce (12 MB for the 30k x 100 table) overlaps
         # the dW kernel instead of trailing the whole backward.
-        dw_at = DW_AT if side is not None else "none"
-        if dw_at not in ("sort", "reduce") and side is not None:
+        if side is not None:
             launch_dw()
-            dw_at = "done"
         dtable = None
         if dense_dx:
             # short sequences (query towers): per-sample dense dX rows (LDS), sorted by token,
@@ -288,41 +256,38 @@ class _ConvPoolFn(torch.autograd.Function):
             keys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
             skeys = torch.empty_like(keys)
             svals = torch.empty(M, dtype=u32, device=dev)
-            bucketed = (REDUCE_V == 8 and k16 and V <= 255 * BUCKET_ROWS and E <= EP and not determinism.enabled())
-            if bucketed:
-                # dead entries keyed 0xFFFF: digit 255 of the bucket pass, which holds no table row
-                check(L_.pv_conv_pool_bwd_emit3_u16d(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L,
-                                                     V, scale, 0xFFFF, s), "pv_conv_pool_bwd_emit3_u16d")
-                tb = int(L_.pv_rsort_bucket_temp_bytes(M))
-                temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
-                totals = torch.empty(256, dtype=u32, device=dev)
-                check(L_.pv_rsort_bucket_u16(P(temp), tb, P(keys), P(skeys), P(svals), P(totals), M, 7, 8, s),
-                      "pv_rsort_bucket_u16")
-                dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
-                check(L_.pv_conv_pool_bwd_reduce8(P(skeys), P(svals), P(totals), P(rec), P(_weight_rows(w3, w4, EP)),
-                                                  P(dtable), REDUCE_SEG, 2 * _grid(dev), L, E, V, seed, P(sp),
-                                                  row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce8")
-            elif k16:
+            if k16:
                 check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L, V,
                                                     scale, s), "pv_conv_pool_bwd_emit3_u16")
             else:
                 check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
-            if not bucketed:
-                sort_pairs_iota(keys, skeys, svals, end_bit)
-                if dw_at == "sort":
-                    launch_dw()
-                    dw_at = "done"
-                dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
-                _table_reduce(L_, skeys, svals, rec, _weight_rows(w3, w4, EP), dtable, M, k16, L, E, V, seed, sp,
-                              row_offset, thr, tok, s)
+            sort_pairs_iota(keys, skeys, svals, end_bit)
+            dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
+            wrow = _weight_rows(w3, w4, EP)
+            if k16 and REDUCE_V == 7 and REDUCE_RB == 0:
+                check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
+                      "pv_conv_pool_bwd_reduce7_u16")
+            elif k16 and REDUCE_RB > 0:
+                check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, REDUCE_RB, s),
+                      "pv_conv_pool_bwd_reduce6_u16")
+            elif k16:
+                check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
+                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
+                      "pv_conv_pool_bwd_reduce5_u16")
+            elif REDUCE_EPW > 0:
+                check(L_.pv_conv_pool_bwd_reduce5(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E,
+                                                  V, seed, P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce5")
+            else:
+                check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
+                                                  P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
         if t_tab is not None:
             grad_sink.done(ptable)  # fires the table's bucket: enqueued after the reduce above
         if side is None:
             launch_dw()
         else:
-            if dw_at != "done":
-                launch_dw()
             main.wait_stream(side)
         for t, prm in ((t3, pw3), (t4, pw4)):
             if t is not None:

@@ -100,46 +100,6 @@ def test_dtable_reduce_long_runs_match_reduce4(epw, variant):
     assert grads[0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("N,L,p,mode", [(5, 130, 0.25, "element"), (5, 130, 0.0, "element"), (5, 130, 0.3, "element"),
-                                        (4, 130, 0.25, "token"), (12, 5000, 0.25, "element")])
-def test_conv_pool_bwd_bucketed_reduce8(N, L, p, mode, monkeypatch):
-    """The one-pass bucket + LDS-accumulation table gradient (reduce8) through the full
-    fp32 reference check of test_conv_pool_fwd_bwd, in every compile-time dropout mode."""
-    monkeypatch.setattr(cops, "REDUCE_V", 8)
-    test_conv_pool_fwd_bwd(N, L, p, mode)
-
-
-@pytest.mark.parametrize("V,seg", [(500, 64), (30000, 1024), (30000, 16384), (32640, 4096)])
-def test_dtable_reduce8_matches_reduce7(V, seg, monkeypatch):
-    """reduce8 (128-row buckets, items of <= seg entries, LDS ds_add_f32 + one float atomic per
-    touched (row, column)) equals the fully sorted reduce7 on Zipf-skewed ids whose hottest
-    buckets split into many items; V = 32640 fills the last row bucket (dead entries: 0xFFFF)."""
-    torch.manual_seed(2)
-    E, F, N, L = 100, 150, 64, 300
-    ranks = torch.arange(1, V, dtype=torch.float64)
-    probs = ranks.pow(-1.05)
-    perm = torch.randperm(V - 1) + 1
-    ids = perm[torch.multinomial(probs / probs.sum(), N * L, replacement=True)].view(N, L).to(torch.int32).to(DEV)
-    ids[:, :3] = V - 1  # the last table row is always touched
-    table = bf(torch.randn(V, E, device=DEV) * 0.5)
-    w3, w4 = bf(torch.randn(F, 3, E, device=DEV) * 0.1), bf(torch.randn(F, 4, E, device=DEV) * 0.1)
-    b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
-    monkeypatch.setattr(cops, "REDUCE_SEG", seg)
-    grads = []
-    for variant in (7, 8):
-        monkeypatch.setattr(cops, "REDUCE_V", variant)
-        t = table.clone().requires_grad_(True)
-        pooled, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], b, 0.25, 99, True)
-        (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
-        grads.append(t.grad)
-    # fp32 sums of up to ~10^4 terms per hot row in a different order: single elements with
-    # heavy cancellation move by more than an elementwise rtol, so compare against the scale
-    d = (grads[1] - grads[0]).abs()
-    assert float(d.max() / grads[0].abs().max()) < 1e-4
-    assert float(d.norm() / grads[0].norm()) < 1e-5
-    assert grads[0].abs().sum() > 0 and grads[0][V - 1].abs().sum() > 0
-
-
 def test_conv_pool_eval_mode_no_dropout():
     V, E, F, N, L = 50, 100, 150, 4, 20
     ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
