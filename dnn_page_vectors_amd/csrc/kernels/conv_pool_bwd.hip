@@ -506,8 +506,10 @@ __global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restr
 // reduce7 = reduce5 with the dropout mode as a template parameter (DM: 0 off, 1 element
 // p = 0.25, 2 element any p, 3 token) and the common round's multiply + add as packed FMAs
 // (reduce5: a separate v = g * w pass, then 8 adds).
-template <typename KT, int DM>
-__global__ __launch_bounds__(256) void conv_bwd_reduce7_kernel(const KT* __restrict__ skeys,
+// OCC: minimum waves per SIMD the register allocation must allow (1 = compiler's choice,
+// 74 VGPRs / 6 waves; 8 caps it at 64 VGPRs)
+template <typename KT, int DM, int OCC = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_bwd_reduce7_kernel(const KT* __restrict__ skeys,
                                                                const unsigned* __restrict__ svals,
                                                                const int2* __restrict__ rec,
                                                                const unsigned short* __restrict__ wrow,
@@ -1088,6 +1090,13 @@ PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals
 }
 
 // reduce7 (compile-time dropout mode, packed FMAs), 2-byte keys; same arguments as reduce5.
+// reduce7 occupancy (tools/reduce_ab.py, same process at the bench shape): capped at 64 VGPRs
+// (8 waves / SIMD, 2 VGPRs spilled) 0.443 ms vs 0.473 ms at the compiler's 74 VGPRs (6 waves);
+// PMC: 47% of wave-cycles parked at s_waitcnt, 26% L2 miss rate (the random {g, argmax}
+// record gathers) — latency-bound, so more waves pay.  PAGEVEC_R7_OCC=1 restores 74 VGPRs.
+static int g_r7_occ = getenv("PAGEVEC_R7_OCC") ? atoi(getenv("PAGEVEC_R7_OCC")) : 8;
+PV_API void pv_conv_r7_set_occ(int occ) { g_r7_occ = occ; }
+
 PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
                                         float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
                                         const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
@@ -1101,6 +1110,11 @@ PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals
   if (det.err) return det.err;
   const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
 #define PV_R7(DMV)                                                                                               \
+  if (g_r7_occ == 8)                                                                                             \
+    hipLaunchKernelGGL((conv_bwd_reduce7_kernel<unsigned short, DMV, 8>), grid, dim3(256), 0, st,                \
+                       (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, \
+                       M, epw, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx);                    \
+  else                                                                                                           \
   hipLaunchKernelGGL((conv_bwd_reduce7_kernel<unsigned short, DMV>), grid, dim3(256), 0, st,                     \
                      (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, \
                      epw, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx)

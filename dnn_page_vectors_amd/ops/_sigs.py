@@ -44,6 +44,7 @@ SIGS = {
     "pv_rsort_set_ipt": "i",
     "pv_rsort_temp_bytes": "lii",
     "pv_rsort_pairs": "plpppp" "lii" "p",
+    "pv_conv_r7_set_occ": "i",
     "pv_csort_temp_bytes": "li",
     "pv_csort_pairs": "plppp" "lii" "p",
     # w2v.hip

@@ -104,15 +104,30 @@ def main():
         print(json.dumps({"rb": rb, "rel_err_vs_reduce5": err}), flush=True)
         assert err < 1e-5, err
     scratch = torch.zeros(V, E, device=dev)
-    res = {"reduce5": [], "reduce7": [], "dw": []}
+    has_occ = hasattr(L_, "pv_conv_r7_set_occ")
+    if has_occ:  # reduce7 capped at 64 VGPRs (8 waves / SIMD, default) vs the compiler's 74 (6 waves)
+        L_.pv_conv_r7_set_occ(1)
+        L_.pv_conv_r7_set_occ(8)
+        out8 = torch.zeros(V, E, device=dev)
+        r7(out8)
+        L_.pv_conv_r7_set_occ(1)
+        torch.cuda.synchronize()
+        err8 = float((out8 - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        print(json.dumps({"reduce7_occ8_rel_err_vs_reduce5": err8}), flush=True)
+        assert err8 < 1e-5, err8
+    res = {"reduce5": [], "reduce7": [], "reduce7_occ8": [], "dw": []}
     res.update({f"reduce6_rb{rb}": [] for rb in rbs})
     for _ in range(a.rounds):
         res["reduce5"].append(ev_time(lambda: r5(scratch), a.iters))
         res["reduce7"].append(ev_time(lambda: r7(scratch), a.iters))
+        if has_occ:
+            L_.pv_conv_r7_set_occ(8)
+            res["reduce7_occ8"].append(ev_time(lambda: r7(scratch), a.iters))
+            L_.pv_conv_r7_set_occ(1)
         res["dw"].append(ev_time(dw, a.iters))
         for rb in rbs:
             res[f"reduce6_rb{rb}"].append(ev_time(lambda: r6(scratch, rb), a.iters))
-    out = {k: round(statistics.median(v), 4) for k, v in res.items()}
+    out = {k: round(statistics.median(v), 4) for k, v in res.items() if v}
     out.update({"N": N, "L": L, "entries": M, "epw": a.epw})
     print(json.dumps(out), flush=True)
 
