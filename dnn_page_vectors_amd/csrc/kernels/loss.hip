@@ -857,37 +857,40 @@ __global__ __launch_bounds__(256) void ib_pos_kernel(const unsigned short* __res
   }
 }
 
-// Row-materialised variant for wide vectors (D > 192, e.g. BERT's 768) or small M: the
-// (B x M) cosine matrix S comes from a hipBLASLt GEMM; one wave per row computes the
-// log-sum-exp, the loss and the full logit gradient dS = gscale*g*(P - onehot)*clip'
-// in place (the two products dQ = dS.D, dD = dS^T.Q are again library GEMMs).
-__global__ __launch_bounds__(256) void ib_rows_kernel(float* __restrict__ S, const int* __restrict__ pos,
-                                                      const float* __restrict__ gscale, float* __restrict__ loss,
-                                                      int B, int M, float gamma, int clip) {
+// Wide vectors (D > 192, e.g. BERT's 768): the flash kernels above keep a query row's D
+// accumulators in registers, which D = 768 does not fit, so the logits are tiled at the
+// GEMM level instead — S is produced one column block (B x Mb, bounded memory) at a time by
+// a bf16 x bf16 -> fp32 library GEMM and never exists whole.  Per block, one wave per row:
+//  * forward (scale == nullptr): part[row] = sum_c exp(g * (clip(S_rc) - 1)) (the logits are
+//    shifted by the largest possible one, as in the flash kernels, so block partial sums
+//    simply add: ib_rowsum sums them in block order and finalises loss / P+);
+//  * backward: S_rc <- scale_r * exp(g * (clip(S_rc) - 1)) * clip'(S_rc) in place (the
+//    negative part of dS; ib_pos adds the positive pair), the block's dQ += dS . D_blk and
+//    dD_blk = dS^T . Q are library GEMMs again.
+__global__ __launch_bounds__(256) void ib_rows_blk_kernel(float* __restrict__ S, int ld, int B, int Mb,
+                                                          const float* __restrict__ scale, float* __restrict__ part,
+                                                          float gamma, int clip) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B) return;
-  float* s = S + (size_t)row * M;
-  float sum = 0.f;
-  for (int c = lane; c < M; c += 64) {
-    float r = s[c];
-    if (clip) r = fminf(fmaxf(r, 0.f), 1.f);
-    sum += __expf(gamma * (r - 1.f));
+  float* s = S + (size_t)row * ld;
+  if (!scale) {
+    float sum = 0.f;
+    for (int c = lane; c < Mb; c += 64) {
+      float r = s[c];
+      if (clip) r = fminf(fmaxf(r, 0.f), 1.f);
+      sum += __expf(gamma * (r - 1.f));
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) part[row] = sum;
+    return;
   }
-  sum = wave_sum(sum);
-  const int p = pos[row];
-  if (!PV_OK(p >= 0 && p < M, PV_ERR_POS)) return;
-  float rp = s[p];
-  if (clip) rp = fminf(fmaxf(rp, 0.f), 1.f);
-  if (lane == 0 && loss) loss[row] = gamma + __logf(sum) - gamma * rp;
-  if (!gscale) return;
-  const float g = gscale[row] * gamma;
-  for (int c = lane; c < M; c += 64) {
+  const float sc = scale[row];
+  for (int c = lane; c < Mb; c += 64) {
     const float raw = s[c];
     const bool pass = !clip || (raw >= 0.f && raw <= 1.f);
     const float r = clip ? fminf(fmaxf(raw, 0.f), 1.f) : raw;
-    const float P = __expf(gamma * (r - 1.f)) / sum;
-    s[c] = pass ? g * (P - (c == p ? 1.f : 0.f)) : 0.f;
+    s[c] = pass ? sc * __expf(gamma * (r - 1.f)) : 0.f;
   }
 }
 
@@ -1217,10 +1220,22 @@ PV_API int pv_ib_pos(const void* X, const void* Y, const int* pos, float* spos, 
   return 0;
 }
 
-PV_API int pv_ib_rows(float* S, const int* pos, const float* gscale, float* loss, int B, int M, float gamma, int clip,
-                      void* stream) {
-  hipLaunchKernelGGL(pv::loss::ib_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, pos, gscale,
-                     loss, B, M, gamma, clip);
+PV_API int pv_ib_rows_blk(float* S, int ld, int B, int Mb, const float* scale, float* part, float gamma, int clip,
+                          void* stream) {
+  if (B <= 0 || Mb <= 0 || ld < Mb || (!scale && !part)) return -1;
+  hipLaunchKernelGGL(pv::loss::ib_rows_blk_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, S, ld, B, Mb,
+                     scale, part, gamma, clip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// sumexp = sum of the ns block partials (part[s][row], fixed order); loss = spos-based
+// g + log(sumexp) - spos, P+ = exp(-loss)
+PV_API int pv_ib_rowsum(const float* part, float* sumexp, int B, int ns, const float* spos, float* loss, float* prob,
+                        float gamma, void* stream) {
+  if (B <= 0 || ns <= 0) return -1;
+  hipLaunchKernelGGL(pv::loss::ib_rowsum_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, part,
+                     sumexp, B, ns, spos, loss, prob, gamma);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -69,7 +69,8 @@ SIGS = {
     "pv_ib_fwd_dq_parts": "ii",
     "pv_ib_fwd_dq": "pppppp" "iiif" "i" "ppp" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",
-    "pv_ib_rows": "pppp" "ii" "fi" "p",
+    "pv_ib_rows_blk": "p" "iii" "pp" "fi" "p",
+    "pv_ib_rowsum": "pp" "ii" "ppp" "f" "p",
     "pv_ib_version": "",
     "pv_ib_set_version": "i",
     # embedding.hip

@@ -20,6 +20,7 @@ Both take L2-normalised vectors (``ops.dense.l2_normalize``).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -183,31 +184,75 @@ class _InBatchFn(torch.autograd.Function):
         return dq[:, :D], dd[:, :D], None, None, None, None
 
 
+# column-block size of the wide-vector path: B x ROWS_BLOCK_ELEMS / B fp32 logits per block
+ROWS_BLOCK_ELEMS = int(os.environ.get("PAGEVEC_IB_ROWS_BLOCK", str(1 << 25)))
+
+
+def _col_blocks(B: int, M: int):
+    mb = max(256, min(M, ROWS_BLOCK_ELEMS // max(B, 1)))
+    return [(c0, min(M, c0 + mb)) for c0 in range(0, M, mb)]
+
+
 class _InBatchRowsFn(torch.autograd.Function):
-    """Wide vectors (D > 192): S by hipBLASLt GEMM, loss/gradient by the ib_rows HIP kernel."""
+    """Wide vectors (D > 192, e.g. BERT's 768; the flash kernels hold D accumulators per query
+    row in registers): the logits are tiled over page-column blocks at the GEMM level — each
+    (B x Mb) block of S comes from a bf16 x bf16 -> fp32 library GEMM, is reduced by
+    loss.hip::ib_rows_blk_kernel and dropped, so memory stays O(B * Mb) for any M; the
+    backward recomputes each block (flash-style) and turns it into the block's dS in place.
+    Positive pairs go through ib_pos as in the fused path."""
 
     @staticmethod
-    def forward(ctx, qn, dn, pos, gamma, clip):
-        B, M = qn.shape[0], dn.shape[0]
-        qb, db = qn.detach().to(torch.bfloat16), dn.detach().to(torch.bfloat16)
-        S = (qb @ db.t()).float().contiguous()
+    def forward(ctx, qn, dn, pos, gamma, clip, reduce=False):
+        B, D = qn.shape
+        M = dn.shape[0]
+        DP = (D + 31) // 32 * 32
+        qb, db = _pad_bf16(qn, DP), _pad_bf16(dn, DP)
         pos = pos.to(torch.int32).contiguous()
-        loss = torch.empty(B, dtype=torch.float32, device=qn.device)
-        check(lib().pv_ib_rows(P(S), P(pos), None, P(loss), B, M, float(gamma), int(clip), stream(qn.device)),
-              "pv_ib_rows")
-        ctx.save_for_backward(qb, db, pos, S)
-        ctx.meta = (float(gamma), int(clip))
-        return loss, torch.exp(-loss).detach()
+        dev, s, L_ = qn.device, stream(qn.device), lib()
+        spos = torch.empty(B, dtype=torch.float32, device=dev)
+        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
+              "pv_ib_pos")
+        blocks = _col_blocks(B, M)
+        part = torch.empty(len(blocks), B, dtype=torch.float32, device=dev)
+        for k, (c0, c1) in enumerate(blocks):
+            S = torch.mm(qb, db[c0:c1].t(), out_dtype=torch.float32)
+            check(L_.pv_ib_rows_blk(P(S), c1 - c0, B, c1 - c0, None, P(part[k]), float(gamma), int(clip), s),
+                  "pv_ib_rows_blk")
+        sumexp = torch.empty(B, dtype=torch.float32, device=dev)
+        loss = torch.empty(B, dtype=torch.float32, device=dev)
+        prob = torch.empty(B, dtype=torch.float32, device=dev)
+        check(L_.pv_ib_rowsum(P(part), P(sumexp), B, len(blocks), P(spos), P(loss), P(prob), float(gamma), s),
+              "pv_ib_rowsum")
+        ctx.save_for_backward(qb, db, pos, sumexp)
+        ctx.meta = (B, M, D, DP, float(gamma), int(clip))
+        ctx.reduce = bool(reduce)
+        ctx.mark_non_differentiable(prob)
+        ctx.set_materialize_grads(False)
+        if reduce:
+            lm, acc = _loss_stats(loss, prob)
+            ctx.mark_non_differentiable(acc)
+            return lm, prob, acc
+        return loss, prob
 
     @staticmethod
-    def backward(ctx, gl, _gp):
-        qb, db, pos, S = ctx.saved_tensors
-        gamma, clip = ctx.meta
-        B, M = S.shape
-        g = gl.contiguous().float()
-        check(lib().pv_ib_rows(P(S), P(pos), P(g), None, B, M, gamma, clip, stream(S.device)), "pv_ib_rows")
-        dS = S.to(torch.bfloat16)
-        return (dS @ db).float(), (dS.t() @ qb).float(), None, None, None
+    def backward(ctx, gl, _gp, _ga=None):
+        if gl is None:
+            return (None,) * len(ctx.needs_input_grad)
+        qb, db, pos, sumexp = ctx.saved_tensors
+        B, M, D, DP, gamma, clip = ctx.meta
+        dev, s, L_ = qb.device, stream(qb.device), lib()
+        scale, g, _ = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, None, DP)
+        dq = torch.zeros(B, DP, dtype=torch.float32, device=dev)
+        dd = torch.empty(M, DP, dtype=torch.float32, device=dev)
+        for c0, c1 in _col_blocks(B, M):
+            S = torch.mm(qb, db[c0:c1].t(), out_dtype=torch.float32)
+            check(L_.pv_ib_rows_blk(P(S), c1 - c0, B, c1 - c0, P(scale), None, float(gamma), int(clip), s),
+                  "pv_ib_rows_blk(dS)")
+            dS = S.to(torch.bfloat16)
+            dq += torch.mm(dS, db[c0:c1], out_dtype=torch.float32)
+            dd[c0:c1] = torch.mm(dS.t(), qb, out_dtype=torch.float32)
+        check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
+        return dq[:, :D], dd[:, :D], None, None, None, None
 
 
 class PageGather:
@@ -351,8 +396,7 @@ def inbatch_loss(qn: torch.Tensor, dn: torch.Tensor, pos_index: torch.Tensor, ga
     _check_gamma(gamma, clip)
     if use_hip(qn, dn):
         if qn.shape[1] > 192:
-            out = _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip))
-            return _reduce_rows(*out) if reduce else out
+            return _InBatchRowsFn.apply(qn, dn, pos_index, float(gamma), bool(clip), bool(reduce))
         return _InBatchFn.apply(qn, dn, pos_index, float(gamma), bool(clip), bool(reduce))
     out = ref.inbatch_softmax_loss(qn, dn, pos_index, gamma, clip)
     return _reduce_rows(*out) if reduce else out

@@ -547,16 +547,29 @@ def test_big_model_train_steps_gpu(preset):
     assert losses[-1] < 0.7 * losses[0], losses
 
 
-def test_inbatch_loss_wide_rows_path():
+@pytest.mark.parametrize("B,M,clip,block", [(40, 160, False, 1 << 25), (40, 1000, True, 40 * 256),
+                                            (300, 3000, False, 300 * 700), (64, 5000, True, 64 * 256)])
+def test_inbatch_loss_wide_rows_path(B, M, clip, block, monkeypatch):
+    """D = 768 (BERT): logits tiled over page-column blocks at the GEMM level (one block, or
+    several with a partial last one), never materialised whole."""
+    monkeypatch.setattr(lops, "ROWS_BLOCK_ELEMS", block)
     torch.manual_seed(4)
-    B, M, D = 40, 160, 768
-    qn = bf(ref.l2_normalize(torch.randn(B, D, device=DEV))).requires_grad_(True)
-    dn = bf(ref.l2_normalize(torch.randn(M, D, device=DEV))).requires_grad_(True)
-    pos = torch.arange(B, device=DEV, dtype=torch.int32) * 4
-    loss, _ = lops.inbatch_loss(qn, dn, pos, 10.0, False)
+    D = 768
+    qn = torch.randn(B, D, device=DEV)
+    dn = torch.randn(M, D, device=DEV)
+    pos = (torch.arange(B, device=DEV, dtype=torch.int32) * 3) % M
+    dn[pos.long()] = qn + 0.5 * dn[pos.long()]  # positives correlated with their queries
+    if clip:
+        qn, dn = qn.abs(), dn.abs()
+    qn = bf(ref.l2_normalize(qn)).requires_grad_(True)
+    dn = bf(ref.l2_normalize(dn)).requires_grad_(True)
+    assert len(lops._col_blocks(B, M)) == (1 if block >= B * M else -(-M // max(256, block // B)))
+    loss, _ = lops.inbatch_loss(qn, dn, pos, 10.0, clip)
     q2, d2 = qn.detach().clone().requires_grad_(True), dn.detach().clone().requires_grad_(True)
-    lr, _ = ref.inbatch_softmax_loss(q2, d2, pos, 10.0, False)
+    lr, _ = ref.inbatch_softmax_loss(q2, d2, pos, 10.0, clip)
     torch.testing.assert_close(loss, lr, rtol=2e-3, atol=2e-3)
+    lm, _, _ = lops.inbatch_loss(qn.detach(), dn.detach(), pos, 10.0, clip, reduce=True)
+    torch.testing.assert_close(lm, lr.mean(), rtol=2e-3, atol=2e-3)
     loss.mean().backward()
     lr.mean().backward()
     torch.testing.assert_close(qn.grad, q2.grad, rtol=3e-2, atol=3e-3)
