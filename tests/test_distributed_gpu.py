@@ -22,7 +22,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, D=150):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
     try:
@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
 
         info = pdist.init_distributed()
         dev = info.device
-        B, S, D = 96, 4, 150
+        B, S = 96, 4
         n = B * S
         g = torch.Generator(device=dev).manual_seed(0)
         qa = torch.nn.functional.normalize(torch.randn(world * B, D, device=dev, generator=g), dim=1)
@@ -69,12 +69,14 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_cross_gpu_loss_ranks_one_gpu(world):
+@pytest.mark.parametrize("world,D", [(2, 150), (4, 150), (2, 768)])
+def test_cross_gpu_loss_ranks_one_gpu(world, D):
+    """D = 768 (BERT): the wide-vector path (autograd page all-gather + column-block tiled
+    logits) across ranks."""
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, D)) for r in range(world)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=300) for _ in ps)
     [p.join(timeout=60) for p in ps]
@@ -82,11 +84,12 @@ def test_cross_gpu_loss_ranks_one_gpu(world):
         assert not isinstance(res[r], str), res[r]
         e_loss, e_q, e_d, h_q, h_d = res[r]
         assert e_loss < 1e-4, res
-        assert e_q < 5e-2 and e_d < 5e-2, res  # bf16 G vs fp32 oracle
+        tol = 5e-2 if D <= 192 else 8e-2  # bf16 dS vs the fp32 oracle (max-norm over D entries per row)
+        assert e_q < tol and e_d < tol, res
         assert h_q < 1e-4 and h_d < 1e-4, res  # vs the single-process HIP path
 
 
-def _ddp_worker(rank, world, port, model, q, ld=64):
+def _ddp_worker(rank, world, port, model, q, ld=64, mode="sink"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
     try:
@@ -106,7 +109,10 @@ def _ddp_worker(rank, world, port, model, q, ld=64):
         di = torch.randint(1, 500, (32, 4, ld), generator=g, dtype=torch.int32).to(dev)
         grads = []
         for enabled in (False, True):
-            grad_sink.ENABLED = enabled
+            if mode == "sink":  # AccumulateGrad hooks vs direct flat-gradient writes
+                grad_sink.ENABLED = enabled
+            else:  # one stream vs the query tower on its side stream (direct writes on)
+                cfg = cfg.replace(query_stream=enabled)
             torch.manual_seed(0)
             tr = Trainer(cfg, build_model(cfg, 500), dev)
             assert tr.buckets is not None and len(tr.buckets.buckets) > 1
@@ -124,18 +130,21 @@ def _ddp_worker(rank, world, port, model, q, ld=64):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("model,ld", [("cdssm", 64), ("cdssm", 96), ("mlp", 64)])
-def test_ddp_buckets_with_direct_grad_writes(model, ld):
+@pytest.mark.parametrize("model,ld,mode", [("cdssm", 64, "sink"), ("cdssm", 96, "sink"), ("mlp", 64, "sink"),
+                                           ("cdssm", 96, "qstream"), ("cdssm", 64, "qstream")])
+def test_ddp_buckets_with_direct_grad_writes(model, ld, mode):
     """Bucketed, backward-overlapped all-reduce (parallel/ddp.py) fired from the direct
     flat-gradient writes (ops/grad_sink.py): the reduced gradients equal those of the
     AccumulateGrad-hook path, and every rank holds the same gradient.  ld = 96 takes the
     long-sequence conv backward (emit / sort / reduce, dW on the side stream, the table's
-    own bucket released before dW)."""
+    own bucket released before dW).  mode "qstream": the query tower on its side stream
+    (direct gradient writes there, a 500-row vocabulary whose table shares buckets with
+    small parameters) gives the same reduced gradients as the one-stream run."""
     world = 2
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, model, q, ld)) for r in range(world)]
+    ps = [ctx.Process(target=_ddp_worker, args=(r, world, port, model, q, ld, mode)) for r in range(world)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=300) for _ in ps)
     [p.join(timeout=60) for p in ps]
