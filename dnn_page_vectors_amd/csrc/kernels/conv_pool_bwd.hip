@@ -158,7 +158,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
     float t = gsw[0] + gsw[1] + gsw[2] + gsw[3];
     if (t != 0.f) {
       if (fxb) fx_add(fxb, fg, t);
-      else atomicAdd(&db[fg], t);
+      else atomicAdd(&db[fl], t);  // db: this width's bias gradient (filter fl of the width)
     }
   }
 }
@@ -167,7 +167,8 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
 template <int DM>
 __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, const float* pooled, const int* argmax,
                                                           const int* ids, const unsigned short* table, float* dw3,
-                                                          float* dw4, float* db, int N, int L, int E, int V, int nsplit,
+                                                          float* dw4, float* db3, float* db4, int N, int L, int E, int V,
+                                                          int nsplit,
                                                           unsigned seed, const unsigned* seed_ptr,
                                                           unsigned row_offset, int thr, int token_mode, float scale,
                                                           int xcd_map, long long* fx) {
@@ -188,10 +189,10 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
   const int per = ((N + nsplit - 1) / nsplit + 255) / 256 * 256;
   const int n0 = split * per, n1 = min(N, n0 + per);
   if (f < FW)
-    dw_filter<3, DM>(gpool, pooled, argmax, ids, table, dw3, db, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
+    dw_filter<3, DM>(gpool, pooled, argmax, ids, table, dw3, db3, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx, fx ? fx + (size_t)7 * FW * E : nullptr);
   else
-    dw_filter<4, DM>(gpool, pooled, argmax, ids, table, dw4, db, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
+    dw_filter<4, DM>(gpool, pooled, argmax, ids, table, dw4, db4, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx ? fx + (size_t)3 * FW * E : nullptr, fx ? fx + (size_t)7 * FW * E : nullptr);
 }
 
@@ -984,10 +985,12 @@ struct DetAcc {
 };
 
 
-PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const int* argmax, const int* ids,
-                               const void* table, float* dw3, float* dw4, float* db, int N, int L, int E, int V,
-                               unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                               float scale, void* stream) {
+// db3 / db4: the two widths' bias gradients (150 floats each; separate so they can be the
+// bias parameters' own slices of the flat gradient buffer — ops/grad_sink.py)
+PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const int* argmax, const int* ids,
+                                const void* table, float* dw3, float* dw4, float* db3, float* db4, int N, int L, int E,
+                                int V, unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr,
+                                int token_mode, float scale, void* stream) {
   using namespace pv::convbwd;
   if (E > EP || L < 4 || (long)V * EP >= (1L << 31)) return -1;  // 32-bit table offsets in the kernel
   int nsplit = (N + 255) / 256;
@@ -1009,8 +1012,8 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
 #define PV_DW(DMV)                                                                                               \
   hipLaunchKernelGGL((conv_bwd_dw_kernel<DMV>), dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled, argmax, ids, \
-                     (const unsigned short*)table, dw3, dw4, db, N, L, E, V, nsplit, seed, seed_ptr, row_offset, thr, \
-                     token_mode, scale, xcd_map, fx)
+                     (const unsigned short*)table, dw3, dw4, db3, db4, N, L, E, V, nsplit, seed, seed_ptr,           \
+                     row_offset, thr, token_mode, scale, xcd_map, fx)
   if (dw_runtime_dm) PV_DW(-1);
   else if (dm == 0) PV_DW(0);
   else if (dm == 1) PV_DW(1);
@@ -1021,10 +1024,20 @@ PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const in
   if (fx) {
     int rc = det_flush(fx, dw3, (size_t)3 * FW * E, st);
     if (!rc) rc = det_flush(fx + (size_t)3 * FW * E, dw4, (size_t)4 * FW * E, st);
-    if (!rc) rc = det_flush(fx + (size_t)7 * FW * E, db, 2 * FW, st);
+    if (!rc) rc = det_flush(fx + (size_t)7 * FW * E, db3, FW, st);
+    if (!rc) rc = det_flush(fx + (size_t)7 * FW * E + FW, db4, FW, st);
     return rc;
   }
   return 0;
+}
+
+// db: both widths' bias gradients as one (2 * FW) array
+PV_API int pv_conv_pool_bwd_dw(const float* gpool, const float* pooled, const int* argmax, const int* ids,
+                               const void* table, float* dw3, float* dw4, float* db, int N, int L, int E, int V,
+                               unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                               float scale, void* stream) {
+  return pv_conv_pool_bwd_dw2(gpool, pooled, argmax, ids, table, dw3, dw4, db, db + pv::convbwd::FW, N, L, E, V, seed,
+                              seed_ptr, row_offset, thr, token_mode, scale, stream);
 }
 
 // keys/vals: M = N * pv_conv_bwd_slots_per_sample() slots; rec: N*2*FW records {g*scale, argmax}.

@@ -70,6 +70,7 @@ struct Params {
   int token_mode;              // 1: one keep decision per row
   float scale;                 // 1/(1-p)
   const unsigned* seed_ptr;    // optional device seed offset (added to seed; captured hipGraph steps)
+  const float* bias4;          // (FW) k=4 filters' bias; bias holds the k=3 filters' (FW)
 };
 
 // Diagnostic ablations are COMPILE-TIME (template DBG; production instantiation DBG = 0
@@ -368,7 +369,7 @@ __device__ __forceinline__ void run_wave(const Params& p, int t3base, int t4base
         int col = colbase + rsub;  // filter index within width
         if (kq == 0 && (col % 160) < FW) {
           int f = (col / 160) * FW + (col % 160);
-          float y = bv * p.scale + p.bias[f];
+          float y = bv * p.scale + (f < FW ? p.bias[f] : p.bias4[f - FW]);
           p.pooled[(size_t)cur.n * (2 * FW) + f] = y > 0.f ? y : 0.f;
           p.argmax[(size_t)cur.n * (2 * FW) + f] = bi;
         }
@@ -712,7 +713,7 @@ __device__ __forceinline__ void run_wave2(const Params& p, int t3base, int t4bas
         if (kq == 0 && (col % 160) < FW) {
           const int f = (col / 160) * FW + (col % 160);
           PV_CHECK(bi >= 0 && bi < (col < 160 ? nw3 : nw4), PV_ERR_ARGMAX);
-          const float y = bv * p.scale + p.bias[f];
+          const float y = bv * p.scale + (f < FW ? p.bias[f] : p.bias4[f - FW]);
           p.pooled[(size_t)cur.n * (2 * FW) + f] = y > 0.f ? y : 0.f;
           p.argmax[(size_t)cur.n * (2 * FW) + f] = bi;
         }
@@ -908,16 +909,17 @@ PV_API int pv_conv_packed_size() {
 static int g_conv_dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
 PV_API void pv_conv_set_dbg(int d) { g_conv_dbg = d; }
 
-PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack, const float* bias,
-                            float* pooled, int* argmax, int N, int L, int V, unsigned seed, const unsigned* seed_ptr,
-                            unsigned row_offset,
-                            int thr, int token_mode, float scale, int grid, void* stream) {
+// bias3 / bias4: the two widths' biases (FW floats each, e.g. the parameters themselves)
+PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpack, const float* bias3,
+                             const float* bias4, float* pooled, int* argmax, int N, int L, int V, unsigned seed,
+                             const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode, float scale,
+                             int grid, void* stream) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
   if ((L - 2 + 15) / 16 > 1024) return -2;  // tagged argmax: block index must fit TAGB bits
   const int dbg = g_conv_dbg;
-  Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias, pooled, argmax, N, L, V,
-           seed, row_offset, thr, token_mode, scale, seed_ptr};
+  Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias3, pooled, argmax, N, L, V,
+           seed, row_offset, thr, token_mode, scale, seed_ptr, bias4};
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
   hipStream_t st = (hipStream_t)stream;
@@ -988,4 +990,12 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
 #undef PV_CONV_LAUNCH
   PV_LAUNCH_CHECK();
   return 0;
+}
+
+// bias: both widths' biases as one (2 * FW) array
+PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack, const float* bias,
+                            float* pooled, int* argmax, int N, int L, int V, unsigned seed, const unsigned* seed_ptr,
+                            unsigned row_offset, int thr, int token_mode, float scale, int grid, void* stream) {
+  return pv_conv_pool_fwd2(ids, table, wpack, bias, bias + pv::convpool::FW, pooled, argmax, N, L, V, seed, seed_ptr,
+                           row_offset, thr, token_mode, scale, grid, stream);
 }

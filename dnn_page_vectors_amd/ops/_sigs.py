@@ -20,8 +20,10 @@ SIGS = {
     "pv_set_deterministic": "i",
     "pv_get_deterministic": "",
     "pv_conv_pool_fwd": "pppppp" "iii" "upu" "ii" "f" "i" "p",
+    "pv_conv_pool_fwd2": "ppppppp" "iii" "upu" "ii" "f" "i" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
+    "pv_conv_pool_bwd_dw2": "ppppp" "pppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "upuii" "p",
     "pv_conv_pool_bwd_reduce5": "ppppp" "liiii" "upuii" "p",
     "pv_conv_pool_bwd_emit3": "ppppppp" "iii" "f" "p",

@@ -163,7 +163,7 @@ def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
 
 class _ConvPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, table, w3, w4, bias, tbl16, wpack, p, seed, row_offset, training, mode):
+    def forward(ctx, ids, table, w3, w4, b3, b4, tbl16, wpack, p, seed, row_offset, training, mode):
         ids = need(ids, torch.int32, "ids", 2)
         N, L = ids.shape
         V, E = table.shape
@@ -175,20 +175,21 @@ class _ConvPoolFn(torch.autograd.Function):
         seed &= 0xFFFFFFFF
         row_offset &= 0xFFFFFFFF
         sp = _SEED_DEV
-        check(lib().pv_conv_pool_fwd(P(ids), P(tbl16), P(wpack), P(bias.contiguous()), P(pooled), P(argmax), N, L, V,
-                                     seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
-              "pv_conv_pool_fwd")
+        b3c, b4c = b3.detach().contiguous(), b4.detach().contiguous()  # the parameters themselves: no cat
+        check(lib().pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(b3c), P(b4c), P(pooled), P(argmax), N, L, V,
+                                      seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
+              "pv_conv_pool_fwd2")
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
         ctx.set_materialize_grads(False)  # no zero-filled (N, 300) int gradient for argmax
-        ctx.params = (table, w3, w4)  # flat-gradient direct-write targets (ops/grad_sink.py)
+        ctx.params = (table, w3, w4, b3, b4)  # flat-gradient direct-write targets (ops/grad_sink.py)
         return pooled, argmax
 
     @staticmethod
     def backward(ctx, gpool, _gargmax):
         if gpool is None:
-            return (None,) * 12
+            return (None,) * 13
         ids, pooled, argmax, tbl16, w3, w4 = ctx.saved_tensors
         V, E, seed, row_offset, thr, tok, scale, sp = ctx.meta
         N, L = ids.shape
@@ -197,13 +198,19 @@ class _ConvPoolFn(torch.autograd.Function):
         gpool = gpool.contiguous().float()
         # the backward kernels accumulate atomically: they can add straight into the flat
         # gradient buffer (no zeroed temporaries, no AccumulateGrad adds)
-        ptable, pw3, pw4 = ctx.params
+        ptable, pw3, pw4, pb3, pb4 = ctx.params
         t_tab = grad_sink.accum_target(ptable) if ctx.needs_input_grad[1] else None
         t3 = grad_sink.accum_target(pw3) if ctx.needs_input_grad[2] else None
         t4 = grad_sink.accum_target(pw4) if ctx.needs_input_grad[3] else None
+        tb3 = grad_sink.accum_target(pb3) if ctx.needs_input_grad[4] else None
+        tb4 = grad_sink.accum_target(pb4) if ctx.needs_input_grad[5] else None
         dw3 = t3 if t3 is not None else torch.zeros_like(w3)
         dw4 = t4 if t4 is not None else torch.zeros_like(w4)
-        db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
+        db = None
+        if tb3 is None or tb4 is None:
+            db = torch.zeros(2 * FW, dtype=torch.float32, device=dev)
+        db3 = tb3 if tb3 is not None else db[:FW]
+        db4 = tb4 if tb4 is not None else db[FW:]
         L_ = lib()
         # every buffer the side stream touches is allocated on the main stream above/before
         # and the main stream joins the side stream before returning: no cross-stream reuse
@@ -217,9 +224,9 @@ class _ConvPoolFn(torch.autograd.Function):
             s_dw = side.cuda_stream
 
         def launch_dw():
-            check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L,
-                                         E, V, seed, P(sp), row_offset, thr, tok, scale, s_dw if side is not None else s),
-                  "pv_conv_pool_bwd_dw")
+            check(L_.pv_conv_pool_bwd_dw2(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db3),
+                                          P(db4), N, L, E, V, seed, P(sp), row_offset, thr, tok, scale,
+                                          s_dw if side is not None else s), "pv_conv_pool_bwd_dw2")
 
         # Order: the side-stream variant starts dW first (it runs beside the table chain);
         # on one stream the TABLE gradient goes first.  Either way the table's data-parallel
@@ -289,12 +296,13 @@ class _ConvPoolFn(torch.autograd.Function):
             launch_dw()
         else:
             main.wait_stream(side)
-        for t, prm in ((t3, pw3), (t4, pw4)):
+        for t, prm in ((t3, pw3), (t4, pw4), (tb3, pb3), (tb4, pb4)):
             if t is not None:
                 grad_sink.done(prm)
         if t_tab is not None:
             dtable = None
-        return (None, dtable, None if t3 is not None else dw3, None if t4 is not None else dw4, db,
+        return (None, dtable, None if t3 is not None else dw3, None if t4 is not None else dw4,
+                None if tb3 is not None else db3, None if tb4 is not None else db4,
                 None, None, None, None, None, None, None)
 
 
@@ -307,12 +315,12 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
     """
     if use_hip(ids, table) and fast_path_supported(table.shape[1], [w.shape[1] for w in weights], weights[0].shape[0]):
         w3, w4 = weights
-        bias = torch.cat(list(biases))
+        b3, b4 = biases
         if compute_cache is None:
             tbl16, wpack = table_bf16(table.detach()), pack_weights(w3.detach(), w4.detach())
         else:
             tbl16, wpack = compute_cache
-        return _ConvPoolFn.apply(ids, table, w3, w4, bias, tbl16, wpack, float(p), int(seed), int(row_offset),
+        return _ConvPoolFn.apply(ids, table, w3, w4, b3, b4, tbl16, wpack, float(p), int(seed), int(row_offset),
                                  bool(training), mode)
     if ids.is_cuda and use_hip(ids, table):
         # no silent eager fallback on the GPU: the fused kernel is built for this geometry only
