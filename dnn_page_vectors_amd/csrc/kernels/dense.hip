@@ -296,12 +296,12 @@ __global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict
 // dx = (dy - y * <y, dy>) * inv   (if |x|^2 < tiny the clamp is active: dx = dy * inv)
 __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ y, const float* __restrict__ inv_norm,
                                                          const float* __restrict__ x, const float* __restrict__ dy,
-                                                         float* __restrict__ dx, int M, int D) {
+                                                         float* __restrict__ dx, int M, int D, long ldy) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= M) return;
   const float* yr = y + (size_t)row * D;
-  const float* gr = dy + (size_t)row * D;
+  const float* gr = dy + (size_t)row * ldy;  // ldy >= D: e.g. the loss kernels' padded (n, DP) gradient
   float s = 0.f, xx = 0.f;
   for (int d = lane; d < D; d += 64) {
     s += yr[d] * gr[d];
@@ -480,13 +480,20 @@ PV_API int pv_l2norm_fwd(const float* x, float* y, float* inv_norm, void* ybf, i
   return 0;
 }
 
-PV_API int pv_l2norm_bwd(const float* y, const float* inv_norm, const float* x, const float* dy, float* dx, int M, int D,
-                         void* stream) {
+// ldy: row stride of dy in floats (>= D)
+PV_API int pv_l2norm_bwd_ld(const float* y, const float* inv_norm, const float* x, const float* dy, long ldy, float* dx,
+                            int M, int D, void* stream) {
   using namespace pv::dense;
+  if (ldy < D) return -1;
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, y, inv_norm, x, dy, dx,
-                     M, D);
+                     M, D, ldy);
   PV_LAUNCH_CHECK();
   return 0;
+}
+
+PV_API int pv_l2norm_bwd(const float* y, const float* inv_norm, const float* x, const float* dy, float* dx, int M, int D,
+                         void* stream) {
+  return pv_l2norm_bwd_ld(y, inv_norm, x, dy, D, dx, M, D, stream);
 }
 
 PV_API int pv_act_bwd(const float* y, const float* dy, float* dz, long n, int act, void* stream) {

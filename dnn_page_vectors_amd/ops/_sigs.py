@@ -57,6 +57,7 @@ SIGS = {
     "pv_linear_dgrad": "pipip" "iii" "p",
     "pv_l2norm_fwd": "pppp" "iii" "p",
     "pv_l2norm_bwd": "ppppp" "ii" "p",
+    "pv_l2norm_bwd_ld": "pppp" "l" "p" "ii" "p",
     "pv_act_bwd_rowscale": "pppp" "p" "lli" "p",
     "pv_act_bwd2": "ppppl" "ip",
     "pv_act_bwd": "ppp" "li" "p",

@@ -235,9 +235,14 @@ class _L2NormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, y, inv = ctx.saved_tensors
         M, D = x2.shape
-        dy2 = dy.reshape(M, D).contiguous().float()
+        dy2 = dy.reshape(M, D)
+        if dy2.dtype != torch.float32 or dy2.stride(1) != 1 or dy2.stride(0) < D:
+            dy2 = dy2.contiguous().float()
+        # row-strided gradients (the loss kernels' (n, DP) padded dQ / dD sliced to D) are read
+        # in place: no copy kernel
         dx = torch.empty_like(x2)
-        check(lib().pv_l2norm_bwd(P(y), P(inv), P(x2), P(dy2), P(dx), M, D, stream(dy.device)), "pv_l2norm_bwd")
+        check(lib().pv_l2norm_bwd_ld(P(y), P(inv), P(x2), P(dy2), dy2.stride(0), P(dx), M, D, stream(dy.device)),
+              "pv_l2norm_bwd_ld")
         return dx.view(ctx.shape)
 
 

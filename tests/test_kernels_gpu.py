@@ -153,15 +153,23 @@ def test_dense_backward_kernels(M, N, K, xbf):
     torch.testing.assert_close(out, ref_dw, rtol=1e-3, atol=float(ref_dw.abs().max()) * 2e-3)
 
 
-def test_l2norm():
+@pytest.mark.parametrize("grad", ["dense", "row_strided", "expanded"])
+def test_l2norm(grad):
+    """Backward with a dense gradient, a row-strided one (the loss kernels' padded (n, 160)
+    gradient sliced to 150 columns, read in place) and a stride-0 expanded one."""
     x = torch.randn(37, 150, device=DEV, requires_grad=True)
     x2 = x.detach().clone().requires_grad_(True)
     y = dops.l2_normalize(x)
     yr = ref.l2_normalize(x2)
     torch.testing.assert_close(y, yr)
-    g = torch.randn_like(y)
-    (y * g).sum().backward()
-    (yr * g).sum().backward()
+    if grad == "dense":
+        g = torch.randn_like(y)
+    elif grad == "row_strided":
+        g = torch.randn(37, 160, device=DEV)[:, :150]
+    else:
+        g = torch.randn(1, 150, device=DEV).expand(37, 150)
+    y.backward(g)
+    yr.backward(g)
     torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
 
 
