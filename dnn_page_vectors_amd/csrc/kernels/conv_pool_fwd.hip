@@ -822,6 +822,45 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_pool_fwd4_kernel(Params p) {
   }
 }
 
+// v6 = v4's tiles over 12 waves, THREE per SIMD (768-thread workgroups, <= 168 VGPRs per
+// wave): SIMD s hosts waves s, s+4, s+8.  SIMDs 0-2 take three k3 and two k4 tiles each as
+// {k3 + k4, k3 + k4, k3}, SIMD 3 the remaining k4 tiles as {two k4, one k4, mixed} — the same
+// {56,56,56,52} MFMAs per 16-window block as v4, but one more wave per SIMD to cover the
+// LDS / staging latencies (v4: 41% of wave-cycles at s_waitcnt) at the price of fewer MFMAs
+// per A-fragment read (1.6 instead of 2.5).
+constexpr int NTH6 = 768;
+template <int PF, int DBG, int OPT, int DM>
+__global__ __launch_bounds__(NTH6, 1) void conv_pool_fwd6_kernel(Params p) {
+  if (p.seed_ptr) p.seed += *p.seed_ptr;
+  __shared__ __attribute__((aligned(16))) char smem[2 * CROWS * ROWB + 4 * CROWS * 4 + 16];
+  char* xl = smem;
+  int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr ((OPT & 1) != 0) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr ((OPT & 32) != 0) {  // only the youngest wave of each SIMD (slot 2) prioritised
+    if (wave >= 8) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr ((OPT & 64) != 0) {  // graded: slot 1 at 1, slot 2 at 2
+    if (wave >= 8) __builtin_amdgcn_s_setprio(2);
+    else if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  const int simd = wave & 3, slot = wave >> 2;
+  if (simd < 3) {
+    if (slot < 2)
+      run_wave2<1, 1, PF, DBG, OPT, DM, false, NTH6>(p, 3 * simd + slot, 2 * simd + slot, xl, ids_lds);
+    else
+      run_wave2<1, 0, PF, DBG, OPT, DM, false, NTH6>(p, 3 * simd + 2, 0, xl, ids_lds);
+  } else if (slot == 0) {
+    run_wave2<0, 2, PF, DBG, OPT, DM, false, NTH6>(p, 0, 6, xl, ids_lds);
+  } else if (slot == 1) {
+    run_wave2<0, 1, PF, DBG, OPT, DM, false, NTH6>(p, 0, 8, xl, ids_lds);
+  } else {
+    run_wave2<0, 1, PF, DBG, OPT, DM, true, NTH6>(p, 0, 0, xl, ids_lds);
+  }
+}
+
 // (v5, measured and removed: v4's tile sets with ONE wave per SIMD in a 256-thread
 // workgroup — A fragments read once per SIMD instead of twice — ran 7.23-7.31 ms against
 // v4's 5.53 ms at the bench shape, bit-identical outputs: without a partner wave nothing
@@ -949,6 +988,13 @@ PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpac
     case 4096 + 4: hipLaunchKernelGGL((conv_pool_fwd4_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 12: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 12, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 9: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 0, 9, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
+    // v6: three waves per SIMD (A/B; bit-identical to v4)
+    case 8192 + 13: hipLaunchKernelGGL((conv_pool_fwd6_kernel<2, 0, 13, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
+    case 8192 + 12: hipLaunchKernelGGL((conv_pool_fwd6_kernel<2, 0, 12, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
+    case 8192 + 44: hipLaunchKernelGGL((conv_pool_fwd6_kernel<2, 0, 44, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
+    case 8192 + 76: hipLaunchKernelGGL((conv_pool_fwd6_kernel<2, 0, 76, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
+    case 8192 + 16 + 12: hipLaunchKernelGGL((conv_pool_fwd6_kernel<1, 0, 12, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
+    case 8192 + 3 * 16 + 12: hipLaunchKernelGGL((conv_pool_fwd6_kernel<3, 0, 12, 1>), dim3(grid), dim3(NTH6), 0, st, p); break;
     case 2048 + 1: hipLaunchKernelGGL((conv_pool_fwd3_kernel<1, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 3: hipLaunchKernelGGL((conv_pool_fwd3_kernel<3, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 2048 + 4: hipLaunchKernelGGL((conv_pool_fwd3_kernel<4, 0, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;

@@ -100,6 +100,32 @@ def test_dtable_reduce_long_runs_match_reduce4(epw, variant):
     assert grads[0].abs().sum() > 0
 
 
+@pytest.mark.parametrize("variant", [8204, 8236])
+@pytest.mark.parametrize("N,L", [(300, 45), (40, 2000), (7, 130)])
+def test_conv_forward_three_waves_per_simd_bit_identical(variant, N, L):
+    """The v6 conv forward (768-thread workgroups, three waves per SIMD; A/B arm) reproduces
+    the production v4 kernel bit for bit: pooled values and argmax windows."""
+    torch.manual_seed(5)
+    V, E, F = 500, 100, 150
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV)
+    table = torch.randn(V, E, device=DEV) * 0.3
+    w3, w4 = torch.randn(F, 3, E, device=DEV) * 0.1, torch.randn(F, 4, E, device=DEV) * 0.1
+    b = [torch.randn(F, device=DEV) * 0.1, torch.randn(F, device=DEV) * 0.1]
+    from dnn_page_vectors_amd.ops._common import lib as _lib
+    lib = _lib()
+    outs = []
+    try:
+        for v in (0, variant):
+            lib.pv_conv_set_dbg(v)
+            with torch.no_grad():
+                outs.append(cops.conv_relu_maxpool_fused(ids, table, [w3, w4], b, 0.25, 11, True))
+            torch.cuda.synchronize()
+    finally:
+        lib.pv_conv_set_dbg(0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_conv_pool_eval_mode_no_dropout():
     V, E, F, N, L = 50, 100, 150, 4, 20
     ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
