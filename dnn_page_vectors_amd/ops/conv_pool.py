@@ -69,6 +69,9 @@ REDUCE_V = int(os.environ.get("PAGEVEC_REDUCE_V", "7"))
 # (round 1: no gain, 9.30 vs 9.30 ms; with the round-2 backward, same box: 7.535 / 7.555 vs
 # 7.596 / 7.624 ms per headline step, so on by default for long sequences)
 DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "1") != "0"
+# conv bias gradients written by the dW kernel straight into the bias parameters' flat-gradient
+# slices (0: a zeroed (2 * FW) buffer returned to autograd, AccumulateGrad adds; A/B switch)
+BIAS_SINK = os.environ.get("PAGEVEC_BIAS_SINK", "1") != "0"
 _side = {}
 
 
@@ -202,8 +205,8 @@ class _ConvPoolFn(torch.autograd.Function):
         t_tab = grad_sink.accum_target(ptable) if ctx.needs_input_grad[1] else None
         t3 = grad_sink.accum_target(pw3) if ctx.needs_input_grad[2] else None
         t4 = grad_sink.accum_target(pw4) if ctx.needs_input_grad[3] else None
-        tb3 = grad_sink.accum_target(pb3) if ctx.needs_input_grad[4] else None
-        tb4 = grad_sink.accum_target(pb4) if ctx.needs_input_grad[5] else None
+        tb3 = grad_sink.accum_target(pb3) if ctx.needs_input_grad[4] and BIAS_SINK else None
+        tb4 = grad_sink.accum_target(pb4) if ctx.needs_input_grad[5] and BIAS_SINK else None
         dw3 = t3 if t3 is not None else torch.zeros_like(w3)
         dw4 = t4 if t4 is not None else torch.zeros_like(w4)
         db = None
