@@ -299,7 +299,15 @@ class Trainer:
                 grad_sink.mark_multi_use(loss, self.flat)
                 self._sink_scanned.add(key)
         range_push("backward")
-        loss.backward()
+        if loss.dim() == 0 and loss.is_cuda:
+            # a cached device 1.0 seeds the backward: no fill kernel per step for autograd's
+            # implicit ones_like(loss)
+            one = getattr(self, "_one", None)
+            if one is None or one.device != loss.device or one.dtype != loss.dtype:
+                one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+            torch.autograd.backward(loss, one)
+        else:
+            loss.backward()
         range_pop()
         if timer:
             timer.mark()
