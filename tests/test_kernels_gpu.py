@@ -100,11 +100,16 @@ def test_dtable_reduce_long_runs_match_reduce4(epw, variant):
     assert grads[0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("variant", [8204, 8236])
-@pytest.mark.parametrize("N,L", [(300, 45), (40, 2000), (7, 130)])
-def test_conv_forward_three_waves_per_simd_bit_identical(variant, N, L):
-    """The v6 conv forward (768-thread workgroups, three waves per SIMD; A/B arm) reproduces
-    the production v4 kernel bit for bit: pooled values and argmax windows."""
+@pytest.mark.parametrize("variant", [0, 16384 + 128 + 5])
+@pytest.mark.parametrize("N,L,p,mode", [(300, 45, 0.25, "element"), (40, 2000, 0.25, "element"), (7, 130, 0.25, "element"),
+                                        (9, 301, 0.0, "element"), (9, 301, 0.3, "element"), (9, 301, 0.25, "token")])
+def test_conv_forward_role_split_bit_identical(variant, N, L, p, mode):
+    """The production v7 conv forward (768-thread workgroups: 8 MFMA waves + 4 loader waves
+    that gather, mask and stage the next chunk) reproduces the v4 kernel (the previous
+    production, 8 waves that all stage) bit for bit: pooled values and argmax windows, in
+    every dropout mode (the A/B arm is built for p = 0.25 only)."""
+    if variant != 0 and (p != 0.25 or mode != "element"):
+        pytest.skip("A/B arm instantiated for the bench dropout mode only")
     torch.manual_seed(5)
     V, E, F = 500, 100, 150
     ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV)
@@ -115,10 +120,10 @@ def test_conv_forward_three_waves_per_simd_bit_identical(variant, N, L):
     lib = _lib()
     outs = []
     try:
-        for v in (0, variant):
+        for v in (4096, variant):
             lib.pv_conv_set_dbg(v)
             with torch.no_grad():
-                outs.append(cops.conv_relu_maxpool_fused(ids, table, [w3, w4], b, 0.25, 11, True))
+                outs.append(cops.conv_relu_maxpool_fused(ids, table, [w3, w4], b, p, 11, True, mode))
             torch.cuda.synchronize()
     finally:
         lib.pv_conv_set_dbg(0)
