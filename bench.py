@@ -48,8 +48,9 @@ MODEL_DESC = {
     "cdssm": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
     "mlp": "Two-tower MLP 512-512-128, 30k hashed tri-grams, Lq=45, Ld=2000, in-batch/cross-GPU negatives",
     "bert": "BERT-base dual encoder (12L/768H/12A, shared), Lq=32, Ld=256, cross-GPU negatives",
-    "cdssm_char": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), char level (reference default), ~100-symbol "
-                  "vocab, Lq=250, Ld=5000, J=3",
+    "cdssm_char": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), char level (reference run config), ~100-symbol "
+                  "vocab, Lq=250, Ld=5000, J=3; bf16 HIP kernels instead of the reference's fp32 (precision "
+                  "override)",
     "chunked": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, MLP 512-512-128 fp8 e4m3, mean-pool",
     "chunked_cdssm": "Long-page chunked encoder, 4096 tokens = 8x512 chunks, CDSSM conv tower per chunk (fused "
                      "conv kernel), mean-pool",

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import dataclasses
 import json
+import logging
 import os
 from dataclasses import dataclass, field, fields
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -129,6 +130,9 @@ class Configuration:
     skip_nonfinite: bool = True
     prefetch: int = 2                     # featurized batches the loader thread keeps ahead (pinned)
     num_workers: int = 0                  # featurizer threads per batch (C++ pool); 0 = min(16, CPUs)
+    # saved-config format: 2 = dtype 'fp32' selects the reference-precision PyTorch path (in
+    # version-1 files, written before the field existed, 'fp32' was the no-op default)
+    config_version: int = 2
 
     # --------------------------------------------------------------------------
     def __post_init__(self) -> None:
@@ -285,7 +289,16 @@ class Configuration:
     @classmethod
     def load_json(cls, path: str) -> "Configuration":
         with open(path) as f:
-            return cls.from_dict(json.load(f))
+            d = json.load(f)
+        if "config_version" not in d:  # version 1 (pre round 3): migrate the old no-op dtype default
+            if d.get("dtype") == "fp32":
+                logging.getLogger(__name__).warning(
+                    "%s: version-1 config with dtype='fp32' (the old default, which selected the HIP "
+                    "kernels) loaded as dtype='bf16'; set dtype='fp32' explicitly for the "
+                    "reference-precision PyTorch path", path)
+                d["dtype"] = "bf16"
+            d["config_version"] = 2
+        return cls.from_dict(d)
 
 
 # ---- presets: the reference run + the five BASELINE.json configs -------------

@@ -179,19 +179,38 @@ enum { PV_ERR_ID = 0, PV_ERR_LDS = 1, PV_ERR_SHAPE = 2, PV_ERR_KEY = 3, PV_ERR_A
 // ordered pass.  Partial sums inside a workgroup are already formed in a fixed order.
 namespace pv {
 constexpr float PV_FX_SCALE = 1099511627776.0f;  // 2^40
-// Only each ADDEND is clamped (to +-2^61, i.e. +-2^21 in value units); the int64 SUM of many
-// addends can still pass +-2^63 and wrap.  det_flush treats any total of magnitude >= 2^62
-// (+-2^22 in value units, far beyond a sane gradient) as an overflow and writes NaN into the
-// target, so the trainer's non-finite guard skips the step instead of applying a wrapped sum.
+constexpr float PV_FX_BIG = 2.3058430e18f;       // 2^61 (2^21 in value units): the addend clamp
+namespace {
+// Per translation unit: set by fx_add when an addend is not finite or had to be clamped to
+// +-2^21 in value units; det_flush then writes NaN into the whole target, so the trainer's
+// non-finite guard skips the step.  The flush also NaNs any element whose int64 total reached
+// +-2^62.  What stays undetected: a TOTAL that wrapped past +-2^23 in value units although
+// every addend was below 2^21 — far outside any gradient this mode sums.
+__device__ unsigned g_fx_flag = 0;
+__host__ inline unsigned* fx_flag_ptr() {
+  void* q = nullptr;
+  return hipGetSymbolAddress(&q, HIP_SYMBOL(g_fx_flag)) == hipSuccess ? (unsigned*)q : nullptr;
+}
+}  // namespace
 __device__ __forceinline__ void fx_add(long long* fx, size_t i, float v) {
-  const float x = fminf(fmaxf(v * PV_FX_SCALE, -2.3058430e18f), 2.3058430e18f);  // |addend| <= 2^61
+  const float s = v * PV_FX_SCALE;
+  if (!(fabsf(s) < PV_FX_BIG)) atomicOr(&g_fx_flag, 1u);
+  const float x = fminf(fmaxf(s, -PV_FX_BIG), PV_FX_BIG);
   atomicAdd(reinterpret_cast<unsigned long long*>(fx) + i, (unsigned long long)__float2ll_rn(x));
 }
 bool det_on();
-// n zeroed int64 accumulators, stream-ordered (one process-wide buffer: deterministic mode
-// runs every kernel of a step on one stream); nullptr on allocation failure
-long long* det_scratch(size_t n, hipStream_t st);
-int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st);  // dst += fx * 2^-40
+// n zeroed int64 accumulators (and this TU's fx_add flag cleared), stream-ordered (one
+// process-wide buffer: deterministic mode runs every kernel of a step on one stream); nullptr
+// on allocation failure
+long long* det_scratch_flag(size_t n, hipStream_t st, unsigned* flag);
+int det_flush_flag(const long long* fx, float* dst, size_t n, hipStream_t st, const unsigned* flag);
+namespace {
+__host__ inline long long* det_scratch(size_t n, hipStream_t st) { return det_scratch_flag(n, st, fx_flag_ptr()); }
+// dst += fx * 2^-40 (NaN where the total overflowed, everywhere when this TU's flag is set)
+__host__ inline int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st) {
+  return det_flush_flag(fx, dst, n, st, fx_flag_ptr());
+}
+}  // namespace
 }  // namespace pv
 
 #define PV_LAUNCH_CHECK() \

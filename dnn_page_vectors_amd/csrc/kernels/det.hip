@@ -13,13 +13,14 @@ long long* g_fx[kMaxDev] = {};  // one buffer per device (the current device at 
 size_t g_cap[kMaxDev] = {};
 
 __global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restrict__ fx, float* __restrict__ dst,
-                                                       long n) {
+                                                       long n, const unsigned* __restrict__ flag) {
   const long stride = (long)gridDim.x * blockDim.x;
+  const bool poisoned = flag != nullptr && *flag != 0u;  // an addend was clamped (common.h fx_add)
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const long long v = fx[i];
-    // |total| >= 2^62: the sum may have wrapped (fx_add clamps addends only) -> NaN, which
-    // the non-finite gradient guard turns into a skipped step
-    const bool overflow = v >= (1LL << 62) || v <= -(1LL << 62);
+    // |total| >= 2^62: the sum may have wrapped -> NaN, which the non-finite gradient guard
+    // turns into a skipped step
+    const bool overflow = poisoned || v >= (1LL << 62) || v <= -(1LL << 62);
     if (overflow) dst[i] = __builtin_nanf("");
     else if (v != 0) dst[i] += (float)((double)v * (1.0 / 1099511627776.0));
   }
@@ -28,7 +29,7 @@ __global__ __launch_bounds__(256) void fx_flush_kernel(const long long* __restri
 
 bool det_on() { return g_det != 0; }
 
-long long* det_scratch(size_t n, hipStream_t st) {
+long long* det_scratch_flag(size_t n, hipStream_t st, unsigned* flag) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
   if (n > g_cap[dev]) {
@@ -46,14 +47,15 @@ long long* det_scratch(size_t n, hipStream_t st) {
     g_cap[dev] = cap;
   }
   if (hipMemsetAsync(g_fx[dev], 0, n * sizeof(long long), st) != hipSuccess) return nullptr;
+  if (flag != nullptr && hipMemsetAsync(flag, 0, sizeof(unsigned), st) != hipSuccess) return nullptr;
   return g_fx[dev];
 }
 
-int det_flush(const long long* fx, float* dst, size_t n, hipStream_t st) {
+int det_flush_flag(const long long* fx, float* dst, size_t n, hipStream_t st, const unsigned* flag) {
   if (n == 0) return 0;
   long blocks = ((long)n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(fx_flush_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fx, dst, (long)n);
+  hipLaunchKernelGGL(fx_flush_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fx, dst, (long)n, flag);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -229,36 +229,41 @@ class InMemoryPairs:
         self.query_length, self.document_length = used(q), used(d)
         self.q = torch.from_numpy(np.ascontiguousarray(q[:, :self.query_length]))
         self.d = torch.from_numpy(np.ascontiguousarray(d[:, :, :self.document_length]))
-        self.n_val = int(round(n * validation_split))
-        self.n_train = n - self.n_val
+        # Keras fit(validation_split=s): split_at = int(n * (1 - s)); rows [split_at, n) validate
+        self.n_train = int(n * (1.0 - validation_split))
+        self.n_val = n - self.n_train
 
     def __len__(self) -> int:
         return self.n_train + self.n_val
 
     def train_loader(self, batch_size: int, shuffle: bool = True, seed: int = 1337,
-                     device: Optional[torch.device] = None, rank: int = 0, world_size: int = 1) -> "_TensorLoader":
+                     device: Optional[torch.device] = None, rank: int = 0, world_size: int = 1,
+                     drop_last: bool = False) -> "_TensorLoader":
+        """Keras fit semantics: the last partial batch is trained on (``drop_last=False``)."""
         return _TensorLoader(self.q[:self.n_train], self.d[:self.n_train], batch_size, shuffle, seed, device, rank,
-                             world_size)
+                             world_size, drop_last)
 
     def val_loader(self, batch_size: int, device: Optional[torch.device] = None, rank: int = 0,
-                   world_size: int = 1) -> "_TensorLoader":
+                   world_size: int = 1, drop_last: bool = False) -> "_TensorLoader":
         return _TensorLoader(self.q[self.n_train:], self.d[self.n_train:], batch_size, False, 0, device, rank,
-                             world_size)
+                             world_size, drop_last)
 
 
 class _TensorLoader:
     """Batches of in-memory (q, d) tensors; per-epoch seeded shuffle; rank shard; cursor."""
 
     def __init__(self, q: torch.Tensor, d: torch.Tensor, batch_size: int, shuffle: bool, seed: int,
-                 device: Optional[torch.device], rank: int, world_size: int):
+                 device: Optional[torch.device], rank: int, world_size: int, drop_last: bool = False):
         self.q, self.d, self.B = q, d, int(batch_size)
+        self.drop_last = bool(drop_last)
         self.shuffle, self.seed, self.device = shuffle, seed, device
         self.rank, self.world = rank, world_size
         self.epoch = 0
         self.cursor = 0
 
     def num_batches(self) -> int:
-        return (self.q.shape[0] // self.world) // self.B
+        per = self.q.shape[0] // self.world  # every rank gets the same number of rows
+        return per // self.B if self.drop_last else (per + self.B - 1) // self.B
 
     def state(self) -> dict:
         return {"epoch": self.epoch, "cursor": self.cursor}

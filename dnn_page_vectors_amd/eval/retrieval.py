@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import topk as tops
+from ..parallel.dist import active as pdist_active
 
 
 def topk_cosine(qn: torch.Tensor, pn: torch.Tensor, k: int = 10, block: int = 65536) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -64,7 +65,7 @@ def distributed_recall_table(qn: torch.Tensor, pn: torch.Tensor, relevant: torch
     (relevant index shifted by the rank's page offset), and the hit counts are summed over
     ranks — the same numbers a single process would get with every rank's queries and pages
     concatenated in rank order.  Single process: ``recall_table``."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not pdist_active():
         return recall_table(qn, pn, relevant, ks)
     rank = dist.get_rank()
     allp, ns = _gather_rows(pn)
@@ -103,7 +104,7 @@ def evaluate_pairs_dataset(model, dataset, device: torch.device, ks: Sequence[in
     (host work) so all ranks agree on the distinct-page numbering, encodes its contiguous
     shard of the queries and of the distinct pages, all-gathers the page vectors
      and the hit counts are summed: the result equals the single-process one."""
-    distributed = dist.is_initialized() and dist.get_world_size() > 1
+    distributed = pdist_active()
     rank, W = (dist.get_rank(), dist.get_world_size()) if distributed else (0, 1)
     n = len(dataset)
     if max_rows:

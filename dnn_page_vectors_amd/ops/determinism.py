@@ -28,10 +28,12 @@ from __future__ import annotations
 from .. import _native
 
 _ON = [False]
+_TORCH_PREV = [None]  # torch's deterministic-algorithm flags before this module switched them on
 
 
 def set_deterministic(on: bool = True):
-    """Switch the mode; returns the previous state (for ``restore``)."""
+    """Switch the mode; returns the previous state (for ``restore``).  Switching it off also
+    gives torch's deterministic-algorithm flags back the values they had before it was on."""
     import torch
     import torch.utils.deterministic as _tud
 
@@ -44,8 +46,15 @@ def set_deterministic(on: bool = True):
     # their deterministic implementations; uninitialised memory is NOT NaN-filled (every
     # kernel output is fully written; padded operands are allocated zeroed)
     if on:
+        if _TORCH_PREV[0] is None:
+            _TORCH_PREV[0] = prev[1:]
         torch.use_deterministic_algorithms(True, warn_only=True)
         _tud.fill_uninitialized_memory = False
+    elif _TORCH_PREV[0] is not None:
+        algos, warn_only, fill = _TORCH_PREV[0]
+        _TORCH_PREV[0] = None
+        torch.use_deterministic_algorithms(algos, warn_only=warn_only)
+        _tud.fill_uninitialized_memory = fill
     lib = _native.hip(required=False)
     if lib is not None:
         lib.pv_set_deterministic(1 if on else 0)
@@ -59,6 +68,8 @@ def restore(prev) -> None:
 
     on, algos, warn_only, fill = prev
     _ON[0] = bool(on)
+    if not on:
+        _TORCH_PREV[0] = None
     if torch.cuda.is_available():
         torch.use_deterministic_algorithms(algos, warn_only=warn_only)
         _tud.fill_uninitialized_memory = fill
@@ -69,3 +80,11 @@ def restore(prev) -> None:
 
 def enabled() -> bool:
     return _ON[0]
+
+
+def ensure(on: bool) -> None:
+    """Put the process-wide mode in state ``on`` if it is not (a Trainer calls this before
+    every step, so trainers with different settings in one process each run in their own
+    mode whatever order they were built or stepped in)."""
+    if _ON[0] != bool(on):
+        set_deterministic(on)

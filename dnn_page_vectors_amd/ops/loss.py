@@ -278,7 +278,8 @@ class PageGather:
 
 def start_page_gather(dn: torch.Tensor, group=None) -> Optional[PageGather]:
     """Begin the cross-GPU page-vector gather early (None when it does not apply)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1 or not use_hip(dn) or dn.shape[1] > 192:
+    from ..parallel.dist import active
+    if not active(group) or not use_hip(dn) or dn.shape[1] > 192:
         return None
     return PageGather(dn, group)
 
@@ -377,7 +378,8 @@ def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, 
     -> (per-row loss, P+); ``reduce``: (mean loss, P+, accuracy), the mean and metric
     computed in the loss kernels' epilogue (no separate reductions)."""
     _check_gamma(gamma, clip)
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    from ..parallel.dist import active
+    if not active(group):
         return inbatch_loss(qn, dn, pos_local, gamma, clip, reduce=reduce)
     if use_hip(qn, dn) and qn.shape[1] <= 192:
         if gathered is not None and gathered.source is not dn:

@@ -33,6 +33,7 @@ import torch.distributed as dist
 
 from ..ops import grad_sink
 from ..ops.optim import FlatParams
+from .dist import active
 
 
 class GradBuckets:
@@ -43,10 +44,11 @@ class GradBuckets:
         """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients)."""
         self.flat = flat
         self.world = dist.get_world_size() if dist.is_initialized() else 1
-        self.overlap = overlap and self.world > 1
+        self.active = active()  # world > 1, or the forced one-rank rehearsal (PAGEVEC_FORCE_DIST)
+        self.overlap = overlap and self.active
         self.sum_only = reduce == "sum"
         self.avg_op = None
-        if self.world > 1 and not self.sum_only:
+        if self.active and not self.sum_only:
             self.avg_op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else None
         cap = max(1, int(bucket_mb * (1 << 20) / 4))
         self.buckets: List[List[int]] = []  # [lo, hi, n_params]
@@ -130,7 +132,7 @@ class GradBuckets:
 
     def finish(self) -> None:
         """Launch the buckets that never completed (unused params) and wait for all."""
-        if self.world == 1:
+        if not self.active:
             return
         for bi in range(len(self.buckets)):
             if self.handles[bi] is None:
@@ -154,5 +156,5 @@ class _Remover:
 
 
 def broadcast_params(flat: FlatParams, src: int = 0) -> None:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if active():
         dist.broadcast(flat.data, src)

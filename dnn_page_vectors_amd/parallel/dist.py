@@ -8,7 +8,13 @@ One process per GPU; ``backend="nccl"`` is RCCL on ROCm.  CPU tests use ``gloo``
   peer surfaces as an error instead of a silent hang.
 * ``all_gather_autograd(x)``: forward all-gather of page vectors (cross-GPU in-batch
   negatives); backward = reduce-scatter(sum) of the gathered gradient
-  back to the owning rank — every rank's loss depends on every rank's documents.
+  back to the owning rank.  This generic form serves the torch / wide-vector paths; the
+  HIP cross-GPU loss (ops/loss.py) instead gathers the queries and scores its LOCAL pages
+  against all of them in the backward, so no gradient is reduce-scattered there.
+* ``active()``: whether collectives run.  ``PAGEVEC_FORCE_DIST=1`` initialises the process
+  group and runs every collective code path even at world size 1 — how the RCCL paths
+  (early page gather, async query / scale gathers, bucketed ``ReduceOp.AVG`` all-reduce,
+  eager ``device_id`` init) are exercised on a one-GPU box (tests/test_rccl_gpu.py).
 
 The reference has no collectives at all; its only multi-device code is manual tower
 placement (dssm_cnn_v2/cnn_dssm_tf.py:139-158), reproduced as ``parallel/placement.py``.
@@ -31,6 +37,7 @@ class DistInfo:
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    forced: bool = False  # PAGEVEC_FORCE_DIST: collective code paths on at world size 1
 
     @property
     def is_main(self) -> bool:
@@ -38,7 +45,17 @@ class DistInfo:
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.forced
+
+
+def force_requested() -> bool:
+    return os.environ.get("PAGEVEC_FORCE_DIST", "0") == "1"
+
+
+def active(group=None) -> bool:
+    """True when the collective code paths run: an initialised process group with more than
+    one rank, or any size under PAGEVEC_FORCE_DIST=1."""
+    return dist.is_initialized() and (dist.get_world_size(group) > 1 or _INFO.forced)
 
 
 _INFO = DistInfo()
@@ -63,7 +80,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    forced = force_requested()
+    if (world > 1 or forced) and not dist.is_initialized():
         # PAGEVEC_DIST_BACKEND=gloo rehearses several ranks on one GPU (RCCL refuses duplicate devices)
         be = backend or os.environ.get("PAGEVEC_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -73,9 +91,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
             kw["device_id"] = dev
         dist.init_process_group(be, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-        _INFO = DistInfo(rank, world, local, be, dev)
+        _INFO = DistInfo(rank, world, local, be, dev, forced)
     elif dist.is_initialized():
-        _INFO = DistInfo(dist.get_rank(), dist.get_world_size(), local, dist.get_backend(), dev)
+        _INFO = DistInfo(dist.get_rank(), dist.get_world_size(), local, dist.get_backend(), dev, forced)
     else:
         _INFO = DistInfo(0, 1, 0, "none", dev)
     return _INFO
@@ -115,25 +133,25 @@ class _AllGather(torch.autograd.Function):
 
 
 def all_gather_autograd(x: torch.Tensor) -> torch.Tensor:
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not active():
         return x
     return _AllGather.apply(x)
 
 
 def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if active():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t.div_(dist.get_world_size())
     return t
 
 
 def all_reduce_max_(t: torch.Tensor) -> torch.Tensor:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if active():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if active():
         dist.broadcast(t, src)
     return t

@@ -22,6 +22,7 @@ import logging
 import math
 import os
 import time
+import weakref
 from typing import Callable, Dict, Iterable, Iterator, List, Optional, Tuple
 
 import torch
@@ -40,6 +41,11 @@ from ..utils.metrics import MetricsLogger, hbm_used_gb
 from ..utils.tracing import range_push, range_pop
 
 log = logging.getLogger(__name__)
+
+
+def _restore_det(prev) -> None:
+    """Give the process-wide deterministic mode back as it was before a trainer switched it on."""
+    determinism.restore(prev)
 
 
 class InjectedFault(RuntimeError):
@@ -121,11 +127,16 @@ class Trainer:
         # deterministic reduction mode (ops/determinism.py) is process-wide: it follows the
         # latest Trainer's config; its fixed-point buffer may grow between steps, so no capture
         self.deterministic = bool(getattr(cfg, "deterministic", False))
-        # only a deterministic config touches the process-wide mode (torch's deterministic-
-        # algorithm flags are left as the user set them otherwise); Trainer.close() restores it
+        # the mode is process-wide: every step of this trainer first puts it in this trainer's
+        # state (determinism.ensure), so a deterministic trainer built earlier in the process
+        # cannot leak its mode (or its one-stream, no-graph rule) into this one; close() or a
+        # finalizer gives the mode back as it was before a deterministic trainer switched it on
         self._det_prev = None
         if self.deterministic:
             self._det_prev = determinism.set_deterministic(True)
+            weakref.finalize(self, _restore_det, self._det_prev)
+        else:
+            determinism.ensure(False)
         self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
                            and not self.deterministic)
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
@@ -144,7 +155,7 @@ class Trainer:
     def close(self) -> None:
         """Restore the process-wide deterministic mode this trainer switched on (if any)."""
         if self._det_prev is not None:
-            determinism.restore(self._det_prev)
+            _restore_det(self._det_prev)
             self._det_prev = None
 
     # ------------------------------------------------------------------ core step
@@ -229,6 +240,7 @@ class Trainer:
     def train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
         if self.step == self._fault_step:
             raise InjectedFault(f"injected fault at step {self.step}")
+        determinism.ensure(self.deterministic)
         if self.graph_mode:
             key = (tuple(q_ids.shape), tuple(d_ids.shape), q_ids.dtype, d_ids.dtype)
             if self._graph is not None and key == self._graph_key:

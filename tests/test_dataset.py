@@ -97,3 +97,42 @@ def test_in_memory_pairs_v1_semantics(tmp_path):
     assert sorted(map(tuple, e0.tolist())) == sorted(map(tuple, e1.tolist()))
     vq = torch.cat([q for q, _ in mem.val_loader(5).epoch_iter()])
     np.testing.assert_array_equal(vq.numpy(), mem.q[15:].numpy())    # the last 25% in file order
+
+
+def test_in_memory_split_and_partial_batch_follow_keras(tmp_path):
+    """Keras fit(validation_split=s): split_at = int(n * (1 - s)) (n = 7, s = 0.2 -> 5 train, 2
+    validation rows), and the last partial batch is trained on."""
+    import json
+
+    from dnn_page_vectors_amd.data.dataset import InMemoryPairs
+    from dnn_page_vectors_amd.data.featurize import Featurizer
+
+    rows = [{"q": f"q{i}", "doc_corr": f"d{i}", "doc_incorr": ["x", "y", "z"]} for i in range(7)]
+    p = tmp_path / "k.jsonl"
+    p.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    mem = InMemoryPairs(str(p), Featurizer("word", hash_size=97), 8, 8, 3, validation_split=0.2)
+    assert (mem.n_train, mem.n_val) == (5, 2)
+    tl = mem.train_loader(2, shuffle=False)
+    sizes = [q.shape[0] for q, _ in tl.epoch_iter()]
+    assert sizes == [2, 2, 1] and tl.num_batches() == 3
+    assert mem.train_loader(2, shuffle=False, drop_last=True).num_batches() == 2
+
+
+def test_legacy_config_json_migrates_fp32_default(tmp_path, caplog):
+    """a config saved before config_version existed carries dtype='fp32' (the old
+    no-op default); loading it keeps the HIP path (bf16) and warns, a current file keeps fp32."""
+    import json
+
+    from dnn_page_vectors_amd.config import Configuration
+
+    d = Configuration().to_dict()
+    d.pop("config_version")
+    d["dtype"] = "fp32"
+    old = tmp_path / "old.json"
+    old.write_text(json.dumps(d))
+    c = Configuration.load_json(str(old))
+    assert c.dtype == "bf16" and c.config_version == 2
+    assert any("version-1" in r.message for r in caplog.records)
+    new = tmp_path / "new.json"
+    Configuration(dtype="fp32").save_json(str(new))
+    assert Configuration.load_json(str(new)).dtype == "fp32"

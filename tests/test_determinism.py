@@ -127,3 +127,54 @@ def test_gpu_deterministic_mode_other_models(preset):
         assert torch.equal(runs[0][1], runs[1][1])
     finally:
         determinism.set_deterministic(False)
+
+
+def test_trainers_do_not_leak_the_deterministic_mode():
+    """a deterministic trainer built first must not leave a later default trainer
+    (which may capture hipGraphs and use side streams) in the deterministic mode; each
+    trainer's step runs in its own mode, and closing the deterministic one restores the
+    previous state."""
+    from dnn_page_vectors_amd.ops import determinism
+    dev = "cpu"
+    try:
+        a, _ = _run_det(dev, True, steps=1)
+        assert determinism.enabled()
+        b, _ = _run_det(dev, False, steps=1)
+        assert not determinism.enabled()
+        g = torch.Generator().manual_seed(9)
+        q = torch.randint(1, 300, (16, 12), generator=g, dtype=torch.int32)
+        d = torch.randint(1, 300, (16, 4, 40), generator=g, dtype=torch.int32)
+        a.train_step(q, d)
+        assert determinism.enabled()
+        b.train_step(q, d)
+        assert not determinism.enabled()
+        a.train_step(q, d)
+        a.close()
+        assert not determinism.enabled()
+    finally:
+        determinism.set_deterministic(False)
+
+
+@pytest.mark.gpu
+def test_graph_trainer_after_deterministic_trainer_gpu():
+    """A graph-mode trainer built after a deterministic one captures its step with the
+    deterministic mode OFF (no fixed-point buffer growth inside a capture)."""
+    from dnn_page_vectors_amd.ops import determinism
+    try:
+        a, _ = _run_det("cuda", True, steps=1)
+        torch.manual_seed(0)
+        cfg = _cfg().replace(document_length=40, dropout_prob=(0.25, 0.5))
+        b = Trainer(cfg, CDSSM(cfg, 300), torch.device("cuda"), graph=True)
+        assert b.graph_mode
+        g = torch.Generator().manual_seed(5)
+        for _ in range(Trainer.GRAPH_WARMUP + 3):
+            q = torch.randint(1, 300, (16, 12), generator=g, dtype=torch.int32).cuda()
+            d = torch.randint(1, 300, (16, 4, 40), generator=g, dtype=torch.int32).cuda()
+            m = b.train_step(q, d)
+            assert not determinism.enabled()
+        torch.cuda.synchronize()
+        assert b._graph is not None and float(m["loss"]) == float(m["loss"])
+        a.train_step(q, d)  # the deterministic trainer still runs in its own mode
+        assert determinism.enabled()
+    finally:
+        determinism.set_deterministic(False)

@@ -75,14 +75,13 @@ def _data(B):
     return out
 
 
-def _dp_worker(rank, world, port, mode, q):
+def _dp_worker(rank, world, port, mode, q, B=8):
     _env(rank, world, port)
     from dnn_page_vectors_amd.models.cdssm import CDSSM
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
     pdist.init_distributed(device="cpu")
-    B = 8
     cfg = _cfg(mode, B // world)
     tr = Trainer(cfg, CDSSM(cfg, 150))
     assert len(tr.buckets.buckets) > 1  # several buckets, launched from grad hooks
@@ -93,24 +92,25 @@ def _dp_worker(rank, world, port, mode, q):
     pdist.destroy()
 
 
-@pytest.mark.parametrize("mode,world", [("explicit", 2), ("cross_gpu", 2), ("cross_gpu", 4)])
+@pytest.mark.parametrize("mode,world", [("explicit", 2), ("cross_gpu", 2), ("cross_gpu", 4), ("cross_gpu", 8)])
 def test_data_parallel_matches_single_process(mode, world):
     from dnn_page_vectors_amd.models.cdssm import CDSSM
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
+    B = 16 if world == 8 else 8  # two queries per rank at W = 8 (the driver's node size)
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dp_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    ps = [ctx.Process(target=_dp_worker, args=(r, world, port, mode, q, B)) for r in range(world)]
     [p.start() for p in ps]
     res = {r: torch.from_numpy(v) for r, v in (q.get(timeout=300) for _ in ps)}
     [p.join(timeout=60) for p in ps]
     # single process reference (cross_gpu with one rank == in-batch over the whole batch)
     pdist.set_info(pdist.DistInfo())
-    cfg = _cfg("in_batch" if mode == "cross_gpu" else mode, 8)
+    cfg = _cfg("in_batch" if mode == "cross_gpu" else mode, B)
     tr = Trainer(cfg, CDSSM(cfg, 150))
-    for qa, da in _data(8):
+    for qa, da in _data(B):
         tr.train_step(qa, da)
     for r in range(1, world):
         torch.testing.assert_close(res[0], res[r], rtol=0, atol=0)

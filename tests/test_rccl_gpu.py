@@ -1,0 +1,136 @@
+"""RCCL on the GPU box: a world-size-1 ``nccl`` (= RCCL) process group with every collective
+code path forced on (``PAGEVEC_FORCE_DIST=1``, parallel/dist.py).
+
+The driver's 8-GPU node is the only place several ranks meet; this test makes sure the RCCL
+branches that only exist for W > 1 are executed on the one-GPU box before that:
+
+* eager ``device_id`` process-group init with backend ``nccl``;
+* the page-vector all-gather started right after the doc tower (``PageGather``, async);
+* the cross-GPU loss (``_CrossGpuFn``): async query / softmax-scale all-gathers, the
+  local-pages-vs-all-queries dD backward;
+* the bucketed, backward-overlapped gradient all-reduce with ``ReduceOp.AVG``.
+
+A fresh child process (spawned, never exec'd) runs one CDSSM and one MLP ``cross_gpu``
+training step through those paths, then the same step with the collectives off (same
+initial weights, same batch, same dropout seeds) and compares the loss and the flat
+gradient.  Reference: the only cross-device data flow of the reference is the tower
+placement of dssm_cnn_v2/cnn_dssm_tf.py:139-158.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(model):
+    from dnn_page_vectors_amd.config import preset_config
+
+    if model == "cdssm":
+        return preset_config("cdssm_ngram_bf16").replace(batch_size=64, document_length=256, grad_bucket_mb=1.0)
+    return preset_config("mlp_xgpu").replace(batch_size=64, document_length=256, grad_bucket_mb=8.0)
+
+
+def _one_step(cfg, dev, q, d):
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    torch.manual_seed(1234)
+    tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), dev, graph=False)
+    m = tr.train_step(q, d)
+    torch.cuda.synchronize()
+    return float(m["loss"]), tr.flat.grad.detach().clone(), tr
+
+
+def _worker(port, models, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      PAGEVEC_FORCE_DIST="1")
+    os.environ.pop("PAGEVEC_DIST_BACKEND", None)
+    try:
+        import torch.distributed as dist
+
+        from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+        from dnn_page_vectors_amd.ops import loss as lops
+        from dnn_page_vectors_amd.parallel import dist as pdist
+
+        info = pdist.init_distributed()
+        assert info.backend == "nccl" and info.enabled and pdist.active(), info
+        dev = info.device
+        calls = {"all_gather_into_tensor": 0, "all_reduce": 0, "page_gather": 0, "cross_gpu_fn": 0}
+        for name in ("all_gather_into_tensor", "all_reduce"):
+            orig = getattr(dist, name)
+
+            def wrapped(*a, _o=orig, _n=name, **k):
+                calls[_n] += 1
+                return _o(*a, **k)
+            setattr(dist, name, wrapped)
+        orig_pg = lops.PageGather.__init__
+
+        def pg_init(self, *a, **k):
+            calls["page_gather"] += 1
+            orig_pg(self, *a, **k)
+        lops.PageGather.__init__ = pg_init
+        orig_fn = lops._CrossGpuFn.forward
+
+        def fn_fwd(*a, **k):
+            calls["cross_gpu_fn"] += 1
+            return orig_fn(*a, **k)
+        lops._CrossGpuFn.forward = staticmethod(fn_fwd)
+        res = {}
+        for model in models:
+            cfg = _cfg(model)
+            data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=512), dev, seed=7)
+            q, d = data.batch(cfg.batch_size)
+            before = dict(calls)
+            loss_d, grad_d, trd = _one_step(cfg, dev, q, d)
+            assert trd.buckets is not None and trd.buckets.avg_op == dist.ReduceOp.AVG
+            used = {k: calls[k] - before[k] for k in calls}
+            # the same step with the collectives off (process group still up, not used)
+            pdist.set_info(pdist.DistInfo(device=dev))
+            assert not pdist.active()
+            before = dict(calls)
+            loss_s, grad_s, trs = _one_step(cfg, dev, q, d)
+            assert trs.buckets is None
+            idle = {k: calls[k] - before[k] for k in calls}
+            pdist.set_info(info)
+            rel = float((grad_d - grad_s).abs().max() / grad_s.abs().max())
+            res[model] = dict(loss_d=loss_d, loss_s=loss_s, grad_rel=rel, used=used, idle=idle,
+                              nbuckets=len(trd.buckets.buckets))
+        out.put(("ok", res))
+        pdist.destroy()
+    except Exception as e:  # surface the failure in the parent
+        import traceback
+
+        out.put(("err", repr(e) + "\n" + traceback.format_exc()))
+
+
+def test_rccl_world1_forced_collectives_match_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), ("cdssm", "mlp"), q))
+    p.start()
+    status, res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert status == "ok", res
+    for model, r in res.items():
+        print(model, r)
+        u, i = r["used"], r["idle"]
+        # every RCCL path ran in the distributed step: page gather + query / scale gathers,
+        # one all-reduce per gradient bucket; none of them in the collectives-off step
+        assert u["page_gather"] == 1 and u["cross_gpu_fn"] == 1, r
+        assert u["all_gather_into_tensor"] >= 3, r
+        assert u["all_reduce"] >= r["nbuckets"] >= 2, r
+        assert i["all_gather_into_tensor"] == 0 and i["page_gather"] == 0 and i["cross_gpu_fn"] == 0, r
+        assert abs(r["loss_d"] - r["loss_s"]) <= 2e-3 * max(1.0, abs(r["loss_s"])), r
+        assert r["grad_rel"] < 2e-2, r
