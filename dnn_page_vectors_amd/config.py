@@ -115,6 +115,10 @@ class Configuration:
     beta2: float = 0.999
     adam_eps: float = 1e-8
     lazy_embedding_adam: bool = False    # Adam skips embedding rows with an all-zero gradient (large vocabularies)
+    # row-sparse embedding gradients (parallel/sparse_rows.py): only the touched rows are zeroed,
+    # exchanged between data-parallel ranks (all-gather of ids + rows, not a dense all-reduce)
+    # and updated (LazyAdam) — for million-row word vocabularies
+    sparse_embedding_grad: bool = False
     optimizer_bf16_mirror: bool = True   # the Adam kernel also writes the bf16 compute copies of big weights
     # compute precision (ops/_common.py::precision_scope): bf16 = the HIP kernels (bf16 MFMA
     # operands, fp32 accumulation / master weights); fp32 = the reference's precision through

@@ -1072,6 +1072,24 @@ PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals
   return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
 }
 
+// Records only (the keys were written by the conv forward's epilogue, conv_pool_fwd.hip
+// emit_keys): rec[pair] = {g * scale, argmax}, one coalesced pass.
+__global__ __launch_bounds__(256) void conv_bwd_rec_kernel(const float* __restrict__ gpool,
+                                                           const int* __restrict__ argmax, int2* __restrict__ rec,
+                                                           long pairs, float scale) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < pairs) rec[i] = int2{__float_as_int(gpool[i] * scale), argmax[i]};
+}
+
+PV_API int pv_conv_pool_bwd_rec(const float* gpool, const int* argmax, void* rec, int N, float scale, void* stream) {
+  using namespace pv::convbwd;
+  const long pairs = (long)N * 2 * FW;
+  hipLaunchKernelGGL(conv_bwd_rec_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     gpool, argmax, (int2*)rec, pairs, scale);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
 // 2-byte-key variants (V < 65535): emit -> pv_sort_iota_u16 -> reduce
 PV_API int pv_conv_pool_bwd_emit3_u16(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                                       void* keys, void* rec, int N, int L, int V, float scale, void* stream) {

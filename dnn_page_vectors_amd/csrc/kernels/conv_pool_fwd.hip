@@ -73,7 +73,32 @@ struct Params {
   float scale;                 // 1/(1-p)
   const unsigned* seed_ptr;    // optional device seed offset (added to seed; captured hipGraph steps)
   const float* bias4;          // (FW) k=4 filters' bias; bias holds the k=3 filters' (FW)
+  void* keys;                  // optional dTable sort keys (conv_pool_bwd.hip slot layout), or null
+  int key_bytes;               // 2 (V < 65535) or 4
 };
+
+// The dTable emit fused into the conv forward (v7 loader waves, one sample behind the MFMA
+// waves): filter f of sample n (its argmax window at a, post-ReLU output y) owns slots
+// n*SPS + {3f | 3*FW + 4(f-FW)} + j, j < k; each slot's key is the token at window row j, or
+// the dead sentinel V when y <= 0 (zero gradient).  Same layout as conv_pool_bwd.hip's emit
+// kernel, which this replaces for the page / query towers.
+constexpr int SPS = 7 * FW;  // slots per sample (3 per k=3 filter, 4 per k=4 filter)
+__device__ __forceinline__ void emit_keys(const Params& p, int n, int f, int a, bool live) {
+  const int K = f < FW ? 3 : 4;
+  const size_t s0 = (size_t)n * SPS + (f < FW ? 3 * f : 3 * FW + 4 * (f - FW));
+  const int* row = p.ids + (size_t)n * p.L + a;
+  int tok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tok[j] = (j < K && live) ? row[j] : p.V;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < K) {
+      const unsigned v = (unsigned)tok[j] < (unsigned)p.V ? (unsigned)tok[j] : (unsigned)p.V;
+      if (p.key_bytes == 2) static_cast<unsigned short*>(p.keys)[s0 + j] = (unsigned short)v;
+      else static_cast<unsigned*>(p.keys)[s0 + j] = v;
+    }
+  }
+}
 
 // Diagnostic ablations are COMPILE-TIME (template DBG; production instantiation DBG = 0
 // carries no branches): 1 no gather, 2 max-only epilogue, 4 no dropout hash,
@@ -518,6 +543,16 @@ __device__ __forceinline__ void loader7_stage(const Params& p, int lt, const int
   }
 }
 
+// loader lane lt emits the dTable keys of filters lt and lt + 256 of sample n (whose pooled /
+// argmax rows another wave of this workgroup stored before the barrier the loader passed)
+__device__ __forceinline__ void loader7_emit(const Params& p, int lt, int n) {
+#pragma unroll
+  for (int f = lt; f < 2 * FW; f += NLD7) {
+    const size_t o = (size_t)n * (2 * FW) + f;
+    emit_keys(p, n, f, p.argmax[o], p.pooled[o] > 0.f);
+  }
+}
+
 template <int DM, int RR>
 __device__ __forceinline__ void loader7(const Params& p, char* xl0, int* ids_lds) {
   constexpr int CROWS = cr_of<RR>(), LPPT = lppt_of<RR>(), R = RR;
@@ -542,6 +577,7 @@ __device__ __forceinline__ void loader7(const Params& p, char* xl0, int* ids_lds
   u32x4 v[LPPT];
   loader7_stage<DM, RR>(p, lt, ids_lds, hs, xl0, v);
   int par = 0;  // parity of cur: its LDS buffer and its id / hash slot
+  int done_n = -1;  // a sample whose pooled / argmax the MFMA waves wrote before the last barrier
   while (cur.n < p.N) {
     __syncthreads();  // B_k: buffer par holds chunk k, slot par^1 chunk k+1's ids
     if (c1.n < p.N) {
@@ -554,11 +590,15 @@ __device__ __forceinline__ void loader7(const Params& p, char* xl0, int* ids_lds
         hs[par * CROWS + lt] = row_hash7<DM, RR>(p, c2, lt);
       }
     }
+    if (p.keys && done_n >= 0) loader7_emit(p, lt, done_n);
+    done_n = cur.c == cur.nchunks - 1 ? cur.n : -1;  // finished by the MFMA waves in iteration k
     cur = c1;
     c1 = c2;
     advance(c2);
     par ^= 1;
   }
+  __syncthreads();  // B_end: the last sample's outputs are written
+  if (p.keys && done_n >= 0) loader7_emit(p, lt, done_n);
 }
 
 // MFMA role: v4's K-loop, running max / argmax and sample epilogue, reading chunk k from
@@ -699,6 +739,7 @@ __device__ __forceinline__ void mfma7(const Params& p, int t3base, int t4base, c
     advance(cur);
     par ^= 1;
   }
+  __syncthreads();  // B_end (the loaders emit the last sample's keys after it)
 }
 
 // OPT: 1 = s_setprio 1 for MFMA waves 4-7, 4 = tag mask in a VGPR
@@ -813,18 +854,22 @@ PV_API int pv_conv_packed_size() {
 // Diagnostic ablation switch (tools/conv_micro.py): 0 in production.
 static int g_conv_dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
 PV_API void pv_conv_set_dbg(int d) { g_conv_dbg = d; }
+PV_API int pv_conv_get_dbg() { return g_conv_dbg; }
 
 // bias3 / bias4: the two widths' biases (FW floats each, e.g. the parameters themselves)
 PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpack, const float* bias3,
                              const float* bias4, float* pooled, int* argmax, int N, int L, int V, unsigned seed,
                              const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode, float scale,
-                             int grid, void* stream) {
+                             int grid, void* stream, void* keys, int key_bytes) {
   using namespace pv::convpool;
   if (L < 4 || N <= 0) return -1;
-  if ((L - 2 + 15) / 16 > 1024) return -2;  // tagged argmax: block index must fit TAGB bits
   const int dbg = g_conv_dbg;
+  if (keys && key_bytes != 2 && key_bytes != 4) return -4;
+  if (keys && dbg != 0 && dbg < 16384) return -6;  // the key emit lives in the v7 loader waves
+  if (keys && key_bytes == 2 && V >= 65535) return -5;
+  if ((L - 2 + 15) / 16 > 1024) return -2;  // tagged argmax: block index must fit TAGB bits
   Params p{ids, (const unsigned short*)table, (const bf16x8*)wpack, bias3, pooled, argmax, N, L, V,
-           seed, row_offset, thr, token_mode, scale, seed_ptr, bias4};
+           seed, row_offset, thr, token_mode, scale, seed_ptr, bias4, keys, key_bytes};
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
   hipStream_t st = (hipStream_t)stream;
@@ -863,5 +908,5 @@ PV_API int pv_conv_pool_fwd(const int* ids, const void* table, const void* wpack
                             float* pooled, int* argmax, int N, int L, int V, unsigned seed, const unsigned* seed_ptr,
                             unsigned row_offset, int thr, int token_mode, float scale, int grid, void* stream) {
   return pv_conv_pool_fwd2(ids, table, wpack, bias, bias + pv::convpool::FW, pooled, argmax, N, L, V, seed, seed_ptr,
-                           row_offset, thr, token_mode, scale, grid, stream);
+                           row_offset, thr, token_mode, scale, grid, stream, nullptr, 0);
 }

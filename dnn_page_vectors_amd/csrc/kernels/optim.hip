@@ -108,7 +108,11 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
                                                              float wd, int torch_style,
                                                              const float* __restrict__ skip,
                                                              const float* __restrict__ tdev,
-                                                             unsigned short* __restrict__ p16) {
+                                                             unsigned short* __restrict__ p16,
+                                                             const int* __restrict__ rowlist) {
+  // rowlist (optional): `rows` entries naming the candidate rows (< 0: none), e.g. the rows a
+  // sparse-gradient table touched this step (parallel/sparse_rows.py); the all-zero test
+  // still applies to each listed row
   constexpr int NJ = LPR == 64 ? 4 : 1;  // column groups per lane
   constexpr int RPW = 64 / LPR;          // rows per wave and trip
   if (skip && *skip != 0.f) return;
@@ -124,23 +128,26 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
   for (long r0 = wave0 * 2 * RPW; r0 < rows; r0 += nwaves * 2 * RPW) {
     f32x4 gg[2][NJ];
     bool live[2];
+    long rr[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const long r = r0 + h * RPW + sub;
+      const long i = r0 + h * RPW + sub;
+      const long r = i >= rows ? -1 : rowlist ? (long)rowlist[i] : i;
+      rr[h] = r;
       bool nz = false;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = 4 * ln + 4 * LPR * j;
-        gg[h][j] = (r < rows && c < cols) ? *reinterpret_cast<const f32x4*>(g + (size_t)r * cols + c)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        gg[h][j] = (r >= 0 && c < cols) ? *reinterpret_cast<const f32x4*>(g + (size_t)r * cols + c)
+                                        : f32x4{0.f, 0.f, 0.f, 0.f};
         nz |= gg[h][j][0] != 0.f || gg[h][j][1] != 0.f || gg[h][j][2] != 0.f || gg[h][j][3] != 0.f;
       }
       live[h] = (__ballot(nz) & gmask) != 0ull;  // any column of MY row
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const long r = r0 + h * RPW + sub;
-      if (!live[h] || r >= rows) continue;
+      const long r = rr[h];
+      if (!live[h] || r < 0) continue;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = 4 * ln + 4 * LPR * j;
@@ -286,13 +293,40 @@ PV_API int pv_adam_seg(float* p, const float* g, float* m, float* v, long n, int
     hipStream_t st = (hipStream_t)stream;
 #define PV_LAZY(LPR)                                                                                          \
   hipLaunchKernelGGL(pv::optim::adam_lazy_rows_kernel<LPR>, grid, dim3(256), 0, st, p, g, m, v, rows, row_len, lr, \
-                     b1, b2, eps, wd, torch_style, skip, tdev, h)
+                     b1, b2, eps, wd, torch_style, skip, tdev, h, (const int*)nullptr)
     if (lpr == 8) PV_LAZY(8);
     else if (lpr == 16) PV_LAZY(16);
     else if (lpr == 32) PV_LAZY(32);
     else PV_LAZY(64);
 #undef PV_LAZY
   }
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Lazy Adam over a LIST of rows of a (rows_total, row_len) table: rowlist[0..nlist) (entries
+// < 0 skipped); p16 (optional) the table's bf16 mirror.  The sparse-gradient tables' update
+// (parallel/sparse_rows.py): it streams only the candidate rows instead of the whole table.
+PV_API int pv_adam_rows(float* p, const float* g, float* m, float* v, int row_len, const int* rowlist, long nlist,
+                        const float* tdev, float lr, float b1, float b2, float eps, float wd, int torch_style,
+                        const float* skip, void* p16, void* stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15 || ((uintptr_t)p16 & 7)) return -1;
+  if (row_len % 4 || row_len > 1024 || row_len <= 0) return -2;
+  if (nlist <= 0) return 0;
+  const int lpr = row_len <= 32 ? 8 : row_len <= 64 ? 16 : row_len <= 128 ? 32 : 64;
+  long blocks = (nlist + 8L * (64 / lpr) - 1) / (8L * (64 / lpr));
+  if (blocks > 16384) blocks = 16384;
+  const dim3 grid((unsigned)blocks);
+  hipStream_t st = (hipStream_t)stream;
+  unsigned short* h = (unsigned short*)p16;
+#define PV_LAZYL(LPR)                                                                                          \
+  hipLaunchKernelGGL(pv::optim::adam_lazy_rows_kernel<LPR>, grid, dim3(256), 0, st, p, g, m, v, nlist, row_len, \
+                     lr, b1, b2, eps, wd, torch_style, skip, tdev, h, rowlist)
+  if (lpr == 8) PV_LAZYL(8);
+  else if (lpr == 16) PV_LAZYL(16);
+  else if (lpr == 32) PV_LAZYL(32);
+  else PV_LAZYL(64);
+#undef PV_LAZYL
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from ..ops import grad_sink
 from ..ops import transformer as tops
+from ..parallel.sparse_rows import note_rows
 from .base import TwoTowerModel
 
 
@@ -75,6 +76,11 @@ class BertLayer(nn.Module):
         f2 = tops.linear(f, self.w2)
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
                                   bias=self.b2, res=r2)
+
+
+def _row_gather(ids, W):
+    note_rows(W, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
+    return _RowGather.apply(ids, W)
 
 
 class _RowGather(torch.autograd.Function):
@@ -130,7 +136,7 @@ class BertEncoder(nn.Module):
         N, L = ids.shape
         mask = (ids != 0)
         mask[:, 0] = True  # [CLS] position always attends
-        x = (_RowGather.apply(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
+        x = (_row_gather(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
         x = tops.add_layernorm(x, None, self.ln_g, self.ln_b)
         if training and p_drop > 0:
             x = F.dropout(x, p_drop, True)
@@ -153,7 +159,7 @@ class BertEncoder(nn.Module):
             N, L = ids.shape
             mask = (ids != 0)
             mask[:, 0] = True
-            xs.append((_RowGather.apply(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
+            xs.append((_row_gather(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
                       .reshape(N * L, -1))
             masks.append(mask)
             shapes.append((N, L))

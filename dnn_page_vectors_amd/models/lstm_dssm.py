@@ -14,6 +14,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..parallel.sparse_rows import note_rows
+
 from .base import TwoTowerModel
 
 
@@ -29,6 +31,7 @@ class LSTMTower(nn.Module):
 
     def forward(self, ids: torch.Tensor, training: bool) -> torch.Tensor:
         ids = ids.long()
+        note_rows(self.embedding.weight, ids)  # sparse-gradient tables (parallel/sparse_rows.py)
         x = F.dropout(self.embedding(ids), self.p, training)
         lengths = (ids != 0).sum(1).clamp(min=1)
         if self.conv is not None:

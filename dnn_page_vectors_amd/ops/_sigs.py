@@ -13,6 +13,7 @@ SIGS = {
     "pv_conv_weight_rows": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
+    "pv_conv_get_dbg": "",
     # chunkpool.hip (chunked long-page encoder, models/chunked.py)
     "pv_chunk_mean_fwd": "pp" "iiii" "pp" "p",
     "pv_chunk_mean_bwd": "pp" "iii" "p" "p",
@@ -20,7 +21,8 @@ SIGS = {
     "pv_set_deterministic": "i",
     "pv_get_deterministic": "",
     "pv_conv_pool_fwd": "pppppp" "iii" "upu" "ii" "f" "i" "p",
-    "pv_conv_pool_fwd2": "ppppppp" "iii" "upu" "ii" "f" "i" "p",
+    "pv_conv_pool_fwd2": "ppppppp" "iii" "upu" "ii" "f" "i" "p" "pi",
+    "pv_conv_pool_bwd_rec": "ppp" "i" "f" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_dw2": "ppppp" "pppp" "iiii" "upuiif" "p",
@@ -107,6 +109,7 @@ SIGS = {
     "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
     "pv_step_inc": "p" "p",
     "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "pp" "p",
+    "pv_adam_rows": "pppp" "i" "pl" "p" "fffff" "i" "pp" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
     "pv_sumsq": "p" "l" "p" "p",

@@ -18,6 +18,7 @@ import torch
 from . import determinism, grad_sink
 from . import reference as ref
 from ._common import P, check, lib, need, stream, use_hip
+from ..parallel.sparse_rows import note_rows
 
 EP = 104          # padded embedding row stride of the bf16 table copy (kernel constant)
 FW = 150          # filters per width the fast kernel is built for
@@ -148,6 +149,22 @@ def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor
 # now opt-in: PAGEVEC_DENSE_DX=1.
 DENSE_DX = os.environ.get("PAGEVEC_DENSE_DX", "0") != "0"
 DENSE_DX_MAXL = 64
+# the dTable sort keys written by the conv FORWARD's loader waves, one sample behind the MFMA
+# waves (each filter's argmax window and ReLU liveness are known then): the backward only
+# writes the {g * scale, argmax} records instead of running the emit kernel's id gathers on
+# its critical path (PAGEVEC_FWD_EMIT=0: the emit kernel)
+FWD_EMIT = os.environ.get("PAGEVEC_FWD_EMIT", "1") != "0"
+
+
+V7_DBG = (16384 + 64 + 5, 16384 + 128 + 5)  # pv_conv_set_dbg variants with the loader-wave key emit
+
+
+def _conv_dbg() -> int:
+    return int(lib().pv_conv_get_dbg())
+
+
+def _dense_dx(L: int) -> bool:
+    return DENSE_DX and L <= min(DENSE_DX_MAXL, lib().pv_conv_dx_dense_maxl())
 
 
 def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
@@ -179,9 +196,15 @@ class _ConvPoolFn(torch.autograd.Function):
         row_offset &= 0xFFFFFFFF
         sp = _SEED_DEV
         b3c, b4c = b3.detach().contiguous(), b4.detach().contiguous()  # the parameters themselves: no cat
+        keys = None
+        if ctx.needs_input_grad[1] and FWD_EMIT and not _dense_dx(L) and _conv_dbg() in (0,) + V7_DBG:
+            k16 = V < 65535 and REDUCE_EPW > 0
+            keys = torch.empty(N * SLOTS_PER_SAMPLE, dtype=torch.int16 if k16 else torch.int32, device=ids.device)
         check(lib().pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(b3c), P(b4c), P(pooled), P(argmax), N, L, V,
-                                      seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device)),
+                                      seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device),
+                                      P(keys), 0 if keys is None else keys.element_size()),
               "pv_conv_pool_fwd2")
+        ctx.keys = keys
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
@@ -217,7 +240,7 @@ class _ConvPoolFn(torch.autograd.Function):
         L_ = lib()
         # every buffer the side stream touches is allocated on the main stream above/before
         # and the main stream joins the side stream before returning: no cross-stream reuse
-        dense_dx = ctx.needs_input_grad[1] and DENSE_DX and L <= min(DENSE_DX_MAXL, L_.pv_conv_dx_dense_maxl())
+        dense_dx = ctx.needs_input_grad[1] and _dense_dx(L)
         # the page tower's dW beside its table chain (not inside a hipGraph capture: one stream)
         side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] and not dense_dx
                 and not torch.cuda.is_current_stream_capturing() and not determinism.enabled() else None)
@@ -263,13 +286,17 @@ class _ConvPoolFn(torch.autograd.Function):
             # entry i's value is its slot i: no value array, the sort reads a counting iterator;
             # token ids < 65535 sort as 2-byte keys
             k16 = V < 65535 and REDUCE_EPW > 0
-            keys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
-            skeys = torch.empty_like(keys)
+            keys, ctx.keys = ctx.keys, None
+            skeys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
             svals = torch.empty(M, dtype=u32, device=dev)
-            if k16:
+            if keys is not None:  # written by the forward: only the records remain
+                check(L_.pv_conv_pool_bwd_rec(P(gpool), P(argmax), P(rec), N, scale, s), "pv_conv_pool_bwd_rec")
+            elif k16:
+                keys = torch.empty(M, dtype=torch.int16, device=dev)
                 check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L, V,
                                                     scale, s), "pv_conv_pool_bwd_emit3_u16")
             else:
+                keys = torch.empty(M, dtype=u32, device=dev)
                 check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
             sort_pairs_iota(keys, skeys, svals, end_bit)
@@ -316,6 +343,7 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
 
     ``compute_cache``: optional (tbl16, wpack) already derived from the current params.
     """
+    note_rows(table, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
     if use_hip(ids, table) and fast_path_supported(table.shape[1], [w.shape[1] for w in weights], weights[0].shape[0]):
         w3, w4 = weights
         b3, b4 = biases

@@ -27,6 +27,7 @@ from . import dense as dops
 from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
+from ..parallel.sparse_rows import note_rows
 from .conv_pool import sort_pairs_iota
 
 
@@ -239,6 +240,7 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
     ``fp8``: long bags (the counts plan) multiply e4m3 counts by the per-tensor-scaled e4m3
     table on the block-scaled fp8 MFMA (``w8`` = ops.fp8.quantize_t(W) of this step, else
     quantised here); the weight gradient stays the exact bf16 C^T G (straight-through)."""
+    note_rows(W, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
     if use_hip(ids, W) and act in _BAG_ACT:
         if W16 is None:
             W16 = W.detach().to(torch.bfloat16).contiguous()

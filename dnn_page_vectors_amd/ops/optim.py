@@ -14,7 +14,7 @@ Keras-1 Adam semantics by default (``torch_style=False``), see optim.hip.
 from __future__ import annotations
 
 import math
-from typing import Dict, Iterable, List, Optional, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -59,8 +59,19 @@ class FlatParams:
     def owns_grad(self, p) -> bool:
         return p.grad is not None and self._gptr.get(id(p)) == p.grad.data_ptr()
 
-    def zero_grad(self) -> None:
-        self.grad.zero_()
+    def zero_grad(self, skip: Sequence[Tuple[int, int]] = ()) -> None:
+        """Zero the gradient buffer; ``skip``: sorted [lo, hi) element ranges left alone (the
+        sparse-gradient tables, which zero only their touched rows: parallel/sparse_rows.py)."""
+        if not skip:
+            self.grad.zero_()
+        else:
+            pos = 0
+            for lo, hi in skip:
+                if lo > pos:
+                    self.grad[pos:lo].zero_()
+                pos = max(pos, hi)
+            if pos < self.numel:
+                self.grad[pos:].zero_()
         self.written.clear()
 
     def reattach_grads(self) -> None:
@@ -80,7 +91,7 @@ class FlatParams:
 class FlatAdam:
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, torch_style: bool = False, lazy: Optional[Iterable[str]] = None,
-                 mirror: Optional[Iterable[str]] = None):
+                 mirror: Optional[Iterable[str]] = None, sparse=None):
         """lazy: names of 2-D embedding tables updated LazyAdam-style — a row whose gradient is
         all zero this step (none of its tokens in the batch) keeps its weights and moments
         (optim.hip::adam_lazy_rows_kernel; the step then streams ~4 B instead of 28 B per
@@ -91,9 +102,14 @@ class FlatAdam:
         same pass (``mirror_for(p)``): the forward's bf16 operands (MLP embedding tables,
         BERT projection weights) then need no per-step cast kernel."""
         self.flat = flat
+        # sparse-gradient tables (parallel/sparse_rows.py): LazyAdam over their step's candidate
+        # rows only (pv_adam_rows); on the CPU they are lazy tables over the whole table
+        self.sparse = sparse
+        sparse_names = set(sparse.tables) if sparse is not None else set()
+        self._sparse_off = {sparse.tables[n].off: sparse.tables[n] for n in sparse_names}
         # [(offset, numel, row_len)] sorted by offset; rows of 4k floats (16-byte aligned)
         self.lazy: List[Tuple[int, int, int]] = []
-        for name in (lazy or ()):
+        for name in sorted(set(lazy or ()) | sparse_names):
             o, k, shp = flat.offsets[name]
             if len(shp) == 2 and shp[1] % 4 == 0 and shp[1] <= 1024:
                 self.lazy.append((o, k, int(shp[1])))
@@ -125,7 +141,7 @@ class FlatAdam:
         self.step_count += 1
         t = self.step_count
         if use_hip(self.flat.data):
-            if self.lazy or self.mirrors:
+            if self.lazy or self.mirrors or self.sparse is not None:
                 self._step_segments(skip_flag)
                 # the trainer bumps the generation right after the step: the mirrors hold
                 # exactly the weights of that next generation
@@ -180,6 +196,13 @@ class FlatAdam:
         for o, n, rl in self._segs:
             ptrs = [b + o * esz for b in base]
             mp = m16.data_ptr() + 2 * o if m16 is not None else None
+            t = self._sparse_off.get(o) if rl else None
+            if t is not None:  # sparse table: only this step's candidate rows
+                rows = self.sparse.candidate_rows(t)
+                check(L_.pv_adam_rows(ptrs[0], ptrs[1], ptrs[2], ptrs[3], rl, P(rows), rows.numel(), P(self.t_dev),
+                                      self.lr, self.b1, self.b2, self.eps, self.wd, int(self.torch_style),
+                                      P(skip_flag), mp, s), "pv_adam_rows")
+                continue
             check(L_.pv_adam_seg(ptrs[0], ptrs[1], ptrs[2], ptrs[3], n, rl, P(self.t_dev), self.lr, self.b1, self.b2,
                                  self.eps, self.wd, int(self.torch_style), P(skip_flag), mp, s), "pv_adam_seg")
 

@@ -40,9 +40,16 @@ class GradBuckets:
     MIN_SPLIT_BYTES = 1 << 20  # embedding tables of at least 1 MB get a bucket of their own
     OWN_BUCKET_LEAVES = ("embedding", "word")  # >= 1 MB embedding tables: one bucket each
 
-    def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg"):
-        """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients)."""
+    def __init__(self, flat: FlatParams, bucket_mb: float = 32.0, overlap: bool = True, reduce: str = "avg",
+                 sparse=None):
+        """reduce: "avg" (data parallel) or "sum" (tower placement: per-rank partial gradients).
+        sparse: parallel/sparse_rows.SparseTables — its tables get a bucket of their own whose
+        "all-reduce" is the touched-row exchange (averaged like the dense buckets)."""
         self.flat = flat
+        self.sparse = sparse
+        if sparse is not None and reduce == "sum":
+            raise ValueError("sparse gradient tables average over ranks (data parallel), not tower placement")
+        self.sparse_bucket = {}
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.active = active()  # world > 1, or the forced one-rank rehearsal (PAGEVEC_FORCE_DIST)
         self.overlap = overlap and self.active
@@ -61,12 +68,17 @@ class GradBuckets:
             o, k, _ = flat.offsets[name]
             end = o + (k + 63) // 64 * 64
             mod = name.split(".", 1)[0]
-            if name.rsplit(".", 1)[-1] in self.OWN_BUCKET_LEAVES and (end - o) >= min_split:
+            own = name.rsplit(".", 1)[-1] in self.OWN_BUCKET_LEAVES and (end - o) >= min_split
+            if sparse is not None and name in sparse.tables:
+                own = True
+            if own:
                 # embedding tables get a bucket of their own: the sparse table backward
                 # releases it before the tower's weight gradients are done (ops/conv_pool.py)
                 if cur_lo is not None:
                     self._add(cur_lo, cur_hi, members)
                 self._add(o, end, [name])
+                if sparse is not None and name in sparse.tables:
+                    self.sparse_bucket[len(self.buckets) - 1] = sparse.tables[name]
                 cur_lo = cur_hi = cur_mod = None
                 members = []
                 continue
@@ -115,11 +127,16 @@ class GradBuckets:
     def _launch(self, bi: int) -> None:
         lo, hi, _ = self.buckets[bi]
         view = self.flat.grad[lo:hi]
+        t = self.sparse_bucket.get(bi)
         if view.is_cuda:  # order the collective after every stream that wrote into the bucket
             cur = torch.cuda.current_stream(view.device)
             for key, st in self.streams[bi].items():
                 if key != cur.cuda_stream:
                     cur.wait_stream(st)
+        if t is not None:  # touched-row exchange instead of the dense all-reduce
+            self.sparse.launch(t)
+            self.handles[bi] = "sparse"
+            return
         if self.avg_op is not None:
             self.handles[bi] = dist.all_reduce(view, op=self.avg_op, async_op=True)
         else:
@@ -138,6 +155,9 @@ class GradBuckets:
             if self.handles[bi] is None:
                 self._launch(bi)
         for bi, h in enumerate(self.handles):
+            if bi in self.sparse_bucket:
+                self.sparse.complete(self.sparse_bucket[bi])
+                continue
             h.wait()
             if self.avg_op is None and not self.sum_only:
                 lo, hi, _ = self.buckets[bi]

@@ -1,0 +1,189 @@
+"""Row-sparse gradients for large embedding tables ("for the 7.5 M-word vocab,
+all-gather (ids, rows) pairs of the touched rows instead of all-reducing 3 GB").
+
+The reference's word-level v1 loads a 7,556,273-row table (dssm_cnn/data_helpers.py:143)
+into ``Embedding(weights=...)`` (dssm_cnn_v2/cnn_dssm_th.py:114-120).  A step touches only
+the rows of the tokens in its batch, yet the dense path of this framework would, per table
+and step: zero-fill the whole table gradient (3 GB), scan it for the gradient norm and the
+non-finite guard, all-reduce it (3 GB over xGMI, ~40 ms per step at W = 8) and run the
+optimizer over it.  With ``Configuration.sparse_embedding_grad`` every >= 2-D embedding
+table registered here instead:
+
+* the ops that gather its rows (the fused conv tower, the embedding bag, the LSTM's
+  F.embedding) ``note`` the token ids of the step; the candidate rows are their union
+  (sorted unique ids, one device sort);
+* only the previous step's rows are zeroed (the rest of the table gradient stays zero by
+  construction), ``FlatParams.zero_grad`` skips the table;
+* data parallel: in place of the table's dense bucket all-reduce, every rank all-gathers
+  (row ids, gradient rows) padded to the largest rank's count (one 4-byte MAX all-reduce
+  to size them), zeroes its own rows and index-adds everyone's rows scaled by 1/W — the
+  average, exactly what the dense all-reduce would have left in those rows, every other
+  row being zero on every rank;
+* the optimizer runs LazyAdam over the union rows only (``pv_adam_rows``: the lazy kernel
+  over a row list, rows whose gradient is all zero keep weights and moments — the
+  ``lazy_embedding_adam`` semantics, so a sparse run equals a lazy dense run);
+* the gradient norm / non-finite check reads the union rows, not the table.
+
+Cost per step: O(touched rows x E) instead of O(V x E); the host learns the gathered row
+count once per table and step (a sync, so these tables rule out hipGraph capture).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .dist import active
+
+
+@dataclass
+class _Table:
+    name: str
+    param: torch.nn.Parameter
+    off: int
+    V: int
+    E: int
+    notes: List[torch.Tensor] = field(default_factory=list)
+    rows: Optional[torch.Tensor] = None      # int32 candidate rows of the current step (after exchange)
+    prev: Optional[torch.Tensor] = None      # rows written last step (zeroed before the next)
+    pending: Optional[Tuple] = None          # in-flight all-gathers
+
+
+class SparseTables:
+    def __init__(self, flat, names: Sequence[str]):
+        self.flat = flat
+        named = dict(flat.named)
+        self.tables: Dict[str, _Table] = {}
+        self._by_id: Dict[int, _Table] = {}
+        for n in names:
+            o, k, shp = flat.offsets[n]
+            if len(shp) != 2:
+                raise ValueError(f"sparse gradient table {n!r} must be 2-D, got {tuple(shp)}")
+            if shp[1] % 4 or shp[1] > 1024:
+                raise ValueError(f"sparse gradient table {n!r}: row length {shp[1]} must be a multiple of 4, <= 1024")
+            t = _Table(n, named[n], o, int(shp[0]), int(shp[1]))
+            self.tables[n] = t
+            self._by_id[id(t.param)] = t
+            t.param._pv_sparse = self
+
+    # ---------------------------------------------------------------- per step
+    def ranges(self) -> List[Tuple[int, int]]:
+        return sorted((t.off, t.off + t.V * t.E) for t in self.tables.values())
+
+    def begin_step(self) -> None:
+        """Before the forward: zero the rows written last step (the dense zero skips tables)."""
+        for t in self.tables.values():
+            if t.prev is not None and t.prev.numel():
+                self.grad2d(t).index_fill_(0, t.prev.long(), 0.0)
+            t.prev = None
+            t.rows = None
+            t.notes = []
+            t.pending = None
+
+    def note(self, p: torch.Tensor, ids: torch.Tensor) -> None:
+        t = self._by_id.get(id(p))
+        if t is not None and torch.is_grad_enabled() and p.requires_grad:
+            t.notes.append(ids.detach().reshape(-1))
+
+    def grad2d(self, t: _Table) -> torch.Tensor:
+        return self.flat.grad[t.off:t.off + t.V * t.E].view(t.V, t.E)
+
+    def _local_rows(self, t: _Table) -> torch.Tensor:
+        if not t.notes:
+            return torch.empty(0, dtype=torch.int32, device=self.flat.grad.device)
+        ids = torch.cat([x.to(torch.int64) for x in t.notes]) if len(t.notes) > 1 else t.notes[0].to(torch.int64)
+        u = torch.unique(ids)  # sorted
+        u = u[(u >= 0) & (u < t.V)]
+        return u.to(torch.int32)
+
+    def launch(self, t: _Table, group=None) -> None:
+        """The table's gradient is complete: start its row exchange (or just fix its rows)."""
+        u = self._local_rows(t)
+        t.notes = []
+        if not active(group):
+            t.rows = u
+            return
+        W = dist.get_world_size(group)
+        cnt = torch.tensor([u.numel()], dtype=torch.int64, device=u.device)
+        dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+        cap = int(cnt.item())  # host sync: the gathered buffers' size
+        rows = torch.full((cap,), -1, dtype=torch.int32, device=u.device)
+        rows[:u.numel()] = u
+        g2 = self.grad2d(t)
+        vals = torch.zeros(cap, t.E, dtype=g2.dtype, device=g2.device)
+        if u.numel():
+            vals[:u.numel()] = g2.index_select(0, u.long())
+        all_rows = torch.empty(W * cap, dtype=torch.int32, device=u.device)
+        all_vals = torch.empty(W * cap, t.E, dtype=g2.dtype, device=g2.device)
+        h1 = dist.all_gather_into_tensor(all_rows, rows, group=group, async_op=True)
+        h2 = dist.all_gather_into_tensor(all_vals, vals, group=group, async_op=True)
+        t.pending = (u, all_rows, all_vals, h1, h2, W)
+
+    def complete(self, t: _Table) -> None:
+        """Wait for the exchange; the table gradient rows := the mean over ranks."""
+        if t.pending is None:
+            return
+        u, all_rows, all_vals, h1, h2, W = t.pending
+        t.pending = None
+        h1.wait()
+        h2.wait()
+        g2 = self.grad2d(t)
+        if u.numel():
+            g2.index_fill_(0, u.long(), 0.0)
+        ok = all_rows >= 0
+        r = all_rows[ok].long()
+        g2.index_add_(0, r, all_vals[ok], alpha=1.0 / W)
+        t.rows = torch.unique(r).to(torch.int32)
+
+    def finish_step(self) -> None:
+        """After the optimizer: the rows written this step are the next step's zero list."""
+        for t in self.tables.values():
+            t.prev = t.rows
+
+    def candidate_rows(self, t: _Table) -> torch.Tensor:
+        if t.rows is None:  # never launched (no data parallel hook): local rows
+            t.rows = self._local_rows(t)
+            t.notes = []
+        return t.rows
+
+    # --------------------------------------------------------------- gradient stats
+    def grad_stats(self, flat_grad: torch.Tensor, dense_stats) -> torch.Tensor:
+        """[sum g^2, nonfinite] over the dense segments (``dense_stats(view)``) + table rows."""
+        out = torch.zeros(2, dtype=torch.float32, device=flat_grad.device)
+        pos = 0
+        for lo, hi in self.ranges():
+            if lo > pos:
+                out += dense_stats(flat_grad[pos:lo])
+            pos = (hi + 63) // 64 * 64
+        if pos < flat_grad.numel():
+            out += dense_stats(flat_grad[pos:])
+        for t in self.tables.values():
+            rows = self.candidate_rows(t)
+            if rows.numel():
+                g = self.grad2d(t).index_select(0, rows.long())
+                fin = torch.isfinite(g)
+                out[0] += torch.where(fin, g, torch.zeros_like(g)).pow(2).sum()
+                out[1] = torch.maximum(out[1], (~fin).any().float())
+        out[1] = (out[1] > 0).float()
+        return out
+
+
+def table_names(model: torch.nn.Module, min_rows: int = 0) -> List[str]:
+    """The model's embedding tables: 2-D parameters named ``*.embedding`` / ``*.word`` or the
+    weight of an ``nn.Embedding`` (``*.embedding.weight``)."""
+    out = []
+    for n, p in model.named_parameters():
+        leaf = n.rsplit(".", 1)[-1]
+        is_table = leaf in ("embedding", "word") or n.endswith("embedding.weight")
+        if p.requires_grad and p.dim() == 2 and is_table and p.shape[0] >= min_rows:
+            out.append(n)
+    return out
+
+
+def note_rows(table: torch.Tensor, ids: torch.Tensor) -> None:
+    """Called by ops that gather rows of ``table``: records the ids if the table is sparse."""
+    sp = getattr(table, "_pv_sparse", None)
+    if sp is not None:
+        sp.note(table, ids)

@@ -36,7 +36,9 @@ from ..ops._common import precision_scope
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
 from ..parallel import placement
+from ..parallel import sparse_rows
 from ..parallel.ddp import GradBuckets, broadcast_params
+from ..parallel.sparse_rows import SparseTables
 from ..utils.metrics import MetricsLogger, hbm_used_gb
 from ..utils.tracing import range_push, range_pop
 
@@ -102,8 +104,11 @@ class Trainer:
             if (hasattr(self.model, "bf16_mirror_params") and getattr(cfg, "optimizer_bf16_mirror", True)
                 and getattr(cfg, "dtype", "bf16") != "fp32"
                 and os.environ.get("PAGEVEC_NO_MIRROR", "0") != "1") else None
+        # row-sparse embedding gradients for large vocabularies (parallel/sparse_rows.py)
+        self.sparse = (SparseTables(self.flat, sparse_rows.table_names(self.model))
+                       if getattr(cfg, "sparse_embedding_grad", False) else None)
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
-                            torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror)
+                            torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror, sparse=self.sparse)
         self.placement = getattr(cfg, "placement", "dp")
         if self.placement not in ("dp", "tower"):
             raise ValueError(f"unknown placement {self.placement!r}")
@@ -113,7 +118,8 @@ class Trainer:
         self._sink_scanned = set()
         self._pos = {}
         self._acc = None
-        self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg")
+        self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg",
+                                    sparse=self.sparse)
                         if self.info.enabled else None)
         self.step = 0
         self.epoch = 0
@@ -138,7 +144,7 @@ class Trainer:
         else:
             determinism.ensure(False)
         self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
-                           and not self.deterministic)
+                           and not self.deterministic and self.sparse is None)
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
         # Round 1 needed it: replays interleaved with eager allocating work faulted after ~97
         # CDSSM steps inside rocPRIM's onesweep radix sort (the dTable gradient's bucketing),
@@ -293,7 +299,11 @@ class Trainer:
                                             (self.step + 1) % le == 0) else None
         if timer:
             timer.mark()
-        self.flat.zero_grad()
+        if self.sparse is not None:  # tables: only last step's rows are zeroed
+            self.flat.zero_grad(skip=self.sparse.ranges())
+            self.sparse.begin_step()
+        else:
+            self.flat.zero_grad()
         if self.buckets is not None:
             self.buckets.start_step()
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
@@ -330,9 +340,14 @@ class Trainer:
         if timer:
             timer.mark()
         range_push("optimizer")
-        stats = grad_sumsq_and_finite(self.flat.grad)
+        if self.sparse is not None:
+            stats = self.sparse.grad_stats(self.flat.grad, grad_sumsq_and_finite)
+        else:
+            stats = grad_sumsq_and_finite(self.flat.grad)
         skip = stats[1:2] if self.cfg.skip_nonfinite else None
         self.opt.step(skip)
+        if self.sparse is not None:
+            self.sparse.finish_step()
         bump_generation()
         range_pop()
         if timer:

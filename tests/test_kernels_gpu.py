@@ -69,6 +69,59 @@ def test_conv_pool_fwd_bwd(N, L, p, mode):
     torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("N,L,V,p", [(6, 130, 70000, 0.25), (3, 400, 70000, 0.0), (20, 45, 66000, 0.25)])
+def test_conv_pool_bwd_word_vocab_u32_path(N, L, V, p):
+    """Word-level vocabularies (dssm_cnn_v2/config.py:80-83, cnn_dssm_th.py:114-120): V >= 65535
+    takes the 4-byte sort keys and the u32 reduce; dTable / dW vs the fp32 reference through
+    the kernel's own argmax windows (untested on the GPU before)."""
+    torch.manual_seed(3)
+    E, F = 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    ids[:, ::7] = V - 1  # the top of the id range (and repeated tokens: runs in the sort)
+    table = bf(torch.randn(V, E, device=DEV) * 0.5).requires_grad_(True)
+    w3 = bf(torch.randn(F, 3, E, device=DEV) * 0.1).requires_grad_(True)
+    w4 = bf(torch.randn(F, 4, E, device=DEV) * 0.1).requires_grad_(True)
+    b3 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    b4 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    pooled, argmax = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], p, 77, True)
+    g = torch.randn_like(pooled)
+    (pooled * g).sum().backward()
+    tr = bf(table.detach()).requires_grad_(True)
+    xr = ref.embed_dropout(ids, tr, p, 77, True)
+    dws, dbs, dx = ref.conv_maxpool_grads_at(xr.detach(), [bf(w3.detach()), bf(w4.detach())], pooled.detach(),
+                                             argmax, g)
+    xr.backward(dx)
+    torch.testing.assert_close(table.grad, tr.grad, rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(w3.grad, dws[0], rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(w4.grad, dws[1], rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(b3.grad, dbs[0], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("V", [500, 70000])
+def test_forward_emitted_keys_equal_emit_kernel(V):
+    """The dTable sort keys written by the conv forward's epilogue (FWD_EMIT) give the same
+    table gradient as the backward's emit kernel (2- and 4-byte keys)."""
+    torch.manual_seed(4)
+    E, F, N, L = 100, 150, 24, 300
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV)
+    table0 = torch.randn(V, E, device=DEV) * 0.3
+    w3, w4 = torch.randn(F, 3, E, device=DEV) * 0.1, torch.randn(F, 4, E, device=DEV) * 0.1
+    b = [torch.randn(F, device=DEV) * 0.1, torch.randn(F, device=DEV) * 0.1]
+    grads = []
+    saved = cops.FWD_EMIT
+    try:
+        for fe in (False, True):
+            cops.FWD_EMIT = fe
+            t = table0.clone().requires_grad_(True)
+            pooled, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], b, 0.25, 5, True)
+            (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
+            grads.append(t.grad)
+    finally:
+        cops.FWD_EMIT = saved
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-5, atol=1e-6)
+    assert grads[0].abs().sum() > 0
+
+
 @pytest.mark.parametrize("variant", [5, 7])
 @pytest.mark.parametrize("epw", [64, 512, 1024])
 def test_dtable_reduce_long_runs_match_reduce4(epw, variant):

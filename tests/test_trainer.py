@@ -153,3 +153,38 @@ def test_inbatch_gamma_overrides_gamma_for_inbatch_losses_only():
     assert losses["ib_override"] == losses["ib_gamma"]
     assert losses["ib_override"] != losses["ib_default"]
     assert losses["ex_override"] == losses["ex_default"]
+
+
+def test_sparse_embedding_grad_single_process_matches_lazy():
+    """One process: sparse-gradient tables (only touched rows zeroed / checked / updated)
+    train exactly like LazyAdam over dense table gradients, and leave the untouched rows'
+    gradient zero between steps."""
+    import torch
+
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.models.cdssm import CDSSM
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo())
+    V = 5000
+    res = []
+    for sparse in (True, False):
+        cfg = Configuration(feature_level="ngram", vocab_hash_size=V, query_length=8, document_length=16,
+                            batch_size=8, embedding_dim=12, hidden_dims=16, dropout_prob=(0.25, 0.5),
+                            loss_mode="in_batch", lazy_embedding_adam=True, sparse_embedding_grad=sparse)
+        tr = Trainer(cfg, CDSSM(cfg, V))
+        g = torch.Generator().manual_seed(1)
+        for _ in range(3):
+            m = tr.train_step(torch.randint(1, V, (8, 8), generator=g, dtype=torch.int32),
+                              torch.randint(1, V, (8, 4, 16), generator=g, dtype=torch.int32))
+        res.append((tr.flat.data.clone(), float(m["grad_sumsq"])))
+        if sparse:
+            t = tr.sparse.tables["query_tower.embedding"]
+            g2 = tr.sparse.grad2d(t).clone()
+            rows = t.rows.long()
+            mask = torch.ones(V, dtype=torch.bool)
+            mask[rows] = False
+            assert g2[mask].abs().sum() == 0 and g2[rows].abs().sum() > 0
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=0, atol=0)
+    assert abs(res[0][1] - res[1][1]) <= 1e-5 * res[1][1]
