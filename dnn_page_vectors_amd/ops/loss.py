@@ -208,21 +208,7 @@ class _InBatchRowsFn(torch.autograd.Function):
         DP = (D + 31) // 32 * 32
         qb, db = _pad_bf16(qn, DP), _pad_bf16(dn, DP)
         pos = pos.to(torch.int32).contiguous()
-        dev, s, L_ = qn.device, stream(qn.device), lib()
-        spos = torch.empty(B, dtype=torch.float32, device=dev)
-        check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
-              "pv_ib_pos")
-        blocks = _col_blocks(B, M)
-        part = torch.empty(len(blocks), B, dtype=torch.float32, device=dev)
-        for k, (c0, c1) in enumerate(blocks):
-            S = torch.mm(qb, db[c0:c1].t(), out_dtype=torch.float32)
-            check(L_.pv_ib_rows_blk(P(S), c1 - c0, B, c1 - c0, None, P(part[k]), float(gamma), int(clip), s),
-                  "pv_ib_rows_blk")
-        sumexp = torch.empty(B, dtype=torch.float32, device=dev)
-        loss = torch.empty(B, dtype=torch.float32, device=dev)
-        prob = torch.empty(B, dtype=torch.float32, device=dev)
-        check(L_.pv_ib_rowsum(P(part), P(sumexp), B, len(blocks), P(spos), P(loss), P(prob), float(gamma), s),
-              "pv_ib_rowsum")
+        loss, prob, sumexp = _rows_forward(qb, db, pos, B, M, DP, gamma, clip)
         ctx.save_for_backward(qb, db, pos, sumexp)
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
         ctx.reduce = bool(reduce)
@@ -244,15 +230,46 @@ class _InBatchRowsFn(torch.autograd.Function):
         scale, g, _ = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, None, DP)
         dq = torch.zeros(B, DP, dtype=torch.float32, device=dev)
         dd = torch.empty(M, DP, dtype=torch.float32, device=dev)
-        for c0, c1 in _col_blocks(B, M):
-            S = torch.mm(qb, db[c0:c1].t(), out_dtype=torch.float32)
-            check(L_.pv_ib_rows_blk(P(S), c1 - c0, B, c1 - c0, P(scale), None, float(gamma), int(clip), s),
-                  "pv_ib_rows_blk(dS)")
-            dS = S.to(torch.bfloat16)
-            dq += torch.mm(dS, db[c0:c1], out_dtype=torch.float32)
-            dd[c0:c1] = torch.mm(dS.t(), qb, out_dtype=torch.float32)
+        _rows_backward(qb, db, scale, gamma, clip, dq=dq, dd=dd)
         check(L_.pv_ib_pos(P(qb), P(db), P(pos), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s), "pv_ib_pos(bwd)")
         return dq[:, :D], dd[:, :D], None, None, None, None
+
+
+def _rows_forward(qb, db, pos, B, M, DP, gamma, clip):
+    """Wide-vector forward over page-column blocks -> (per-row loss, P+, sumexp)."""
+    dev, s, L_ = qb.device, stream(qb.device), lib()
+    spos = torch.empty(B, dtype=torch.float32, device=dev)
+    check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
+          "pv_ib_pos")
+    blocks = _col_blocks(B, M)
+    part = torch.empty(len(blocks), B, dtype=torch.float32, device=dev)
+    for k, (c0, c1) in enumerate(blocks):
+        S = torch.mm(qb, db[c0:c1].t(), out_dtype=torch.float32)
+        check(L_.pv_ib_rows_blk(P(S), c1 - c0, B, c1 - c0, None, P(part[k]), float(gamma), int(clip), s),
+              "pv_ib_rows_blk")
+    sumexp = torch.empty(B, dtype=torch.float32, device=dev)
+    loss = torch.empty(B, dtype=torch.float32, device=dev)
+    prob = torch.empty(B, dtype=torch.float32, device=dev)
+    check(L_.pv_ib_rowsum(P(part), P(sumexp), B, len(blocks), P(spos), P(loss), P(prob), float(gamma), s),
+          "pv_ib_rowsum")
+    return loss, prob, sumexp
+
+
+def _rows_backward(xb, yb, scale, gamma, clip, dq=None, dd=None):
+    """Flash-style wide-vector backward of the (R x C) logits of rows xb against columns yb,
+    recomputed per column block: dS = rows_blk(S, per-row scale); dq += dS yb (rows' gradient,
+    accumulated), dd[block] = dS^T xb (columns' gradient, written)."""
+    R, C = xb.shape[0], yb.shape[0]
+    s, L_ = stream(xb.device), lib()
+    for c0, c1 in _col_blocks(R, C):
+        S = torch.mm(xb, yb[c0:c1].t(), out_dtype=torch.float32)
+        check(L_.pv_ib_rows_blk(P(S), c1 - c0, R, c1 - c0, P(scale), None, float(gamma), int(clip), s),
+              "pv_ib_rows_blk(dS)")
+        dS = S.to(torch.bfloat16)
+        if dq is not None:
+            dq += torch.mm(dS, yb[c0:c1], out_dtype=torch.float32)
+        if dd is not None:
+            dd[c0:c1] = torch.mm(dS.t(), xb, out_dtype=torch.float32)
 
 
 class PageGather:
@@ -279,7 +296,7 @@ class PageGather:
 def start_page_gather(dn: torch.Tensor, group=None) -> Optional[PageGather]:
     """Begin the cross-GPU page-vector gather early (None when it does not apply)."""
     from ..parallel.dist import active
-    if not active(group) or not use_hip(dn) or dn.shape[1] > 192:
+    if not active(group) or not use_hip(dn):
         return None
     return PageGather(dn, group)
 
@@ -353,6 +370,69 @@ class _CrossGpuFn(torch.autograd.Function):
         return dq[:, :D], dd[:, :D], None, None, None, None, None, None
 
 
+class _CrossGpuRowsFn(torch.autograd.Function):
+    """Cross-GPU negatives for wide vectors (D > 192: BERT's 768) with the same communication
+    design as _CrossGpuFn — the page gather started after the doc tower, the bf16 queries and
+    the per-query softmax scales gathered asynchronously, and NO reduce-scatter in backward:
+    dQ = local queries x all pages, dD of the LOCAL pages = all W*B queries x local pages —
+    with the logits tiled over column blocks at the GEMM level (_rows_forward / _rows_backward)
+    instead of the register-resident flash kernels."""
+
+    @staticmethod
+    def forward(ctx, qn, dn, pos_local, gamma, clip, group, pre, reduce=False):
+        W = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        B, D = qn.shape
+        n = dn.shape[0]
+        M = n * W
+        DP = (D + 31) // 32 * 32
+        qb = _pad_bf16(qn, DP)
+        if pre is not None:
+            dbl, db = pre.wait()
+        else:
+            dbl = _pad_bf16(dn, DP)
+            db = torch.empty(M, DP, dtype=torch.bfloat16, device=qn.device)
+            dist.all_gather_into_tensor(db, dbl, group=group)
+        pos_local = pos_local.to(torch.int32).contiguous()
+        pos = (pos_local + rank * n).contiguous()
+        loss, prob, sumexp = _rows_forward(qb, db, pos, B, M, DP, gamma, clip)
+        ctx.mark_non_differentiable(prob)
+        ctx.set_materialize_grads(False)
+        qall = torch.empty(B * W, DP, dtype=torch.bfloat16, device=qn.device)
+        ctx.qwork = dist.all_gather_into_tensor(qall, qb, group=group, async_op=True)
+        ctx.qall = qall
+        ctx.save_for_backward(qb, db, dbl, pos_local, sumexp)
+        ctx.meta = (B, M, n, D, DP, float(gamma), int(clip), group, W)
+        ctx.reduce = bool(reduce)
+        if reduce:
+            lm, acc = _loss_stats(loss, prob)
+            ctx.mark_non_differentiable(acc)
+            return lm, prob, acc
+        return loss, prob
+
+    @staticmethod
+    def backward(ctx, gl, _gp, _ga=None):
+        if gl is None:
+            return (None,) * len(ctx.needs_input_grad)
+        qb, db, dbl, pos_local, sumexp = ctx.saved_tensors
+        B, M, n, D, DP, gamma, clip, group, W = ctx.meta
+        dev, s, L_ = qb.device, stream(qb.device), lib()
+        scale, g, _ = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, None, DP)
+        scale_all = torch.empty(B * W, dtype=torch.float32, device=dev)
+        swork = dist.all_gather_into_tensor(scale_all, scale, group=group, async_op=True)
+        dq = torch.zeros(B, DP, dtype=torch.float32, device=dev)
+        _rows_backward(qb, db, scale, gamma, clip, dq=dq)  # local queries x all pages
+        ctx.qwork.wait()
+        ctx.qwork = None
+        qall, ctx.qall = ctx.qall, None
+        swork.wait()
+        dd = torch.empty(n, DP, dtype=torch.float32, device=dev)
+        _rows_backward(qall, dbl, scale_all, gamma, clip, dd=dd)  # all queries x local pages
+        check(L_.pv_ib_pos(P(qb), P(dbl), P(pos_local), None, P(g), P(dq), P(dd), B, DP, gamma, clip, s),
+              "pv_ib_pos(bwd)")
+        return dq[:, :D], dd[:, :D], None, None, None, None, None, None
+
+
 def _reduce_rows(loss: torch.Tensor, prob: torch.Tensor):
     return loss.mean(), prob, (prob > 0.5).float().mean()
 
@@ -381,10 +461,11 @@ def cross_gpu_loss(qn: torch.Tensor, dn: torch.Tensor, pos_local: torch.Tensor, 
     from ..parallel.dist import active
     if not active(group):
         return inbatch_loss(qn, dn, pos_local, gamma, clip, reduce=reduce)
-    if use_hip(qn, dn) and qn.shape[1] <= 192:
+    if use_hip(qn, dn):
         if gathered is not None and gathered.source is not dn:
             raise ValueError("the prefetched gather belongs to another page tensor")
-        return _CrossGpuFn.apply(qn, dn, pos_local, float(gamma), bool(clip), group, gathered, bool(reduce))
+        fn = _CrossGpuFn if qn.shape[1] <= 192 else _CrossGpuRowsFn
+        return fn.apply(qn, dn, pos_local, float(gamma), bool(clip), group, gathered, bool(reduce))
     from ..parallel.dist import all_gather_autograd
     docs = all_gather_autograd(dn)
     pos = pos_local + dist.get_rank(group) * dn.shape[0]

@@ -22,7 +22,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q, D=150):
+def _worker(rank, world, port, q, D=150, gather=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", PAGEVEC_DIST_BACKEND="gloo")
     try:
@@ -32,6 +32,10 @@ def _worker(rank, world, port, q, D=150):
 
         info = pdist.init_distributed()
         dev = info.device
+        import torch.distributed as dist
+        rs_calls = []
+        orig_rs = dist.reduce_scatter_tensor
+        dist.reduce_scatter_tensor = lambda *a, **k: (rs_calls.append(1), orig_rs(*a, **k))[1]
         B, S = 96, 4
         n = B * S
         g = torch.Generator(device=dev).manual_seed(0)
@@ -42,7 +46,10 @@ def _worker(rank, world, port, q, D=150):
         pos_local = torch.arange(B, device=dev, dtype=torch.int32) * S
         ql = qa[rank * B:(rank + 1) * B].clone().requires_grad_(True)
         dl = da[rank * n:(rank + 1) * n].clone().requires_grad_(True)
-        loss, _ = L.cross_gpu_loss(ql, dl, pos_local, 10.0, True)
+        pre = L.start_page_gather(dl.detach()) if gather else None
+        if pre is not None:
+            pre.source = dl
+        loss, _ = L.cross_gpu_loss(ql, dl, pos_local, 10.0, True, gathered=pre)
         (loss * (1.0 + 0.5 * rank)).sum().backward()
         # oracle: all queries vs all pages in one process, rank-weighted like above
         qf = qa.clone().requires_grad_(True)
@@ -63,30 +70,35 @@ def _worker(rank, world, port, q, D=150):
 
         q.put((rank, (float((loss.detach() - lf.detach()[sl]).abs().max()),
                       rel(ql.grad, qf.grad[sl]), rel(dl.grad, dfull.grad[sd]),
-                      rel(ql.grad, qh.grad[sl]), rel(dl.grad, dh.grad[sd]))))
+                      rel(ql.grad, qh.grad[sl]), rel(dl.grad, dh.grad[sd]), len(rs_calls))))
         pdist.destroy()
     except Exception as e:  # surface the failure in the parent
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world,D", [(2, 150), (4, 150), (2, 768)])
-def test_cross_gpu_loss_ranks_one_gpu(world, D):
-    """D = 768 (BERT): the wide-vector path (autograd page all-gather + column-block tiled
-    logits) across ranks."""
+@pytest.mark.parametrize("world,D,gather", [(2, 150, False), (4, 150, True), (2, 768, False), (4, 768, True)])
+def test_cross_gpu_loss_ranks_one_gpu(world, D, gather):
+    """D = 768 (BERT): the wide-vector cross-GPU path (_CrossGpuRowsFn: early page gather,
+    async query / scale gathers, column-block tiled logits) — like the narrow kernels it
+    needs no reduce-scatter of the page gradient (counted: zero calls)."""
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, D)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, D, gather)) for r in range(world)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=300) for _ in ps)
     [p.join(timeout=60) for p in ps]
     for r in range(world):
         assert not isinstance(res[r], str), res[r]
-        e_loss, e_q, e_d, h_q, h_d = res[r]
+        e_loss, e_q, e_d, h_q, h_d, n_rs = res[r]
         assert e_loss < 1e-4, res
         tol = 5e-2 if D <= 192 else 8e-2  # bf16 dS vs the fp32 oracle (max-norm over D entries per row)
         assert e_q < tol and e_d < tol, res
-        assert h_q < 1e-4 and h_d < 1e-4, res  # vs the single-process HIP path
+        # vs the single-process HIP path (the wide path's GEMM blocks differ in shape: fp32
+        # summation order can move a bf16 dS element by one ulp)
+        htol = 1e-4 if D <= 192 else 3e-3
+        assert h_q < htol and h_d < htol, res
+        assert n_rs == 0, res  # no reduce-scatter of the page gradient
 
 
 def _ddp_worker(rank, world, port, model, q, ld=64, mode="sink"):
