@@ -44,6 +44,10 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 import torch  # noqa: E402
 
 
+# fp32 gradient megabytes per model (parallel/topology.py picks the RCCL message
+# class from it before the process group exists)
+GRAD_MB = {"cdssm": 12.6, "mlp": 126.0, "bert": 440.0, "chunked": 126.0, "chunked_cdssm": 12.6, "cdssm_char": 0.5}
+
 MODEL_DESC = {
     "cdssm": "CDSSM-300d (conv 2x150, k=3,4 -> dense 150), 30k hashed tri-grams, Lq=45, Ld=2000, J=3",
     "mlp": "Two-tower MLP 512-512-128, 30k hashed tri-grams, Lq=45, Ld=2000, in-batch/cross-GPU negatives",
@@ -155,6 +159,11 @@ def main():
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
 
+    from dnn_page_vectors_amd.parallel import topology
+
+    # xGMI message-class policy (parallel/topology.py): RCCL environment defaults must be in
+    # place before the communicator is created (eager device_id init inside init_distributed)
+    topology.apply_env(GRAD_MB[a.model], int(os.environ.get("WORLD_SIZE", "1")))
     info = pdist.init_distributed(device="cpu" if a.dry_run else None)
     if info.world_size != a.gpus:
         raise SystemExit(f"bench.py: world size {info.world_size} != --gpus {a.gpus} (launch N ranks with "
@@ -290,7 +299,10 @@ def main():
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend,
                        "softmax_scale": (cfg.inbatch_gamma or cfg.GAMMA) if a.loss != "explicit" else cfg.GAMMA,
                        "deterministic": bool(a.deterministic),
-                       "dist_backend": info.backend, "grad_bucket_mb": cfg.grad_bucket_mb,
+                       "dist_backend": info.backend,
+                       "comm": topology.report(topology.grad_mb(model),
+                                               trainer.buckets.bucket_mb if trainer.buckets is not None else
+                                               topology.bucket_mb(topology.grad_mb(model), cfg.grad_bucket_mb)),
                        "launch": "torchrun-env" if os.environ.get("TORCHELASTIC_RUN_ID") else
                                  ("bench-spawn" if W > 1 else "single"),
                        "rccl_env": {k: v for k, v in sorted(os.environ.items())

@@ -79,6 +79,10 @@ def cmd_train(a) -> int:
     from .utils.metrics import MetricsLogger
 
     cfg = _config(a)
+    from .parallel import topology  # RCCL defaults for the job's message class, before the communicator exists
+
+    topology.apply_env(topology.grad_mb(build_model(cfg, cfg.vocab_hash_size)) if int(os.environ.get("WORLD_SIZE", "1")) > 1
+                       else 0.0, int(os.environ.get("WORLD_SIZE", "1")))
     info = pdist.init_distributed()
     if cfg.backend != "auto":
         set_backend(cfg.backend)

@@ -46,6 +46,7 @@ class GradBuckets:
         sparse: parallel/sparse_rows.SparseTables — its tables get a bucket of their own whose
         "all-reduce" is the touched-row exchange (averaged like the dense buckets)."""
         self.flat = flat
+        self.bucket_mb = float(bucket_mb)
         self.sparse = sparse
         if sparse is not None and reduce == "sum":
             raise ValueError("sparse gradient tables average over ranks (data parallel), not tower placement")

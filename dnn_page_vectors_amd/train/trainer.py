@@ -36,7 +36,7 @@ from ..ops._common import precision_scope
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
 from ..parallel import placement
-from ..parallel import sparse_rows
+from ..parallel import sparse_rows, topology
 from ..parallel.ddp import GradBuckets, broadcast_params
 from ..parallel.sparse_rows import SparseTables
 from ..utils.metrics import MetricsLogger, hbm_used_gb
@@ -118,7 +118,9 @@ class Trainer:
         self._sink_scanned = set()
         self._pos = {}
         self._acc = None
-        self.buckets = (GradBuckets(self.flat, cfg.grad_bucket_mb, reduce="sum" if self.placement == "tower" else "avg",
+        # bucket size by xGMI message class (parallel/topology.py; an explicit grad_bucket_mb wins)
+        bucket = topology.bucket_mb(topology.grad_mb(self.model), cfg.grad_bucket_mb)
+        self.buckets = (GradBuckets(self.flat, bucket, reduce="sum" if self.placement == "tower" else "avg",
                                     sparse=self.sparse)
                         if self.info.enabled else None)
         self.step = 0
