@@ -281,7 +281,13 @@ class Configuration:
             if k not in types:
                 raise KeyError(f"unknown configuration key {k!r}")
             val = yaml.safe_load(v)
-            if isinstance(getattr(self, k), tuple) and not isinstance(val, (list, tuple)):
+            cur = getattr(self, k)
+            # YAML 1.1 reads "2e-3" (no dot) as a string: coerce to the field's current type
+            if isinstance(val, str) and isinstance(cur, float):
+                val = float(val)
+            elif isinstance(val, str) and isinstance(cur, int) and not isinstance(cur, bool):
+                val = int(val)
+            if isinstance(cur, tuple) and not isinstance(val, (list, tuple)):
                 val = [val]
             kw[k] = val
         return self.replace(**kw)
@@ -348,10 +354,12 @@ def preset_config(name: str) -> Configuration:
     if name in ("longpage_cdssm", "config5_cdssm"):
         # config 5 with the reference's conv tower as the chunk encoder (8 x 512-trigram chunks
         # through the fused conv kernel, chunk vectors mean-pooled)
+        # lr 3e-3: Recall@10 after 500 steps 0.147 (lr 1e-3) -> 0.25 (round-4 sweep, lr 2e-3..2e-2,
+        # softmax scale 20..80, no embedding dropout: profiles/r4_quality/README.md)
         return Configuration(model="chunked", chunk_encoder="cdssm", feature_level="ngram",
                              vocab_hash_size=30000, chunk_len=512, num_chunks=8, query_length=45,
                              document_length=4096, batch_size=512, dtype="bf16", loss_mode="cross_gpu",
-                             J=0, inbatch_gamma=40.0)
+                             J=0, inbatch_gamma=40.0, lr=3e-3)
     if name in ("lstm", "legacy_lstm"):
         return Configuration(model="lstm", feature_level="word", batch_size=64, nb_epoch=2)
     raise KeyError(f"unknown preset {name!r}")

@@ -553,7 +553,7 @@ __device__ __forceinline__ void loader7_emit(const Params& p, int lt, int n) {
   }
 }
 
-template <int DM, int RR>
+template <int DM, int RR, int OPT = 0>
 __device__ __forceinline__ void loader7(const Params& p, char* xl0, int* ids_lds) {
   constexpr int CROWS = cr_of<RR>(), LPPT = lppt_of<RR>(), R = RR;
   static_assert(CROWS <= NLD7, "one loader lane per chunk row for the id / hash publish");
@@ -579,7 +579,7 @@ __device__ __forceinline__ void loader7(const Params& p, char* xl0, int* ids_lds
   int par = 0;  // parity of cur: its LDS buffer and its id / hash slot
   int done_n = -1;  // a sample whose pooled / argmax the MFMA waves wrote before the last barrier
   while (cur.n < p.N) {
-    __syncthreads();  // B_k: buffer par holds chunk k, slot par^1 chunk k+1's ids
+    if constexpr ((OPT & 512) == 0) __syncthreads();  // B_k: buffer par holds chunk k, slot par^1 chunk k+1's ids
     if (c1.n < p.N) {
       // chunk k+2's ids issued first: their latency hides behind the row gathers
       const int tk = lt < CROWS ? chunk_tok<RR>(p, c2, lt) : -1;
@@ -637,7 +637,7 @@ __device__ __forceinline__ void mfma7(const Params& p, int t3base, int t4base, c
   __syncthreads();  // S1 (the loaders publish chunk 0's and 1's ids)
   int par = 0;
   while (cur.n < p.N) {
-    __syncthreads();  // B_k
+    if constexpr ((OPT & 512) == 0) __syncthreads();  // B_k (OPT 512: timing ablation only)
     const char* xl = xl0 + par * (CROWS * ROWB);
     const int tc = cur.c * R;
     const char* abase0 = xl + win_of_row(rsub) * ROWB + chunk_of_kq(kq) * 16;
@@ -661,16 +661,27 @@ __device__ __forceinline__ void mfma7(const Params& p, int t3base, int t4base, c
         bf16x8 a = ab[0];
 #pragma unroll
         for (int u = 0; u + 1 < PF; ++u) ab[u] = ab[u + 1];
-        if (s + PF < NS) ab[PF - 1] = *reinterpret_cast<const bf16x8*>(abase + (s + PF) * 64);
-        else ab[PF - 1] = *reinterpret_cast<const bf16x8*>(anext + (s + PF - NS) * 64);
+        if constexpr ((OPT & 256) == 0) {  // OPT 256: no A-fragment reads (timing ablation only)
+          if (s + PF < NS) ab[PF - 1] = *reinterpret_cast<const bf16x8*>(abase + (s + PF) * 64);
+          else ab[PF - 1] = *reinterpret_cast<const bf16x8*>(anext + (s + PF - NS) * 64);
+        }
         if (s < S3) {
 #pragma unroll
           for (int i = 0; i < N3; ++i) c3[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w3[i][s], c3[i], 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < N4; ++i) c4[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, w4[i][s], c4[i], 0, 0, 0);
+        // OPT 1024: pin the step order (prefetch read, then this step's MFMAs) — left alone,
+        // hipcc pairs two steps' reads and waits for the first right away (PF 1 becomes PF 0
+        // on every other step)
+        if constexpr ((OPT & 1024) != 0) __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (FULL) {
+      if constexpr ((OPT & 128) != 0) {  // OPT 128: sum instead of max/argmax (timing ablation only)
+#pragma unroll
+        for (int i = 0; i < N3; ++i) m3[i] += c3[i];
+#pragma unroll
+        for (int i = 0; i < N4; ++i) m4[i] += c4[i];
+      } else if constexpr (FULL) {
 #pragma unroll
         for (int i = 0; i < N3; ++i)
 #pragma unroll
@@ -752,7 +763,7 @@ __global__ __launch_bounds__(NTH7, 1) void conv_pool_fwd7_kernel(Params p) {
   int* ids_lds = reinterpret_cast<int*>(smem + 2 * CROWS * ROWB);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave >= 8) {
-    loader7<DM, RR>(p, xl, ids_lds);
+    loader7<DM, RR, OPT>(p, xl, ids_lds);
     return;
   }
   if constexpr ((OPT & 1) != 0) {
@@ -893,9 +904,19 @@ PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpac
     case 4096 + 512 + 8: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 8, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     case 4096 + 512 + 128: hipLaunchKernelGGL((conv_pool_fwd4_kernel<2, 128, 13, 1>), dim3(grid), dim3(NTHREADS), 0, st, p); break;
     // v7: role-split workgroup (8 MFMA waves + 4 loader waves), 16384 + 64 * PF + OPT
-    case 0:  // production: v7, A prefetch depth 1 (same process at the bench shape: 4.838 vs v4 5.349 ms)
-    case 16384 + 64 + 5: PV_CONV_DM(conv_pool_fwd7_kernel, NTH7, 1, 5, 112) break;
+    case 0:  // production: v7, A prefetch depth 1, pinned K-step order (same process at the bench shape:
+             // 4.858 vs 5.025 ms unpinned; v4 5.349 vs unpinned v7 4.838 on another box)
+    case 16384 + 64 + 5 + 1024: PV_CONV_DM(conv_pool_fwd7_kernel, NTH7, 1, 5 + 1024, 112) break;
+    case 16384 + 64 + 5: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
     case 16384 + 128 + 5: hipLaunchKernelGGL((conv_pool_fwd7_kernel<2, 5, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    // pinned step order (OPT 1024) at A prefetch depth 2 / 3
+    case 16384 + 128 + 5 + 1024: hipLaunchKernelGGL((conv_pool_fwd7_kernel<2, 5 + 1024, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    case 16384 + 192 + 5 + 1024: hipLaunchKernelGGL((conv_pool_fwd7_kernel<3, 5 + 1024, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    // timing ablations of v7 (wrong outputs): +128 max-only epilogue, +256 no A reads, +512 no chunk barriers
+    case 16384 + 64 + 5 + 128: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5 + 128, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    case 16384 + 64 + 5 + 256: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5 + 256, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    case 16384 + 64 + 5 + 512: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5 + 512, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
+    case 16384 + 64 + 5 + 896: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5 + 896, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
     default: return -3;
   }
 #undef PV_CONV_DM

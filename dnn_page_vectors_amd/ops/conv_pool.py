@@ -156,7 +156,7 @@ DENSE_DX_MAXL = 64
 FWD_EMIT = os.environ.get("PAGEVEC_FWD_EMIT", "1") != "0"
 
 
-V7_DBG = (16384 + 64 + 5, 16384 + 128 + 5)  # pv_conv_set_dbg variants with the loader-wave key emit
+V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5)  # pv_conv_set_dbg variants with the loader key emit
 
 
 def _conv_dbg() -> int:

@@ -73,3 +73,13 @@ def test_config_validation_and_precision_scope():
     assert get_backend() == before
     with precision_scope(Configuration(dtype="bf16")):
         assert get_backend() == before
+
+
+def test_override_coerces_yaml_strings_to_the_field_type():
+    """`--set lr=2e-3`: YAML 1.1 parses exponent floats without a dot as strings."""
+    from dnn_page_vectors_amd.config import Configuration
+
+    c = Configuration().override(["lr=2e-3", "inbatch_gamma=60", "batch_size=64"])
+    assert c.lr == 2e-3 and isinstance(c.lr, float)
+    assert c.inbatch_gamma == 60.0 and isinstance(c.inbatch_gamma, float)
+    assert c.batch_size == 64

@@ -153,7 +153,7 @@ def test_dtable_reduce_long_runs_match_reduce4(epw, variant):
     assert grads[0].abs().sum() > 0
 
 
-@pytest.mark.parametrize("variant", [0, 16384 + 128 + 5])
+@pytest.mark.parametrize("variant", [0, 16384 + 64 + 5, 16384 + 128 + 5])
 @pytest.mark.parametrize("N,L,p,mode", [(300, 45, 0.25, "element"), (40, 2000, 0.25, "element"), (7, 130, 0.25, "element"),
                                         (9, 301, 0.0, "element"), (9, 301, 0.3, "element"), (9, 301, 0.25, "token")])
 def test_conv_forward_role_split_bit_identical(variant, N, L, p, mode):
@@ -1555,6 +1555,65 @@ def test_cdssm_training_curve_hip_matches_torch():
     assert tail_h < 0.9 * lh[0] and tail_t < 0.9 * lt[0]  # both learn
     assert abs(tail_h - tail_t) < 0.05 * tail_t, (tail_h, tail_t)
     assert abs(rh - rt) < 0.05, (rh, rt)
+
+
+def _curve_parity(preset, overrides, steps, num_pages=4096, eval_pairs=1024, seed=21):
+    """Train the same initial model on the same batches (same dropout seeds) through the HIP
+    kernels (bf16) and through eager fp32 PyTorch ops; -> {dtype: (losses, Recall@10)}."""
+    import copy
+
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.eval.retrieval import recall_at_k
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    base = preset_config(preset).replace(**overrides)
+    V = base.vocab_hash_size
+    torch.manual_seed(seed)
+    m0 = build_model(base, V)
+    out = {}
+    cudnn_prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False  # fp32 arm: no MIOpen kernel search on a fresh box
+    try:
+        for dtype in ("bf16", "fp32"):
+            cfg = base.replace(dtype=dtype)
+            model = copy.deepcopy(m0)
+            model.cfg = cfg
+            tr = Trainer(cfg, model, torch.device(DEV))
+            data = SyntheticPairs(spec_from_config(cfg, V, num_pages=num_pages), DEV, seed=77)
+            losses = [float(tr.train_step(*data.batch(cfg.batch_size))["loss"]) for _ in range(steps)]
+            qe, pe = data.eval_set(eval_pairs)
+            with torch.no_grad():
+                r = recall_at_k(model.encode(qe, "query"), model.encode(pe, "doc"),
+                                torch.arange(eval_pairs, device=DEV), k=10)
+            out[dtype] = (losses, r)
+    finally:
+        torch.backends.cudnn.enabled = cudnn_prev
+    return out
+
+
+@pytest.mark.parametrize("preset,overrides,steps,learn,pages", [
+    ("longpage_cdssm", dict(batch_size=128, num_chunks=4, chunk_len=256, document_length=1024), 200, 0.97, 512),
+    ("bert_dp8", dict(bert_layers=2, batch_size=32, document_length=64, query_length=16, lr=3e-4), 200, 0.9, 256),
+])
+def test_new_config_training_curve_hip_matches_torch(preset, overrides, steps, learn, pages):
+    """the fp32-torch parity arm for the chunked-CDSSM (config 5, conv chunk
+    encoder) and BERT (config 4) presets, as for the CDSSM headline: the HIP step (bf16 MFMA,
+    fused kernels) learns what the fp32 PyTorch implementation of the same model learns, so a
+    quality gap between presets is the model / recipe, not the kernels."""
+    out = _curve_parity(preset, overrides, steps, num_pages=pages)  # a small page pool: it can be learned
+    (lh, rh), (lt, rt) = out["bf16"], out["fp32"]
+    k = max(10, steps // 6)
+    tail_h, tail_t = sum(lh[-k:]) / k, sum(lt[-k:]) / k
+    print(f"{preset} HIP bf16: loss {lh[0]:.3f} -> {tail_h:.3f}, R@10 {rh:.3f} | torch fp32: loss {lt[0]:.3f} -> "
+          f"{tail_t:.3f}, R@10 {rt:.3f}")
+    assert abs(lh[0] - lt[0]) < 0.02 * lt[0]
+    assert tail_h < learn * lh[0] and tail_t < learn * lt[0]  # both learn
+    assert abs(tail_h - tail_t) < 0.08 * tail_t, (tail_h, tail_t)
+    assert abs(rh - rt) < 0.08, (rh, rt)
 
 
 @pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, False), (True, True)])

@@ -1,0 +1,18 @@
+# Round 4: quality -- parity arms, CDSSM lr sweep (bench quality phase), chunked-CDSSM recipe sweep
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r4_quality
+export TMPDIR=/tmp
+
+
+summ() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d.get("recall_at_10"), d.get("loss_after_quality_steps"))'; }
+for S in "lr=2e-3" "lr=3e-3"; do
+  ARGS=""; for kv in $S; do ARGS="$ARGS --set $kv"; done
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --eager-compare 0 $ARGS > "gpurun_out/r4_quality/cdssm_${S}.log" 2>&1
+  rc=$?; echo "cdssm [$S] rc=$rc $(tail -1 "gpurun_out/r4_quality/cdssm_${S}.log" | summ 2>&1 | tail -1)"; [ $rc -eq 0 ] || exit $rc
+done
+i=0
+for S in "" "lr=3e-3" "inbatch_gamma=60" "lr=3e-3 inbatch_gamma=60" "dropout_prob=[0.0,0.5]"; do
+  i=$((i+1)); ARGS=""; for kv in $S; do ARGS="$ARGS --set $kv"; done
+  timeout -k 10 300 python -u bench.py --model chunked_cdssm --steps 10 --warmup 3 --eager-compare 0 $ARGS > gpurun_out/r4_quality/cc_$i.log 2>&1
+  rc=$?; echo "chunked_cdssm [$S] rc=$rc $(tail -1 gpurun_out/r4_quality/cc_$i.log | summ 2>&1 | tail -1)"; [ $rc -eq 0 ] || exit $rc
+done
