@@ -968,12 +968,15 @@ def test_embedding_bag_counts_split_k():
 
 
 def test_cdssm_recall_quality_guard():
-    """Training-quality guard for the headline config: 1000 steps of CDSSM-300d (B 4096,
-    cross-GPU loss on one rank, in-batch softmax scale 40) on fresh synthetic batches must
-    reach Recall@10 >= 0.30 on held-out pairs (2x the reference-head plateau).  The
-    float-atomic gradient sums make runs differ: 0.36 (this test, round 3) to 0.41-0.45
-    (driver and builder benches, BENCH_r02.json 0.413, round-3 runs 0.443 / 0.452).  A kernel regression that halves the learning signal lands
-    near the reference-head plateau (~0.15-0.2, profiles/quality_r2_final.md) and fails."""
+    """Training-quality guard for the headline config, on bench.py's own protocol (so it
+    guards the number the driver reports): CDSSM-300d (B 4096, cross-GPU loss on one rank,
+    in-batch softmax scale 40), 25 steps cycling a pool of 4 pre-built batches (bench warmup +
+    timed steps), then fresh synthetic batches up to 1000 steps; Recall@10 on the bench's 2048
+    held-out pairs must reach 0.38.  This protocol measures 0.443-0.452 (round-3 / round-4
+    driver and builder benches); 1000 fresh-batch steps alone give 0.35-0.40 over data seeds
+    and reduction modes (tools/recall_spread.py, profiles/r4_quality/).  A kernel regression
+    that halves the learning signal lands near the reference-head plateau (~0.15-0.2,
+    profiles/quality_r2_final.md) and fails."""
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
     from dnn_page_vectors_amd.eval.retrieval import recall_at_k
@@ -987,9 +990,12 @@ def test_cdssm_recall_quality_guard():
     model = build_model(cfg, V)
     tr = Trainer(cfg, model, torch.device(DEV))
     data = SyntheticPairs(spec_from_config(cfg, V, num_pages=65536), DEV, seed=1337)
-    for _ in range(1000):
+    pool = [data.batch(cfg.batch_size) for _ in range(4)]
+    for i in range(25):
+        m = tr.train_step(*pool[i % 4])
+    for _ in range(1000 - 25):
         m = tr.train_step(*data.batch(cfg.batch_size))
-    qe, pe = data.eval_set(2048)
+    qe, pe = data.eval_set(2048, seed=7)
     qv, pv = model.encode(qe, "query"), model.encode(pe, "doc")
     r = recall_at_k(qv, pv, torch.arange(2048, device=DEV), k=10)
     # the HIP top-k agrees with an exact torch top-k on the same (bf16) vectors
@@ -1000,7 +1006,7 @@ def test_cdssm_recall_quality_guard():
     assert float(m["loss"]) == float(m["loss"])
     print(f"recall@10 after 1000 steps: {r:.4f} (exact top-k {r_ref:.4f})")
     assert abs(r - r_ref) <= 2.0 / 2048, (r, r_ref)
-    assert r >= 0.30, r
+    assert r >= 0.38, r
 
 
 def test_resume_restores_device_adam_step(tmp_path):
