@@ -283,7 +283,7 @@ class Configuration:
             val = yaml.safe_load(v)
             cur = getattr(self, k)
             # YAML 1.1 reads "2e-3" (no dot) as a string: coerce to the field's current type
-            if isinstance(val, str) and isinstance(cur, float):
+            if isinstance(val, (str, int)) and not isinstance(val, bool) and isinstance(cur, float):
                 val = float(val)
             elif isinstance(val, str) and isinstance(cur, int) and not isinstance(cur, bool):
                 val = int(val)

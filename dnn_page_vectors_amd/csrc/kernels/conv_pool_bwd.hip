@@ -13,13 +13,14 @@
 // (same function as the forward staging), never stored.
 //
 // dTable without 17M x 400-byte float atomics:
-//   emit   : one thread per (n, f) writes its 4 slot keys (token id, sentinel V when
-//            dead) + slot ids, and one {g*scale, argmax} record per pair;
-//   sort   : stable radix sort of (key, slot id) (sort.hip);
-//   reduce : each wave walks 64 sorted entries, 4 at a time (one per 16-lane group),
+//   keys   : the slot keys (token id, sentinel V when dead) of every (n, f) pair — written
+//            by the conv forward's loader waves (conv_pool_fwd.hip, loader7_emit), or by
+//            the emit kernel here — plus one {g*scale, argmax} record per pair;
+//   sort   : stable radix sort of (key, slot id) (radix_sort.hip);
+//   reduce : each wave walks EPW sorted entries, 4 at a time (one per 16-lane group),
 //            recomputes the contribution s*g*W[f,j,:]*m on the fly (bf16 W rows are
-//            L2-resident) and sums it in registers per token; one row-atomic per
-//            (chunk, token) boundary.
+//            L2-resident) and sums it in registers per token, carrying its open run
+//            across sub-chunks; one row-atomic per (wave, token) boundary.
 #include "common.h"
 
 namespace pv {
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(256) void conv_bwd_emit3_kernel(const float* gpool,
   }
 }
 
-// ---- dTable reduce, 4 entries per wave-instruction ------------------------------------
+// ---- dTable reduce: the round (4 entries per wave-instruction) --------------------------
 // A 16-lane group owns one sorted entry per round (4 entries per round per wave); lane p
 // of the group owns columns 8p..8p+7 of the 104-wide padded row: one 16-byte load of the
 // bf16 weight row W[f][j] (layout [2*FW][4][EP], zero padded), the two dropout group
@@ -279,105 +280,8 @@ __device__ __forceinline__ void reduce4_flush(float* slab, const float (&acc)[8]
   __builtin_amdgcn_s_waitcnt(0xC07F);  // slab reads done before the next flush overwrites it
 }
 
-__global__ __launch_bounds__(256) void conv_bwd_reduce4_kernel(const unsigned* __restrict__ skeys,
-                                                               const unsigned* __restrict__ svals,
-                                                               const int2* __restrict__ rec,
-                                                               const unsigned short* __restrict__ wrow,
-                                                               float* __restrict__ dtable, long M, int L, int E,
-                                                               int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
-  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
-  if (seed_ptr) seed += *seed_ptr;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, p = lane & 15;
-  float* slab = slabs[wave];
-  const long chunk = (long)blockIdx.x * 4 + wave;
-  const long b = chunk * 64;
-  if (b >= M) return;
-  const long i = b + lane;
-  unsigned key = (unsigned)V, fj = 0, hr = 0;
-  float gg = 0.f;
-  if (i < M) {
-    key = skeys[i];
-    PV_CHECK(key <= (unsigned)V, PV_ERR_KEY);
-    const unsigned sl = key < (unsigned)V ? svals[i] : 0u;
-    if (key < (unsigned)V && PV_OK((long)sl < M, PV_ERR_SLOT)) {
-      unsigned nn, f, j;
-      slot_decode(sl, nn, f, j);
-      const int2 rc = rec[nn * (2 * FW) + f];
-      fj = (f << 2) | j;
-      gg = __int_as_float(rc.x);
-      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)rc.y + j);
-    }
-  }
-  const int n = __popcll(__ballot(key < (unsigned)V));  // live entries are a prefix (sorted)
-  if (n == 0) return;
-  unsigned cur = __builtin_amdgcn_readfirstlane(key);
-  const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);  // largest live key
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const bool act = p < RPIECES;
-  for (int r0 = 0; r0 < n; r0 += 4) {
-    const int e = r0 + g;                 // this group's entry (lane index in the wave)
-    const bool valid = e < n;
-    const int src = (valid ? e : r0) * 4;
-    unsigned kg = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
-    const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
-    float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
-    const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
-    if (!valid) ge = 0.f;
-    // contribution of this group's entry to columns 8p..8p+7
-    float v[8];
-    {
-      u32x4 w = u32x4{0u, 0u, 0u, 0u};
-      if (act) w = *reinterpret_cast<const u32x4*>(wrow + (size_t)f_j * EP + 8 * p);
-      if (thr > 0) {  // zero the dropped columns of the weight row (bf16 pairs)
-        if (token_mode) {
-          const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
-          w &= u32x4{k, k, k, k};
-        } else {
-          w &= keep_piece(he, p, thr);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
-        v[k] = ge * __uint_as_float(wk);
-      }
-    }
-    // keys of the 4 groups (ascending); groups past the live prefix take the largest live
-    // key (keeps the order ascending, so k0 == k3 == cur still means "all equal") and v = 0
-    if (!valid) kg = klast;
-    const unsigned k0 = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
-    const unsigned k3 = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
-    if (k0 == cur && k3 == cur) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += v[k];
-      continue;
-    }
-    // boundary round: runs end inside it
-    bool done = false;
-    for (int it = 0; it < 5; ++it) {
-      const bool mine = !done && kg == cur;
-      if (mine) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += v[k];
-        done = true;
-      }
-      const unsigned long long left = __ballot(!done);
-      if (left == 0) break;
-      reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-      cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
-    }
-  }
-  reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-}
-
 // ---- dTable reduce, long runs: each wave owns EPW consecutive sorted entries --------------
-// Same per-round arithmetic as reduce4, but a wave walks EPW entries (64 per sub-chunk) and
+// The rounds above, with a wave walking EPW entries (64 per sub-chunk) and
 // carries its open run (key + register partials) across sub-chunks, so a token whose run
 // spans many sub-chunks is flushed once per wave instead of once per 64 entries: under the
 // Zipf token distribution of real (and synthetic) pages the most frequent rows otherwise
@@ -395,118 +299,10 @@ __device__ __forceinline__ void rd_meta(const KT* __restrict__ skeys, const unsi
   }
 }
 
-template <typename KT>
-__global__ __launch_bounds__(256) void conv_bwd_reduce5_kernel(const KT* __restrict__ skeys,
-                                                               const unsigned* __restrict__ svals,
-                                                               const int2* __restrict__ rec,
-                                                               const unsigned short* __restrict__ wrow,
-                                                               float* __restrict__ dtable, long M, int EPW, int L,
-                                                               int E, int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
-  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
-  if (seed_ptr) seed += *seed_ptr;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, p = lane & 15;
-  float* slab = slabs[wave];
-  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
-  if (wbeg >= M) return;
-  const long wend = min(M, wbeg + (long)EPW);
-  const unsigned UV = (unsigned)V;
-  // pipeline: (k0, s0, r0) = current sub-chunk, (k1, s1) = next, (k2, s2) = the one after
-  unsigned k0, s0, k1, s1, k2, s2;
-  rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
-  rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
-  auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
-    if (!(key < UV && PV_OK((long)sl < M, PV_ERR_SLOT))) return int2{0, 0};
-    unsigned nn, f, j;
-    slot_decode(sl, nn, f, j);
-    return rec[nn * (2 * FW) + f];
-  };
-  int2 r0 = ld_rec(k0, s0);
-  unsigned cur = UV;
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const bool act = p < RPIECES;
-  for (long b = wbeg; b < wend; b += 64) {
-    rd_meta(skeys, svals, b + 128 + lane, wend, UV, k2, s2);
-    const int2 r1 = ld_rec(k1, s1);
-    // this lane's entry of sub-chunk b
-    const unsigned key = k0;
-    unsigned fj = 0, hr = 0;
-    float gg = 0.f;
-    if (key < UV) {
-      unsigned nn, f, j;
-      slot_decode(s0, nn, f, j);
-      fj = (f << 2) | j;
-      gg = __int_as_float(r0.x);
-      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
-    }
-    const int n = __popcll(__ballot(key < UV));  // live entries are a prefix (sorted)
-    if (n == 0) break;
-    if (cur == UV) cur = __builtin_amdgcn_readfirstlane(key);
-    const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);
-    for (int q0 = 0; q0 < n; q0 += 4) {
-      const int e = q0 + g;
-      const bool valid = e < n;
-      const int src = (valid ? e : q0) * 4;
-      unsigned kg = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
-      const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
-      float ge = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
-      const unsigned he = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
-      if (!valid) ge = 0.f;
-      float v[8];
-      {
-        u32x4 w = u32x4{0u, 0u, 0u, 0u};
-        if (act) w = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * p));
-        if (thr > 0) {
-          if (token_mode) {
-            const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
-            w &= u32x4{k, k, k, k};
-          } else {
-            w &= keep_piece(he, p, thr);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
-          v[k] = ge * __uint_as_float(wk);
-        }
-      }
-      if (!valid) kg = klast;
-      const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
-      const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
-      if (ka == cur && kb == cur) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += v[k];
-        continue;
-      }
-      bool done = false;
-      for (int it = 0; it < 5; ++it) {
-        const bool mine = !done && kg == cur;
-        if (mine) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] += v[k];
-          done = true;
-        }
-        const unsigned long long left = __ballot(!done);
-        if (left == 0) break;
-        reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-        cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
-      }
-    }
-    if (n < 64) break;  // the dead (key == V) tail starts inside this sub-chunk
-    k0 = k1; s0 = s1; r0 = r1;
-    k1 = k2; s1 = s2;
-  }
-  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-}
-
-// reduce7 = reduce5 with the dropout mode as a template parameter (DM: 0 off, 1 element
-// p = 0.25, 2 element any p, 3 token) and the common round's multiply + add as packed FMAs
-// (reduce5: a separate v = g * w pass, then 8 adds).
+// DM: dropout mode as a template parameter (0 off, 1 element p = 0.25, 2 element any p,
+// 3 token); the common round's multiply + add are packed FMAs.  Earlier generations (a
+// 64-entry-per-wave kernel, a runtime dropout mode, RB rounds of row gathers in flight) were
+// measured slower and removed: docs/PERF.md "dTable reduce generations".
 // OCC: minimum waves per SIMD the register allocation must allow (1 = compiler's choice,
 // 74 VGPRs / 6 waves; 8 caps it at 64 VGPRs)
 template <typename KT, int DM, int OCC = 1>
@@ -624,131 +420,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   }
   if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 }
-
-// reduce6 = reduce5 with the weight-row gathers of RB rounds (4 entries each) issued
-// together before any is consumed: reduce5 waits on each round's 16-byte L2 gather before
-// its FMAs (one load in flight per wave); here RB loads are in flight per wave.  Same
-// per-entry arithmetic and flush order as reduce5 (identical per-wave partial sums).
-template <typename KT, int RB>
-__global__ __launch_bounds__(256) void conv_bwd_reduce6_kernel(const KT* __restrict__ skeys,
-                                                               const unsigned* __restrict__ svals,
-                                                               const int2* __restrict__ rec,
-                                                               const unsigned short* __restrict__ wrow,
-                                                               float* __restrict__ dtable, long M, int EPW, int L,
-                                                               int E, int V, unsigned seed, const unsigned* seed_ptr,
-                                                               unsigned row_offset, int thr, int token_mode, long long* fx) {
-  static_assert(RB >= 1 && 16 % RB == 0, "RB rounds of 4 entries tile a 64-entry sub-chunk");
-  __shared__ __attribute__((aligned(16))) float slabs[4][4 * EP];
-  if (seed_ptr) seed += *seed_ptr;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, p = lane & 15;
-  float* slab = slabs[wave];
-  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
-  if (wbeg >= M) return;
-  const long wend = min(M, wbeg + (long)EPW);
-  const unsigned UV = (unsigned)V;
-  unsigned k0, s0, k1, s1, k2, s2;
-  rd_meta(skeys, svals, wbeg + lane, wend, UV, k0, s0);
-  rd_meta(skeys, svals, wbeg + 64 + lane, wend, UV, k1, s1);
-  auto ld_rec = [&](unsigned key, unsigned sl) -> int2 {
-    if (!(key < UV && PV_OK((long)sl < M, PV_ERR_SLOT))) return int2{0, 0};
-    unsigned nn, f, j;
-    slot_decode(sl, nn, f, j);
-    return rec[nn * (2 * FW) + f];
-  };
-  int2 r0 = ld_rec(k0, s0);
-  unsigned cur = UV;
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const bool act = p < RPIECES;
-  for (long b = wbeg; b < wend; b += 64) {
-    rd_meta(skeys, svals, b + 128 + lane, wend, UV, k2, s2);
-    const int2 r1 = ld_rec(k1, s1);
-    const unsigned key = k0;
-    unsigned fj = 0, hr = 0;
-    float gg = 0.f;
-    if (key < UV) {
-      unsigned nn, f, j;
-      slot_decode(s0, nn, f, j);
-      fj = (f << 2) | j;
-      gg = __int_as_float(r0.x);
-      if (thr > 0) hr = dropout_row_hash(seed, row_offset + nn * (unsigned)L + (unsigned)r0.y + j);
-    }
-    const int n = __popcll(__ballot(key < UV));
-    if (n == 0) break;
-    if (cur == UV) cur = __builtin_amdgcn_readfirstlane(key);
-    const unsigned klast = (unsigned)__builtin_amdgcn_readlane((int)key, n - 1);
-    for (int qb = 0; qb < n; qb += 4 * RB) {
-      unsigned kgs[RB], hes[RB];
-      float ges[RB];
-      u32x4 ws[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {  // issue: every round's metadata exchange + row gather
-        const int e = qb + 4 * r + g;
-        const bool valid = e < n;
-        const int src = (valid ? e : 0) * 4;
-        kgs[r] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)key);
-        const unsigned f_j = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)fj);
-        ges[r] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(gg)));
-        hes[r] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)hr);
-        if (!valid) {
-          ges[r] = 0.f;
-          kgs[r] = klast;
-        }
-        ws[r] = u32x4{0u, 0u, 0u, 0u};
-        if (act && valid) ws[r] = *reinterpret_cast<const u32x4*>(wrow + (unsigned)(f_j * EP + 8 * p));
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {  // consume in entry order (reduce5's arithmetic)
-        if (qb + 4 * r >= n) break;
-        u32x4 w = ws[r];
-        if (thr > 0) {
-          if (token_mode) {
-            const unsigned k = ((int)(hes[r] & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
-            w &= u32x4{k, k, k, k};
-          } else {
-            w &= keep_piece(hes[r], p, thr);
-          }
-        }
-        float v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const unsigned wk = (k & 1) ? (w[k >> 1] & 0xFFFF0000u) : (w[k >> 1] << 16);
-          v[k] = ges[r] * __uint_as_float(wk);
-        }
-        const unsigned kg = kgs[r];
-        const unsigned ka = (unsigned)__builtin_amdgcn_readlane((int)kg, 0);
-        const unsigned kb = (unsigned)__builtin_amdgcn_readlane((int)kg, 48);
-        if (ka == cur && kb == cur) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] += v[k];
-          continue;
-        }
-        bool done = false;
-        for (int it = 0; it < 5; ++it) {
-          const bool mine = !done && kg == cur;
-          if (mine) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[k] += v[k];
-            done = true;
-          }
-          const unsigned long long left = __ballot(!done);
-          if (left == 0) break;
-          reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-          cur = (unsigned)__builtin_amdgcn_readlane((int)kg, (int)__builtin_ctzll(left));
-        }
-      }
-    }
-    if (n < 64) break;
-    k0 = k1; s0 = s1; r0 = r1;
-    k1 = k2; s1 = s2;
-  }
-  if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
-}
-
 
 // ---- dTable for short sequences (query towers: L <= DENSE_MAXL) ------------------------------
 // A 45-token query has ~45 touched embedding rows but 1050 (f, j) gradient entries, so the
@@ -1054,24 +725,6 @@ PV_API int pv_conv_pool_bwd_emit3(const float* gpool, const float* pooled, const
   return 0;
 }
 
-// wrow: bf16 [2*FW][4][EP] weight rows (zero padded); requires E <= EP.
-// epw: sorted entries per wave (multiple of 64); 0 = the 64-entry reduce4 kernel.
-PV_API int pv_conv_pool_bwd_reduce5(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
-                                    float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
-                                    const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                                    void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63) || (long)V * E >= (1L << 32)) return -1;
-  const long waves = (M + epw - 1) / epw;
-  const DetAcc det((size_t)V * E, (hipStream_t)stream);
-  if (det.err) return det.err;
-  hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                     skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed,
-                     seed_ptr, row_offset, thr, token_mode, det.fx);
-  PV_LAUNCH_CHECK();
-  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
-}
-
 // Records only (the keys were written by the conv forward's epilogue, conv_pool_fwd.hip
 // emit_keys): rec[pair] = {g * scale, argmax}, one coalesced pass.
 __global__ __launch_bounds__(256) void conv_bwd_rec_kernel(const float* __restrict__ gpool,
@@ -1103,52 +756,33 @@ PV_API int pv_conv_pool_bwd_emit3_u16(const float* gpool, const float* pooled, c
   return 0;
 }
 
-PV_API int pv_conv_pool_bwd_reduce5_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
-                                        float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
-                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                                        void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
-  const long waves = (M + epw - 1) / epw;
-  const DetAcc det((size_t)V * E, (hipStream_t)stream);
-  if (det.err) return det.err;
-  hipLaunchKernelGGL(conv_bwd_reduce5_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                     (hipStream_t)stream, (const unsigned short*)skeys, svals, (const int2*)rec,
-                     (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
-                     token_mode, det.fx);
-  PV_LAUNCH_CHECK();
-  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
-}
-
-// reduce7 (compile-time dropout mode, packed FMAs), 2-byte keys; same arguments as reduce5.
-// reduce7 occupancy (tools/reduce_ab.py, same process at the bench shape): capped at 64 VGPRs
+// reduce7 occupancy (same process at the bench shape): capped at 64 VGPRs
 // (8 waves / SIMD, 2 VGPRs spilled) 0.443 ms vs 0.473 ms at the compiler's 74 VGPRs (6 waves);
 // PMC: 47% of wave-cycles parked at s_waitcnt, 26% L2 miss rate (the random {g, argmax}
 // record gathers) — latency-bound, so more waves pay.  PAGEVEC_R7_OCC=1 restores 74 VGPRs.
 static int g_r7_occ = getenv("PAGEVEC_R7_OCC") ? atoi(getenv("PAGEVEC_R7_OCC")) : 8;
 PV_API void pv_conv_r7_set_occ(int occ) { g_r7_occ = occ; }
 
-PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
-                                        float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
-                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                                        void* stream) {
+template <typename KT>
+int launch_reduce7(const void* skeys, const unsigned* svals, const void* rec, const void* wrow, float* dtable, long M,
+                   int epw, int L, int E, int V, unsigned seed, const unsigned* seed_ptr, unsigned row_offset,
+                   int thr, int token_mode, hipStream_t st) {
   using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
+  if (E > EP || epw < 64 || (epw & 63) || (sizeof(KT) == 2 && V >= 65535) || (long)V * E >= (1L << 32)) return -1;
   const long waves = (M + epw - 1) / epw;
   const dim3 grid((unsigned)((waves + 3) / 4));
-  hipStream_t st = (hipStream_t)stream;
   const DetAcc det((size_t)V * E, st);
   if (det.err) return det.err;
   const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
 #define PV_R7(DMV)                                                                                               \
   if (g_r7_occ == 8)                                                                                             \
-    hipLaunchKernelGGL((conv_bwd_reduce7_kernel<unsigned short, DMV, 8>), grid, dim3(256), 0, st,                \
-                       (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, \
-                       M, epw, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx);                    \
+    hipLaunchKernelGGL((conv_bwd_reduce7_kernel<KT, DMV, 8>), grid, dim3(256), 0, st, (const KT*)skeys, svals,   \
+                       (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr,    \
+                       row_offset, thr, token_mode, det.fx);                                                     \
   else                                                                                                           \
-  hipLaunchKernelGGL((conv_bwd_reduce7_kernel<unsigned short, DMV>), grid, dim3(256), 0, st,                     \
-                     (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, \
-                     epw, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx)
+    hipLaunchKernelGGL((conv_bwd_reduce7_kernel<KT, DMV>), grid, dim3(256), 0, st, (const KT*)skeys, svals,      \
+                       (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, L, E, V, seed, seed_ptr,    \
+                       row_offset, thr, token_mode, det.fx)
   switch (dm) {
     case 0: PV_R7(0); break;
     case 1: PV_R7(1); break;
@@ -1160,32 +794,23 @@ PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals
   return det.finish(dtable, (size_t)V * E, st);
 }
 
-// reduce6 (RB rounds of row gathers in flight per wave); rb in {2, 4, 8, 16}, 2-byte keys.
-PV_API int pv_conv_pool_bwd_reduce6_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
+// skeys: sorted 2-byte (V < 65535) or 4-byte token keys (dead sentinel V), svals their slots;
+// rec: {g * scale, argmax} per (n, f); wrow: bf16 [2*FW][4][EP] weight rows; epw: sorted entries
+// per wave (multiple of 64)
+PV_API int pv_conv_pool_bwd_reduce7_u16(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
                                         float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
-                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode, int rb,
+                                        const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
                                         void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63) || V >= 65535) return -1;
-  const long waves = (M + epw - 1) / epw;
-  const dim3 grid((unsigned)((waves + 3) / 4));
-  hipStream_t st = (hipStream_t)stream;
-  const DetAcc det((size_t)V * E, st);
-  if (det.err) return det.err;
-#define PV_R6(RBV)                                                                                                   \
-  hipLaunchKernelGGL((conv_bwd_reduce6_kernel<unsigned short, RBV>), grid, dim3(256), 0, st,                         \
-                     (const unsigned short*)skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, epw, \
-                     L, E, V, seed, seed_ptr, row_offset, thr, token_mode, det.fx)
-  switch (rb) {
-    case 2: PV_R6(2); break;
-    case 4: PV_R6(4); break;
-    case 8: PV_R6(8); break;
-    case 16: PV_R6(16); break;
-    default: return -2;
-  }
-#undef PV_R6
-  PV_LAUNCH_CHECK();
-  return det.finish(dtable, (size_t)V * E, st);
+  return launch_reduce7<unsigned short>(skeys, svals, rec, wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset,
+                                        thr, token_mode, (hipStream_t)stream);
+}
+
+PV_API int pv_conv_pool_bwd_reduce7(const void* skeys, const unsigned* svals, const void* rec, const void* wrow,
+                                    float* dtable, long M, int epw, int L, int E, int V, unsigned seed,
+                                    const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
+                                    void* stream) {
+  return launch_reduce7<unsigned>(skeys, svals, rec, wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
+                                  token_mode, (hipStream_t)stream);
 }
 
 // Short-sequence dTable, step 1: rows (N*L, EP) fp32 (touched rows written), keys (N*L) u16
@@ -1242,20 +867,3 @@ PV_API int pv_conv_bwd_rows_reduce(const void* skeys, int key_bytes, const unsig
   PV_LAUNCH_CHECK();
   return det.finish(dtable, (size_t)V * E, st);
 }
-
-PV_API int pv_conv_pool_bwd_reduce4(const unsigned* skeys, const unsigned* svals, const void* rec, const void* wrow,
-                                    float* dtable, long M, int L, int E, int V, unsigned seed,
-                                    const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                                    void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || (long)V * E >= (1L << 32)) return -1;
-  const long chunks = (M + 63) / 64;
-  const DetAcc det((size_t)V * E, (hipStream_t)stream);
-  if (det.err) return det.err;
-  hipLaunchKernelGGL(conv_bwd_reduce4_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                     skeys, svals, (const int2*)rec, (const unsigned short*)wrow, dtable, M, L, E, V, seed,
-                     seed_ptr, row_offset, thr, token_mode, det.fx);
-  PV_LAUNCH_CHECK();
-  return det.finish(dtable, (size_t)V * E, (hipStream_t)stream);
-}
-

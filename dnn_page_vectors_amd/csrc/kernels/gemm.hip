@@ -26,6 +26,7 @@
 // stored; K must be a multiple of 64 (callers pad — the operands here all are).
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace pv {
 namespace gemm {
@@ -398,18 +399,48 @@ __device__ __forceinline__ void epilogue3(const Params& p, f32x4 (&acc)[8][4], i
 // Segment = ds_reads + glds + vmcnt | barrier | lgkmcnt(0) setprio(1) 16 MFMAs setprio(0) | barrier.
 constexpr int HALF_BYTES = 128 * 64 * 2;  // 16 KB: 128 rows x 64 k bf16
 
+// Half tile = 128 operand rows x 64 k.  ROW: [128][64] (128-B rows, chunk c of row r at
+// c ^ (r & 7)); COL: [64 k][128] (256-B k-rows, chunk c of k-row r at c ^ 2h(r): the 4 k-rows
+// x 32 bytes of a 16-lane transposed read land on 4 disjoint bank groups, and the two
+// 16-lane groups of a 32-lane half on different ones through bit 3 of r).
 template <int LAY>
 __device__ __forceinline__ void stage_half(const unsigned short* __restrict__ X, long ld, int r0, int rmax, int k0,
                                            char* dst) {
-  static_assert(LAY == ROW, "v3: row-major operands");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int piece = wave * 2 + u;                  // 0..15, 1 KB each
-    const int r = piece * 8 + (lane >> 3);           // half row 0..127
-    const int c = (lane & 7) ^ (r & 7);
-    const int gr = min(r0 + r, rmax);
-    glds16(X + (size_t)gr * ld + k0 + c * 8, dst + piece * 1024);
+    if constexpr (LAY == ROW) {
+      const int r = piece * 8 + (lane >> 3);         // half row 0..127
+      const int c = (lane & 7) ^ (r & 7);
+      const int gr = min(r0 + r, rmax);
+      glds16(X + (size_t)gr * ld + k0 + c * 8, dst + piece * 1024);
+    } else {
+      const int kr = piece * 4 + (lane >> 4);        // k-row 0..63
+      const int c = (lane & 15) ^ (2 * h_of(kr));    // logical chunk (8 operand rows)
+      int col = r0 + c * 8;
+      col = col <= rmax ? col : 0;                   // groups past the edge: never stored
+      glds16(X + (size_t)(k0 + kr) * ld + col, dst + piece * 1024);
+    }
+  }
+}
+
+// fragment of operand rows [rb, rb + 16) (half-local), k-step s from a staged half tile
+template <int LAY>
+__device__ __forceinline__ bf16x8 frag_h(const char* t, int rb, int s) {
+  if constexpr (LAY == ROW) {
+    return frag<ROW>(t, rb, s);
+  } else {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int klo = 32 * s + 8 * g + q, khi = klo + 4;
+    const int col = rb + 4 * p;
+    const int c = col >> 3, half = (col & 7) * 2;
+    const char* plo = t + klo * 256 + ((c ^ (2 * h_of(klo))) * 16) + half;
+    const char* phi = t + khi * 256 + ((c ^ (2 * h_of(khi))) * 16) + half;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)plo);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)phi);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 }
 
@@ -511,6 +542,168 @@ __global__ __launch_bounds__(NTH, 1) void gemm3_kernel(Params p) {
   epilogue3(p, acc, split, m0, n0, wr, wc, lane);
 }
 
+// ---- v4: the 8-phase schedule, two K tiles per iteration ---------------------------------
+// (cdna_hip_programming.md §5 "The 256² 8-phase template".)  Same wave / quadrant / half-tile
+// decomposition as v3 (a wave owns rows {64 wr + [0, 64)} of both A halves and columns
+// {32 wc + [0, 32)} of both B halves; epilogue3's accumulator map), but the K loop covers two
+// K tiles per iteration — tile T in buffer E (phases 1-4), tile T + 1 in buffer O (phases
+// 5-8) — so every LDS address is a compile-time offset, and the loads wait only twice per
+// iteration (vmcnt(6) in phases 4 and 8: three half-tiles stay in flight, each load gets 4-6
+// phases of latency instead of v3's per-phase 3).  Per phase: fragment reads, one half-tile
+// staged (2 glds per thread), barrier, lgkmcnt(0), 16 MFMAs at priority 1, barrier; waves 4-7
+// run one barrier behind waves 0-3 (on every SIMD an MFMA segment meets a load segment).
+//
+//   phase  reads            MFMAs (A, B)  stages (half -> buffer, tile)      waits
+//   1      B0_E, A0_E       A0 B0         A1 -> O, T+1                      lgkmcnt(8) (B0_E reads)
+//   2      B1_E             A0 B1         B0 -> E, T+2
+//   3      A1_E             A1 B0         A0 -> E, T+2
+//   4      -                A1 B1         B1 -> E, T+2                      vmcnt(6): O complete
+//   5      B0_O, A0_O       A0 B0         A1 -> E, T+2                      lgkmcnt(8)
+//   6      B1_O             A0 B1         B0 -> O, T+3
+//   7      A1_O             A1 B0         A0 -> O, T+3
+//   8      -                A1 B1         B1 -> O, T+3                      vmcnt(6): E complete
+// WAR: every half is restaged >= 2 phases after its last read, or 1 phase after when the
+// reading phase retired those reads (the B reads are issued first and lgkmcnt(8) retires
+// them before that phase's first barrier).  RAW: a buffer is read one phase after the wait
+// that retires it (the staggered group passes that wait's barrier before its reads).
+// Prologue: E = tile kt0 and B0 / A0 / B1 of kt0 + 1 issued, vmcnt(6) -> the steady state
+// at phase 1.  Past the split's end a stage reloads the last tile (uniform counts, never
+// read); an odd tile count skips the MFMAs of the missing tile T + 1 (uniform branch).
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(NTH, 1) void gemm4_kernel(Params p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * HALF_BYTES];  // [E, O][A0 B0 B1 A1]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int grp = wave >> 2, wr = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int split = bid / ntile, t = bid - split * ntile;
+  const int tm = p.n_fastest ? t / p.tiles_n : t % p.tiles_m;
+  const int tn = p.n_fastest ? t % p.tiles_n : t / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = split * per, kt1 = min(ktiles, kt0 + per);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    // half q (0 A0, 1 B0, 2 B1, 3 A1) of tile kt into buffer b (0 E, 1 O)
+    auto stg = [&](int b, int q, int kt) {
+      char* dst = smem + b * 4 * HALF_BYTES + q * HALF_BYTES;
+      const int kk = min(kt, kt1 - 1) * BK;
+      if (q == 0) stage_half<ALAY>(p.A, p.lda, m0, p.M - 1, kk, dst);
+      else if (q == 3) stage_half<ALAY>(p.A, p.lda, m0 + 128, p.M - 1, kk, dst);
+      else stage_half<BLAY>(p.B, p.ldb, n0 + 128 * (q - 1), p.N - 1, kk, dst);
+    };
+    bf16x8 a[4][2], b0[2][2], b1[2][2];
+    const int arow = wr * 64, bcol = wc * 32;
+    auto rd_b = [&](const char* half, bf16x8 (&b)[2][2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) b[j][s2] = frag_h<BLAY>(half, bcol + 16 * j, s2);
+    };
+    auto rd_a = [&](const char* half) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag_h<ALAY>(half, arow + 16 * i, s2);
+    };
+    // the B reads (issued first) retired, the A reads (8 ds_read_b128 or 16 transposed
+    // reads) may stay in flight
+    auto wait_b = [&]() {
+      if constexpr (ALAY == ROW) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+    };
+    // barrier, reads retired, 16 MFMAs of quadrant (AH, BH), barrier
+    auto mma = [&](auto ah_c, auto bh_c, bf16x8 (&b)[2][2], bool live) {
+      constexpr int AH = decltype(ah_c)::value, BH = decltype(bh_c)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (live) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[4 * AH + i][2 * BH + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b[j][s2], acc[4 * AH + i][2 * BH + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    const char* E = smem;
+    const char* O = smem + 4 * HALF_BYTES;
+    // prologue
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stg(0, q, kt0);
+    stg(1, 1, kt0 + 1);
+    stg(1, 0, kt0 + 1);
+    stg(1, 2, kt0 + 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 one barrier behind
+#pragma unroll 1
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      const bool two = kt + 1 < kt1;
+      // phase 1
+      rd_b(E + 1 * HALF_BYTES, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd_a(E + 0 * HALF_BYTES);
+      stg(1, 3, kt + 1);
+      wait_b();
+      mma(I0{}, I0{}, b0, true);
+      // phase 2
+      rd_b(E + 2 * HALF_BYTES, b1);
+      stg(0, 1, kt + 2);
+      mma(I0{}, I1{}, b1, true);
+      // phase 3
+      rd_a(E + 3 * HALF_BYTES);
+      stg(0, 0, kt + 2);
+      mma(I1{}, I0{}, b0, true);
+      // phase 4
+      stg(0, 2, kt + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      mma(I1{}, I1{}, b1, true);
+      // phase 5
+      rd_b(O + 1 * HALF_BYTES, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd_a(O + 0 * HALF_BYTES);
+      stg(0, 3, kt + 2);
+      wait_b();
+      mma(I0{}, I0{}, b0, two);
+      // phase 6
+      rd_b(O + 2 * HALF_BYTES, b1);
+      stg(1, 1, kt + 3);
+      mma(I0{}, I1{}, b1, two);
+      // phase 7
+      rd_a(O + 3 * HALF_BYTES);
+      stg(1, 0, kt + 3);
+      mma(I1{}, I0{}, b0, two);
+      // phase 8
+      stg(1, 2, kt + 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      mma(I1{}, I1{}, b1, two);
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  epilogue3(p, acc, split, m0, n0, wr, wc, lane);
+}
+
 PV_DEBUG_EXPORT(gemm)
 }  // namespace gemm
 }  // namespace pv
@@ -546,7 +739,8 @@ PV_API int pv_gemm_bf16(const void* A, long lda, int a_col, const void* B, long 
     else if (a_col && !b_col) hipLaunchKernelGGL((KER<COL, ROW>), dim3(grid), dim3(NTH), 0, st, p); \
     else hipLaunchKernelGGL((KER<COL, COL>), dim3(grid), dim3(NTH), 0, st, p);                     \
   } while (0)
-  if (g_gemm_sched == 3 && !a_col && !b_col)
+  if (g_gemm_sched == 4) PV_GEMM_LAUNCH(gemm4_kernel);
+  else if (g_gemm_sched == 3 && !a_col && !b_col)
     hipLaunchKernelGGL((gemm3_kernel<ROW, ROW>), dim3(grid), dim3(NTH), 0, st, p);
   else if (g_gemm_sched == 1) PV_GEMM_LAUNCH(gemm_kernel);
   else PV_GEMM_LAUNCH(gemm2_kernel);

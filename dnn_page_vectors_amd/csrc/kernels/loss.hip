@@ -261,6 +261,7 @@ __global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restri
   }
 }
 
+// The S-tile epilogue variants (ROW / CLIP / FWD) of the ib3 and ib5 kernels below:
 // ROW = true : X = queries, Y = docs,    out = dQ, scale indexed by X row
 // ROW = false: X = docs,    Y = queries, out = dD, scale indexed by Y row
 // Each split writes its partial product with plain stores into out (a single split) or
@@ -271,144 +272,11 @@ __global__ void ib_rowsum_kernel(const float* __restrict__ part, float* __restri
 // sum_j exp(g*(S_ij - 1)) into `part` like ib_fwd.  dQ_i is a per-row multiple of U_i
 // (scale_i = g_up_i * gamma / sumexp_i, known only in backward, is a row scalar), so the
 // backward's dQ pass — a third recomputation of S — disappears: dQ = scale * U.
-template <int KS, bool ROW, bool CLIP, bool FWD = false>
-__global__ __launch_bounds__(256, 2) void ib_bwd_kernel(const unsigned short* __restrict__ X,
-                                                         const unsigned short* __restrict__ Y,
-                                                         const float* __restrict__ scale, float* __restrict__ out,
-                                                         float* __restrict__ ws, int nx, int ny, int per_split,
-                                                         float gamma, float* __restrict__ part = nullptr) {
-  static_assert(!FWD || ROW, "the fused forward runs over query rows");
-  using T = IbTile<KS>;
-  constexpr int NC = T::DP / 16;
-  __shared__ __attribute__((aligned(16))) unsigned short yt[2][TD * T::LDY];
-  __shared__ __attribute__((aligned(16))) float ysc[2][TD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int r0 = blockIdx.x * TQ + wave * 32;
-  const int c_begin = blockIdx.y * per_split, c_end = min(ny, c_begin + per_split);
-  const float gl = gamma * 1.4426950408889634f;
-  bf16x8 xb[2][KS];
-  load_xb<KS>(X, r0, nx, xb);
-  float rsc[2] = {0.f, 0.f};
-  float rs[2] = {0.f, 0.f};  // FWD: row sums of exp(g*(S-1))
-  if (ROW) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = r0 + i * 16 + (lane & 15);
-      rsc[i] = FWD ? 1.f : r < nx ? scale[r] : 0.f;
-    }
-  }
-  f32x4 o[NC][2];
-#pragma unroll
-  for (int n = 0; n < NC; ++n)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) o[n][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u32x4 st[T::NLD];
-  float scv = 0.f;
-  ib_load<KS>(Y, c_begin, c_end, st);
-  if (!ROW && threadIdx.x < TD) scv = c_begin + (int)threadIdx.x < c_end ? scale[c_begin + threadIdx.x] : 0.f;
-  ib_store<KS>(yt[0], st);
-  if (!ROW && threadIdx.x < TD) ysc[0][threadIdx.x] = scv;
-  __syncthreads();
-  // transposed-read lane address: row (4g + (lane&15)/4), column 4*((lane&15)&3) within the block
-  const int trow = 4 * g + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
-  int buf = 0;
-  for (int c0 = c_begin; c0 < c_end; c0 += TD, buf ^= 1) {
-    const bool more = c0 + TD < c_end;
-    if (more) {
-      ib_load<KS>(Y, c0 + TD, c_end, st);
-      if (!ROW && threadIdx.x < TD) scv = c0 + TD + (int)threadIdx.x < c_end ? scale[c0 + TD + threadIdx.x] : 0.f;
-    }
-    const unsigned short* yb = yt[buf];
-    f32x4 acc[4][2];
-    st_tile<KS>(xb, yb, acc);
-    // G^T in registers -> bf16 B fragments gb[s2][i] (s2: 32-row k-step of the tile);
-    // exp(g*(v-1)) = exp2(v*gl - gl) with gl = g*log2(e).  A dropped element (outside the
-    // clip range, or past the split's last row) gets exponent -inf: exp2 returns 0, one
-    // select instead of a compare-and-select on the product.
-    u32x4 gp[2][2];
-    auto epi = [&](auto full_c) {
-      constexpr bool FULL = decltype(full_c)::value;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        f32x4 ysv;
-        if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[buf][c * 16 + 4 * g]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          float gv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int yr = c * 16 + 4 * g + r;
-            const float v = acc[c][i][r];
-            float x;
-            if constexpr (FWD) {  // every valid element counts in the row sum; clip' masks G
-              const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
-              x = __builtin_fmaf(vc, gl, -gl);
-              if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
-              const float e = __builtin_amdgcn_exp2f(x);
-              rs[i] += e;
-              gv[r] = (!CLIP || vc == v) ? e : 0.f;
-              continue;
-            }
-            if constexpr (CLIP) {
-              const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
-              x = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
-            } else {
-              x = __builtin_fmaf(v, gl, -gl);
-            }
-            if constexpr (!FULL) x = c0 + yr < c_end ? x : -INFINITY;
-            gv[r] = (ROW ? rsc[i] : ysv[r]) * __builtin_amdgcn_exp2f(x);
-          }
-          gp[c >> 1][i][(c & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
-          gp[c >> 1][i][(c & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
-        }
-      }
-    };
-    if (c0 + TD <= c_end) epi(std::true_type{});
-    else epi(std::false_type{});
-    // out^T[feat][x] += Y^T[feat][y] . G^T[y][x]
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int n = 0; n < NC; ++n) {
-        typedef __attribute__((address_space(3))) v4s lds_v4s;
-        const unsigned short* p0 = yb + (s2 * 32 + trow) * T::LDY + n * 16 + tcol;
-        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
-        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0 + 16 * T::LDY));
-        const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          o[n][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, gp[s2][i]), o[n][i], 0, 0, 0);
-      }
-    if (more) {
-      ib_store<KS>(yt[buf ^ 1], st);
-      if (!ROW && threadIdx.x < TD) ysc[buf ^ 1][threadIdx.x] = scv;
-    }
-    __syncthreads();
-  }
-  if constexpr (FWD) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      float v = rs[i];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      const int r = r0 + i * 16 + (lane & 15);
-      if (g == 0 && r < nx) part[(size_t)blockIdx.y * nx + r] = v;  // summed in split order by ib_rowsum
-    }
-  }
-  // o[n][i][r] = out[x = r0 + i*16 + (lane&15)][feat = n*16 + 4g + r]
-  float* dst = gridDim.y == 1 ? out : ws + (size_t)blockIdx.y * nx * T::DP;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int x = r0 + i * 16 + (lane & 15);
-    if (x >= nx) continue;
-    float* orow = dst + (size_t)x * T::DP;
-#pragma unroll
-    for (int n = 0; n < NC; ++n) *reinterpret_cast<f32x4*>(orow + n * 16 + 4 * g) = o[n][i];
-  }
-}
+// (The round-2 256-thread generation of these kernels and a 4-wave-workgroup variant of
+// ib3 / ib5 were measured slower and removed: docs/PERF.md "In-batch loss generations".)
 
 // ---- ib3: 512-thread workgroups, Y tiles by LDS-DMA into a 3-slot ring --------------------
-// Same per-tile math as ib_bwd_kernel (S^T tile -> G^T in registers -> out^T += Y^T G^T), with
+// The per-tile math above (S^T tile -> G^T in registers -> out^T += Y^T G^T), with
 // the three costs that kept that kernel at ~0.75 PF/s at the W = 8 shape removed:
 //  * 8 waves x 32 X rows = 256 rows per workgroup (one per CU, 2 waves per SIMD): each
 //    staged Y tile feeds twice the MFMAs, half the Y bytes per FLOP;
@@ -1026,27 +894,16 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
   return 0;
 }
 
-static int ib2_splits(int nx, int ny) {
-  // 2 resident workgroups per CU (242 VGPRs): 512 fill the chip; keep >= 16 tiles per split
-  const int rb = (nx + pv::loss::TQ - 1) / pv::loss::TQ;
-  int ns = (512 + rb - 1) / rb;
-  const int maxs = (ny + 16 * pv::loss::TD - 1) / (16 * pv::loss::TD);
-  if (ns > maxs) ns = maxs;
-  return ns < 1 ? 1 : ns;
-}
-
 // Kernel generation (PAGEVEC_IB / pv_ib_set_version), read once per process so the
 // workspace queries and the launches always agree:
 //   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for
 //                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
-//   6: as 5 with 4-wave workgroups (two independent workgroups per CU; A/B)
-//   3: ib3 everywhere;  2: the round-2 256-thread kernels (ib_bwd_kernel)
+//   3: ib3 everywhere (A/B and the ib5-vs-ib3 numerics test)
 static int g_ib_version = -1;
 static int ib_version() {
   if (g_ib_version < 0) {
     const char* e = getenv("PAGEVEC_IB");
-    const int v = e ? atoi(e) : 5;
-    g_ib_version = (v == 2 || v == 3 || v == 6) ? v : 5;
+    g_ib_version = (e && atoi(e) == 3) ? 3 : 5;
   }
   return g_ib_version;
 }
@@ -1054,21 +911,15 @@ static int ib_version() {
 PV_API int pv_ib_version() { return ib_version(); }
 // A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)
 PV_API int pv_ib_set_version(int v) {
-  if (v != 2 && v != 3 && v != 5 && v != 6) return -1;
+  if (v != 3 && v != 5) return -1;
   g_ib_version = v;
   return 0;
 }
 
-// waves per workgroup of the ib3 / ib5 kernels: 8 (one 512-thread workgroup per CU, the two
-// waves of a SIMD in lockstep) or 4 (version 6: two independent 256-thread workgroups per CU)
-static int ib_nw() { return ib_version() == 6 ? 4 : 8; }
-
 static int ib3_splits(int nx, int ny) {
-  // 2048 / NW resident waves' worth of workgroups fill the chip (256 at NW = 8); keep >= 16
-  // tiles per split
-  const int tq = 32 * ib_nw();
-  const int rb = (nx + tq - 1) / tq;
-  int ns = (256 * 8 / ib_nw() + rb - 1) / rb;
+  // 256 workgroups of 8 waves fill the chip (one per CU); keep >= 16 tiles per split
+  const int rb = (nx + 255) / 256;
+  int ns = (256 + rb - 1) / rb;
   const int maxs = (ny + 16 * pv::loss::TD - 1) / (16 * pv::loss::TD);
   if (ns > maxs) ns = maxs;
   return ns < 1 ? 1 : ns;
@@ -1076,7 +927,7 @@ static int ib3_splits(int nx, int ny) {
 
 // (splits, Y rows per split) of the current kernel version, every split non-empty
 static void ib_split_plan(int nx, int ny, int& ns, int& per) {
-  ns = ib_version() >= 3 ? ib3_splits(nx, ny) : ib2_splits(nx, ny);
+  ns = ib3_splits(nx, ny);
   per = ((ny + ns - 1) / ns + pv::loss::TD - 1) / pv::loss::TD * pv::loss::TD;
   ns = (ny + per - 1) / per;
 }
@@ -1097,37 +948,19 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws) return -3;
   hipStream_t s = (hipStream_t)stream;
-  const int NWV = ib_nw();
-  const int nrb = (nx + 32 * NWV - 1) / (32 * NWV);
-  const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
+  const int nrb = (nx + 255) / 256;
+  const dim3 grid3(nrb * ns);
 #define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
-  if (ib_version() >= 5 && ROWV && (DP == 160 || DP == 128)) {                                                  \
-    if (NWV == 4) {                                                                                             \
-      if (DP == 160) hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,         \
-                                        (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, \
-                                        ny, per, nrb, gamma);                                                   \
-      else hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,                   \
-                              (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, nx, ny, per,  \
-                              nrb, gamma);                                                                      \
-    } else if (DP == 160) {                                                                                     \
-      hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
-                         (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
-    } else {                                                                                                    \
-      hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,        \
-                         (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                    \
-    }                                                                                                           \
-  } else if (ib_version() >= 3 && NWV == 4) {                                                                   \
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV, false, 4>), grid3, dim3(256), 0, s,    \
-                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
-                                            nx, ny, per, nrb, gamma));                                          \
-  } else if (ib_version() >= 3) {                                                                               \
+  if (ib_version() == 5 && ROWV && DP == 160) {                                                                 \
+    hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else if (ib_version() == 5 && ROWV && DP == 128) {                                                          \
+    hipLaunchKernelGGL((ib5_kernel<4, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else {                                                                                                      \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, ROWV, CLIPV>), grid3, dim3(512), 0, s,              \
                                             (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
                                             nx, ny, per, nrb, gamma));                                          \
-  } else {                                                                                                      \
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, ROWV, CLIPV>), grid, dim3(256), 0, s,            \
-                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
-                                            nx, ny, per, gamma));                                               \
   }
   if (row_scale) {
     if (clip) { PV_IB_BWD(true, true); } else { PV_IB_BWD(true, false); }
@@ -1163,37 +996,19 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   ib_split_plan(nx, ny, ns, per);
   if (ns > 1 && !ws_u) return -3;
   hipStream_t s = (hipStream_t)stream;
-  const int NWV = ib_nw();
-  const int nrb = (nx + 32 * NWV - 1) / (32 * NWV);
-  const dim3 grid3(nrb * ns), grid((nx + TQ - 1) / TQ, ns);
+  const int nrb = (nx + 255) / 256;
+  const dim3 grid3(nrb * ns);
 #define PV_IB_FWDDQ(CLIPV)                                                                                      \
-  if (ib_version() >= 5 && (DP == 160 || DP == 128)) {                                                          \
-    if (NWV == 4) {                                                                                             \
-      if (DP == 160) hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,          \
-                                        (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u,   \
-                                        nx, ny, per, nrb, gamma, part);                                         \
-      else hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,                    \
-                              (const unsigned short*)X, (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, \
-                              nrb, gamma, part);                                                                \
-    } else if (DP == 160) {                                                                                     \
-      hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
-                         (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
-    } else {                                                                                                    \
-      hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,  \
-                         (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);            \
-    }                                                                                                           \
-  } else if (ib_version() >= 3 && NWV == 4) {                                                                   \
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true, 4>), grid3, dim3(256), 0, s,     \
-                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
-                                            ws_u, nx, ny, per, nrb, gamma, part));                              \
-  } else if (ib_version() >= 3) {                                                                               \
+  if (ib_version() == 5 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 5 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else {                                                                                                      \
     IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true>), grid3, dim3(512), 0, s,        \
                                             (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
                                             ws_u, nx, ny, per, nrb, gamma, part));                              \
-  } else {                                                                                                      \
-    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib_bwd_kernel<KS, true, CLIPV, true>), grid, dim3(256), 0, s,      \
-                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
-                                            ws_u, nx, ny, per, gamma, part));                                   \
   }
   if (clip) { PV_IB_FWDDQ(true); } else { PV_IB_FWDDQ(false); }
 #undef PV_IB_FWDDQ

@@ -26,31 +26,20 @@ SIGS = {
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_dw2": "ppppp" "pppp" "iiii" "upuiif" "p",
-    "pv_conv_pool_bwd_reduce4": "ppppp" "liii" "upuii" "p",
-    "pv_conv_pool_bwd_reduce5": "ppppp" "liiii" "upuii" "p",
     "pv_conv_pool_bwd_emit3": "ppppppp" "iii" "f" "p",
     "pv_conv_bwd_slots_per_sample": "",
     "pv_conv_dx_dense_maxl": "",
     "pv_conv_pool_bwd_dx_dense": "ppppppp" "iiii" "upuii" "f" "p",
     "pv_conv_bwd_rows_reduce": "pippp" "liii" "p",
-    # sort.hip
-    "pv_sort_pairs_temp_bytes": "li",
-    "pv_sort_pairs_u32": "plpppp" "li" "p",
-    "pv_sort_iota_temp_bytes": "li",
-    "pv_sort_iota_u16_temp_bytes": "li",
-    "pv_sort_iota_u16": "plppp" "li" "p",
+    # conv_pool_bwd.hip: dTable reduce
     "pv_conv_pool_bwd_emit3_u16": "pppppp" "iii" "f" "p",
-    "pv_conv_pool_bwd_reduce5_u16": "ppppp" "liiii" "upuii" "p",
-    "pv_conv_pool_bwd_reduce6_u16": "ppppp" "liiii" "upuii" "ip",
     "pv_conv_pool_bwd_reduce7_u16": "ppppp" "liiii" "upuii" "p",
-    "pv_sort_iota_u32": "plppp" "li" "p",
+    "pv_conv_pool_bwd_reduce7": "ppppp" "liiii" "upuii" "p",
     # radix_sort.hip
     "pv_rsort_set_ipt": "i",
     "pv_rsort_temp_bytes": "lii",
     "pv_rsort_pairs": "plpppp" "lii" "p",
     "pv_conv_r7_set_occ": "i",
-    "pv_csort_temp_bytes": "li",
-    "pv_csort_pairs": "plppp" "lii" "p",
     # w2v.hip
     "pv_w2v_train": "pppppp" "ll" "iiii" "u" "f" "i" "p",
     # dense.hip
@@ -123,7 +112,7 @@ SIGS = {
     "pv_bag_counts8": "p" "p" "i" "p" "i" "p" "iiii" "p",
 }
 
-_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_csort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_sort_iota_u16_temp_bytes": ctypes.c_long, "pv_sort_pairs_temp_bytes": ctypes.c_long, "pv_sort_iota_temp_bytes": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
+_RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
             "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
 
 

@@ -1,7 +1,7 @@
 """Fused embedding-gather -> dropout -> Conv1D(3,4) -> max-pool -> ReLU (the CDSSM tower body).
 
 GPU: ``csrc/kernels/conv_pool_fwd.hip`` (forward, MFMA, weights register-resident)
-and ``conv_pool_bwd.hip`` + ``sort.hip`` (sparse argmax backward).  CPU:
+and ``conv_pool_bwd.hip`` + ``radix_sort.hip`` (sparse argmax backward).  CPU:
 ``ops/reference.py`` (identical semantics incl. the counter-based dropout mask).
 
 Reference layers: Embedding -> Dropout(0.25) -> Graph{Convolution1D(150, k, relu) ->
@@ -57,13 +57,14 @@ def _dropout_args(p: float, training: bool, mode: str) -> Tuple[int, int, float]
 
 _grid_cache = {}
 
-# sorted dTable entries per wave in the reduce (conv_bwd_reduce5_kernel); 0 = 64-entry reduce4
+# sorted dTable entries per wave in the reduce (conv_bwd_reduce7_kernel; multiple of 64)
 REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
-# reduce6: weight-row gathers of RB 4-entry rounds in flight per wave (0 = reduce5)
-REDUCE_RB = int(os.environ.get("PAGEVEC_REDUCE_RB", "0"))
-# reduce7: compile-time dropout mode + packed FMAs (5 = reduce5); same process at the bench
-# shape 0.468 vs 0.558 ms (tools/reduce_ab.py), headline step 7.72-7.79 vs 7.79-7.83 ms
-REDUCE_V = int(os.environ.get("PAGEVEC_REDUCE_V", "7"))
+# 4-byte sort keys even when the vocabulary fits 2-byte keys (tests: u16 vs u32 reduce)
+KEYS32 = os.environ.get("PAGEVEC_KEYS32", "0") != "0"
+
+
+def _k16(V: int) -> bool:
+    return V < 65535 and not KEYS32
 
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
 # (both halves are gather/latency-bound and leave CU slots idle when run back to back)
@@ -100,41 +101,18 @@ def _grid(device: torch.device) -> int:
 
 
 # dTable sort: the in-tree stable LSD radix sort (radix_sort.hip: graph-safe, no memsets /
-# atomics).  PAGEVEC_SORT=csort selects the one-pass 15-bit counting sort (count_sort.hip;
-# measured SLOWER: 0.435 vs 0.291 ms at 17.2 M keys — its scattered 2-/4-byte writes into
-# 30k buckets combine far worse than the LSD passes' 256 buckets — kept as an A/B arm),
-# =rocprim rocPRIM's onesweep sort (A/B and reference only: its hipMemsetAsync-reset state
-# faulted under long hipGraph replays, docs/PERF.md)
-SORT_IMPL = os.environ.get("PAGEVEC_SORT", "rsort")
+# atomics).  The one-pass counting sort (0.435 vs 0.291 ms at 17.2 M keys) and rocPRIM's
+# onesweep sort (its memset-reset state faulted under long hipGraph replays) were measured
+# and removed: docs/PERF.md "dTable sort".
 
 
-def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor, end_bit: int,
-                    impl: Optional[str] = None) -> None:
-    """Sort of ``keys`` (int16 / int32, read as unsigned) by bits [0, end_bit): sorted keys ->
-    ``skeys``, their input positions -> ``svals`` (int32).  Stable except for the counting
-    sort (``csort``: equal keys in arbitrary order; the dTable reduce sums them either way)."""
+def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor, end_bit: int) -> None:
+    """Stable sort of ``keys`` (int16 / int32, read as unsigned) by bits [0, end_bit): sorted
+    keys -> ``skeys``, their input positions -> ``svals`` (int32)."""
     L_ = lib()
     M = keys.numel()
     s = stream(keys.device)
     kb = keys.element_size()
-    impl = impl or SORT_IMPL
-    if impl == "csort" and (end_bit > 15 or determinism.enabled() or keys.data_ptr() % 16):
-        impl = "rsort"  # stable order needed / keys too wide for one LDS histogram
-    if impl == "csort":
-        tb = int(L_.pv_csort_temp_bytes(M, end_bit))
-        temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
-        check(L_.pv_csort_pairs(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, kb, s), "pv_csort_pairs")
-        return
-    if impl == "rocprim":
-        if kb == 2:
-            tb = int(L_.pv_sort_iota_u16_temp_bytes(M, end_bit))
-            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
-            check(L_.pv_sort_iota_u16(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u16")
-        else:
-            tb = int(L_.pv_sort_iota_temp_bytes(M, end_bit))
-            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
-            check(L_.pv_sort_iota_u32(P(temp), tb, P(keys), P(skeys), P(svals), M, end_bit, s), "pv_sort_iota_u32")
-        return
     tb = int(L_.pv_rsort_temp_bytes(M, end_bit, kb))
     temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
     check(L_.pv_rsort_pairs(P(temp), tb, P(keys), P(skeys), None, P(svals), M, end_bit, kb, s), "pv_rsort_pairs")
@@ -154,6 +132,9 @@ DENSE_DX_MAXL = 64
 # writes the {g * scale, argmax} records instead of running the emit kernel's id gathers on
 # its critical path (PAGEVEC_FWD_EMIT=0: the emit kernel)
 FWD_EMIT = os.environ.get("PAGEVEC_FWD_EMIT", "1") != "0"
+# ... and sorted right after the forward, on the side stream (PAGEVEC_EARLY_SORT=0: in the
+# backward, on its critical path)
+EARLY_SORT = os.environ.get("PAGEVEC_EARLY_SORT", "1") != "0"
 
 
 V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5)  # pv_conv_set_dbg variants with the loader key emit
@@ -198,13 +179,31 @@ class _ConvPoolFn(torch.autograd.Function):
         b3c, b4c = b3.detach().contiguous(), b4.detach().contiguous()  # the parameters themselves: no cat
         keys = None
         if ctx.needs_input_grad[1] and FWD_EMIT and not _dense_dx(L) and _conv_dbg() in (0,) + V7_DBG:
-            k16 = V < 65535 and REDUCE_EPW > 0
+            k16 = _k16(V)
             keys = torch.empty(N * SLOTS_PER_SAMPLE, dtype=torch.int16 if k16 else torch.int32, device=ids.device)
         check(lib().pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(b3c), P(b4c), P(pooled), P(argmax), N, L, V,
                                       seed, P(sp), row_offset, thr, tok, scale, _grid(ids.device), stream(ids.device),
                                       P(keys), 0 if keys is None else keys.element_size()),
               "pv_conv_pool_fwd2")
         ctx.keys = keys
+        ctx.sorted = None
+        if keys is not None and EARLY_SORT and not torch.cuda.is_current_stream_capturing() \
+                and not determinism.enabled():
+            # the sort of the table-gradient keys depends on the forward alone: run it now on
+            # the side stream, beside the rest of the forward and the loss, instead of on the
+            # backward's critical path (the backward waits for its event before the reduce)
+            main = torch.cuda.current_stream(ids.device)
+            side = _side_stream(ids.device)
+            skeys = torch.empty_like(keys)
+            svals = torch.empty(keys.numel(), dtype=torch.int32, device=ids.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
+            for t in (keys, skeys, svals):
+                t.record_stream(side)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            ctx.sorted = (skeys, svals, ev)
         ctx.save_for_backward(ids, pooled, argmax, tbl16, w3, w4)
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
         ctx.mark_non_differentiable(argmax)
@@ -285,10 +284,14 @@ class _ConvPoolFn(torch.autograd.Function):
             rec = torch.empty(N * 2 * FW, 2, dtype=torch.int32, device=dev)  # {g * scale, argmax}
             # entry i's value is its slot i: no value array, the sort reads a counting iterator;
             # token ids < 65535 sort as 2-byte keys
-            k16 = V < 65535 and REDUCE_EPW > 0
+            k16 = _k16(V)
             keys, ctx.keys = ctx.keys, None
-            skeys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
-            svals = torch.empty(M, dtype=u32, device=dev)
+            early, ctx.sorted = ctx.sorted, None
+            if early is not None:  # keys written and sorted during the forward
+                skeys, svals, ev = early
+            else:
+                skeys = torch.empty(M, dtype=torch.int16 if k16 else u32, device=dev)
+                svals = torch.empty(M, dtype=u32, device=dev)
             if keys is not None:  # written by the forward: only the records remain
                 check(L_.pv_conv_pool_bwd_rec(P(gpool), P(argmax), P(rec), N, scale, s), "pv_conv_pool_bwd_rec")
             elif k16:
@@ -299,27 +302,15 @@ class _ConvPoolFn(torch.autograd.Function):
                 keys = torch.empty(M, dtype=u32, device=dev)
                 check(L_.pv_conv_pool_bwd_emit3(P(gpool), P(pooled), P(argmax), P(ids), P(keys), None, P(rec), N, L,
                                                 V, scale, s), "pv_conv_pool_bwd_emit3")
-            sort_pairs_iota(keys, skeys, svals, end_bit)
+            if early is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+            else:
+                sort_pairs_iota(keys, skeys, svals, end_bit)
             dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
             wrow = _weight_rows(w3, w4, EP)
-            if k16 and REDUCE_V == 7 and REDUCE_RB == 0:
-                check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
-                      "pv_conv_pool_bwd_reduce7_u16")
-            elif k16 and REDUCE_RB > 0:
-                check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                                      L, E, V, seed, P(sp), row_offset, thr, tok, REDUCE_RB, s),
-                      "pv_conv_pool_bwd_reduce6_u16")
-            elif k16:
-                check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW,
-                                                      L, E, V, seed, P(sp), row_offset, thr, tok, s),
-                      "pv_conv_pool_bwd_reduce5_u16")
-            elif REDUCE_EPW > 0:
-                check(L_.pv_conv_pool_bwd_reduce5(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E,
-                                                  V, seed, P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce5")
-            else:
-                check(L_.pv_conv_pool_bwd_reduce4(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, L, E, V, seed,
-                                                  P(sp), row_offset, thr, tok, s), "pv_conv_pool_bwd_reduce4")
+            fn = "pv_conv_pool_bwd_reduce7_u16" if k16 else "pv_conv_pool_bwd_reduce7"
+            check(getattr(L_, fn)(P(skeys), P(svals), P(rec), P(wrow), P(dtable), M, REDUCE_EPW, L, E, V, seed, P(sp),
+                                  row_offset, thr, tok, s), fn)
         if t_tab is not None:
             grad_sink.done(ptable)  # fires the table's bucket: enqueued after the reduce above
         if side is None:

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--M", type=int, default=16384)
     ap.add_argument("--D", type=int, default=150)
     ap.add_argument("--clip", type=int, default=0)
-    ap.add_argument("--vers", default="2,3,5")
+    ap.add_argument("--vers", default="3,5")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(3)

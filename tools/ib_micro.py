@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--M", default="16384,131072")
     ap.add_argument("--D", type=int, default=150)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--ib", default="5,3,2", help="kernel generations to time (loss.hip pv_ib_set_version)")
+    ap.add_argument("--ib", default="5,3", help="kernel generations to time (loss.hip pv_ib_set_version)")
     a = ap.parse_args()
     from dnn_page_vectors_amd.ops._common import lib
     dev = torch.device("cuda")

@@ -1,9 +1,11 @@
-"""Same-process A/B of the page-tower dTable reduce: reduce5 vs reduce6 (RB rounds of
-weight-row gathers in flight per wave), bench shape, Zipf synthetic pages.
+"""Same-process A/B of the page-tower dTable reduce (conv_bwd_reduce7_kernel) at the bench
+shape, Zipf synthetic pages: 2-byte vs 4-byte sort keys, 64-VGPR cap (8 waves / SIMD, the
+default) vs the compiler's allocation, and the dW kernel beside it for scale.
 
-    python tools/reduce_ab.py [--N 16384] [--L 2000] [--rb 2,4,8,16] [--rounds 5]
+    python tools/reduce_ab.py [--N 16384] [--L 2000] [--rounds 5]
 
-Every variant's dTable is compared with reduce5's (fp32 atomics between waves: allclose).
+Every arm's dTable is compared with the default arm's (fp32 atomics between waves: allclose).
+(The reduce4 / 5 / 6 generations this tool once compared are gone: docs/PERF.md.)
 """
 import argparse
 import json
@@ -34,7 +36,6 @@ def main():
     ap.add_argument("--N", type=int, default=16384)
     ap.add_argument("--L", type=int, default=2000)
     ap.add_argument("--V", type=int, default=30000)
-    ap.add_argument("--rb", default="2,4,8,16")
     ap.add_argument("--epw", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=5)
@@ -55,8 +56,8 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     pooled = torch.empty(N, 2 * F, device=dev)
     argmax = torch.empty(N, 2 * F, dtype=torch.int32, device=dev)
-    check(L_.pv_conv_pool_fwd(P(ids), P(tbl16), P(wpack), P(bias), P(pooled), P(argmax), N, L, V, 7, None, 0, thr, 0,
-                              scale, 256, s), "fwd")
+    check(L_.pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(bias[:F]), P(bias[F:]), P(pooled), P(argmax), N, L, V, 7,
+                               None, 0, thr, 0, scale, 256, s, None, 0), "fwd")
     gpool = torch.randn(N, 2 * F, generator=g).to(dev) * 1e-3
     M = N * cops.SLOTS_PER_SAMPLE
     keys = torch.empty(M, dtype=torch.int16, device=dev)
@@ -65,68 +66,51 @@ def main():
     rec = torch.empty(N * 2 * F, 2, dtype=torch.int32, device=dev)
     check(L_.pv_conv_pool_bwd_emit3_u16(P(gpool), P(pooled), P(argmax), P(ids), P(keys), P(rec), N, L, V, scale, s),
           "emit")
-    cops.sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
+    end_bit = max(1, int(V).bit_length())
+    cops.sort_pairs_iota(keys, skeys, svals, end_bit)
+    keys32 = keys.to(torch.int32) & 0xFFFF
+    skeys32 = torch.empty_like(keys32)
+    svals32 = torch.empty_like(svals)
+    cops.sort_pairs_iota(keys32, skeys32, svals32, end_bit)
     wrow = cops._weight_rows(w3, w4, cops.EP)
 
-    def r5(out):
-        check(L_.pv_conv_pool_bwd_reduce5_u16(P(skeys), P(svals), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7,
-                                              None, 0, thr, 0, s), "reduce5")
-
-    def r6(out, rb):
-        check(L_.pv_conv_pool_bwd_reduce6_u16(P(skeys), P(svals), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7,
-                                              None, 0, thr, 0, rb, s), "reduce6")
-
-    def r7(out):
-        check(L_.pv_conv_pool_bwd_reduce7_u16(P(skeys), P(svals), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7,
-                                              None, 0, thr, 0, s), "reduce7")
+    def r7(out, k32=False):
+        fn = "pv_conv_pool_bwd_reduce7" if k32 else "pv_conv_pool_bwd_reduce7_u16"
+        sk, sv = (skeys32, svals32) if k32 else (skeys, svals)
+        check(getattr(L_, fn)(P(sk), P(sv), P(rec), P(wrow), P(out), M, a.epw, L, E, V, 7, None, 0, thr, 0, s), fn)
 
     dw3, dw4, db = torch.zeros_like(w3), torch.zeros_like(w4), torch.zeros(2 * F, device=dev)
 
     def dw():
-        check(L_.pv_conv_pool_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db), N, L, E,
-                                     V, 7, None, 0, thr, 0, scale, s), "dw")
+        check(L_.pv_conv_pool_bwd_dw2(P(gpool), P(pooled), P(argmax), P(ids), P(tbl16), P(dw3), P(dw4), P(db[:F]),
+                                      P(db[F:]), N, L, E, V, 7, None, 0, thr, 0, scale, s), "dw")
+
+    def occ1(fn):
+        def run():
+            L_.pv_conv_r7_set_occ(1)
+            try:
+                fn()
+            finally:
+                L_.pv_conv_r7_set_occ(8)
+        return run
 
     ref = torch.zeros(V, E, device=dev)
-    r5(ref)
-    torch.cuda.synchronize()
-    out7 = torch.zeros(V, E, device=dev)
-    r7(out7)
-    torch.cuda.synchronize()
-    err7 = float((out7 - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-    print(json.dumps({"reduce7_rel_err_vs_reduce5": err7}), flush=True)
-    assert err7 < 1e-5, err7
-    rbs = [int(x) for x in a.rb.split(",") if x]
-    for rb in rbs:
+    r7(ref)
+    arms = {"reduce7_u16": lambda o: r7(o), "reduce7_u32": lambda o: r7(o, True),
+            "reduce7_u16_occ1": lambda o: occ1(lambda: r7(o))()}
+    for name, fn in arms.items():
         out = torch.zeros(V, E, device=dev)
-        r6(out, rb)
+        fn(out)
         torch.cuda.synchronize()
         err = float((out - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-        print(json.dumps({"rb": rb, "rel_err_vs_reduce5": err}), flush=True)
-        assert err < 1e-5, err
+        print(json.dumps({name + "_rel_err": err}), flush=True)
+        assert err < 1e-5, (name, err)
     scratch = torch.zeros(V, E, device=dev)
-    has_occ = hasattr(L_, "pv_conv_r7_set_occ")
-    if has_occ:  # reduce7 capped at 64 VGPRs (8 waves / SIMD, default) vs the compiler's 74 (6 waves)
-        L_.pv_conv_r7_set_occ(1)
-        L_.pv_conv_r7_set_occ(8)
-        out8 = torch.zeros(V, E, device=dev)
-        r7(out8)
-        L_.pv_conv_r7_set_occ(1)
-        torch.cuda.synchronize()
-        err8 = float((out8 - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-        print(json.dumps({"reduce7_occ8_rel_err_vs_reduce5": err8}), flush=True)
-        assert err8 < 1e-5, err8
-    res = {"reduce5": [], "reduce7": [], "reduce7_occ8": [], "dw": []}
-    res.update({f"reduce6_rb{rb}": [] for rb in rbs})
+    res = {k: [] for k in list(arms) + ["dw"]}
     for _ in range(a.rounds):
-        res["reduce5"].append(ev_time(lambda: r5(scratch), a.iters))
-        res["reduce7"].append(ev_time(lambda: r7(scratch), a.iters))
-        if has_occ:
-            L_.pv_conv_r7_set_occ(8)
-            res["reduce7_occ8"].append(ev_time(lambda: r7(scratch), a.iters))
-            L_.pv_conv_r7_set_occ(1)
+        for name, fn in arms.items():
+            res[name].append(ev_time(lambda: fn(scratch), a.iters))
         res["dw"].append(ev_time(dw, a.iters))
-        for rb in rbs:
-            res[f"reduce6_rb{rb}"].append(ev_time(lambda: r6(scratch, rb), a.iters))
     out = {k: round(statistics.median(v), 4) for k, v in res.items() if v}
     out.update({"N": N, "L": L, "entries": M, "epw": a.epw})
     print(json.dumps(out), flush=True)

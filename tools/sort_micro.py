@@ -1,5 +1,7 @@
-"""dTable sort A/B: in-tree LSD radix sort (radix_sort.hip) vs rocPRIM onesweep, same process,
-interleaved, at the conv-backward shapes (2-byte keys < 2^15, values = positions).
+"""dTable sort micro-benchmark: the in-tree LSD radix sort (radix_sort.hip) at its automatic
+items-per-thread and forced ones, same process, interleaved, at the conv-backward shapes
+(2-byte keys < 2^15, values = positions).  (The rocPRIM onesweep and counting-sort arms it
+once compared are gone: docs/PERF.md "dTable sort".)
 
     python tools/sort_micro.py --M 17203200 4300800
 """
@@ -32,25 +34,23 @@ def main():
         res = {}
         lib = cops.lib()
         ref_k = ref_v = None
-        arms = ["rsort", "rocprim", "csort"] + [f"rsort_ipt{i}" for i in a.ipt]
+        arms = ["rsort"] + [f"rsort_ipt{i}" for i in a.ipt]
 
         def run(arm):
             if arm.startswith("rsort_ipt"):
                 lib.pv_rsort_set_ipt(int(arm[9:]))
                 try:
-                    cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl="rsort")
+                    cops.sort_pairs_iota(keys, skeys, svals, a.end_bit)
                 finally:
                     lib.pv_rsort_set_ipt(0)
             else:
-                cops.sort_pairs_iota(keys, skeys, svals, a.end_bit, impl=arm)
+                cops.sort_pairs_iota(keys, skeys, svals, a.end_bit)
 
         for arm in arms:
             run(arm)  # warm + every arm must give the same (stable) result
             torch.cuda.synchronize()
             if ref_k is None:
                 ref_k, ref_v = skeys.clone(), svals.clone()
-            elif arm == "csort":  # not stable: same keys, positions a key-preserving permutation
-                assert torch.equal(skeys, ref_k) and torch.equal(keys[svals.long()], skeys), arm
             else:
                 assert torch.equal(skeys, ref_k) and torch.equal(svals, ref_v), arm
         times = {arm: [] for arm in arms}
