@@ -105,7 +105,7 @@ SIGS = {
     "pv_scale": "p" "lf" "p",
     # gemm.hip
     "pv_gemm_bf16": "p" "l" "i" "p" "l" "i" "p" "l" "iii" "i" "l" "p" "f" "iii" "p",
-    "pv_gemm_set_sched": "i",
+    "pv_gemm_set_group": "i",
     "pv_mx_probe": "ppppp" "p",
     "pv_gemm_mx8": "p" "l" "p" "l" "p" "l" "iii" "i" "l" "p" "f" "p" "ii" "p",
     "pv_amax_quant_fp8_t": "p" "ii" "ppp" "i" "p",

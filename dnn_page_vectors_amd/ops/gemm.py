@@ -17,12 +17,11 @@ Requirements of the kernel: bf16 operands, 16-byte aligned, row strides multiple
 elements, K a multiple of 64, M (N) a multiple of 8 for a transposed A (B).  ``supported``
 checks them; callers fall back to the library GEMM otherwise.
 
-Status (round 3, measured): correct for every storage combination, split-K and epilogue
-(tests/test_kernels_gpu.py::test_gemm_engine_*), but at 0.47-0.96 PF/s it is 60-70% of
-hipBLASLt on the same shapes (0.75-1.48 PF/s, profiles/r3_gemm_engine.md): its
-double-buffered K loop lacks the 8-phase interleave (counted vmcnt with loads in flight
-across barriers) that the library's kernels have.  The model paths therefore keep the
-library GEMMs (``USE`` is empty); the engine is the base for fused-epilogue / fp8 work.
+Status (round 4, measured, profiles/r4_gemm/): correct for every storage combination,
+split-K and epilogue (tests/test_kernels_gpu.py::test_gemm_engine_*); with the grouped tile
+order 0.5-1.2 PF/s, 60-90% of hipBLASLt on the same shapes.  The 8-phase schedule (v4) and
+the staggered 4-phase one (v3) were exact but not faster and are gone; the model paths keep
+the library GEMMs (``USE`` is empty).
 """
 from __future__ import annotations
 

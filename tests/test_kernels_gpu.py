@@ -1616,8 +1616,8 @@ def test_gemm_engine_layouts(a_col, b_col, M, N, K):
     a = (A.t().contiguous() if a_col else A).to(DEV)
     b = (B.t().contiguous() if b_col else B).to(DEV)
     L = _native.hip()
-    for sched in ((2, 3) if not a_col and not b_col else (2,)):  # v3: staggered 4-phase, row/row
-        L.pv_gemm_set_sched(sched)
+    for group in (4, 0):  # grouped tile order (default) and the panel order
+        L.pv_gemm_set_group(group)
         try:
             for ks in (1, 0, 4):
                 if ks == 4 and K < 4 * 64:
@@ -1625,9 +1625,9 @@ def test_gemm_engine_layouts(a_col, b_col, M, N, K):
                 c = gops.gemm(a, b, a_col, b_col, ksplit=ks)
                 torch.cuda.synchronize()
                 err = float((c.cpu() - ref_c).abs().max() / ref_c.abs().max())
-                assert err < 1e-5, (sched, ks, err)
+                assert err < 1e-5, (group, ks, err)
         finally:
-            L.pv_gemm_set_sched(2)
+            L.pv_gemm_set_group(4)
 
 
 def test_gemm_engine_epilogues():

@@ -63,57 +63,31 @@ def main():
         def ours():
             return gops.gemm(a_, b_, a_col, b_col)
 
-        def ours1():  # the plain double-buffered schedule (A/B arm)
-            L.pv_gemm_set_sched(1)
+        def ours_g0():  # the row / column panel tile order (A/B arm)
+            L.pv_gemm_set_group(0)
             try:
                 return gops.gemm(a_, b_, a_col, b_col)
             finally:
-                L.pv_gemm_set_sched(2)
-
-        def ours3():  # the staggered 8-wave / 4-phase schedule (row/row operands only)
-            L.pv_gemm_set_sched(3)
-            try:
-                return gops.gemm(a_, b_, a_col, b_col)
-            finally:
-                L.pv_gemm_set_sched(2)
-
-        def ours4():  # the 8-phase schedule, two K tiles per iteration (row/row operands only)
-            L.pv_gemm_set_sched(4)
-            try:
-                return gops.gemm(a_, b_, a_col, b_col)
-            finally:
-                L.pv_gemm_set_sched(2)
+                L.pv_gemm_set_group(4)
 
         def lib():
             return torch.mm(lib_a, lib_b, out_dtype=torch.float32)
 
         c1, c2 = ours(), lib()
         err = float((c1 - c2).abs().max() / c2.abs().max())
-        err1 = float((ours1() - c2).abs().max() / c2.abs().max())
-        row = not a_col and not b_col
-        err3 = float((ours3() - c2).abs().max() / c2.abs().max()) if row else None
-        err4 = float((ours4() - c2).abs().max() / c2.abs().max())
-        t1, t2, t3, t4, t5 = [], [], [], [], []
+        err0 = float((ours_g0() - c2).abs().max() / c2.abs().max())
+        t1, t2, t3 = [], [], []
         for _ in range(a.rounds):
             t1.append(timeit(ours, a.iters))
-            t3.append(timeit(ours1, a.iters))
+            t3.append(timeit(ours_g0, a.iters))
             t2.append(timeit(lib, a.iters))
-            t5.append(timeit(ours4, a.iters))
-            if row:
-                t4.append(timeit(ours3, a.iters))
         m1, m2, m3 = statistics.median(t1), statistics.median(t2), statistics.median(t3)
-        m4 = statistics.median(t4) if row else None
-        m5 = statistics.median(t5)
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "a_col": a_col, "b_col": b_col,
-                          "ksplit": gops.auto_ksplit(M, N, K), "engine_ms": round(m1, 4), "engine_v1_ms": round(m3, 4),
-                          "library_ms": round(m2, 4), "engine_tflops": round(fl / m1 / 1e9, 1),
-                          "engine_v1_tflops": round(fl / m3 / 1e9, 1), "library_tflops": round(fl / m2 / 1e9, 1),
-                          "max_rel_err": err, "v1_max_rel_err": err1,
-                          **({"engine_v3_ms": round(m4, 4), "engine_v3_tflops": round(fl / m4 / 1e9, 1),
-                              "v3_max_rel_err": err3} if row else {}),
-                          "engine_v4_ms": round(m5, 4), "engine_v4_tflops": round(fl / m5 / 1e9, 1),
-                          "v4_max_rel_err": err4}),
+                          "ksplit": gops.auto_ksplit(M, N, K), "engine_ms": round(m1, 4),
+                          "engine_group0_ms": round(m3, 4), "library_ms": round(m2, 4),
+                          "engine_tflops": round(fl / m1 / 1e9, 1), "engine_group0_tflops": round(fl / m3 / 1e9, 1),
+                          "library_tflops": round(fl / m2 / 1e9, 1), "max_rel_err": err, "group0_max_rel_err": err0}),
               flush=True)
         del A, B, a_, b_, c1, c2
         torch.cuda.empty_cache()
