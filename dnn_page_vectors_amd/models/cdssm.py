@@ -67,11 +67,19 @@ class CDSSMTower(nn.Module):
                     cops.pack_weights(self.conv_w[0].detach(), self.conv_w[1].detach()))
         return None
 
-    def forward(self, ids: torch.Tensor, training: bool, seed: int, cache=None) -> torch.Tensor:
+    def features(self, ids: torch.Tensor, training: bool, seed: int, cache=None) -> torch.Tensor:
+        """The max-pooled, ReLU'd conv features (N, 2F) — cnn_dssm_th.py:86-134 before the Dense."""
         if ids.dtype != torch.int32:
             ids = ids.to(torch.int32)
         pooled, _ = cops.conv_relu_maxpool_fused(ids, self.embedding, list(self.conv_w), list(self.conv_b), self.p,
                                                  seed, training, self.mode, compute_cache=cache)
+        return pooled
+
+    def forward(self, ids: torch.Tensor, training: bool, seed: int, cache=None) -> torch.Tensor:
+        return self.head(self.features(ids, training, seed, cache), training)
+
+    def head(self, pooled: torch.Tensor, training: bool) -> torch.Tensor:
+        """Dense + ReLU (cnn_dssm_th.py:136-138), with the v1 final dropout when configured."""
         if self.p_final > 0.0 and training:
             y = dops.linear_act(pooled, self.dense_w, self.dense_b, "none")
             y = torch.nn.functional.dropout(y, self.p_final, True)

@@ -18,10 +18,15 @@ MLP or BERT)"):
   with ``use_fp8``);
 * ``"cdssm"`` — the reference's conv tower (cnn_dssm_th.py:83-139) on every chunk through
   the fused gather -> dropout -> conv -> max-pool HIP kernel (the N x C chunks are the
-  kernel's samples; each chunk max-pools over its own windows, like the reference's global
-  max-pool over a page, cnn_dssm_th.py:94), then Dense + ReLU; chunk vectors mean-pooled
-  as above.  Needs the CDSSM geometry (embedding_dim <= 104, filters (3, 4) x 150):
-  preset ``longpage_cdssm``.
+  kernel's samples; each chunk max-pools over its own windows), and ``chunk_pool``
+  combines the chunks: ``max`` (the default for this encoder) takes the element-wise max of
+  the chunks' pooled conv features before ONE Dense + ReLU — exactly the reference's global
+  max-pool over all windows of the page (cnn_dssm_th.py:94), for pages of up to
+  num_chunks x chunk_len tokens instead of a truncated one; ``mean`` runs Dense + ReLU per
+  chunk and mean-pools the chunk vectors as above (round 3's recipe: a query's span lives in
+  one chunk, so averaging eight chunk vectors dilutes its signal — Recall@10 0.25, see
+  profiles/r4_quality/).  Needs the CDSSM geometry (embedding_dim <= 104, filters (3, 4) x
+  150): preset ``longpage_cdssm``.
 """
 from __future__ import annotations
 
@@ -43,6 +48,10 @@ class ChunkedPageEncoder(TwoTowerModel):
         self.chunk_len = int(cfg.chunk_len)
         self.num_chunks = int(cfg.num_chunks)
         self.encoder = getattr(cfg, "chunk_encoder", "mlp")
+        pool = getattr(cfg, "chunk_pool", "auto")
+        self.chunk_pool = ("max" if self.encoder == "cdssm" else "mean") if pool == "auto" else pool
+        if self.chunk_pool not in ("mean", "max") or (self.chunk_pool == "max" and self.encoder != "cdssm"):
+            raise ValueError(f"chunk_pool={pool!r}: 'mean', or 'max' with chunk_encoder='cdssm'")
         if self.encoder == "cdssm":
             if cfg.use_fp8:
                 raise ValueError("chunk_encoder='cdssm' runs the bf16 conv kernel: set use_fp8=False")
@@ -82,6 +91,14 @@ class ChunkedPageEncoder(TwoTowerModel):
         if pad:
             ids = torch.nn.functional.pad(ids, (0, pad))
         chunks = ids.reshape(N * C, self.chunk_len)
+        if self.encoder == "cdssm" and self.chunk_pool == "max":
+            t = self.doc_towers[0]
+            f = t.features(chunks, training, seed, cache.get("doc0")).view(N, C, -1)
+            # empty chunks (all padding) must not win the max: their features -> 0 (every
+            # real feature is a ReLU output >= 0)
+            live = (ids.view(N, C, self.chunk_len) != 0).any(dim=2, keepdim=True)
+            f = torch.where(live, f, torch.zeros((), dtype=f.dtype, device=f.device))
+            return t.head(f.amax(dim=1), training)
         v = self._tower(self.doc_towers[0], chunks, training, seed, cache.get("doc0")).view(N, C, -1)
         # masked mean over the non-empty chunks (one fused HIP kernel per direction on GPU)
         return dops.chunk_mean_pool(v, ids.reshape(N, C * self.chunk_len), self.chunk_len)

@@ -75,13 +75,20 @@ DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "1") != "0"
 # slices (0: a zeroed (2 * FW) buffer returned to autograd, AccumulateGrad adds; A/B switch)
 BIAS_SINK = os.environ.get("PAGEVEC_BIAS_SINK", "1") != "0"
 _side = {}
+# one side stream per calling stream (page / query tower) or one shared (A/B)
+SIDE_PER_STREAM = os.environ.get("PAGEVEC_SIDE_PER_STREAM", "1") != "0"
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """The side stream of the CALLING stream: the page tower (main stream) and the query tower
+    (its own stream, models/base.py) each get one, so one tower's dW / early sort never queues
+    behind the other's (one shared side stream serialized the two dW kernels: the page dW
+    started only after the query dW, and ran alone at the end of the step)."""
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx not in _side:
-        _side[idx] = torch.cuda.Stream(device=idx)
-    return _side[idx]
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream if SIDE_PER_STREAM else 0)
+    if key not in _side:
+        _side[key] = torch.cuda.Stream(device=idx)
+    return _side[key]
 
 # Device seed offset for captured (hipGraph) training steps: when set, every conv kernel
 # adds *_SEED_DEV to its seed, so one captured graph draws fresh dropout masks per replay.
