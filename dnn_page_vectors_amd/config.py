@@ -98,7 +98,7 @@ class Configuration:
     chunk_len: int = 512
     num_chunks: int = 8
     chunk_encoder: str = "mlp"           # mlp | cdssm
-    chunk_pool: str = "auto"             # auto (cdssm: max of the conv features, mlp: mean of chunk vectors) | mean | max
+    chunk_pool: str = "auto"             # auto = mean of the chunk vectors | max (cdssm: max of the chunks' conv features)
     use_fp8: bool = False
     # LSTM legacy tower (old_scripts/lstm.py:125-200)
     lstm_output_size: int = 64

@@ -18,15 +18,14 @@ MLP or BERT)"):
   with ``use_fp8``);
 * ``"cdssm"`` — the reference's conv tower (cnn_dssm_th.py:83-139) on every chunk through
   the fused gather -> dropout -> conv -> max-pool HIP kernel (the N x C chunks are the
-  kernel's samples; each chunk max-pools over its own windows), and ``chunk_pool``
-  combines the chunks: ``max`` (the default for this encoder) takes the element-wise max of
-  the chunks' pooled conv features before ONE Dense + ReLU — exactly the reference's global
-  max-pool over all windows of the page (cnn_dssm_th.py:94), for pages of up to
-  num_chunks x chunk_len tokens instead of a truncated one; ``mean`` runs Dense + ReLU per
-  chunk and mean-pools the chunk vectors as above (round 3's recipe: a query's span lives in
-  one chunk, so averaging eight chunk vectors dilutes its signal — Recall@10 0.25, see
-  profiles/r4_quality/).  Needs the CDSSM geometry (embedding_dim <= 104, filters (3, 4) x
-  150): preset ``longpage_cdssm``.
+  kernel's samples; each chunk max-pools over its own windows), then Dense + ReLU;
+  chunk vectors mean-pooled as above (``chunk_pool='mean'``, the default).  ``chunk_pool='max'``
+  instead takes the element-wise max of the chunks' pooled conv features before ONE Dense +
+  ReLU — exactly the reference's global max-pool over all windows of the page
+  (cnn_dssm_th.py:94) for pages of up to num_chunks x chunk_len tokens — but it learns slower
+  in the 500-step quality protocol (Recall@10 0.13 vs 0.22 for the mean, lr 3e-3; the max
+  routes each feature's gradient to one chunk: profiles/r4_quality/README.md).  Needs the
+  CDSSM geometry (embedding_dim <= 104, filters (3, 4) x 150): preset ``longpage_cdssm``.
 """
 from __future__ import annotations
 
@@ -49,7 +48,7 @@ class ChunkedPageEncoder(TwoTowerModel):
         self.num_chunks = int(cfg.num_chunks)
         self.encoder = getattr(cfg, "chunk_encoder", "mlp")
         pool = getattr(cfg, "chunk_pool", "auto")
-        self.chunk_pool = ("max" if self.encoder == "cdssm" else "mean") if pool == "auto" else pool
+        self.chunk_pool = "mean" if pool == "auto" else pool
         if self.chunk_pool not in ("mean", "max") or (self.chunk_pool == "max" and self.encoder != "cdssm"):
             raise ValueError(f"chunk_pool={pool!r}: 'mean', or 'max' with chunk_encoder='cdssm'")
         if self.encoder == "cdssm":

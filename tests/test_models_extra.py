@@ -63,6 +63,24 @@ def test_chunked_mean_pool_masks_empty_chunks():
     torch.testing.assert_close(full, one)
 
 
+def test_chunked_cdssm_max_pool_is_max_of_chunk_features():
+    """chunk_pool='max': the element-wise max of the non-empty chunks' pooled conv features
+    through ONE Dense + ReLU (an all-padding chunk never wins)."""
+    cfg = preset_config("longpage_cdssm").replace(vocab_hash_size=100, chunk_len=8, num_chunks=3,
+                                                  document_length=24, chunk_pool="max")
+    m = build_model(cfg, 100).eval()
+    ids = torch.zeros(2, 24, dtype=torch.int32)
+    ids[0, :16] = torch.randint(1, 100, (16,), dtype=torch.int32)
+    ids[1, :] = torch.randint(1, 100, (24,), dtype=torch.int32)
+    t = m.doc_towers[0]
+    got = m.tower_forward("doc", ids, False, 0)
+    f = t.features(ids.view(6, 8), False, 0).view(2, 3, -1)
+    want = t.head(torch.stack([f[0, :2].amax(0), f[1].amax(0)]), False)
+    torch.testing.assert_close(got, want)
+    with pytest.raises(ValueError):
+        build_model(preset_config("longpage_fp8").replace(chunk_pool="max", use_fp8=False), 100)
+
+
 def test_bert_shared_tower_is_siamese():
     cfg = preset_config("bert_dp8").replace(bert_layers=1, bert_hidden=32, bert_heads=2, bert_intermediate=64,
                                             vocab_hash_size=100)
