@@ -164,7 +164,8 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
   }
 }
 
-// DM: compile-time dropout mode (-1 runtime, 0 off, 1 element p = 0.25, 2 element any p, 3 token)
+// DM: compile-time dropout mode (0 off, 1 element p = 0.25, 2 element any p, 3 token; the runtime-mode
+// instantiation, 0.537 vs 0.495 ms, is gone)
 template <int DM>
 __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, const float* pooled, const int* argmax,
                                                           const int* ids, const unsigned short* table, float* dw3,
@@ -667,10 +668,6 @@ PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const i
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
-  static const bool dw_runtime_dm = [] {  // PAGEVEC_DW_DM=runtime: the runtime-mode kernel (A/B switch)
-    const char* e = getenv("PAGEVEC_DW_DM");
-    return e && e[0] == 'r';
-  }();
   static const int xcd_map = [] {  // PAGEVEC_DW_XCD=0: natural block order (A/B switch)
     const char* e = getenv("PAGEVEC_DW_XCD");
     return (e && e[0] == '0') ? 0 : 1;
@@ -685,8 +682,7 @@ PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const i
   hipLaunchKernelGGL((conv_bwd_dw_kernel<DMV>), dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled, argmax, ids, \
                      (const unsigned short*)table, dw3, dw4, db3, db4, N, L, E, V, nsplit, seed, seed_ptr,           \
                      row_offset, thr, token_mode, scale, xcd_map, fx)
-  if (dw_runtime_dm) PV_DW(-1);
-  else if (dm == 0) PV_DW(0);
+  if (dm == 0) PV_DW(0);
   else if (dm == 1) PV_DW(1);
   else if (dm == 3) PV_DW(3);
   else PV_DW(2);

@@ -1581,7 +1581,11 @@ def _curve_parity(preset, overrides, steps, num_pages=4096, eval_pairs=1024, see
 
 
 @pytest.mark.parametrize("preset,overrides,steps,learn,pages", [
-    ("longpage_cdssm", dict(batch_size=128, num_chunks=4, chunk_len=256, document_length=1024), 200, 0.97, 512),
+    # lr 1e-3 (the preset's 3e-3 is tuned for the 500-step recall protocol): at 3e-3 the bf16 and
+    # fp32 trajectories drift apart run to run with the float-atomic summation order (tails
+    # 0.477 vs 0.430 in one run, within 8% in the next); the kernels' parity is the question here
+    ("longpage_cdssm", dict(batch_size=128, num_chunks=4, chunk_len=256, document_length=1024, lr=1e-3), 200, 0.97,
+     512),
     ("bert_dp8", dict(bert_layers=2, batch_size=32, document_length=64, query_length=16, lr=3e-4), 200, 0.9, 256),
 ])
 def test_new_config_training_curve_hip_matches_torch(preset, overrides, steps, learn, pages):
