@@ -98,6 +98,7 @@ class Configuration:
     chunk_len: int = 512
     num_chunks: int = 8
     chunk_encoder: str = "mlp"           # mlp | cdssm
+    cdssm_act: str = "relu"              # the CDSSM tower's Dense activation: relu (reference) | tanh
     chunk_pool: str = "auto"             # auto = mean of the chunk vectors | max (cdssm: max of the chunks' conv features)
     use_fp8: bool = False
     # LSTM legacy tower (old_scripts/lstm.py:125-200)
@@ -354,13 +355,17 @@ def preset_config(name: str) -> Configuration:
                              cos_clip=False, lr=3e-3)
     if name in ("longpage_cdssm", "config5_cdssm"):
         # config 5 with the reference's conv tower as the chunk encoder (8 x 512-trigram chunks
-        # through the fused conv kernel, chunk vectors mean-pooled)
-        # lr 3e-3: Recall@10 after 500 steps 0.147 (lr 1e-3) -> 0.25 (round-4 sweep, lr 2e-3..2e-2,
-        # softmax scale 20..80, no embedding dropout: profiles/r4_quality/README.md)
+        # through the fused conv kernel, chunk vectors mean-pooled).  Recipe (round-4 sweeps,
+        # profiles/r4_quality/README.md, Recall@10 after the 500-step protocol): the reference's
+        # ReLU Dense head + cosine clip made every chunk vector non-negative, and their mean
+        # washed out a query's chunk (0.15 at lr 1e-3, 0.22-0.25 at 3e-3); a tanh head without
+        # the clip (like the MLP chunk encoder) 0.35, and embedding dropout 0.1 instead of 0.25
+        # 0.39-0.42; 0.125 = 2/16 keeps the one-hash-per-8-columns mask path (0.1 does not)
         return Configuration(model="chunked", chunk_encoder="cdssm", feature_level="ngram",
                              vocab_hash_size=30000, chunk_len=512, num_chunks=8, query_length=45,
                              document_length=4096, batch_size=512, dtype="bf16", loss_mode="cross_gpu",
-                             J=0, inbatch_gamma=40.0, lr=3e-3)
+                             J=0, inbatch_gamma=40.0, lr=3e-3, cdssm_act="tanh", cos_clip=False,
+                             dropout_prob=(0.125, 0.5))
     if name in ("lstm", "legacy_lstm"):
         return Configuration(model="lstm", feature_level="word", batch_size=64, nb_epoch=2)
     raise KeyError(f"unknown preset {name!r}")

@@ -91,7 +91,9 @@ __device__ __forceinline__ u32x4 keep_piece(unsigned hrow, int q, int thr) {
     const unsigned h = dropout_group_hash(hrow, (unsigned)q);
     const int t = thr >> 4;
     unsigned b;  // bit 0 of nibble k = keep column k
-    if (t == 4) {
+    if (t == 2) {  // nibble >= 2: any of bits 1..3
+      b = ((h >> 1) | (h >> 2) | (h >> 3)) & 0x11111111u;
+    } else if (t == 4) {
       b = ((h | (h >> 1)) >> 2) & 0x11111111u;
     } else if (t == 8) {
       b = (h >> 3) & 0x11111111u;
@@ -110,6 +112,14 @@ __device__ __forceinline__ u32x4 keep_piece(unsigned hrow, int q, int thr) {
   const unsigned k0 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q)), thr);
   const unsigned k1 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q + 1)), thr);
   return u32x4{keep_pair(k0, 0), keep_pair(k0, 1), keep_pair(k1, 0), keep_pair(k1, 1)};
+}
+
+// Dropout modes of the conv kernels (template DM): 0 off, 1 element p = 64/256 (the reference's
+// 0.25), 2 element any p (runtime threshold), 3 token, 4 element p = 32/256 (the chunked-CDSSM
+// preset's 0.125): 1 and 4 fold the threshold into keep_piece at compile time.
+__host__ __device__ constexpr int dm_thr(int dm, int thr) { return dm == 1 ? 64 : dm == 4 ? 32 : thr; }
+inline int dm_of(int thr, int token_mode) {
+  return thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : thr == 32 ? 4 : 2;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

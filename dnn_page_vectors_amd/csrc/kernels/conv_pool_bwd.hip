@@ -116,7 +116,7 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
             const unsigned k = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
             raw[u] &= u32x4{k, k, k, k};
           } else {
-            raw[u] &= keep_piece(hr, pc, DM == 1 ? 64 : thr);
+            raw[u] &= keep_piece(hr, pc, dm_thr(DM, thr));
           }
         }
       }
@@ -374,8 +374,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         if constexpr (DM == 3) {
           const unsigned k = ((int)(he & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
           w &= u32x4{k, k, k, k};
-        } else if constexpr (DM == 1) {
-          w &= keep_piece(he, p, 64);  // compile-time p = 0.25 (the reference's rate)
+        } else if constexpr (DM == 1 || DM == 4) {
+          w &= keep_piece(he, p, dm_thr(DM, thr));  // compile-time p = 0.25 (the reference's rate) / 0.125
         } else if constexpr (DM == 2) {
           w &= keep_piece(he, p, thr);
         }
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(DX_THREADS) void conv_bwd_dx_dense_kernel(const flo
       if (DM == 3 || (DM < 0 && token_mode)) {
         keep_row = (int)(hr & 0xFFu) >= thr;
       } else {
-        const u32x4 k = keep_piece(hr, c >> 2, DM == 1 ? 64 : thr);
+        const u32x4 k = keep_piece(hr, c >> 2, dm_thr(DM, thr));
         const unsigned kw = k[c & 3];
         x0 = (kw & 1u) ? x0 : 0.f;
         x1 = (kw & 0x10000u) ? x1 : 0.f;
@@ -677,13 +677,14 @@ PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const i
   const size_t nfx = (size_t)7 * FW * E + 2 * FW;
   long long* fx = det_on() ? det_scratch(nfx, st) : nullptr;
   if (det_on() && !fx) return -4;
-  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+  const int dm = dm_of(thr, token_mode);
 #define PV_DW(DMV)                                                                                               \
   hipLaunchKernelGGL((conv_bwd_dw_kernel<DMV>), dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled, argmax, ids, \
                      (const unsigned short*)table, dw3, dw4, db3, db4, N, L, E, V, nsplit, seed, seed_ptr,           \
                      row_offset, thr, token_mode, scale, xcd_map, fx)
   if (dm == 0) PV_DW(0);
   else if (dm == 1) PV_DW(1);
+  else if (dm == 4) PV_DW(4);
   else if (dm == 3) PV_DW(3);
   else PV_DW(2);
 #undef PV_DW
@@ -769,7 +770,7 @@ int launch_reduce7(const void* skeys, const unsigned* svals, const void* rec, co
   const dim3 grid((unsigned)((waves + 3) / 4));
   const DetAcc det((size_t)V * E, st);
   if (det.err) return det.err;
-  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+  const int dm = dm_of(thr, token_mode);
 #define PV_R7(DMV)                                                                                               \
   if (g_r7_occ == 8)                                                                                             \
     hipLaunchKernelGGL((conv_bwd_reduce7_kernel<KT, DMV, 8>), grid, dim3(256), 0, st, (const KT*)skeys, svals,   \
@@ -782,6 +783,7 @@ int launch_reduce7(const void* skeys, const unsigned* svals, const void* rec, co
   switch (dm) {
     case 0: PV_R7(0); break;
     case 1: PV_R7(1); break;
+    case 4: PV_R7(4); break;
     case 3: PV_R7(3); break;
     default: PV_R7(2); break;
   }
@@ -820,7 +822,7 @@ PV_API int pv_conv_pool_bwd_dx_dense(const float* gpool, const float* pooled, co
   using namespace pv::convbwd;
   if (L > DENSE_MAXL || L < 4 || N <= 0 || (key_bytes == 2 && V >= 65535)) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+  const int dm = dm_of(thr, token_mode);
 #define PV_DX_LAUNCH(KT, DMV)                                                                                   \
   hipLaunchKernelGGL((conv_bwd_dx_dense_kernel<KT, DMV>), dim3(N), dim3(DX_THREADS), 0, st, gpool, pooled, argmax, ids, \
                      (const unsigned short*)wrow, rows, (KT*)keys, L, V, seed, seed_ptr, row_offset, thr,        \

@@ -195,7 +195,7 @@ __device__ __forceinline__ void store_rows(const Params& p, char* xl, const unsi
           unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
           x = x & u32x4{m, m, m, m};
         } else {
-          x &= keep_piece(hr, pc, DM == 1 ? 64 : p.thr);
+          x &= keep_piece(hr, pc, dm_thr(DM, p.thr));
         }
       }
       *reinterpret_cast<u32x4*>(xl + r * ROWB + pc * 16) = x;
@@ -535,7 +535,7 @@ __device__ __forceinline__ void loader7_stage(const Params& p, int lt, const int
           const unsigned m = ((int)(hr & 0xFF) >= p.thr) ? 0xFFFFFFFFu : 0u;
           x = x & u32x4{m, m, m, m};
         } else {
-          x &= keep_piece(hr, pc, DM == 1 ? 64 : p.thr);
+          x &= keep_piece(hr, pc, dm_thr(DM, p.thr));
         }
       }
       *reinterpret_cast<u32x4*>(xl + r * ROWB + pc * 16) = x;
@@ -884,12 +884,13 @@ PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpac
   if (grid <= 0) grid = 256;
   if (grid > N) grid = N;
   hipStream_t st = (hipStream_t)stream;
-  const int dm = thr <= 0 ? 0 : token_mode ? 3 : thr == 64 ? 1 : 2;
+  const int dm = dm_of(thr, token_mode);
 #define PV_CONV_DM(KERNEL, NT_, ...)                                                             \
   switch (dm) {                                                                                  \
     case 0: hipLaunchKernelGGL((KERNEL<__VA_ARGS__, 0>), dim3(grid), dim3(NT_), 0, st, p); break; \
     case 1: hipLaunchKernelGGL((KERNEL<__VA_ARGS__, 1>), dim3(grid), dim3(NT_), 0, st, p); break; \
     case 2: hipLaunchKernelGGL((KERNEL<__VA_ARGS__, 2>), dim3(grid), dim3(NT_), 0, st, p); break; \
+    case 4: hipLaunchKernelGGL((KERNEL<__VA_ARGS__, 4>), dim3(grid), dim3(NT_), 0, st, p); break; \
     default: hipLaunchKernelGGL((KERNEL<__VA_ARGS__, 3>), dim3(grid), dim3(NT_), 0, st, p); break; \
   }
   switch (dbg) {

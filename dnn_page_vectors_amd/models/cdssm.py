@@ -57,6 +57,7 @@ class CDSSMTower(nn.Module):
         self.p = float(cfg.dropout_prob[0])
         self.p_final = float(cfg.dropout_prob[1]) if cfg.final_dropout else 0.0
         self.mode = cfg.embed_dropout_mode
+        self.act = getattr(cfg, "cdssm_act", "relu")  # Dense activation (reference: ReLU, cnn_dssm_th.py:136-138)
 
     def fast_ok(self) -> bool:
         return cops.fast_path_supported(self.embedding.shape[1], self.widths, self.conv_w[0].shape[0])
@@ -84,7 +85,7 @@ class CDSSMTower(nn.Module):
             y = dops.linear_act(pooled, self.dense_w, self.dense_b, "none")
             y = torch.nn.functional.dropout(y, self.p_final, True)
             return torch.relu(y)
-        return dops.linear_act(pooled, self.dense_w, self.dense_b, "relu")
+        return dops.linear_act(pooled, self.dense_w, self.dense_b, self.act)
 
 
 class CDSSM(TwoTowerModel):
