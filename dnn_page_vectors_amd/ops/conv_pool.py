@@ -86,6 +86,8 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     started only after the query dW, and ran alone at the end of the step)."""
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream if SIDE_PER_STREAM else 0)
+    if key not in _side and sum(1 for k in _side if k[0] == idx) >= 4:
+        key = (idx, 0)  # callers on many streams share one (bounded: no stream per caller stream)
     if key not in _side:
         _side[key] = torch.cuda.Stream(device=idx)
     return _side[key]
