@@ -40,6 +40,12 @@ import time
 
 # RCCL on this driver needs dmabuf IPC: set before anything can initialise HIP
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# Multi-rank: the step uses four streams (page tower, query tower, one side stream each) and
+# RCCL adds its own; with HIP's default 4 hardware queues two of them would share a queue, and
+# a side-stream kernel queued behind a collective waits for the other ranks.  8 queues keep
+# them apart (neutral at one rank: 6.94-6.96 vs 6.93-6.94 ms, profiles/r4_prune/hwq_ab.txt).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch  # noqa: E402
 
