@@ -97,6 +97,9 @@ def parse():
                          "gradient sums, one stream, no hipGraph")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launch / process group / JSON path (gloo, eager ops, tiny model)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="compute precision (default: the preset's; bf16 for cdssm_char). fp32 = the "
+                         "reference's precision: fp32-MFMA conv kernels (conv_pool_f32.hip), fp32 PyTorch ops elsewhere")
     ap.add_argument("--model", default="cdssm", choices=["cdssm", "mlp", "bert", "chunked", "chunked_cdssm",
                                                          "cdssm_char"],
                     help="cdssm = headline (config 2); mlp = config 3; bert = config 4; chunked = config 5; "
@@ -188,13 +191,15 @@ def main():
     if a.loss is None:
         a.loss = "explicit" if a.model == "cdssm_char" else "cross_gpu"
     if a.model == "cdssm_char":  # reference run config (char, 250 / 5000) on the HIP fast path
-        cfg = cfg.replace(dtype="bf16", vocab_hash_size=100)
+        cfg = cfg.replace(dtype=a.dtype or "bf16", vocab_hash_size=100)
         if a.batch == 4096:
             a.batch = 1024
     batch = a.batch if a.model in ("cdssm", "cdssm_char") or a.batch != 4096 else cfg.batch_size
     cfg = cfg.replace(batch_size=batch, loss_mode=a.loss if a.model in ("cdssm", "cdssm_char") else cfg.loss_mode,
                       deterministic=bool(a.deterministic))
     a.batch = batch
+    if a.dtype is not None:
+        cfg = cfg.replace(dtype=a.dtype)
     if a.set:
         cfg = cfg.override(a.set)
     if a.dry_run:
@@ -298,9 +303,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp8_e4m3 MFMA (bf16 elsewhere)" if a.model == "chunked" else "bf16",
+            "dtype": "fp32" if cfg.dtype == "fp32" else
+                     "fp8_e4m3 MFMA (bf16 elsewhere)" if a.model == "chunked" else "bf16",
             "data": "synthetic (device-resident pre-featurized Zipf trigram-id pages; random-init weights)",
-            "config": {"model": MODEL_DESC[a.model],
+            "config": {"model": MODEL_DESC[a.model] if a.model != "cdssm_char" or cfg.dtype != "fp32" else
+                       MODEL_DESC[a.model].split("; bf16")[0] + "; fp32 (reference precision)",
                        "global_batch": a.batch * W, "seq_len": cfg.document_length,
                        "parallelism": f"dp{W}", "loss": a.loss, "backend": a.backend,
                        "softmax_scale": (cfg.inbatch_gamma or cfg.GAMMA) if a.loss != "explicit" else cfg.GAMMA,

@@ -30,7 +30,7 @@ _hip: Optional[ctypes.CDLL] = None
 _hip_err: Optional[str] = None
 _hip_debug: Optional[ctypes.CDLL] = None
 _use_debug = os.environ.get("PAGEVEC_DEBUG_KERNELS", "0") == "1"
-DEBUG_UNITS = ("convfwd", "convbwd", "embed", "loss")
+DEBUG_UNITS = ("convfwd", "convbwd", "convf32", "embed", "loss")
 DEBUG_BITS = {0: "id out of range", 1: "LDS index out of range", 2: "shape precondition", 3: "sort key out of range",
               4: "argmax out of range", 5: "sorted slot out of range", 6: "positive index out of range"}
 

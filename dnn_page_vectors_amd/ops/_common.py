@@ -34,21 +34,34 @@ def precision_scope(cfg):
 
     ``bf16`` (default): the HIP kernels — bf16 MFMA operands, fp32 accumulation, fp32 master
     weights and optimizer state.  ``fp32``: the reference's precision (Keras/Theano trains in
-    fp32, dssm_cnn_v2/cnn_dssm_th.py:182) — inside this scope every op runs its fp32 PyTorch
-    implementation (rocBLAS / MIOpen on the GPU), none of the bf16 HIP kernels; the fused
-    Adam kernel is fp32 already.  CPU runs are fp32 either way."""
+    fp32, dssm_cnn_v2/cnn_dssm_th.py:182) — inside this scope no bf16 HIP kernel runs: the CDSSM
+    conv tower runs its fp32 HIP kernels (csrc/kernels/conv_pool_f32.hip, fp32 MFMA; see
+    ``ref_precision``), every other op its fp32 PyTorch implementation (rocBLAS on the GPU);
+    the fused Adam kernel is fp32 already.  CPU runs are fp32 either way."""
     global _FORCE
     if getattr(cfg, "dtype", "bf16") != "fp32" or _FORCE == "torch":
         yield
         return
     if not _FP32_NOTED[0]:
-        logging.getLogger(__name__).info("dtype=fp32: reference-precision PyTorch ops (no bf16 HIP kernels)")
+        logging.getLogger(__name__).info("dtype=fp32: reference-precision ops (fp32 conv kernels, no bf16 HIP kernels)")
         _FP32_NOTED[0] = True
     prev, _FORCE = _FORCE, "torch"
+    _REF_PREC[0] += 1
     try:
         yield
     finally:
         _FORCE = prev
+        _REF_PREC[0] -= 1
+
+
+_REF_PREC = [0]
+# 0: dtype="fp32" runs the conv tower as PyTorch ops too (conv1d materialises (N, F, L); A/B)
+F32_NATIVE = os.environ.get("PAGEVEC_F32_NATIVE", "1") != "0"
+
+
+def ref_precision() -> bool:
+    """Inside a dtype="fp32" precision scope with the native fp32 kernels enabled."""
+    return _REF_PREC[0] > 0 and F32_NATIVE
 
 
 def use_hip(*tensors: torch.Tensor) -> bool:

@@ -17,7 +17,7 @@ import torch
 
 from . import determinism, grad_sink
 from . import reference as ref
-from ._common import P, check, lib, need, stream, use_hip
+from ._common import P, check, lib, need, ref_precision, stream, use_hip
 from ..parallel.sparse_rows import note_rows
 
 EP = 104          # padded embedding row stride of the bf16 table copy (kernel constant)
@@ -336,6 +336,99 @@ class _ConvPoolFn(torch.autograd.Function):
                 None, None, None, None, None, None, None)
 
 
+# ---- reference precision (dtype="fp32"): csrc/kernels/conv_pool_f32.hip -------------------
+F32_EMAX = 112  # conv_pool_f32.hip EMAX (LDS sizing)
+# 0: the fp32 dTable always uses global row atomics (A/B of the LDS-privatised small-V path)
+F32_DX_LDS = os.environ.get("PAGEVEC_F32_DX_LDS", "1") != "0"
+
+
+def f32_supported(E: int, widths, num_filters: int) -> bool:
+    return tuple(widths) == WIDTHS and num_filters == FW and E % 4 == 0 and 4 <= E <= F32_EMAX
+
+
+def f32_plan(N: int, L: int, n_cu: int) -> Tuple[int, int, int]:
+    """(nslots, nseg, sw) of the fp32 forward: nslots persistent workgroups per filter group
+    (5 groups, one workgroup per CU: 159 KB of LDS), each sample's L - 2 windows cut into nseg
+    segments of sw windows (a multiple of the 128-window chunk) so that every group has >= 32
+    (sample, segment) items per workgroup (tail imbalance <= 3 %)."""
+    cw, ng = 128, 5
+    nslots = max(1, n_cu // ng)
+    nch = -(-(L - 2) // cw)
+    nseg = max(1, min(nch, -(-32 * nslots // max(N, 1))))
+    sw = -(-nch // nseg) * cw
+    nseg = -(-(L - 2) // sw)
+    return max(1, min(nslots, N * nseg)), nseg, sw
+
+
+class _ConvPoolF32Fn(torch.autograd.Function):
+    """fp32 gather -> dropout -> conv(3, 4) -> max-pool -> ReLU with fp32 MFMAs, and its sparse
+    argmax backward (dW / db per-split partials summed in order; dTable fp32 row atomics)."""
+
+    @staticmethod
+    def forward(ctx, ids, table, w3, w4, b3, b4, p, seed, row_offset, training, mode):
+        ids = need(ids, torch.int32, "ids", 2)
+        N, L = ids.shape
+        V, E = table.shape
+        if L < 4:
+            raise ValueError("sequence length must be >= 4 for filter widths (3,4)")
+        thr, tok, scale = _dropout_args(p, training, mode)
+        tab = table.detach().contiguous()
+        w3c, w4c = w3.detach().contiguous(), w4.detach().contiguous()
+        nslots, nseg, sw = f32_plan(N, L, _grid(ids.device))
+        part = torch.empty(N * nseg, 2 * FW, 2, dtype=torch.float32, device=ids.device)
+        pooled = torch.empty(N, 2 * FW, dtype=torch.float32, device=ids.device)
+        argmax = torch.empty(N, 2 * FW, dtype=torch.int32, device=ids.device)
+        seed &= 0xFFFFFFFF
+        row_offset &= 0xFFFFFFFF
+        sp = _SEED_DEV
+        check(lib().pv_conv_f32_fwd(P(ids), P(tab), P(w3c), P(w4c), P(b3.detach().contiguous()),
+                                    P(b4.detach().contiguous()), P(part), P(pooled), P(argmax), N, L, V, E, nseg, sw,
+                                    nslots, seed, P(sp), row_offset, thr, tok, scale, stream(ids.device)),
+              "pv_conv_f32_fwd")
+        ctx.save_for_backward(ids, tab, w3c, w4c, pooled, argmax)
+        ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
+        ctx.mark_non_differentiable(argmax)
+        ctx.set_materialize_grads(False)
+        return pooled, argmax
+
+    @staticmethod
+    def backward(ctx, gpool, _gargmax):
+        if gpool is None:
+            return (None,) * 11
+        ids, tab, w3, w4, pooled, argmax = ctx.saved_tensors
+        V, E, seed, row_offset, thr, tok, scale, sp = ctx.meta
+        N, L = ids.shape
+        dev = ids.device
+        s = stream(dev)
+        gpool = gpool.contiguous().float()
+        dtable = None
+        if ctx.needs_input_grad[1]:
+            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            if V * E <= lib().pv_conv_f32_dx_lds_max() and F32_DX_LDS:
+                # small (char-level) vocabularies: per-workgroup LDS tables, summed in order
+                nparts = max(1, min(_grid(dev), -(-N * 2 * FW // 256)))
+                partial = torch.empty(nparts, V, E, dtype=torch.float32, device=dev)
+                check(lib().pv_conv_f32_bwd_dx_lds(P(gpool), P(pooled), P(argmax), P(ids), P(w3), P(w4), P(partial),
+                                                   P(dtable), N, L, E, V, nparts, seed, P(sp), row_offset, thr, tok,
+                                                   scale, s), "pv_conv_f32_bwd_dx_lds")
+            else:
+                check(lib().pv_conv_f32_bwd_dx(P(gpool), P(pooled), P(argmax), P(ids), P(w3), P(w4), P(dtable), N, L,
+                                               E, V, seed, P(sp), row_offset, thr, tok, scale, s), "pv_conv_f32_bwd_dx")
+        dw3 = dw4 = db3 = db4 = None
+        if any(ctx.needs_input_grad[2:6]):
+            nsplit = max(1, min(128, N // 16))  # 16 samples per (filter, split) block: 4 per wave
+            dwpart = torch.empty(nsplit, 2 * FW, 4 * E, dtype=torch.float32, device=dev)
+            dbpart = torch.empty(nsplit, 2 * FW, dtype=torch.float32, device=dev)
+            check(lib().pv_conv_f32_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tab), P(dwpart), P(dbpart), N,
+                                           L, E, V, nsplit, seed, P(sp), row_offset, thr, tok, scale, s),
+                  "pv_conv_f32_bwd_dw")
+            dw3 = dwpart[:, :FW, :3 * E].sum(0).view(FW, 3, E)
+            dw4 = dwpart[:, FW:, :].sum(0).view(FW, 4, E)
+            db = dbpart.sum(0)
+            db3, db4 = db[:FW], db[FW:]
+        return (None, dtable, dw3, dw4, db3, db4, None, None, None, None, None)
+
+
 def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, biases, p: float, seed: int,
                             training: bool, mode: str = "element", row_offset: int = 0,
                             compute_cache=None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -344,6 +437,11 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
     ``compute_cache``: optional (tbl16, wpack) already derived from the current params.
     """
     note_rows(table, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
+    if ids.is_cuda and ref_precision() and table.dtype == torch.float32 and \
+            f32_supported(table.shape[1], [w.shape[1] for w in weights], weights[0].shape[0]):
+        (w3, w4), (b3, b4) = weights, biases
+        return _ConvPoolF32Fn.apply(ids, table, w3, w4, b3, b4, float(p), int(seed), int(row_offset), bool(training),
+                                    mode)
     if use_hip(ids, table) and fast_path_supported(table.shape[1], [w.shape[1] for w in weights], weights[0].shape[0]):
         w3, w4 = weights
         b3, b4 = biases
@@ -358,7 +456,7 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
         raise NotImplementedError(
             f"fused CDSSM conv kernel supports filter_sizes={WIDTHS}, num_filters={FW}, embedding_dim<={EP}; got "
             f"filter_sizes={tuple(w.shape[1] for w in weights)}, num_filters={weights[0].shape[0]}, "
-            f"embedding_dim={table.shape[1]}. Use dtype='fp32' (reference-precision PyTorch ops, any geometry) "
+            f"embedding_dim={table.shape[1]}. Use dtype='fp32' (reference precision; PyTorch ops for other geometries) "
             f"or the supported geometry.")
     x = ref.embed_dropout(ids, table, p, seed, training, mode) if row_offset == 0 else \
         _embed_dropout_offset(ids, table, p, seed, training, mode, row_offset)

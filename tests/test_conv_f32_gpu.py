@@ -1,0 +1,114 @@
+"""dtype="fp32" (the reference's precision): the fp32 HIP conv tower (csrc/kernels/conv_pool_f32.hip,
+fp32 MFMA) vs the plain-PyTorch fp32 reference of the same op (run on MI355X: pytest -m gpu)."""
+import types
+
+import pytest
+import torch
+
+from dnn_page_vectors_amd.ops import _common
+from dnn_page_vectors_amd.ops import conv_pool as cops
+from dnn_page_vectors_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+FP32 = types.SimpleNamespace(dtype="fp32")
+
+
+def _spy(monkeypatch):
+    calls = []
+    orig = cops._ConvPoolF32Fn.apply
+    monkeypatch.setattr(cops._ConvPoolF32Fn, "apply", lambda *a: calls.append(1) or orig(*a))
+    return calls
+
+
+@pytest.mark.parametrize("N,L,V,E,p,mode", [
+    (5, 130, 97, 100, 0.25, "element"),   # two segments, nibble-mode dropout (the reference's 0.25)
+    (4, 1400, 300, 100, 0.3, "element"),  # eleven segments, byte-mode dropout
+    (3, 64, 97, 100, 0.25, "token"),
+    (6, 4, 50, 100, 0.0, "element"),      # one window per width (k = 4: one, k = 3: two)
+    (7, 300, 500, 64, 0.125, "element"),  # E = 64
+    (2, 5000, 120, 100, 0.25, "element"), # char-level page length
+    (40, 45, 1000, 100, 0.25, "element"),
+    (3, 260, 90, 112, 0.0, "element"),    # E = EMAX
+])
+def test_conv_f32_fwd_bwd_matches_fp32_reference(N, L, V, E, p, mode, monkeypatch):
+    calls = _spy(monkeypatch)
+    torch.manual_seed(0)
+    F = 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    table = (torch.randn(V, E, device=DEV) * 0.5).requires_grad_(True)
+    w3 = (torch.randn(F, 3, E, device=DEV) * 0.1).requires_grad_(True)
+    w4 = (torch.randn(F, 4, E, device=DEV) * 0.1).requires_grad_(True)
+    b3 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    b4 = (torch.randn(F, device=DEV) * 0.1).requires_grad_(True)
+    seed = 4321
+    with _common.precision_scope(FP32):
+        pooled, argmax = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], p, seed, True, mode)
+    assert calls, "dtype=fp32 did not take the native fp32 kernel"
+    tr = table.detach().clone().requires_grad_(True)
+    w3r, w4r = w3.detach().clone(), w4.detach().clone()
+    x = ref.embed_dropout(ids, tr, p, seed, True, mode)
+    pr, ar = ref.conv_relu_maxpool(x, [w3r, w4r], [b3.detach(), b4.detach()])
+    torch.testing.assert_close(pooled, pr, rtol=1e-5, atol=2e-5)
+    live = pr > 1e-4
+    assert ((argmax == ar) | ~live).float().mean() > 0.999
+    g = torch.randn_like(pooled)
+    (pooled * g).sum().backward()
+    dws, dbs, dx = ref.conv_maxpool_grads_at(x.detach(), [w3r, w4r], pooled.detach(), argmax, g)
+    x.backward(dx)
+    torch.testing.assert_close(b3.grad, dbs[0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(b4.grad, dbs[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(w3.grad, dws[0], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(w4.grad, dws[1], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(table.grad, tr.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_conv_f32_eval_and_row_offset(monkeypatch):
+    """Eval mode (no mask) and a nonzero flat-row offset (chunked encoders) on the fp32 path."""
+    calls = _spy(monkeypatch)
+    torch.manual_seed(1)
+    N, L, V, E, F = 4, 90, 60, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    table = torch.randn(V, E, device=DEV) * 0.5
+    w3, w4 = torch.randn(F, 3, E, device=DEV) * 0.1, torch.randn(F, 4, E, device=DEV) * 0.1
+    b3, b4 = torch.randn(F, device=DEV) * 0.1, torch.randn(F, device=DEV) * 0.1
+    with _common.precision_scope(FP32):
+        pe, _ = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], 0.25, 7, False)
+        po, _ = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], 0.25, 7, True, row_offset=12345)
+    assert len(calls) == 2
+    pr, _ = ref.conv_relu_maxpool(ref.embed_dropout(ids, table, 0.25, 7, False), [w3, w4], [b3, b4])
+    torch.testing.assert_close(pe, pr, rtol=1e-5, atol=2e-5)
+    xo = cops._embed_dropout_offset(ids, table, 0.25, 7, True, "element", 12345)
+    pro, _ = ref.conv_relu_maxpool(xo, [w3, w4], [b3, b4])
+    torch.testing.assert_close(po, pro, rtol=1e-5, atol=2e-5)
+
+
+def test_cdssm_fp32_step_native_matches_torch_ops(monkeypatch):
+    """One dtype="fp32" CDSSM training step: the native fp32 conv tower gives the loss and the
+    flat gradient of the all-PyTorch fp32 path (PAGEVEC_F32_NATIVE=0)."""
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.set_info(pdist.DistInfo(device=torch.device(DEV)))
+    V = 500
+    cfg = Configuration(model="cdssm", feature_level="ngram", vocab_hash_size=V, query_length=12,
+                        document_length=200, batch_size=32, embedding_dim=100, dtype="fp32")
+    g = torch.Generator().manual_seed(4)
+    q = torch.randint(1, V, (32, 12), generator=g, dtype=torch.int32).to(DEV)
+    d = torch.randint(1, V, (32, cfg.J + 1, 200), generator=g, dtype=torch.int32).to(DEV)
+    out = []
+    for native in (False, True):
+        monkeypatch.setattr(_common, "F32_NATIVE", native)
+        calls = _spy(monkeypatch)
+        torch.manual_seed(0)
+        tr = Trainer(cfg, build_model(cfg, V), torch.device(DEV))
+        m = tr.train_step(q, d)
+        torch.cuda.synchronize()
+        assert bool(calls) == native
+        out.append((float(m["loss"]), tr.flat.grad.clone()))
+    (la, ga), (lb, gb) = out
+    assert abs(la - lb) <= 1e-5 * max(1.0, abs(la))
+    err = float((ga - gb).abs().max() / ga.abs().max())
+    assert err < 1e-4, err
