@@ -67,3 +67,18 @@ def test_conv_grads_at_given_argmax_match_autograd():
     dws, dbs, dx = ref.conv_maxpool_grads_at(x.detach(), [w3.detach(), w4.detach()], p.detach(), a, g)
     for got, want in ((dws[0], w3.grad), (dws[1], w4.grad), (dbs[0], b3.grad), (dbs[1], b4.grad), (dx, x.grad)):
         torch.testing.assert_close(got, want)
+
+
+def test_f32_forward_plan_covers_every_window():
+    """ops/conv_pool.py::f32_plan: segments are whole 128-window chunks, cover the L - 2 windows
+    exactly (the kernel's launcher rejects anything else) and give every workgroup work."""
+    from dnn_page_vectors_amd.ops import conv_pool as cops
+
+    for N in (1, 3, 64, 128, 512, 4096):
+        for L in (4, 5, 130, 131, 250, 1000, 5000, 20000):
+            for cus in (8, 80, 256):
+                nslots, nseg, sw = cops.f32_plan(N, L, cus)
+                nw3 = L - 2
+                assert sw % 128 == 0 and sw >= 128
+                assert (nseg - 1) * sw < nw3 <= nseg * sw
+                assert 1 <= nslots <= max(1, cus // 5) and nslots <= N * nseg
