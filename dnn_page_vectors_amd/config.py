@@ -123,8 +123,9 @@ class Configuration:
     sparse_embedding_grad: bool = False
     optimizer_bf16_mirror: bool = True   # the Adam kernel also writes the bf16 compute copies of big weights
     # compute precision (ops/_common.py::precision_scope): bf16 = the HIP kernels (bf16 MFMA
-    # operands, fp32 accumulation / master weights); fp32 = the reference's precision through
-    # PyTorch's fp32 ops (no bf16 anywhere).  CPU runs compute fp32 either way.
+    # operands, fp32 accumulation / master weights); fp32 = the reference's precision, no bf16
+    # anywhere: the CDSSM conv tower on fp32-MFMA kernels (conv_pool_f32.hip), the other ops
+    # through PyTorch's fp32 ops.  CPU runs compute fp32 either way.
     dtype: str = "bf16"
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
@@ -136,7 +137,7 @@ class Configuration:
     skip_nonfinite: bool = True
     prefetch: int = 2                     # featurized batches the loader thread keeps ahead (pinned)
     num_workers: int = 0                  # featurizer threads per batch (C++ pool); 0 = min(16, CPUs)
-    # saved-config format: 2 = dtype 'fp32' selects the reference-precision PyTorch path (in
+    # saved-config format: 2 = dtype 'fp32' selects the reference-precision path (in
     # version-1 files, written before the field existed, 'fp32' was the no-op default)
     config_version: int = 2
 
