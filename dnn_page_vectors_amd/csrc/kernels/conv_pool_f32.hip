@@ -43,7 +43,15 @@ struct Params {
   const unsigned* seed_ptr;
   unsigned row_offset;
   int thr, token_mode;
+  const unsigned* mask;  // keep-bit plane (conv_f32_mask_kernel) or nullptr: hash inline
+  int wpr;               // mask words per row
 };
+
+// keep bits of the 4 fp32 columns 4pc .. 4pc+3 from their row's mask word -> AND masks
+__device__ __forceinline__ u32x4 bits4(unsigned word, int pc) {
+  const unsigned nib = word >> (4 * (pc & 7));
+  return u32x4{0u - (nib & 1u), 0u - ((nib >> 1) & 1u), 0u - ((nib >> 2) & 1u), 0u - ((nib >> 3) & 1u)};
+}
 
 // keep masks of fp32 columns 4pc .. 4pc+3 of a row with row hash hr (ops/reference.py
 // dropout_keep_mask: nibble mode for thr % 16 == 0, byte mode otherwise, token mode)
@@ -118,6 +126,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
   // (the validity selects wait for their loads, so they are kept as bit masks and applied
   // only where the loaded values are consumed)
   int tk[PPT];
+  unsigned mk[PPT], mk1[PPT];  // mask words of the chunk whose ids are in tk / whose rows are in v
   u32x4 v[PPT];
   unsigned idok = 0u, rowok = 0u;
   auto ids_load = [&](int it, int c) {
@@ -128,7 +137,9 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
       const int q = threadIdx.x + i * NTH;
       const int r = q / E4, t = t0 + r;
       const bool ok = r < CR && t < p.L;
-      tk[i] = p.ids[(size_t)n * p.L + (ok ? t : 0)];
+      const size_t row = (size_t)n * p.L + (ok ? t : 0);
+      tk[i] = p.ids[row];
+      if (p.mask) mk[i] = p.mask[row * p.wpr + ((q - r * E4) >> 3)];
       idok |= (ok ? 1u : 0u) << i;
     }
   };
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
       const int pc = q % E4, tok = tk[i];
       const bool ok = ((idok >> i) & 1u) && tok >= 0 && tok < p.V;
       v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)(ok ? tok : 0) * E + 4 * pc);
+      mk1[i] = mk[i];
       rowok |= (ok ? 1u : 0u) << i;
     }
   };
@@ -153,8 +165,9 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
         u32x4 x = v[i];
         const unsigned m = ((rowok >> i) & 1u) ? 0xFFFFFFFFu : 0u;
         x &= u32x4{m, m, m, m};
-        if (p.thr > 0) x &= keep4(dropout_row_hash(seed, p.row_offset + (unsigned)(n * p.L + t0 + r)), pc, p.thr,
-                                  p.token_mode);
+        if (p.mask) x &= bits4(mk1[i], pc);
+        else if (p.thr > 0)
+          x &= keep4(dropout_row_hash(seed, p.row_offset + (unsigned)(n * p.L + t0 + r)), pc, p.thr, p.token_mode);
         *reinterpret_cast<u32x4*>(xl + r * E + 4 * pc) = x;
       }
     }
@@ -319,6 +332,283 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
   }
 }
 
+// ---- v2: role-split workgroup (the bf16 forward's v7 pattern) ----------------------------
+// 512 threads: waves 0-3 (one per SIMD) run the MFMAs of a 64-window chunk (one 16-window
+// block each) from LDS buffer k % 2 while waves 4-7 gather, mask and store chunk k + 1 into the
+// other buffer; one workgroup barrier per chunk.  The loaders also merge the MFMA waves'
+// per-item maxima (written to red[k % 2] before the barrier) into `part`.  E is fixed at 100
+// (LDS: 89.6 KB weights + 2 x 26.8 KB rows).
+constexpr int NTH2 = 512, CW2 = 64, CR2 = CW2 + 3, E2 = 100;
+constexpr int PPT2 = (CR2 * (E2 / 4) + 255) / 256;  // 16-byte pieces per loader thread (7)
+
+__global__ __launch_bounds__(NTH2, 1) void conv_f32_fwd2_kernel(Params p) {
+  constexpr int E = E2, E4 = E / 4;
+  __shared__ __attribute__((aligned(16))) float wl[7 * E * FG];
+  __shared__ __attribute__((aligned(16))) float xl[2][CR2 * E];
+  __shared__ float2 red[2][4][2][FG];
+  const unsigned seed = p.seed + (p.seed_ptr ? *p.seed_ptr : 0u);
+  const int g = blockIdx.x % NG, slot = blockIdx.x / NG, nslots = gridDim.x / NG;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int items = p.N * p.nseg;
+  if (slot >= items) return;
+  for (int x = threadIdx.x; x < 7 * E * FG; x += NTH2) {
+    const int kk = x / FG, r = x - kk * FG;
+    const int f = g * FG + (r & 1) * 16 + (r >> 1);
+    float v = 0.f;
+    if (f < FW) v = kk < 3 * E ? p.w3[(size_t)f * 3 * E + kk] : p.w4[(size_t)f * 4 * E + (kk - 3 * E)];
+    wl[x] = v;
+  }
+  const int nw3 = p.L - 2, nw4 = p.L - 3;
+  auto seg_end = [&](int seg) { return min((seg + 1) * p.sw, nw3); };
+  auto nch = [&](int it) {
+    const int seg = it % p.nseg;
+    return (seg_end(seg) - seg * p.sw + CW2 - 1) / CW2;
+  };
+  auto next = [&](int& it, int& c) {
+    if (++c >= nch(it)) {
+      c = 0;
+      it += nslots;
+    }
+  };
+  if (wave >= 4) {
+    // ---------------- loader role
+    const int lt = threadIdx.x - 256;
+    int tk[PPT2];
+    unsigned mk[PPT2], mk1[PPT2];
+    u32x4 v[PPT2];
+    unsigned idok = 0u, rowok = 0u;
+    auto ids_load = [&](int it, int c) {
+      const int n = it / p.nseg, t0 = (it % p.nseg) * p.sw + c * CW2;
+      idok = 0u;
+#pragma unroll
+      for (int i = 0; i < PPT2; ++i) {
+        const int q = lt + i * 256;
+        const int r = q / E4, t = t0 + r;
+        const bool ok = r < CR2 && t < p.L;
+        const size_t row = (size_t)n * p.L + (ok ? t : 0);
+        tk[i] = p.ids[row];
+        if (p.mask) mk[i] = p.mask[row * p.wpr + ((q - r * E4) >> 3)];
+        idok |= (ok ? 1u : 0u) << i;
+      }
+    };
+    auto rows_load = [&]() {
+      rowok = 0u;
+#pragma unroll
+      for (int i = 0; i < PPT2; ++i) {
+        const int q = lt + i * 256;
+        const int pc = q % E4, tok = tk[i];
+        const bool ok = ((idok >> i) & 1u) && tok >= 0 && tok < p.V;
+        v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)(ok ? tok : 0) * E + 4 * pc);
+        mk1[i] = mk[i];
+        rowok |= (ok ? 1u : 0u) << i;
+      }
+    };
+    auto stage_store = [&](int it, int c, float* dst) {
+      const int n = it / p.nseg, t0 = (it % p.nseg) * p.sw + c * CW2;
+#pragma unroll
+      for (int i = 0; i < PPT2; ++i) {
+        const int q = lt + i * 256;
+        const int r = q / E4, pc = q - r * E4;
+        if (r < CR2) {
+          u32x4 x = v[i];
+          const unsigned m = ((rowok >> i) & 1u) ? 0xFFFFFFFFu : 0u;
+          x &= u32x4{m, m, m, m};
+          if (p.mask) x &= bits4(mk1[i], pc);
+          else if (p.thr > 0)
+            x &= keep4(dropout_row_hash(seed, p.row_offset + (unsigned)(n * p.L + t0 + r)), pc, p.thr,
+                       p.token_mode);
+          *reinterpret_cast<u32x4*>(dst + r * E + 4 * pc) = x;
+        }
+      }
+    };
+    // the item whose maxima the MFMA waves left in red[par] before the barrier just passed
+    auto merge = [&](int it, int par) {
+      if (lt < 2 * FG) {
+        const int w = lt / FG, fl = lt % FG;
+        float2 best = red[par][0][w][fl];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          const float2 o = red[par][q][w][fl];
+          if (better(o.x, __float_as_int(o.y), best.x, __float_as_int(best.y))) best = o;
+        }
+        const int f = g * FG + fl;
+        if (f < FW) p.part[(size_t)it * (2 * FW) + w * FW + f] = best;
+      }
+    };
+    int it = slot, c = 0;
+    ids_load(it, c);
+    rows_load();
+    stage_store(it, c, xl[0]);
+    int it1 = it, c1 = c;
+    next(it1, c1);
+    if (it1 < items) ids_load(it1, c1);
+    int par = 0, done_it = -1;
+    __syncthreads();  // S0: weights + chunk 0
+    while (it < items) {
+      // chunk k = (it, c) is being computed from xl[par]; stage chunk k + 1 into xl[par ^ 1]
+      if (it1 < items) {
+        rows_load();
+        int it2 = it1, c2 = c1;
+        next(it2, c2);
+        if (it2 < items) ids_load(it2, c2);
+        stage_store(it1, c1, xl[par ^ 1]);
+      }
+      if (done_it >= 0) merge(done_it, par ^ 1);
+      done_it = (it1 != it) ? it : -1;  // chunk k ends its item: red[par] after the barrier
+      __syncthreads();  // B_{k+1}
+      it = it1;
+      c = c1;
+      next(it1, c1);
+      par ^= 1;
+    }
+    if (done_it >= 0) merge(done_it, par ^ 1);
+    return;
+  }
+  // ---------------- MFMA role
+  f32x4 m[2][2];
+  int ix[2][2][4];
+  auto reset = [&]() {
+#pragma unroll
+    for (int w = 0; w < 2; ++w)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        m[w][t] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ix[w][t][r] = 0x7FFFFFFF;
+      }
+  };
+  reset();
+  const int a_off = (wave * 16 + (lane & 15)) * E + (lane >> 4);
+  const int b_off = (lane >> 4) * FG + 2 * (lane & 15);
+  constexpr int S3 = 3 * E / 4, S4 = E;
+  int it = slot, c = 0, par = 0;
+  __syncthreads();  // S0
+  while (it < items) {
+    const float* xa = xl[par] + a_off;
+    const float* wb3 = wl + b_off;
+    const float* wb4 = wl + 3 * E * FG + b_off;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[w][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float an = xa[0];
+    float2 b3n = *reinterpret_cast<const float2*>(wb3), b4n = *reinterpret_cast<const float2*>(wb4);
+#pragma unroll
+    for (int s = 0; s < S3; ++s) {
+      const float a = an;
+      const float2 b3 = b3n, b4 = b4n;
+      an = xa[4 * (s + 1)];
+      b3n = *reinterpret_cast<const float2*>(wb3 + 4 * (s + 1) * FG);
+      b4n = *reinterpret_cast<const float2*>(wb4 + 4 * (s + 1) * FG);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b3.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b3.y, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4.x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4.y, acc[1][1], 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = S3; s < S4; ++s) {
+      const float a = an;
+      const float2 b4 = b4n;
+      const int sn = s + 1 < S4 ? s + 1 : s;
+      an = xa[4 * sn];
+      b4n = *reinterpret_cast<const float2*>(wb4 + 4 * sn * FG);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4.x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b4.y, acc[1][1], 0, 0, 0);
+    }
+    const int seg = it % p.nseg;
+    const int wend = seg_end(seg);
+    const int t0 = seg * p.sw + c * CW2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int win = t0 + wave * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const bool ok = win < min(wend, w == 0 ? nw3 : nw4);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float y = acc[w][t][r];
+          if (ok && y > m[w][t][r]) {
+            m[w][t][r] = y;
+            ix[w][t][r] = win;
+          }
+        }
+      }
+    }
+    int it1 = it, c1 = c;
+    next(it1, c1);
+    if (it1 != it) {  // item end: rows and lanes -> red[par] (the loaders merge the waves)
+#pragma unroll
+      for (int w = 0; w < 2; ++w)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          float bv = m[w][t][0];
+          int bi = ix[w][t][0];
+#pragma unroll
+          for (int r = 1; r < 4; ++r)
+            if (better(m[w][t][r], ix[w][t][r], bv, bi)) {
+              bv = m[w][t][r];
+              bi = ix[w][t][r];
+            }
+#pragma unroll
+          for (int o = 16; o < 64; o <<= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (better(ov, oi, bv, bi)) {
+              bv = ov;
+              bi = oi;
+            }
+          }
+          if (lane < 16) red[par][wave][w][t * 16 + lane] = make_float2(bv, __int_as_float(bi));
+        }
+      reset();
+    }
+    __syncthreads();  // B_{k+1}
+    it = it1;
+    c = c1;
+    par ^= 1;
+  }
+}
+
+// ---- dropout keep-bit plane: bit j of word w of local row R = keep(column 32w + j) of flat row
+// row_offset + R (ops/reference.py dropout_keep_mask).  The forward's five filter-group
+// workgroups of a chunk, dW and dTable read one u32 per 32 columns instead of recomputing the
+// hashes (the fp32 MFMA shares the SIMD's vector issue: every hash instruction cost MFMA time).
+__global__ __launch_bounds__(256) void conv_f32_mask_kernel(unsigned* __restrict__ mask, long rows, int wpr,
+                                                            unsigned seed, const unsigned* seed_ptr,
+                                                            unsigned row_offset, int thr, int token_mode) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * wpr) return;
+  if (seed_ptr) seed += *seed_ptr;
+  const long R = i / wpr;
+  const int w = (int)(i - R * wpr);
+  const unsigned hr = dropout_row_hash(seed, row_offset + (unsigned)R);
+  unsigned bits = 0u;
+  if (token_mode) {
+    bits = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
+  } else if ((thr & 15) == 0) {
+    const unsigned t = (unsigned)thr >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned h = dropout_group_hash(hr, (unsigned)(4 * w + q));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (((h >> (4 * j)) & 0xFu) >= t ? 1u : 0u) << (8 * q + j);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const unsigned h = dropout_group_hash(hr, (unsigned)(8 * w + q));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bits |= ((int)((h >> (8 * j)) & 0xFFu) >= thr ? 1u : 0u) << (4 * q + j);
+    }
+  }
+  mask[i] = bits;
+}
+
 // segments in window order (strict >: the earliest maximum wins), bias, ReLU
 __global__ __launch_bounds__(256) void conv_f32_finalize_kernel(const float2* __restrict__ part,
                                                                 const float* __restrict__ b3,
@@ -352,7 +642,8 @@ __global__ __launch_bounds__(256) void conv_f32_dw_kernel(const float* __restric
                                                           const float* __restrict__ table, float* dwpart,
                                                           float* dbpart, int N, int L, int E, int V, int per,
                                                           unsigned seed, const unsigned* seed_ptr, unsigned row_offset,
-                                                          int thr, int token_mode, float scale) {
+                                                          int thr, int token_mode, float scale,
+                                                          const unsigned* __restrict__ mask, int wpr) {
   __shared__ float red[4][4 * EMAX];
   __shared__ float gs[4];
   if (seed_ptr) seed += *seed_ptr;
@@ -399,10 +690,12 @@ __global__ __launch_bounds__(256) void conv_f32_dw_kernel(const float* __restric
       for (int q = 0; q < DW_M; ++q) {
         const int t = tok[u][q];
         float xv = (t >= 0 && t < V) ? table[(size_t)t * E + eq[q]] : 0.f;
-        if (thr > 0 && xv != 0.f &&
-            !keep1(dropout_row_hash(seed, row_offset + (unsigned)((nb + u) * L + a[u] + jq[q])), eq[q], thr,
-                   token_mode))
-          xv = 0.f;
+        if (thr > 0 && xv != 0.f) {
+          const unsigned R = (unsigned)((nb + u) * L + a[u] + jq[q]);
+          const bool keep = mask ? ((mask[(size_t)R * wpr + (eq[q] >> 5)] >> (eq[q] & 31)) & 1u) != 0u
+                                 : keep1(dropout_row_hash(seed, row_offset + R), eq[q], thr, token_mode);
+          if (!keep) xv = 0.f;
+        }
         acc[q] = fmaf(g[u], xv, acc[q]);
       }
   }
@@ -425,7 +718,7 @@ __global__ __launch_bounds__(256) void conv_f32_dx_kernel(const float* __restric
                                                           const float* __restrict__ w3, const float* __restrict__ w4,
                                                           float* dtable, int N, int L, int E, int V, unsigned seed,
                                                           const unsigned* seed_ptr, unsigned row_offset, int thr,
-                                                          int token_mode, float scale) {
+                                                          int token_mode, float scale, const unsigned* __restrict__ mask, int wpr) {
   if (seed_ptr) seed += *seed_ptr;
   const int lane = threadIdx.x & 63;
   const long pair = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -440,9 +733,10 @@ __global__ __launch_bounds__(256) void conv_f32_dx_kernel(const float* __restric
     const int t = a + j;
     const int tok = ids[(size_t)n * L + t];
     if (!PV_OK(tok >= 0 && tok < V, PV_ERR_ID) || tok < 0 || tok >= V) continue;
-    const unsigned hr = thr > 0 ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + t)) : 0u;
+    const unsigned hr = thr > 0 && !mask ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + t)) : 0u;
+    const unsigned* mrow = mask ? mask + (size_t)(n * L + t) * wpr : nullptr;
     for (int e = lane; e < E; e += 64) {
-      if (thr > 0 && !keep1(hr, e, thr, token_mode)) continue;
+      if (thr > 0 && !(mrow ? ((mrow[e >> 5] >> (e & 31)) & 1u) != 0u : keep1(hr, e, thr, token_mode))) continue;
       atomicAdd(dtable + (size_t)tok * E + e, gs * w[j * E + e]);
     }
   }
@@ -462,7 +756,7 @@ __global__ __launch_bounds__(256) void conv_f32_dx_lds_kernel(const float* __res
                                                               const float* __restrict__ w4, float* partial, int N,
                                                               int L, int E, int V, unsigned seed,
                                                               const unsigned* seed_ptr, unsigned row_offset, int thr,
-                                                              int token_mode, float scale) {
+                                                              int token_mode, float scale, const unsigned* __restrict__ mask, int wpr) {
   __shared__ float tab[DXP_LDS / 4];
   if (seed_ptr) seed += *seed_ptr;
   const int VE = V * E;
@@ -481,9 +775,10 @@ __global__ __launch_bounds__(256) void conv_f32_dx_lds_kernel(const float* __res
       const int t = a + j;
       const int tok = ids[(size_t)n * L + t];
       if (tok < 0 || tok >= V) continue;
-      const unsigned hr = thr > 0 ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + t)) : 0u;
+      const unsigned hr = thr > 0 && !mask ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + t)) : 0u;
+      const unsigned* mrow = mask ? mask + (size_t)(n * L + t) * wpr : nullptr;
       for (int e = lane; e < E; e += 64) {
-        if (thr > 0 && !keep1(hr, e, thr, token_mode)) continue;
+        if (thr > 0 && !(mrow ? ((mrow[e >> 5] >> (e & 31)) & 1u) != 0u : keep1(hr, e, thr, token_mode))) continue;
         atomicAdd(tab + tok * E + e, gs * w[j * E + e]);
       }
     }
@@ -508,22 +803,42 @@ PV_DEBUG_EXPORT(convf32)
 
 using namespace pv::convf32;
 
+static int g_fwd2 = 1;  // 1: role-split forward (v2) at E = 100; 0: v1 (A/B)
+PV_API void pv_conv_f32_set_v2(int on) { g_fwd2 = on; }
 PV_API int pv_conv_f32_groups() { return NG; }
+
+// keep-bit plane of rows local rows 0 .. rows-1 (flat rows row_offset + R), wpr words per row
+PV_API int pv_conv_f32_mask(unsigned* mask, long rows, int wpr, unsigned seed, const unsigned* seed_ptr,
+                            unsigned row_offset, int thr, int token_mode, void* stream) {
+  if (rows < 0 || wpr < 1 || thr <= 0) return -1;
+  if (rows == 0) return 0;
+  const long n = rows * wpr;
+  hipLaunchKernelGGL(conv_f32_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
+                     rows, wpr, seed, seed_ptr, row_offset, thr, token_mode);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
 PV_API int pv_conv_f32_chunk() { return CW; }
 PV_API int pv_conv_f32_emax() { return EMAX; }
 
 PV_API int pv_conv_f32_fwd(const int* ids, const float* table, const float* w3, const float* w4, const float* b3,
                            const float* b4, void* part, float* pooled, int* argmax, int N, int L, int V, int E,
                            int nseg, int sw, int nslots, unsigned seed, const unsigned* seed_ptr, unsigned row_offset,
-                           int thr, int token_mode, float scale, void* stream) {
+                           int thr, int token_mode, float scale, const unsigned* mask, int wpr, void* stream) {
   if (N <= 0) return 0;
   const int nw3 = L - 2;
-  if (L < 4 || E < 4 || E > EMAX || (E & 3) || nseg < 1 || sw < CW || sw % CW || (long)nseg * sw < nw3 ||
+  const bool v2 = E == E2 && g_fwd2;
+  const int cw = v2 ? CW2 : CW;
+  if (L < 4 || E < 4 || E > EMAX || (E & 3) || nseg < 1 || sw < cw || sw % cw || (long)nseg * sw < nw3 ||
       (long)(nseg - 1) * sw >= nw3 || nslots < 1)
     return -1;
   hipStream_t st = (hipStream_t)stream;
-  Params p{ids, table, w3, w4, (float2*)part, N, L, V, E, nseg, sw, seed, seed_ptr, row_offset, thr, token_mode};
-  if (E == 100)
+  if (mask && wpr < (E + 31) / 32) return -1;
+  Params p{ids,  table,    w3,         w4,  (float2*)part, N,          L,    V,   E, nseg, sw,
+           seed, seed_ptr, row_offset, thr, token_mode,    thr > 0 ? mask : nullptr, wpr};
+  if (v2)
+    hipLaunchKernelGGL(conv_f32_fwd2_kernel, dim3(nslots * NG), dim3(NTH2), 0, st, p);
+  else if (E == 100)
     hipLaunchKernelGGL(conv_f32_fwd_kernel<100>, dim3(nslots * NG), dim3(NTH), 0, st, p);
   else
     hipLaunchKernelGGL(conv_f32_fwd_kernel<0>, dim3(nslots * NG), dim3(NTH), 0, st, p);
@@ -538,13 +853,13 @@ PV_API int pv_conv_f32_fwd(const int* ids, const float* table, const float* w3, 
 PV_API int pv_conv_f32_bwd_dw(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                               const float* table, float* dwpart, float* dbpart, int N, int L, int E, int V, int nsplit,
                               unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                              float scale, void* stream) {
-  if (E < 1 || E > EMAX || nsplit < 1) return -1;
+                              float scale, const unsigned* mask, int wpr, void* stream) {
+  if (E < 1 || E > EMAX || nsplit < 1 || (mask && wpr < (E + 31) / 32)) return -1;
   if (N <= 0) return 0;
   const int per = (N + nsplit - 1) / nsplit;
   hipLaunchKernelGGL(conv_f32_dw_kernel, dim3(2 * FW, nsplit), dim3(256), 0, (hipStream_t)stream, gpool, pooled,
                      argmax, ids, table, dwpart, dbpart, N, L, E, V, per, seed, seed_ptr, row_offset, thr, token_mode,
-                     scale);
+                     scale, mask, wpr);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -555,12 +870,12 @@ PV_API int pv_conv_f32_dx_lds_max() { return DXP_LDS / 4; }
 PV_API int pv_conv_f32_bwd_dx_lds(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                                   const float* w3, const float* w4, float* partial, float* dtable, int N, int L, int E,
                                   int V, int nparts, unsigned seed, const unsigned* seed_ptr, unsigned row_offset,
-                                  int thr, int token_mode, float scale, void* stream) {
-  if (E < 1 || V < 1 || (long)V * E > DXP_LDS / 4 || nparts < 1) return -1;
+                                  int thr, int token_mode, float scale, const unsigned* mask, int wpr, void* stream) {
+  if (E < 1 || V < 1 || (long)V * E > DXP_LDS / 4 || nparts < 1 || (mask && wpr < (E + 31) / 32)) return -1;
   if (N <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv_f32_dx_lds_kernel, dim3(nparts), dim3(256), 0, st, gpool, pooled, argmax, ids, w3, w4,
-                     partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale);
+                     partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale, mask, wpr);
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(conv_f32_dx_sum_kernel, dim3((V * E + 255) / 256), dim3(256), 0, st, (const float*)partial,
                      dtable, V * E, nparts);
@@ -571,13 +886,13 @@ PV_API int pv_conv_f32_bwd_dx_lds(const float* gpool, const float* pooled, const
 PV_API int pv_conv_f32_bwd_dx(const float* gpool, const float* pooled, const int* argmax, const int* ids,
                               const float* w3, const float* w4, float* dtable, int N, int L, int E, int V,
                               unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr, int token_mode,
-                              float scale, void* stream) {
-  if (E < 1) return -1;
+                              float scale, const unsigned* mask, int wpr, void* stream) {
+  if (E < 1 || (mask && wpr < (E + 31) / 32)) return -1;
   if (N <= 0) return 0;
   const long pairs = (long)N * 2 * FW;
   hipLaunchKernelGGL(conv_f32_dx_kernel, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, (hipStream_t)stream, gpool,
                      pooled, argmax, ids, w3, w4, dtable, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode,
-                     scale);
+                     scale, mask, wpr);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -25,13 +25,15 @@ SIGS = {
     "pv_conv_pool_bwd_rec": "ppp" "i" "f" "p",
     # conv_pool_f32.hip (dtype="fp32": reference-precision conv tower)
     "pv_conv_f32_groups": "",
+    "pv_conv_f32_set_v2": "i",
     "pv_conv_f32_chunk": "",
     "pv_conv_f32_emax": "",
-    "pv_conv_f32_fwd": "ppppppppp" "iiiiiii" "upu" "ii" "f" "p",
-    "pv_conv_f32_bwd_dw": "ppppppp" "iiiii" "upu" "ii" "f" "p",
-    "pv_conv_f32_bwd_dx": "ppppppp" "iiii" "upu" "ii" "f" "p",
+    "pv_conv_f32_fwd": "ppppppppp" "iiiiiii" "upu" "ii" "f" "pi" "p",
+    "pv_conv_f32_mask": "pli" "upu" "ii" "p",
+    "pv_conv_f32_bwd_dw": "ppppppp" "iiiii" "upu" "ii" "f" "pi" "p",
+    "pv_conv_f32_bwd_dx": "ppppppp" "iiii" "upu" "ii" "f" "pi" "p",
     "pv_conv_f32_dx_lds_max": "",
-    "pv_conv_f32_bwd_dx_lds": "pppppppp" "iiiii" "upu" "ii" "f" "p",
+    "pv_conv_f32_bwd_dx_lds": "pppppppp" "iiiii" "upu" "ii" "f" "pi" "p",
     # conv_pool_bwd.hip
     "pv_conv_pool_bwd_dw": "ppppp" "ppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_dw2": "ppppp" "pppp" "iiii" "upuiif" "p",

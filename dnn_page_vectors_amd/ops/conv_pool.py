@@ -340,6 +340,8 @@ class _ConvPoolFn(torch.autograd.Function):
 F32_EMAX = 112  # conv_pool_f32.hip EMAX (LDS sizing)
 # 0: the fp32 dTable always uses global row atomics (A/B of the LDS-privatised small-V path)
 F32_DX_LDS = os.environ.get("PAGEVEC_F32_DX_LDS", "1") != "0"
+# 0: the fp32 kernels recompute the dropout hashes instead of reading the keep-bit plane (A/B)
+F32_MASK = os.environ.get("PAGEVEC_F32_MASK", "1") != "0"
 
 
 def f32_supported(E: int, widths, num_filters: int) -> bool:
@@ -381,12 +383,22 @@ class _ConvPoolF32Fn(torch.autograd.Function):
         seed &= 0xFFFFFFFF
         row_offset &= 0xFFFFFFFF
         sp = _SEED_DEV
+        # dropout keep bits, one u32 per 32 columns per row, shared by the forward's five filter
+        # groups and the backward (instead of each recomputing the hashes)
+        wpr = (E + 31) // 32
+        mask = None
+        if thr > 0 and F32_MASK:
+            mask = torch.empty(N * L * wpr, dtype=torch.int32, device=ids.device)
+            check(lib().pv_conv_f32_mask(P(mask), N * L, wpr, seed, P(sp), row_offset, thr, tok, stream(ids.device)),
+                  "pv_conv_f32_mask")
         check(lib().pv_conv_f32_fwd(P(ids), P(tab), P(w3c), P(w4c), P(b3.detach().contiguous()),
                                     P(b4.detach().contiguous()), P(part), P(pooled), P(argmax), N, L, V, E, nseg, sw,
-                                    nslots, seed, P(sp), row_offset, thr, tok, scale, stream(ids.device)),
+                                    nslots, seed, P(sp), row_offset, thr, tok, scale, P(mask), wpr,
+                                    stream(ids.device)),
               "pv_conv_f32_fwd")
         ctx.save_for_backward(ids, tab, w3c, w4c, pooled, argmax)
-        ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp)
+        ctx.mask = mask
+        ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp, wpr)
         ctx.mark_non_differentiable(argmax)
         ctx.set_materialize_grads(False)
         return pooled, argmax
@@ -396,7 +408,8 @@ class _ConvPoolF32Fn(torch.autograd.Function):
         if gpool is None:
             return (None,) * 11
         ids, tab, w3, w4, pooled, argmax = ctx.saved_tensors
-        V, E, seed, row_offset, thr, tok, scale, sp = ctx.meta
+        V, E, seed, row_offset, thr, tok, scale, sp, wpr = ctx.meta
+        mask, ctx.mask = ctx.mask, None
         N, L = ids.shape
         dev = ids.device
         s = stream(dev)
@@ -410,17 +423,19 @@ class _ConvPoolF32Fn(torch.autograd.Function):
                 partial = torch.empty(nparts, V, E, dtype=torch.float32, device=dev)
                 check(lib().pv_conv_f32_bwd_dx_lds(P(gpool), P(pooled), P(argmax), P(ids), P(w3), P(w4), P(partial),
                                                    P(dtable), N, L, E, V, nparts, seed, P(sp), row_offset, thr, tok,
-                                                   scale, s), "pv_conv_f32_bwd_dx_lds")
+                                                   scale, P(mask), wpr, s), "pv_conv_f32_bwd_dx_lds")
             else:
                 check(lib().pv_conv_f32_bwd_dx(P(gpool), P(pooled), P(argmax), P(ids), P(w3), P(w4), P(dtable), N, L,
-                                               E, V, seed, P(sp), row_offset, thr, tok, scale, s), "pv_conv_f32_bwd_dx")
+                                               E, V, seed, P(sp), row_offset, thr, tok, scale, P(mask), wpr, s),
+                      "pv_conv_f32_bwd_dx")
         dw3 = dw4 = db3 = db4 = None
         if any(ctx.needs_input_grad[2:6]):
             nsplit = max(1, min(128, N // 16))  # 16 samples per (filter, split) block: 4 per wave
             dwpart = torch.empty(nsplit, 2 * FW, 4 * E, dtype=torch.float32, device=dev)
             dbpart = torch.empty(nsplit, 2 * FW, dtype=torch.float32, device=dev)
             check(lib().pv_conv_f32_bwd_dw(P(gpool), P(pooled), P(argmax), P(ids), P(tab), P(dwpart), P(dbpart), N,
-                                           L, E, V, nsplit, seed, P(sp), row_offset, thr, tok, scale, s),
+                                           L, E, V, nsplit, seed, P(sp), row_offset, thr, tok, scale, P(mask), wpr,
+                                           s),
                   "pv_conv_f32_bwd_dw")
             dw3 = dwpart[:, :FW, :3 * E].sum(0).view(FW, 3, E)
             dw4 = dwpart[:, FW:, :].sum(0).view(FW, 4, E)

@@ -112,3 +112,53 @@ def test_cdssm_fp32_step_native_matches_torch_ops(monkeypatch):
     assert abs(la - lb) <= 1e-5 * max(1.0, abs(la))
     err = float((ga - gb).abs().max() / ga.abs().max())
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("N,L,p", [(5, 130, 0.25), (3, 5000, 0.25), (64, 45, 0.0), (2, 700, 0.3)])
+def test_conv_f32_role_split_forward_bit_identical(N, L, p):
+    """The role-split forward (v2, E = 100) and the one-role kernel (v1) accumulate every
+    output in the same order: pooled and argmax bit-identical."""
+    from dnn_page_vectors_amd.ops._common import lib
+
+    torch.manual_seed(2)
+    V, E, F = 300, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    table = torch.randn(V, E, device=DEV) * 0.5
+    w3, w4 = torch.randn(F, 3, E, device=DEV) * 0.1, torch.randn(F, 4, E, device=DEV) * 0.1
+    b3, b4 = torch.randn(F, device=DEV) * 0.1, torch.randn(F, device=DEV) * 0.1
+    out = []
+    try:
+        for v2 in (0, 1):
+            lib().pv_conv_f32_set_v2(v2)
+            with _common.precision_scope(FP32):
+                out.append(cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], p, 9, True))
+    finally:
+        lib().pv_conv_f32_set_v2(1)
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("p,mode", [(0.25, "element"), (0.3, "element"), (0.25, "token")])
+def test_conv_f32_mask_plane_matches_inline_hash(p, mode, monkeypatch):
+    """The keep-bit plane (conv_f32_mask_kernel) and the inline hashes give the same forward
+    (bit-identical) and the same gradients."""
+    torch.manual_seed(3)
+    N, L, V, E, F = 4, 333, 80, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    res = []
+    for use_mask in (False, True):
+        monkeypatch.setattr(cops, "F32_MASK", use_mask)
+        torch.manual_seed(4)
+        table = (torch.randn(V, E, device=DEV) * 0.5).requires_grad_(True)
+        w3 = (torch.randn(F, 3, E, device=DEV) * 0.1).requires_grad_(True)
+        w4 = (torch.randn(F, 4, E, device=DEV) * 0.1).requires_grad_(True)
+        b3 = torch.zeros(F, device=DEV, requires_grad=True)
+        b4 = torch.zeros(F, device=DEV, requires_grad=True)
+        with _common.precision_scope(FP32):
+            y, a = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], p, 11, True, mode, row_offset=77)
+        (y * torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)).sum().backward()
+        res.append((y.detach(), a, table.grad, w3.grad, w4.grad))
+    (y0, a0, *g0), (y1, a1, *g1) = res
+    assert torch.equal(y0, y1) and torch.equal(a0, a1)
+    for u, v in zip(g0, g1):
+        torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)

@@ -23,8 +23,13 @@ def main():
     ap.add_argument("--E", type=int, default=100)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bwd", type=int, default=0)
+    ap.add_argument("--v2", type=int, default=1, help="role-split forward (0: v1)")
+    ap.add_argument("--mask", type=int, default=1, help="dropout keep-bit plane (0: inline hashes)")
     a = ap.parse_args()
     dev = "cuda"
+    from dnn_page_vectors_amd.ops._common import lib
+    lib().pv_conv_f32_set_v2(a.v2)
+    cops.F32_MASK = bool(a.mask)
     torch.manual_seed(0)
     F = 150
     ids = torch.randint(0, a.V, (a.N, a.L), dtype=torch.int32, device=dev)
@@ -49,7 +54,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / a.iters
-        print(json.dumps({"N": a.N, "L": a.L, "E": a.E, "p": p, "bwd": a.bwd, "ms": round(ms, 3),
+        print(json.dumps({"v2": a.v2, "mask": a.mask, "N": a.N, "L": a.L, "E": a.E, "p": p, "bwd": a.bwd, "ms": round(ms, 3),
                           "fwd_tflops": round(flops / ms / 1e9, 1)}), flush=True)
 
 
