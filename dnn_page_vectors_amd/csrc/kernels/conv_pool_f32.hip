@@ -748,7 +748,8 @@ __global__ __launch_bounds__(256) void conv_f32_dx_kernel(const float* __restric
 // the table (LDS atomics), then writes it as one partial table; a second kernel sums the
 // partials in workgroup order into dtable.
 constexpr int DXP_LDS = 64 * 1024;
-__global__ __launch_bounds__(256) void conv_f32_dx_lds_kernel(const float* __restrict__ gpool,
+constexpr int DXP_NTH = 256;  // (1024 measured slower: 0.68 -> 0.82 ms per step)
+__global__ __launch_bounds__(DXP_NTH) void conv_f32_dx_lds_kernel(const float* __restrict__ gpool,
                                                               const float* __restrict__ pooled,
                                                               const int* __restrict__ argmax,
                                                               const int* __restrict__ ids,
@@ -760,32 +761,105 @@ __global__ __launch_bounds__(256) void conv_f32_dx_lds_kernel(const float* __res
   __shared__ float tab[DXP_LDS / 4];
   if (seed_ptr) seed += *seed_ptr;
   const int VE = V * E;
-  for (int x = threadIdx.x; x < VE; x += 256) tab[x] = 0.f;
+  for (int x = threadIdx.x; x < VE; x += DXP_NTH) tab[x] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const long pairs = (long)N * 2 * FW;
-  for (long pair = (long)blockIdx.x * 4 + (threadIdx.x >> 6); pair < pairs; pair += (long)gridDim.x * 4) {
+  for (long pair = (long)blockIdx.x * (DXP_NTH / 64) + (threadIdx.x >> 6); pair < pairs;
+       pair += (long)gridDim.x * (DXP_NTH / 64)) {
     const float g = gpool[pair];
     if (!(pooled[pair] > 0.f) || g == 0.f) continue;  // wave-uniform
     const int n = (int)(pair / (2 * FW)), f = (int)(pair - (long)n * 2 * FW);
     const int a = argmax[pair], K = f < FW ? 3 : 4;
     const float* w = f < FW ? w3 + (size_t)f * 3 * E : w4 + (size_t)(f - FW) * 4 * E;
     const float gs = g * scale;
-    for (int j = 0; j < K; ++j) {
+    // the window's token ids and weight rows loaded together (one latency per pair, not per row)
+    int tok[4];
+    float wv[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tok[j] = j < K ? ids[(size_t)n * L + a + j] : -1;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int e = lane + 64 * c;
+        wv[j][c] = (j < K && e < E) ? w[j * E + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (tok[j] < 0 || tok[j] >= V) continue;
       const int t = a + j;
-      const int tok = ids[(size_t)n * L + t];
-      if (tok < 0 || tok >= V) continue;
       const unsigned hr = thr > 0 && !mask ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + t)) : 0u;
       const unsigned* mrow = mask ? mask + (size_t)(n * L + t) * wpr : nullptr;
-      for (int e = lane; e < E; e += 64) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int e = lane + 64 * c;
+        if (e >= E) continue;
         if (thr > 0 && !(mrow ? ((mrow[e >> 5] >> (e & 31)) & 1u) != 0u : keep1(hr, e, thr, token_mode))) continue;
-        atomicAdd(tab + tok * E + e, gs * w[j * E + e]);
+        atomicAdd(tab + tok[j] * E + e, gs * wv[j][c]);
       }
     }
   }
   __syncthreads();
   float* out = partial + (size_t)blockIdx.x * VE;
-  for (int x = threadIdx.x; x < VE; x += 256) out[x] = tab[x];
+  for (int x = threadIdx.x; x < VE; x += DXP_NTH) out[x] = tab[x];
+}
+
+// V x E <= DXW_MAX (the ~100-symbol char tables): one PRIVATE LDS table per wave (4 x 40 KB),
+// updated by plain read-add-write (a wave's LDS operations complete in order and its lanes
+// hold distinct columns) instead of ds_add_f32, whose float-atomic unit retires ~0.3 lanes per
+// clock per CU and serialised this kernel (0.6-0.7 ms per step); the four tables are summed
+// into the workgroup's partial.
+constexpr int DXW_MAX = 10240;
+__global__ __launch_bounds__(256, 1) void conv_f32_dx_wave_kernel(const float* __restrict__ gpool,
+                                                                  const float* __restrict__ pooled,
+                                                                  const int* __restrict__ argmax,
+                                                                  const int* __restrict__ ids,
+                                                                  const float* __restrict__ w3,
+                                                                  const float* __restrict__ w4, float* partial,
+                                                                  int N, int L, int E, int V, unsigned seed,
+                                                                  const unsigned* seed_ptr, unsigned row_offset,
+                                                                  int thr, int token_mode, float scale) {
+  __shared__ float tabs[4 * DXW_MAX];
+  if (seed_ptr) seed += *seed_ptr;
+  const int VE = V * E;
+  for (int x = threadIdx.x; x < 4 * VE; x += 256) tabs[x] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* tab = tabs + wave * VE;
+  const long pairs = (long)N * 2 * FW;
+  for (long pair = (long)blockIdx.x * 4 + wave; pair < pairs; pair += (long)gridDim.x * 4) {
+    const float g = gpool[pair];
+    if (!(pooled[pair] > 0.f) || g == 0.f) continue;  // wave-uniform
+    const int n = (int)(pair / (2 * FW)), f = (int)(pair - (long)n * 2 * FW);
+    const int a = argmax[pair], K = f < FW ? 3 : 4;
+    const float* w = f < FW ? w3 + (size_t)f * 3 * E : w4 + (size_t)(f - FW) * 4 * E;
+    const float gs = g * scale;
+    int tok[4];
+    float wv[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tok[j] = j < K ? ids[(size_t)n * L + a + j] : -1;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int e = lane + 64 * c;
+        wv[j][c] = (j < K && e < E) ? w[j * E + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (tok[j] < 0 || tok[j] >= V) continue;
+      const unsigned hr = thr > 0 ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + a + j)) : 0u;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int e = lane + 64 * c;
+        if (e < E && (thr <= 0 || keep1(hr, e, thr, token_mode))) tab[tok[j] * E + e] += gs * wv[j][c];
+      }
+    }
+  }
+  __syncthreads();
+  float* out = partial + (size_t)blockIdx.x * VE;
+  for (int x = threadIdx.x; x < VE; x += 256) out[x] = ((tabs[x] + tabs[VE + x]) + tabs[2 * VE + x]) + tabs[3 * VE + x];
 }
 
 __global__ __launch_bounds__(256) void conv_f32_dx_sum_kernel(const float* __restrict__ partial, float* dtable,
@@ -804,6 +878,8 @@ PV_DEBUG_EXPORT(convf32)
 using namespace pv::convf32;
 
 static int g_fwd2 = 1;  // 1: role-split forward (v2) at E = 100; 0: v1 (A/B)
+static int g_dxw = 1;   // 1: wave-private LDS dTable for V x E <= DXW_MAX; 0: shared table + ds_add_f32 (A/B)
+PV_API void pv_conv_f32_set_dxw(int on) { g_dxw = on; }
 PV_API void pv_conv_f32_set_v2(int on) { g_fwd2 = on; }
 PV_API int pv_conv_f32_groups() { return NG; }
 
@@ -871,10 +947,15 @@ PV_API int pv_conv_f32_bwd_dx_lds(const float* gpool, const float* pooled, const
                                   const float* w3, const float* w4, float* partial, float* dtable, int N, int L, int E,
                                   int V, int nparts, unsigned seed, const unsigned* seed_ptr, unsigned row_offset,
                                   int thr, int token_mode, float scale, const unsigned* mask, int wpr, void* stream) {
-  if (E < 1 || V < 1 || (long)V * E > DXP_LDS / 4 || nparts < 1 || (mask && wpr < (E + 31) / 32)) return -1;
+  if (E < 1 || E > 128 || V < 1 || (long)V * E > DXP_LDS / 4 || nparts < 1 || (mask && wpr < (E + 31) / 32))
+    return -1;
   if (N <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv_f32_dx_lds_kernel, dim3(nparts), dim3(256), 0, st, gpool, pooled, argmax, ids, w3, w4,
+  if (V * E <= DXW_MAX && g_dxw)
+    hipLaunchKernelGGL(conv_f32_dx_wave_kernel, dim3(nparts), dim3(256), 0, st, gpool, pooled, argmax, ids, w3, w4,
+                       partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale);
+  else
+    hipLaunchKernelGGL(conv_f32_dx_lds_kernel, dim3(nparts), dim3(DXP_NTH), 0, st, gpool, pooled, argmax, ids, w3, w4,
                      partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale, mask, wpr);
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(conv_f32_dx_sum_kernel, dim3((V * E + 255) / 256), dim3(256), 0, st, (const float*)partial,

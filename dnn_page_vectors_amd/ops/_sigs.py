@@ -26,6 +26,7 @@ SIGS = {
     # conv_pool_f32.hip (dtype="fp32": reference-precision conv tower)
     "pv_conv_f32_groups": "",
     "pv_conv_f32_set_v2": "i",
+    "pv_conv_f32_set_dxw": "i",
     "pv_conv_f32_chunk": "",
     "pv_conv_f32_emax": "",
     "pv_conv_f32_fwd": "ppppppppp" "iiiiiii" "upu" "ii" "f" "pi" "p",

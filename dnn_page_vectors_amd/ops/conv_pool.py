@@ -384,7 +384,7 @@ class _ConvPoolF32Fn(torch.autograd.Function):
         row_offset &= 0xFFFFFFFF
         sp = _SEED_DEV
         # dropout keep bits, one u32 per 32 columns per row, shared by the forward's five filter
-        # groups and the backward (instead of each recomputing the hashes)
+        # groups (instead of each recomputing the hashes)
         wpr = (E + 31) // 32
         mask = None
         if thr > 0 and F32_MASK:
@@ -397,7 +397,10 @@ class _ConvPoolF32Fn(torch.autograd.Function):
                                     stream(ids.device)),
               "pv_conv_f32_fwd")
         ctx.save_for_backward(ids, tab, w3c, w4c, pooled, argmax)
-        ctx.mask = mask
+        # the backward kernels recompute the hashes: they are latency-bound on their gathers, and
+        # a dependent mask-word load cost more than the VALU (dx 0.58 -> 0.74, dW 0.17 -> 0.30 ms
+        # per step with the plane)
+        ctx.mask = None
         ctx.meta = (V, E, seed, row_offset, thr, tok, scale, sp, wpr)
         ctx.mark_non_differentiable(argmax)
         ctx.set_materialize_grads(False)
@@ -417,9 +420,9 @@ class _ConvPoolF32Fn(torch.autograd.Function):
         dtable = None
         if ctx.needs_input_grad[1]:
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
-            if V * E <= lib().pv_conv_f32_dx_lds_max() and F32_DX_LDS:
+            if V * E <= lib().pv_conv_f32_dx_lds_max() and E <= 128 and F32_DX_LDS:
                 # small (char-level) vocabularies: per-workgroup LDS tables, summed in order
-                nparts = max(1, min(_grid(dev), -(-N * 2 * FW // 256)))
+                nparts = max(1, min(_grid(dev), -(-N * 2 * FW // 256)))  # one workgroup per CU at most
                 partial = torch.empty(nparts, V, E, dtype=torch.float32, device=dev)
                 check(lib().pv_conv_f32_bwd_dx_lds(P(gpool), P(pooled), P(argmax), P(ids), P(w3), P(w4), P(partial),
                                                    P(dtable), N, L, E, V, nparts, seed, P(sp), row_offset, thr, tok,

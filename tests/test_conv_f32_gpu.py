@@ -162,3 +162,31 @@ def test_conv_f32_mask_plane_matches_inline_hash(p, mode, monkeypatch):
     assert torch.equal(y0, y1) and torch.equal(a0, a1)
     for u, v in zip(g0, g1):
         torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dxw", [0, 1])
+def test_conv_f32_small_vocab_table_grad_paths(dxw):
+    """Both small-vocabulary dTable kernels (wave-private LDS tables / shared table with LDS
+    float atomics) against the fp32 reference, hot rows included (a 7-symbol vocabulary)."""
+    from dnn_page_vectors_amd.ops._common import lib
+
+    torch.manual_seed(5)
+    N, L, V, E, F = 6, 400, 7, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    table = (torch.randn(V, E, device=DEV) * 0.5).requires_grad_(True)
+    w3 = torch.randn(F, 3, E, device=DEV) * 0.1
+    w4 = torch.randn(F, 4, E, device=DEV) * 0.1
+    b3, b4 = torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)
+    try:
+        lib().pv_conv_f32_set_dxw(dxw)
+        with _common.precision_scope(FP32):
+            y, a = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], 0.25, 3, True)
+        g = torch.randn_like(y)
+        (y * g).sum().backward()
+    finally:
+        lib().pv_conv_f32_set_dxw(1)
+    tr = table.detach().clone().requires_grad_(True)
+    x = ref.embed_dropout(ids, tr, 0.25, 3, True)
+    _, _, dx = ref.conv_maxpool_grads_at(x.detach(), [w3, w4], y.detach(), a, g)
+    x.backward(dx)
+    torch.testing.assert_close(table.grad, tr.grad, rtol=1e-4, atol=1e-4)
