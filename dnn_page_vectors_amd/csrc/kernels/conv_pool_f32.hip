@@ -22,6 +22,7 @@
 
 namespace pv {
 namespace convf32 {
+PV_DEBUG_FLAG
 
 constexpr int FW = 150;                  // filters per width
 constexpr int FG = 32;                   // filters per group: two 16-wide MFMA tiles
