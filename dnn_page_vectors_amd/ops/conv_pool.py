@@ -362,6 +362,32 @@ def f32_plan(N: int, L: int, n_cu: int) -> Tuple[int, int, int]:
     return max(1, min(nslots, N * nseg)), nseg, sw
 
 
+F32_DXW_MAX = 10240  # conv_pool_f32.hip DXW_MAX: wave-private tables (deterministic sums)
+
+
+def _f32_dtable_ordered(gpool, pooled, argmax, ids, w3, w4, dtable, seed, row_offset, thr, tok, scale):
+    """dTable += scale * g[n, f] * W[f, j, :] * keep(n, a + j, :) at row ids[n, a + j] for every live
+    (n, f) pair, accumulated by torch's deterministic index_add_ (determinism mode)."""
+    N, L = ids.shape
+    V, E = dtable.shape
+    live = (pooled > 0) & (gpool != 0)
+    n_i, f_i = live.nonzero(as_tuple=True)
+    a = argmax[n_i, f_i].long()
+    g = gpool[n_i, f_i] * scale
+    for W, K, lo, hi in ((w3, 3, 0, FW), (w4, 4, FW, 2 * FW)):
+        sel = (f_i >= lo) & (f_i < hi)
+        n_, f_, a_, g_ = n_i[sel], f_i[sel] - lo, a[sel], g[sel]
+        t = a_[:, None] + torch.arange(K, device=ids.device)
+        tk = ids[n_[:, None], t].long()
+        contrib = g_[:, None, None] * W[f_]
+        if thr > 0:
+            keep = ref.dropout_keep_mask(seed, 0, E, thr / 256.0, row_offset, "token" if tok else "element",
+                                         rows=n_[:, None] * L + t)
+            contrib = contrib * keep.view(-1, K, E).to(contrib.dtype)
+        ok = (tk >= 0) & (tk < V)
+        dtable.index_add_(0, tk[ok], contrib[ok])
+
+
 class _ConvPoolF32Fn(torch.autograd.Function):
     """fp32 gather -> dropout -> conv(3, 4) -> max-pool -> ReLU with fp32 MFMAs, and its sparse
     argmax backward (dW / db per-split partials summed in order; dTable fp32 row atomics)."""
@@ -418,7 +444,12 @@ class _ConvPoolF32Fn(torch.autograd.Function):
         s = stream(dev)
         gpool = gpool.contiguous().float()
         dtable = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and determinism.enabled() and V * E > F32_DXW_MAX:
+            # deterministic mode: the LDS / global float-atomic table kernels sum in arrival
+            # order; torch's deterministic index_add_ over the (pair, row) contributions instead
+            dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
+            _f32_dtable_ordered(gpool, pooled, argmax, ids, w3, w4, dtable, seed, row_offset, thr, tok, scale)
+        elif ctx.needs_input_grad[1]:
             dtable = torch.zeros(V, E, dtype=torch.float32, device=dev)
             if V * E <= lib().pv_conv_f32_dx_lds_max() and E <= 128 and F32_DX_LDS:
                 # small (char-level) vocabularies: per-workgroup LDS tables, summed in order

@@ -41,8 +41,9 @@ def dropout_threshold(p: float) -> int:
 
 
 def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: int = 0,
-                      mode: str = "element", device=None) -> torch.Tensor:
-    """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r``.
+                      mode: str = "element", device=None, rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r`` (r < n_rows,
+    or r in ``rows`` when given: any local row ids, n_rows = rows.numel()).
 
     element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25):
              h_row = mix(row ^ mix(seed)); nibble b of mix(h_row + g*0x9E3779B9) decides column
@@ -51,7 +52,11 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     token:   one decision per row: byte 0 of h_row.
     """
     thr = dropout_threshold(p)
-    rows = torch.arange(n_rows, dtype=torch.int64, device=device) + int(row_offset)
+    if rows is None:
+        rows = torch.arange(n_rows, dtype=torch.int64, device=device) + int(row_offset)
+    else:
+        rows = rows.reshape(-1).to(torch.int64) + int(row_offset)
+        n_rows, device = rows.numel(), rows.device
     h_row = _mix32(rows ^ _mix32(torch.tensor(int(seed) & _M32, dtype=torch.int64, device=device)))
     if mode == "token":
         b = h_row & 0xFF

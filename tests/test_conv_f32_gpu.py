@@ -190,3 +190,35 @@ def test_conv_f32_small_vocab_table_grad_paths(dxw):
     _, _, dx = ref.conv_maxpool_grads_at(x.detach(), [w3, w4], y.detach(), a, g)
     x.backward(dx)
     torch.testing.assert_close(table.grad, tr.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("V", [1000, 150])  # global-atomic and shared-LDS-atomic table paths
+def test_conv_f32_deterministic_mode_bit_identical(V):
+    """Deterministic mode on the fp32 path: two backward passes give bit-identical gradients
+    (the float-atomic table kernels are replaced by an ordered index_add_), close to the
+    atomic path's."""
+    from dnn_page_vectors_amd.ops import determinism
+
+    torch.manual_seed(6)
+    N, L, E, F = 8, 300, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    w3 = torch.randn(F, 3, E, device=DEV) * 0.1
+    w4 = torch.randn(F, 4, E, device=DEV) * 0.1
+    b3, b4 = torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)
+    base = torch.randn(V, E, device=DEV) * 0.5
+
+    def grads():
+        table = base.clone().requires_grad_(True)
+        with _common.precision_scope(FP32):
+            y, _ = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], [b3, b4], 0.25, 5, True)
+        (y * torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)).sum().backward()
+        return table.grad
+
+    prev = determinism.set_deterministic(True)
+    try:
+        g1, g2 = grads(), grads()
+    finally:
+        determinism.restore(prev)
+    g3 = grads()
+    assert torch.equal(g1, g2)
+    torch.testing.assert_close(g1, g3, rtol=1e-5, atol=1e-5)

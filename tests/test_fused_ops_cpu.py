@@ -1,6 +1,7 @@
 """CPU semantics of the fused-op entry points (the reference path the HIP kernels are
 checked against on the GPU): column sums with accumulate / epilogue, the bag with fused
 bias + activation, and the loss ``reduce`` mode."""
+import pytest
 import torch
 
 from dnn_page_vectors_amd.ops import dense as dops
@@ -82,3 +83,29 @@ def test_f32_forward_plan_covers_every_window():
                 assert sw % 128 == 0 and sw >= 128
                 assert (nseg - 1) * sw < nw3 <= nseg * sw
                 assert 1 <= nslots <= max(1, cus // 5) and nslots <= N * nseg
+
+
+@pytest.mark.parametrize("p,mode", [(0.25, "element"), (0.3, "element"), (0.25, "token"), (0.0, "element")])
+def test_f32_ordered_table_grad_matches_reference(p, mode):
+    """ops/conv_pool.py::_f32_dtable_ordered (the fp32 table gradient of deterministic mode)
+    against autograd through the reference embedding dropout + conv + max-pool."""
+    from dnn_page_vectors_amd.ops import conv_pool as cops
+    from dnn_page_vectors_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    N, L, V, E, F = 3, 40, 50, 16, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32)
+    table = torch.randn(V, E)
+    w3, w4 = torch.randn(F, 3, E) * 0.2, torch.randn(F, 4, E) * 0.2
+    b3, b4 = torch.randn(F) * 0.1, torch.randn(F) * 0.1
+    seed, row_offset = 99, 1234
+    tr = table.clone().requires_grad_(True)
+    x = cops._embed_dropout_offset(ids, tr, p, seed, True, mode, row_offset)
+    pooled, argmax = ref.conv_relu_maxpool(x, [w3, w4], [b3, b4])
+    g = torch.randn_like(pooled)
+    _, _, dx = ref.conv_maxpool_grads_at(x.detach(), [w3, w4], pooled, argmax, g)
+    x.backward(dx)
+    thr, tok, scale = cops._dropout_args(p, True, mode)
+    dt = torch.zeros(V, E)
+    cops._f32_dtable_ordered(g, pooled, argmax, ids, w3, w4, dt, seed, row_offset, thr, tok, scale)
+    torch.testing.assert_close(dt, tr.grad, rtol=1e-5, atol=1e-5)
