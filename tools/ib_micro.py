@@ -60,8 +60,30 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
             t = sorted(ts[2:])[len(ts[2:]) // 2]
+            # GPU time of the same fwd + bwd back to back (CUDA events, no host sync between
+            # iterations: the launch latency overlaps as it does inside a training step; the
+            # leaves are built once, their .grad reset to None)
+            q = qn.clone().requires_grad_(True)
+            d = dn.clone().requires_grad_(True)
+
+            def step():
+                q.grad = None
+                d.grad = None
+                loss, _ = L.inbatch_loss(q, d, pos, 10.0, True)
+                loss.sum().backward()
+
+            step()
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(a.iters):
+                step()
+            ev1.record()
+            torch.cuda.synchronize()
+            tg = ev0.elapsed_time(ev1) / a.iters / 1e3
             fl = 2.0 * a.B * M * 160 * 5
-            print(f"ib{ver} M={M}: fwd+bwd {t*1e3:.3f} ms ({fl / t / 1e12:.0f} TF/s incl. glue) "
+            print(f"ib{ver} M={M}: fwd+bwd {t*1e3:.3f} ms host-synced per call incl. clones ({fl / t / 1e12:.0f} TF/s), "
+                  f"{tg*1e3:.3f} ms GPU back to back ({fl / tg / 1e12:.0f} TF/s); "
                   f"err loss {e[0]:.2e} dq {e[1]:.2e} dd {e[2]:.2e}", flush=True)
 
 
