@@ -12,12 +12,18 @@
 // A read per block and one B pair read per width feed 8 MFMAs of 32 cycles.  The k = 3 and
 // k = 4 windows share their first 3E reduction indices, so their A fragments are the same
 // reads.  Per-segment max / argmax -> `part`; a finalize kernel merges segments in window
-// order (first maximum wins), adds the bias, applies ReLU.
+// order (first maximum wins), adds the bias, applies ReLU.  That is v1 (any E % 4 == 0 up to
+// EMAX; fully unrolled at E = 100).  At E = 100 the production kernel is v2: the same MFMA
+// stream in 4 waves over 64-window chunks while 4 loader waves stage the next chunk into a
+// second LDS buffer.  With dropout, a keep-bit plane (conv_f32_mask_kernel, one u32 per 32
+// columns per row) is computed once and read by all five filter groups.
 //
 // Backward (same algebra as conv_pool_bwd.hip, fp32 operands): the gradient of filter f of
 // sample n reaches only its argmax window.  dW / db: one workgroup per (filter, sample
 // split), partial sums per split (summed in order on the host side: deterministic).  dTable:
-// one wave per (sample, filter) pair, fp32 row atomics (E per window row).
+// wave-private LDS tables for V x E <= 10 K (the char vocabularies; deterministic), a shared
+// LDS table with float atomics up to 16 K, fp32 row atomics above (deterministic mode replaces
+// those two with an ordered index_add_ in ops/conv_pool.py).
 #include "common.h"
 
 namespace pv {
