@@ -3,6 +3,8 @@
 GPU: ``csrc/kernels/conv_pool_fwd.hip`` (forward, MFMA, weights register-resident)
 and ``conv_pool_bwd.hip`` + ``radix_sort.hip`` (sparse argmax backward).  CPU:
 ``ops/reference.py`` (identical semantics incl. the counter-based dropout mask).
+``dtype="fp32"`` (reference precision) on the GPU: ``csrc/kernels/conv_pool_f32.hip`` (fp32 MFMA
+forward, fp32 sparse backward; ``_ConvPoolF32Fn``).
 
 Reference layers: Embedding -> Dropout(0.25) -> Graph{Convolution1D(150, k, relu) ->
 MaxPooling1D(L-k+1) -> Flatten} x k in (3,4) -> concat (dssm_cnn_v2/cnn_dssm_th.py:83-134).
