@@ -979,7 +979,7 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   return 0;
 }
 
-// Fused forward + dQ part (see ib_bwd_kernel FWD): sumexp (nx), U (nx, DP) fp32 fully
+// Fused forward + dQ part (ib5 / ib3 with FWD = true): sumexp (nx), U (nx, DP) fp32 fully
 // written; ws_u = pv_ib_bwd_ws(nx, ny, DP) floats, part = pv_ib_fwd_dq_parts(nx, ny) floats.
 PV_API long pv_ib_fwd_dq_parts(int nx, int ny) {
   int ns, per;
