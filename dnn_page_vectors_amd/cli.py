@@ -125,7 +125,10 @@ def cmd_train(a) -> int:
                               cfg.num_negative_examples)
         train_loader = PairLoader(tr, cfg.batch_size, shuffle=a.shuffle, seed=cfg.seed, rank=d_rank,
                                   world_size=d_world, prefetch=cfg.prefetch, device=info.device)
-        val_loader = PairLoader(va, cfg.batch_size, rank=d_rank, world_size=d_world, device=info.device)
+        # validation keeps the last partial batch (Keras evaluates every row; each rank gets the
+        # same row count, so the partial batch has one shape on every rank)
+        val_loader = PairLoader(va, cfg.batch_size, rank=d_rank, world_size=d_world, device=info.device,
+                                drop_last=False)
         steps = min(train_loader.num_batches(), max(1, cfg.num_train_samples // (cfg.batch_size * d_world)))
     model = build_model(cfg, V)
     if cfg.feature_level == "word" and cfg.vocab_hash_size <= 1 and os.path.exists(cfg.word_vectors_file):
@@ -140,7 +143,7 @@ def cmd_train(a) -> int:
     if a.resume and ck.resume(trainer, cfg.trained_model_dir):
         log.info("resumed at epoch %d step %d", trainer.epoch, trainer.step)
     hist = trainer.fit(lambda ep: train_loader.epoch_iter(ep), steps_per_epoch=steps,
-                       validation_batches=lambda ep: val_loader.epoch_iter(0),
+                       validation_batches=lambda ep: val_loader.epoch_iter(0, fresh=True),
                        callbacks=[ck.ModelCheckpoint(cfg.trained_model_dir)])
     ck.save_final(trainer, cfg.trained_model_dir)
     if info.is_main:

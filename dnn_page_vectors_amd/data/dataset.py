@@ -124,9 +124,11 @@ class PairLoader:
     def load_state(self, st: dict) -> None:
         self.epoch, self.cursor = int(st["epoch"]), int(st["cursor"])
 
-    def epoch_iter(self, epoch: Optional[int] = None) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
-        if epoch is not None and epoch != self.epoch:
-            self.epoch, self.cursor = epoch, 0
+    def epoch_iter(self, epoch: Optional[int] = None, fresh: bool = False) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
+        """Batches of ``epoch`` from the saved cursor (resume); ``fresh``: from its first batch
+        (validation passes, whose consumer may stop before the end)."""
+        if fresh or (epoch is not None and epoch != self.epoch):
+            self.epoch, self.cursor = (self.epoch if epoch is None else epoch), 0
         rows = self._rank_rows(self.epoch)
         nb = self.num_batches()
         start = self.cursor
@@ -187,7 +189,12 @@ class SyntheticLoader:
     def load_state(self, st: dict) -> None:
         self.epoch, self.cursor = int(st["epoch"]), int(st["cursor"])
 
-    def epoch_iter(self, epoch: Optional[int] = None):
+    def epoch_iter(self, epoch: Optional[int] = None, fresh: bool = False):
+        # a consumer that stops after exactly ``steps`` batches never runs the epilogue below:
+        # a new epoch index (or fresh) restarts the cursor, as in PairLoader (without it every
+        # other epoch of a CLI run was empty)
+        if fresh or (epoch is not None and epoch != self.epoch):
+            self.epoch, self.cursor = (self.epoch if epoch is None else epoch), 0
         for _ in range(self.cursor, self.steps):
             self.cursor += 1
             yield self.gen.batch(self.B)
@@ -271,9 +278,9 @@ class _TensorLoader:
     def load_state(self, st: dict) -> None:
         self.epoch, self.cursor = int(st["epoch"]), int(st["cursor"])
 
-    def epoch_iter(self, epoch: Optional[int] = None) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
-        if epoch is not None and epoch != self.epoch:
-            self.epoch, self.cursor = epoch, 0
+    def epoch_iter(self, epoch: Optional[int] = None, fresh: bool = False) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
+        if fresh or (epoch is not None and epoch != self.epoch):
+            self.epoch, self.cursor = (self.epoch if epoch is None else epoch), 0
         n = self.q.shape[0]
         order = (np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n))
         per = n // self.world

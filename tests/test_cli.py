@@ -1,4 +1,5 @@
 import json
+import math
 import os
 import subprocess
 import sys
@@ -30,10 +31,12 @@ def test_cli_setup_train_encode(tmp_path):
     out = _run(["train"] + common, tmp_path)
     hist = json.loads(out.strip().splitlines()[-1])["history"]
     assert len(hist["loss"]) == 2 and len(hist["val_loss"]) == 2
+    assert all(math.isfinite(v) for k in ("loss", "val_loss") for v in hist[k]), hist
     # v1 data path: one in-memory file, Keras validation_split, per-epoch shuffle
     out = _run(["train", "--data", str(src), "--validation-split", "0.25"] + common, tmp_path)
     hist = json.loads(out.strip().splitlines()[-1])["history"]
     assert len(hist["loss"]) == 2 and len(hist["val_loss"]) == 2
+    assert all(math.isfinite(v) for k in ("loss", "val_loss") for v in hist[k]), hist
     texts = tmp_path / "pages.txt"
     texts.write_text("topic 3 page text\nother 1 text\n")
     out = _run(["encode", "--input", str(texts), "--output", str(tmp_path / "v.npy")] + common, tmp_path)
@@ -81,3 +84,41 @@ def test_evaluate_pairs_dataset_dedup_and_oracle(tmp_path):
     assert r["recall@1"] == 1.0
     r = evaluate_pairs_dataset(Oracle(), ds, torch.device("cpu"), ks=(1,), include_negatives=False)
     assert r["pages"] == 5
+
+
+def test_cli_synthetic_train_every_epoch_has_batches(tmp_path):
+    """`train --synthetic` over several epochs: every epoch (and its validation pass) runs its
+    batches.  The synthetic loader used to restart only when its generator was exhausted, which
+    the trainer (it takes exactly steps_per_epoch batches) never does: every other epoch was
+    empty and logged NaN."""
+    out = _run(["train", "--preset", "reference_char", "--synthetic", "--set", f"experiment_root_directory={tmp_path}",
+                "--set", "num_train_samples=64", "--set", "num_validation_samples=32", "--set", "batch_size=16",
+                "--set", "nb_epoch=3", "--set", "document_length=24", "--set", "query_length=8"], tmp_path)
+    hist = json.loads(out.strip().splitlines()[-1])["history"]
+    assert len(hist["loss"]) == 3 and len(hist["val_loss"]) == 3
+    assert all(math.isfinite(v) for k in ("loss", "val_loss") for v in hist[k]), hist
+    state = json.loads(open(os.path.join(json.loads(out.strip().splitlines()[-1])["model_dir"],
+                                         "trainer_state.json")).read())
+    assert state["step"] == 3 * 4
+
+
+def test_loaders_restart_after_a_consumer_stops_at_the_last_batch():
+    """A consumer taking exactly the epoch's batches (the trainer) never triggers a generator's
+    epilogue: the next epoch index (or fresh=True) must restart the cursor anyway."""
+    import torch
+
+    from dnn_page_vectors_amd.data.dataset import SyntheticLoader, _TensorLoader
+
+    class Gen:
+        def batch(self, B):
+            return torch.zeros(B, 2), torch.zeros(B, 1, 3)
+
+    for loader in (SyntheticLoader(Gen(), 4, 3),
+                   _TensorLoader(torch.zeros(12, 2), torch.zeros(12, 1, 3), 4, True, 0, None, 0, 1)):
+        for ep in range(3):
+            it = loader.epoch_iter(ep)
+            assert sum(1 for _ in zip(range(3), it)) == 3, (type(loader), ep)
+        it = loader.epoch_iter(0, fresh=True)
+        assert sum(1 for _ in zip(range(3), it)) == 3
+        it = loader.epoch_iter(0, fresh=True)
+        assert sum(1 for _ in zip(range(3), it)) == 3
