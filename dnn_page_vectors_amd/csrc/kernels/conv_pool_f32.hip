@@ -348,6 +348,9 @@ __global__ __launch_bounds__(NTH, 1) void conv_f32_fwd_kernel(Params p) {
 constexpr int NTH2 = 512, CW2 = 64, CR2 = CW2 + 3, E2 = 100;
 constexpr int PPT2 = (CR2 * (E2 / 4) + 255) / 256;  // 16-byte pieces per loader thread (7)
 
+// MM: the loader's mask source at compile time (0 no dropout, 1 keep-bit plane, 2 inline
+// hashes): no per-piece runtime branches in the staging code
+template <int MM>
 __global__ __launch_bounds__(NTH2, 1) void conv_f32_fwd2_kernel(Params p) {
   constexpr int E = E2, E4 = E / 4;
   __shared__ __attribute__((aligned(16))) float wl[7 * E * FG];
@@ -394,7 +397,7 @@ __global__ __launch_bounds__(NTH2, 1) void conv_f32_fwd2_kernel(Params p) {
         const bool ok = r < CR2 && t < p.L;
         const size_t row = (size_t)n * p.L + (ok ? t : 0);
         tk[i] = p.ids[row];
-        if (p.mask) mk[i] = p.mask[row * p.wpr + ((q - r * E4) >> 3)];
+        if constexpr (MM == 1) mk[i] = p.mask[row * 4 + ((q - r * E4) >> 3)];  // wpr = 4 at E = 100
         idok |= (ok ? 1u : 0u) << i;
       }
     };
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(NTH2, 1) void conv_f32_fwd2_kernel(Params p) {
         const int pc = q % E4, tok = tk[i];
         const bool ok = ((idok >> i) & 1u) && tok >= 0 && tok < p.V;
         v[i] = *reinterpret_cast<const u32x4*>(p.table + (size_t)(ok ? tok : 0) * E + 4 * pc);
-        mk1[i] = mk[i];
+        if constexpr (MM == 1) mk1[i] = mk[i];
         rowok |= (ok ? 1u : 0u) << i;
       }
     };
@@ -420,8 +423,8 @@ __global__ __launch_bounds__(NTH2, 1) void conv_f32_fwd2_kernel(Params p) {
           u32x4 x = v[i];
           const unsigned m = ((rowok >> i) & 1u) ? 0xFFFFFFFFu : 0u;
           x &= u32x4{m, m, m, m};
-          if (p.mask) x &= bits4(mk1[i], pc);
-          else if (p.thr > 0)
+          if constexpr (MM == 1) x &= bits4(mk1[i], pc);
+          else if constexpr (MM == 2)
             x &= keep4(dropout_row_hash(seed, p.row_offset + (unsigned)(n * p.L + t0 + r)), pc, p.thr,
                        p.token_mode);
           *reinterpret_cast<u32x4*>(dst + r * E + 4 * pc) = x;
@@ -919,8 +922,12 @@ PV_API int pv_conv_f32_fwd(const int* ids, const float* table, const float* w3, 
   if (mask && wpr < (E + 31) / 32) return -1;
   Params p{ids,  table,    w3,         w4,  (float2*)part, N,          L,    V,   E, nseg, sw,
            seed, seed_ptr, row_offset, thr, token_mode,    thr > 0 ? mask : nullptr, wpr};
-  if (v2)
-    hipLaunchKernelGGL(conv_f32_fwd2_kernel, dim3(nslots * NG), dim3(NTH2), 0, st, p);
+  if (v2 && p.thr <= 0)
+    hipLaunchKernelGGL(conv_f32_fwd2_kernel<0>, dim3(nslots * NG), dim3(NTH2), 0, st, p);
+  else if (v2 && p.mask)
+    hipLaunchKernelGGL(conv_f32_fwd2_kernel<1>, dim3(nslots * NG), dim3(NTH2), 0, st, p);
+  else if (v2)
+    hipLaunchKernelGGL(conv_f32_fwd2_kernel<2>, dim3(nslots * NG), dim3(NTH2), 0, st, p);
   else if (E == 100)
     hipLaunchKernelGGL(conv_f32_fwd_kernel<100>, dim3(nslots * NG), dim3(NTH), 0, st, p);
   else
