@@ -821,7 +821,10 @@ __global__ __launch_bounds__(DXP_NTH) void conv_f32_dx_lds_kernel(const float* _
 // clock per CU and serialised this kernel (0.6-0.7 ms per step); the four tables are summed
 // into the workgroup's partial.
 constexpr int DXW_MAX = 10240;
-__global__ __launch_bounds__(256, 1) void conv_f32_dx_wave_kernel(const float* __restrict__ gpool,
+// 8 waves: waves w and w + 4 share table w % 4 and walk the same pairs, wave w adding columns
+// 0..63 and wave w + 4 columns 64..127 (each address still has one writer), so twice as many
+// waves hide the pairs' dependent loads
+__global__ __launch_bounds__(512, 1) void conv_f32_dx_wave_kernel(const float* __restrict__ gpool,
                                                                   const float* __restrict__ pooled,
                                                                   const int* __restrict__ argmax,
                                                                   const int* __restrict__ ids,
@@ -833,43 +836,38 @@ __global__ __launch_bounds__(256, 1) void conv_f32_dx_wave_kernel(const float* _
   __shared__ float tabs[4 * DXW_MAX];
   if (seed_ptr) seed += *seed_ptr;
   const int VE = V * E;
-  for (int x = threadIdx.x; x < 4 * VE; x += 256) tabs[x] = 0.f;
+  for (int x = threadIdx.x; x < 4 * VE; x += 512) tabs[x] = 0.f;
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* tab = tabs + wave * VE;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, grp = wave & 3;
+  const int e = lane + 64 * (wave >> 2);
+  float* tab = tabs + grp * VE;
   const long pairs = (long)N * 2 * FW;
-  for (long pair = (long)blockIdx.x * 4 + wave; pair < pairs; pair += (long)gridDim.x * 4) {
-    const float g = gpool[pair];
-    if (!(pooled[pair] > 0.f) || g == 0.f) continue;  // wave-uniform
-    const int n = (int)(pair / (2 * FW)), f = (int)(pair - (long)n * 2 * FW);
-    const int a = argmax[pair], K = f < FW ? 3 : 4;
-    const float* w = f < FW ? w3 + (size_t)f * 3 * E : w4 + (size_t)(f - FW) * 4 * E;
-    const float gs = g * scale;
-    int tok[4];
-    float wv[4][2];
+  if (e - lane < E) {  // wave-uniform: the upper half has columns
+    for (long pair = (long)blockIdx.x * 4 + grp; pair < pairs; pair += (long)gridDim.x * 4) {
+      const float g = gpool[pair];
+      if (!(pooled[pair] > 0.f) || g == 0.f) continue;  // wave-uniform
+      const int n = (int)(pair / (2 * FW)), f = (int)(pair - (long)n * 2 * FW);
+      const int a = argmax[pair], K = f < FW ? 3 : 4;
+      const float* w = f < FW ? w3 + (size_t)f * 3 * E : w4 + (size_t)(f - FW) * 4 * E;
+      const float gs = g * scale;
+      int tok[4];
+      float wv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      tok[j] = j < K ? ids[(size_t)n * L + a + j] : -1;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int e = lane + 64 * c;
-        wv[j][c] = (j < K && e < E) ? w[j * E + e] : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        tok[j] = j < K ? ids[(size_t)n * L + a + j] : -1;
+        wv[j] = (j < K && e < E) ? w[j * E + e] : 0.f;
       }
-    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (tok[j] < 0 || tok[j] >= V) continue;
-      const unsigned hr = thr > 0 ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + a + j)) : 0u;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int e = lane + 64 * c;
-        if (e < E && (thr <= 0 || keep1(hr, e, thr, token_mode))) tab[tok[j] * E + e] += gs * wv[j][c];
+      for (int j = 0; j < 4; ++j) {
+        if (tok[j] < 0 || tok[j] >= V) continue;
+        const unsigned hr = thr > 0 ? dropout_row_hash(seed, row_offset + (unsigned)(n * L + a + j)) : 0u;
+        if (e < E && (thr <= 0 || keep1(hr, e, thr, token_mode))) tab[tok[j] * E + e] += gs * wv[j];
       }
     }
   }
   __syncthreads();
   float* out = partial + (size_t)blockIdx.x * VE;
-  for (int x = threadIdx.x; x < VE; x += 256) out[x] = ((tabs[x] + tabs[VE + x]) + tabs[2 * VE + x]) + tabs[3 * VE + x];
+  for (int x = threadIdx.x; x < VE; x += 512) out[x] = ((tabs[x] + tabs[VE + x]) + tabs[2 * VE + x]) + tabs[3 * VE + x];
 }
 
 __global__ __launch_bounds__(256) void conv_f32_dx_sum_kernel(const float* __restrict__ partial, float* dtable,
@@ -965,8 +963,8 @@ PV_API int pv_conv_f32_bwd_dx_lds(const float* gpool, const float* pooled, const
     return -1;
   if (N <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (V * E <= DXW_MAX && g_dxw)
-    hipLaunchKernelGGL(conv_f32_dx_wave_kernel, dim3(nparts), dim3(256), 0, st, gpool, pooled, argmax, ids, w3, w4,
+  if (V * E <= DXW_MAX && E <= 128 && g_dxw)
+    hipLaunchKernelGGL(conv_f32_dx_wave_kernel, dim3(nparts), dim3(512), 0, st, gpool, pooled, argmax, ids, w3, w4,
                        partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale);
   else
     hipLaunchKernelGGL(conv_f32_dx_lds_kernel, dim3(nparts), dim3(DXP_NTH), 0, st, gpool, pooled, argmax, ids, w3, w4,
