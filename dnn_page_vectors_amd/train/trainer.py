@@ -51,7 +51,8 @@ def _restore_det(prev) -> None:
 
 
 # 1: on one rank the query tower runs before the page tower (models/base.py
-# _forward_query_first).  Off: no measurable gain at the headline shape (alternated runs on one
+# _forward_query_first).  Off: no measurable gain at the headline shape (same process, interleaved:
+# 7.311 vs 7.304 ms, tools/step_flag_ab.py; alternated processes on one
 # box: 7.09 / 7.12 / 7.01 vs 6.79 / 7.14 / 7.04 ms, profiles/r4_prune/qfirst_ab.txt)
 QUERY_FIRST = os.environ.get("PAGEVEC_QUERY_FIRST", "0") != "0"
 

@@ -1,0 +1,63 @@
+"""Same-process A/B of a trainer-level module flag on the headline step (interleaved rounds,
+CUDA-event timed), e.g. the query-tower-first forward order:
+
+    python tools/step_flag_ab.py --module dnn_page_vectors_amd.train.trainer --flag QUERY_FIRST
+"""
+import argparse
+import importlib
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--module", default="dnn_page_vectors_amd.train.trainer")
+    ap.add_argument("--flag", default="QUERY_FIRST")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=15)
+    a = ap.parse_args()
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    info = pdist.init_distributed()
+    cfg = preset_config("cdssm_ngram_bf16")
+    V = cfg.vocab_hash_size
+    dev = info.device
+    tr = Trainer(cfg, build_model(cfg, V), dev, graph=False)
+    data = SyntheticPairs(spec_from_config(cfg, V, num_pages=65536), dev, seed=1337)
+    pool = [data.batch(cfg.batch_size) for _ in range(4)]
+    mod = importlib.import_module(a.module)
+    for i in range(5):
+        tr.train_step(*pool[i % 4])
+    res = {False: [], True: []}
+    k = 0
+    for r in range(a.rounds):
+        for val in ((False, True) if r % 2 == 0 else (True, False)):
+            setattr(mod, a.flag, val)
+            tr.train_step(*pool[k % 4])
+            k += 1
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.steps):
+                tr.train_step(*pool[k % 4])
+                k += 1
+            e1.record()
+            torch.cuda.synchronize()
+            res[val].append(e0.elapsed_time(e1) / a.steps)
+    print(json.dumps({"flag": a.flag, "off_ms": [round(x, 3) for x in res[False]],
+                      "on_ms": [round(x, 3) for x in res[True]],
+                      "off_median": round(statistics.median(res[False]), 3),
+                      "on_median": round(statistics.median(res[True]), 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
