@@ -71,8 +71,11 @@ def _k16(V: int) -> bool:
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
 # (both halves are gather/latency-bound and leave CU slots idle when run back to back)
 # (round 1: no gain, 9.30 vs 9.30 ms; with the round-2 backward, same box: 7.535 / 7.555 vs
-# 7.596 / 7.624 ms per headline step, so on by default for long sequences)
-DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "1") != "0"
+# 7.596 / 7.624 ms per headline step, so it was on).  Round 4, with the sort moved into the
+# forward and a side stream per tower, same-process interleaved A/B (tools/step_flag_ab.py,
+# profiles/r4_prune/flags_ab.txt): OFF is faster in 15 of 16 rounds on two boxes, 6.848 vs
+# 6.869 and 7.266 vs 7.292 ms medians — dW after the page tower's reduce on its own stream
+DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "0") != "0"
 # conv bias gradients written by the dW kernel straight into the bias parameters' flat-gradient
 # slices (0: a zeroed (2 * FW) buffer returned to autograd, AccumulateGrad adds; A/B switch)
 BIAS_SINK = os.environ.get("PAGEVEC_BIAS_SINK", "1") != "0"
