@@ -1815,3 +1815,25 @@ def test_fp8_bag_matches_reference():
     gw = float((Wd.grad.cpu() - W.grad).abs().max() / W.grad.abs().max())
     assert gw < 1e-2, gw  # bf16 dz on the GPU
     torch.testing.assert_close(bd.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("side", [False, True])
+def test_conv_pool_backward_dw_stream_placement(side, monkeypatch):
+    """dW on the calling stream (default) or on the side stream (PAGEVEC_DW_STREAM=1): the
+    same gradients (float-atomic sums: to rounding)."""
+    torch.manual_seed(11)
+    N, L, V, E, F = 64, 300, 500, 100, 150
+    ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
+    base = [bf(torch.randn(V, E, device=DEV) * 0.5), bf(torch.randn(F, 3, E, device=DEV) * 0.1),
+            bf(torch.randn(F, 4, E, device=DEV) * 0.1), torch.randn(F, device=DEV) * 0.1,
+            torch.randn(F, device=DEV) * 0.1]
+    grads = []
+    for s in (False, side):
+        monkeypatch.setattr(cops, "DW_SIDE_STREAM", s)
+        t, w3, w4, b3, b4 = [x.clone().requires_grad_(True) for x in base]
+        y, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], [b3, b4], 0.25, 3, True)
+        (y * torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)).sum().backward()
+        torch.cuda.synchronize()
+        grads.append([t.grad, w3.grad, w4.grad, b3.grad, b4.grad])
+    for u, v in zip(*grads):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5)
