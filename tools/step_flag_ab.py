@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--flag", default="QUERY_FIRST")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=15)
+    ap.add_argument("--vals", default="0,1", help="the two values A/B'd (Python literals); 0/1 -> False/True")
+    ap.add_argument("--setter", default="", help="a libpagevec_hip setter (e.g. pv_conv_r7_set_occ) instead of a flag")
     a = ap.parse_args()
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
@@ -34,14 +36,26 @@ def main():
     tr = Trainer(cfg, build_model(cfg, V), dev, graph=False)
     data = SyntheticPairs(spec_from_config(cfg, V, num_pages=65536), dev, seed=1337)
     pool = [data.batch(cfg.batch_size) for _ in range(4)]
+    import ast
+
     mod = importlib.import_module(a.module)
+    va, vb = (ast.literal_eval(v) for v in a.vals.split(","))
+    if a.vals == "0,1" and not a.setter:
+        va, vb = False, True
+    from dnn_page_vectors_amd.ops._common import lib
+
+    def setv(v):
+        if a.setter:
+            getattr(lib(), a.setter)(int(v))
+        else:
+            setattr(mod, a.flag, v)
     for i in range(5):
         tr.train_step(*pool[i % 4])
-    res = {False: [], True: []}
+    res = {va: [], vb: []}
     k = 0
     for r in range(a.rounds):
-        for val in ((False, True) if r % 2 == 0 else (True, False)):
-            setattr(mod, a.flag, val)
+        for val in ((va, vb) if r % 2 == 0 else (vb, va)):
+            setv(val)
             tr.train_step(*pool[k % 4])
             k += 1
             torch.cuda.synchronize()
@@ -53,10 +67,10 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[val].append(e0.elapsed_time(e1) / a.steps)
-    print(json.dumps({"flag": a.flag, "off_ms": [round(x, 3) for x in res[False]],
-                      "on_ms": [round(x, 3) for x in res[True]],
-                      "off_median": round(statistics.median(res[False]), 3),
-                      "on_median": round(statistics.median(res[True]), 3)}), flush=True)
+    print(json.dumps({"flag": a.setter or a.flag, "a": str(va), "b": str(vb),
+                      "a_ms": [round(x, 3) for x in res[va]], "b_ms": [round(x, 3) for x in res[vb]],
+                      "a_median": round(statistics.median(res[va]), 3),
+                      "b_median": round(statistics.median(res[vb]), 3)}), flush=True)
 
 
 if __name__ == "__main__":
