@@ -151,7 +151,8 @@ FWD_EMIT = os.environ.get("PAGEVEC_FWD_EMIT", "1") != "0"
 EARLY_SORT = os.environ.get("PAGEVEC_EARLY_SORT", "1") != "0"
 
 
-V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5)  # pv_conv_set_dbg variants with the loader key emit
+V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5, 16384 + 128 + 5 + 1024,
+          16384 + 192 + 5 + 1024)  # pv_conv_set_dbg variants with the loader key emit (every v7 arm)
 
 
 def _conv_dbg() -> int:
