@@ -870,13 +870,31 @@ __global__ __launch_bounds__(512, 1) void conv_f32_dx_wave_kernel(const float* _
   for (int x = threadIdx.x; x < VE; x += 512) out[x] = ((tabs[x] + tabs[VE + x]) + tabs[2 * VE + x]) + tabs[3 * VE + x];
 }
 
-__global__ __launch_bounds__(256) void conv_f32_dx_sum_kernel(const float* __restrict__ partial, float* dtable,
-                                                              int VE, int nparts) {
+// partial tables -> dtable in a fixed order, in two levels (one thread per element walking all
+// 256 partials was latency-bound at 40-60 us): level 1, thread (x, gy) sums its group's
+// partials into the group's first partial row; level 2 adds the DXS_G group sums in order
+constexpr int DXS_G = 16;
+__global__ __launch_bounds__(256) void conv_f32_dx_sum1_kernel(float* __restrict__ partial, int VE, int nparts) {
+  const int x = blockIdx.x * 256 + threadIdx.x, gy = blockIdx.y;
+  const int chunk = (nparts + DXS_G - 1) / DXS_G, b0 = gy * chunk, b1 = min(nparts, b0 + chunk);
+  if (x >= VE || b0 >= b1) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = b0;
+  for (; b + 4 <= b1; b += 4)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] += partial[(size_t)(b + k) * VE + x];
+  for (; b < b1; ++b) s[0] += partial[(size_t)b * VE + x];
+  partial[(size_t)b0 * VE + x] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+__global__ __launch_bounds__(256) void conv_f32_dx_sum2_kernel(const float* __restrict__ partial, float* dtable,
+                                                               int VE, int nparts) {
   const int x = blockIdx.x * 256 + threadIdx.x;
   if (x >= VE) return;
-  float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += partial[(size_t)b * VE + x];
-  dtable[x] += s;
+  const int chunk = (nparts + DXS_G - 1) / DXS_G;
+  float t = 0.f;
+  for (int gy = 0; gy * chunk < nparts; ++gy) t += partial[(size_t)gy * chunk * VE + x];
+  dtable[x] += t;
 }
 
 PV_DEBUG_EXPORT(convf32)
@@ -970,7 +988,10 @@ PV_API int pv_conv_f32_bwd_dx_lds(const float* gpool, const float* pooled, const
     hipLaunchKernelGGL(conv_f32_dx_lds_kernel, dim3(nparts), dim3(DXP_NTH), 0, st, gpool, pooled, argmax, ids, w3, w4,
                      partial, N, L, E, V, seed, seed_ptr, row_offset, thr, token_mode, scale, mask, wpr);
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(conv_f32_dx_sum_kernel, dim3((V * E + 255) / 256), dim3(256), 0, st, (const float*)partial,
+  hipLaunchKernelGGL(conv_f32_dx_sum1_kernel, dim3((V * E + 255) / 256, DXS_G), dim3(256), 0, st, partial, V * E,
+                     nparts);
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(conv_f32_dx_sum2_kernel, dim3((V * E + 255) / 256), dim3(256), 0, st, (const float*)partial,
                      dtable, V * E, nparts);
   PV_LAUNCH_CHECK();
   return 0;
