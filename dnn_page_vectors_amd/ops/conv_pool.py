@@ -74,7 +74,8 @@ def _k16(V: int) -> bool:
 # 7.596 / 7.624 ms per headline step, so it was on).  Round 4, with the sort moved into the
 # forward and a side stream per tower, same-process interleaved A/B (tools/step_flag_ab.py,
 # profiles/r4_prune/flags_ab.txt): OFF is faster in 15 of 16 rounds on two boxes, 6.848 vs
-# 6.869 and 7.266 vs 7.292 ms medians — dW after the page tower's reduce on its own stream
+# 6.869 and 7.266 vs 7.292 ms medians; chunked CDSSM 1.331 vs 1.384 ms; char level (B 1024)
+# neutral, 3.587 vs 3.571 — dW after the page tower's reduce on its own stream
 DW_SIDE_STREAM = os.environ.get("PAGEVEC_DW_STREAM", "0") != "0"
 # conv bias gradients written by the dW kernel straight into the bias parameters' flat-gradient
 # slices (0: a zeroed (2 * FW) buffer returned to autograd, AccumulateGrad adds; A/B switch)

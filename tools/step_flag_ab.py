@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=15)
     ap.add_argument("--vals", default="0,1", help="the two values A/B'd (Python literals); 0/1 -> False/True")
+    ap.add_argument("--preset", default="cdssm_ngram_bf16")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--setter", default="", help="a libpagevec_hip setter (e.g. pv_conv_r7_set_occ) instead of a flag")
     a = ap.parse_args()
     from dnn_page_vectors_amd.config import preset_config
@@ -30,7 +32,9 @@ def main():
     from dnn_page_vectors_amd.train.trainer import Trainer
 
     info = pdist.init_distributed()
-    cfg = preset_config("cdssm_ngram_bf16")
+    cfg = preset_config(a.preset)
+    if a.set:
+        cfg = cfg.override(a.set)
     V = cfg.vocab_hash_size
     dev = info.device
     tr = Trainer(cfg, build_model(cfg, V), dev, graph=False)
@@ -67,7 +71,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[val].append(e0.elapsed_time(e1) / a.steps)
-    print(json.dumps({"flag": a.setter or a.flag, "a": str(va), "b": str(vb),
+    print(json.dumps({"preset": a.preset, "flag": a.setter or a.flag, "a": str(va), "b": str(vb),
                       "a_ms": [round(x, 3) for x in res[va]], "b_ms": [round(x, 3) for x in res[vb]],
                       "a_median": round(statistics.median(res[va]), 3),
                       "b_median": round(statistics.median(res[vb]), 3)}), flush=True)
