@@ -150,6 +150,19 @@ FWD_EMIT = os.environ.get("PAGEVEC_FWD_EMIT", "1") != "0"
 # ... and sorted right after the forward, on the side stream (PAGEVEC_EARLY_SORT=0: in the
 # backward, on its critical path)
 EARLY_SORT = os.environ.get("PAGEVEC_EARLY_SORT", "1") != "0"
+# ... except for mid-length sequences (EARLY_SORT_SKIP_L[0] < L < EARLY_SORT_SKIP_L[1], the
+# chunk encoders' 512-token chunks): there the early sort competes with a short forward and the
+# loss instead of hiding behind a long page conv.  Same-process A/B (tools/step_flag_ab.py,
+# profiles/r4_prune/flags_ab.txt): early sort always on vs only for L >= 1024 — chunked CDSSM
+# 1.247 vs 1.148 ms, but the headline 6.764 vs 6.886 (its 45-token query tower gains from it)
+# and char level neutral; hence the skip window instead of a threshold.
+EARLY_SORT_SKIP = os.environ.get("PAGEVEC_EARLY_SORT_SKIP", "1") != "0"
+EARLY_SORT_SKIP_L = (128, 1024)
+
+
+def _early_sort(L: int) -> bool:
+    lo, hi = EARLY_SORT_SKIP_L
+    return EARLY_SORT and not (EARLY_SORT_SKIP and lo < L < hi)
 
 
 V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5, 16384 + 128 + 5 + 1024,
@@ -203,7 +216,7 @@ class _ConvPoolFn(torch.autograd.Function):
               "pv_conv_pool_fwd2")
         ctx.keys = keys
         ctx.sorted = None
-        if keys is not None and EARLY_SORT and not torch.cuda.is_current_stream_capturing() \
+        if keys is not None and _early_sort(L) and not torch.cuda.is_current_stream_capturing() \
                 and not determinism.enabled():
             # the sort of the table-gradient keys depends on the forward alone: run it now on
             # the side stream, beside the rest of the forward and the loss, instead of on the
