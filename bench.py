@@ -44,8 +44,10 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # RCCL adds its own; with HIP's default 4 hardware queues two of them would share a queue, and
 # a side-stream kernel queued behind a collective waits for the other ranks.  8 queues keep
 # them apart (neutral at one rank: 6.94-6.96 vs 6.93-6.94 ms, profiles/r4_prune/hwq_ab.txt).
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# A node that exports the default 4 explicitly gets 8 as well; the value in effect is recorded
+# in the JSON (runtime_knobs).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import torch  # noqa: E402
 
@@ -167,6 +169,7 @@ def main():
     from dnn_page_vectors_amd.ops._common import set_backend
     from dnn_page_vectors_amd.parallel import dist as pdist
     from dnn_page_vectors_amd.train.trainer import Trainer
+    from dnn_page_vectors_amd.utils import knobs
 
     from dnn_page_vectors_amd.parallel import topology
 
@@ -286,9 +289,22 @@ def main():
         per_pair = (cfg.query_length * bert_flops_per_token(cfg, cfg.query_length) +
                     (1 + cfg.J) * cfg.document_length * bert_flops_per_token(cfg, cfg.document_length))
         train_mult = 3.0  # dense backward: 2 x forward
-    else:
-        per_pair = 0.0
+    else:  # mlp (config 3) / chunked with the MLP chunk encoder (config 5): towers of bag + dense
+        from dnn_page_vectors_amd.models.mlp_dssm import mlp_bag_gemm_flops, mlp_tower_flops
+
+        dims = cfg.mlp_dims
+        if a.model == "chunked":
+            C = -(-cfg.document_length // cfg.chunk_len)
+            page = C * mlp_tower_flops(cfg.chunk_len, dims)
+            long_bags = C  # chunk bags through the counts GEMM
+        else:
+            page = mlp_tower_flops(cfg.document_length, dims)
+            long_bags = 1
+        per_pair = mlp_tower_flops(cfg.query_length, dims) + (1 + cfg.J) * page
         train_mult = None
+        # what the MFMAs execute for the long bags (dense counts row x table, fwd + the C^T G
+        # weight gradient), to put the step against the bf16 / fp8 MFMA roofline
+        exec_pair = (1 + cfg.J) * long_bags * 2 * mlp_bag_gemm_flops(V, dims[0])
     flops = per_pair * a.batch * W * a.steps / dt
     if info.is_main:
         out = {
@@ -331,7 +347,10 @@ def main():
             "train_model_tflops": round(flops * train_mult / 1e12, 1) if train_mult else None,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else None,
             "hip_graph": graph_used,
+            "runtime_knobs": knobs.in_effect(),
         }
+        if a.model in ("mlp", "chunked"):
+            out["bag_gemm_executed_tflops"] = round(exec_pair * a.batch * W * a.steps / dt / 1e12, 1)
         if a.dry_run:
             out["dry_run"] = True
             out["data"] = "synthetic (CPU dry run: gloo, eager PyTorch ops, tiny model; not a measurement)"

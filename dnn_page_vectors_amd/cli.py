@@ -81,8 +81,15 @@ def cmd_train(a) -> int:
     cfg = _config(a)
     from .parallel import topology  # RCCL defaults for the job's message class, before the communicator exists
 
-    topology.apply_env(topology.grad_mb(build_model(cfg, cfg.vocab_hash_size)) if int(os.environ.get("WORLD_SIZE", "1")) > 1
-                       else 0.0, int(os.environ.get("WORLD_SIZE", "1")))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    gmb = 0.0
+    if world > 1:
+        # the gradient size of the model this job will train: the real vocabulary (a word-level
+        # config's vocab_hash_size is <= 1), parameters on the meta device (no allocation)
+        V0 = (cfg.vocab_hash_size if cfg.vocab_hash_size > 1 else 1000) if a.synthetic else _featurizer(cfg).num_ids
+        with torch.device("meta"):
+            gmb = topology.grad_mb(build_model(cfg, V0))
+    topology.apply_env(gmb, world)
     info = pdist.init_distributed()
     if cfg.backend != "auto":
         set_backend(cfg.backend)

@@ -303,13 +303,14 @@ class Configuration:
     def load_json(cls, path: str) -> "Configuration":
         with open(path) as f:
             d = json.load(f)
-        if "config_version" not in d:  # version 1 (pre round 3): migrate the old no-op dtype default
+        if "config_version" not in d:  # version 1: saved before the version field existed
             if d.get("dtype") == "fp32":
+                # a version-1 file cannot tell the old no-op fp32 default (before 066a651) from an
+                # explicit choice of reference precision made later: keep what the file says
                 logging.getLogger(__name__).warning(
-                    "%s: version-1 config with dtype='fp32' (the old default, which selected the HIP "
-                    "kernels) loaded as dtype='bf16'; set dtype='fp32' explicitly for the "
-                    "reference-precision PyTorch path", path)
-                d["dtype"] = "bf16"
+                    "%s: version-1 config with dtype='fp32' loads as reference precision (fp32 "
+                    "kernels); configs saved before 066a651 meant the bf16 HIP path by it — set "
+                    "dtype='bf16' for that", path)
             d["config_version"] = 2
         return cls.from_dict(d)
 

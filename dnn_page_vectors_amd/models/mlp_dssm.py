@@ -89,6 +89,18 @@ class MLPTower(nn.Module):
         return h
 
 
+def mlp_tower_flops(L: int, dims) -> float:
+    """Forward model FLOPs of one MLP tower over an L-token bag: the bag mean (L x d1 adds) +
+    2 x MAC of the dense stack (bias / activation not counted, as for the CDSSM count)."""
+    return float(L * dims[0] + sum(2 * a * b for a, b in zip(dims[:-1], dims[1:])))
+
+
+def mlp_bag_gemm_flops(V: int, d1: int) -> float:
+    """MFMA FLOPs the counts-matrix bag plan EXECUTES per long bag (2 x V x d1: the dense
+    counts row times the table), for hardware-utilisation figures; most of it multiplies zeros."""
+    return 2.0 * V * d1
+
+
 def _bias_act(h: torch.Tensor, b: torch.Tensor, act: str) -> torch.Tensor:
     h = h + b
     if act == "tanh":

@@ -12,6 +12,7 @@ MaxPooling1D(L-k+1) -> Flatten} x k in (3,4) -> concat (dssm_cnn_v2/cnn_dssm_th.
 from __future__ import annotations
 
 import os
+import threading
 
 from typing import Optional, Tuple
 
@@ -191,6 +192,10 @@ def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
     return wrow
 
 
+_CALLER_GRAD = threading.local()  # grad mode at the _ConvPoolFn.apply call site
+_CALLER_GRAD.on = True
+
+
 class _ConvPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, table, w3, w4, b3, b4, tbl16, wpack, p, seed, row_offset, training, mode):
@@ -207,7 +212,11 @@ class _ConvPoolFn(torch.autograd.Function):
         sp = _SEED_DEV
         b3c, b4c = b3.detach().contiguous(), b4.detach().contiguous()  # the parameters themselves: no cat
         keys = None
-        if ctx.needs_input_grad[1] and FWD_EMIT and not _dense_dx(L) and _conv_dbg() in (0,) + V7_DBG:
+        # needs_input_grad reflects requires_grad, not grad mode, and forward() itself runs with
+        # grad disabled: the caller's grad mode (_CALLER_GRAD) says whether a backward can
+        # follow.  Under no_grad (eval, Recall / encode batches) no keys are emitted or sorted.
+        if _CALLER_GRAD.on and ctx.needs_input_grad[1] and FWD_EMIT and not _dense_dx(L) \
+                and _conv_dbg() in (0,) + V7_DBG:
             k16 = _k16(V)
             keys = torch.empty(N * SLOTS_PER_SAMPLE, dtype=torch.int16 if k16 else torch.int32, device=ids.device)
         check(lib().pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(b3c), P(b4c), P(pooled), P(argmax), N, L, V,
@@ -518,6 +527,7 @@ def conv_relu_maxpool_fused(ids: torch.Tensor, table: torch.Tensor, weights, bia
             tbl16, wpack = table_bf16(table.detach()), pack_weights(w3.detach(), w4.detach())
         else:
             tbl16, wpack = compute_cache
+        _CALLER_GRAD.on = torch.is_grad_enabled()
         return _ConvPoolFn.apply(ids, table, w3, w4, b3, b4, tbl16, wpack, float(p), int(seed), int(row_offset),
                                  bool(training), mode)
     if ids.is_cuda and use_hip(ids, table):

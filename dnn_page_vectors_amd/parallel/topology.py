@@ -35,6 +35,10 @@ LATENCY_GRAD_MB = 32.0
 BANDWIDTH_BUCKET_MB = 64.0
 BANDWIDTH_MIN_CHANNELS = 16
 XGMI_LINKS_PER_GPU = 7
+# provenance of the three policy constants above: derived from the link arithmetic in the
+# module docstring, NOT yet tuned on an 8-GPU node (no node was available to this build; the
+# sweep is tools/comm_micro.py --sweep-channels).  Reported with every bench record.
+CONSTANTS_STATUS = "unmeasured (derived from xGMI link arithmetic; no 8-GPU sweep yet)"
 
 _APPLIED: Dict[str, str] = {}
 
@@ -70,4 +74,6 @@ def apply_env(total_grad_mb: float, world: int) -> Dict[str, str]:
 
 def report(total_grad_mb: float, bucket: float) -> Dict[str, object]:
     return {"class": message_class(total_grad_mb), "grad_mb": round(total_grad_mb, 1), "bucket_mb": round(bucket, 1),
-            "policy_env": dict(_APPLIED), "xgmi_links_per_gpu": XGMI_LINKS_PER_GPU}
+            "policy_env": dict(_APPLIED), "xgmi_links_per_gpu": XGMI_LINKS_PER_GPU,
+            "policy_constants": {"latency_grad_mb": LATENCY_GRAD_MB, "bandwidth_bucket_mb": BANDWIDTH_BUCKET_MB,
+                                 "bandwidth_min_channels": BANDWIDTH_MIN_CHANNELS, "status": CONSTANTS_STATUS}}

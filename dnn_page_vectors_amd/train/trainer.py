@@ -146,9 +146,10 @@ class Trainer:
         # cannot leak its mode (or its one-stream, no-graph rule) into this one; close() or a
         # finalizer gives the mode back as it was before a deterministic trainer switched it on
         self._det_prev = None
+        self._det_fin = None
         if self.deterministic:
             self._det_prev = determinism.set_deterministic(True)
-            weakref.finalize(self, _restore_det, self._det_prev)
+            self._det_fin = weakref.finalize(self, _restore_det, self._det_prev)
         else:
             determinism.ensure(False)
         self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
@@ -168,6 +169,9 @@ class Trainer:
 
     def close(self) -> None:
         """Restore the process-wide deterministic mode this trainer switched on (if any)."""
+        if self._det_fin is not None:  # a later GC must not restore a stale snapshot
+            self._det_fin.detach()
+            self._det_fin = None
         if self._det_prev is not None:
             _restore_det(self._det_prev)
             self._det_prev = None
@@ -370,6 +374,7 @@ class Trainer:
 
     @torch.no_grad()
     def eval_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        determinism.ensure(self.deterministic)
         self.model.eval()
         loss, P = self.compute_loss(q_ids, d_ids, 0)
         self.model.train()

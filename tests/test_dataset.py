@@ -119,8 +119,9 @@ def test_in_memory_split_and_partial_batch_follow_keras(tmp_path):
 
 
 def test_legacy_config_json_migrates_fp32_default(tmp_path, caplog):
-    """a config saved before config_version existed carries dtype='fp32' (the old
-    no-op default); loading it keeps the HIP path (bf16) and warns, a current file keeps fp32."""
+    """A config saved before config_version existed with dtype='fp32' is ambiguous (the old
+    no-op default before 066a651, or reference precision chosen on purpose after it; no field
+    tells them apart): it keeps fp32 and warns, a current file keeps fp32 silently."""
     import json
 
     from dnn_page_vectors_amd.config import Configuration
@@ -131,7 +132,7 @@ def test_legacy_config_json_migrates_fp32_default(tmp_path, caplog):
     old = tmp_path / "old.json"
     old.write_text(json.dumps(d))
     c = Configuration.load_json(str(old))
-    assert c.dtype == "bf16" and c.config_version == 2
+    assert c.dtype == "fp32" and c.config_version == 2
     assert any("version-1" in r.message for r in caplog.records)
     new = tmp_path / "new.json"
     Configuration(dtype="fp32").save_json(str(new))

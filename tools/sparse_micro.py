@@ -67,7 +67,10 @@ def run(sparse: bool, V: int, E: int, touched: float, steps: int, dev):
         step(i)
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / steps, flat.data[o:o + k].view(V, E)[:4].clone()
+    touched = torch.unique(torch.cat(batches).long())
+    # the WHOLE table after the run (the rows no step touched must be unchanged as well) and the
+    # list of rows some step touched
+    return s.elapsed_time(e) / steps, flat.data[o:o + k].view(V, E).clone(), touched
 
 
 def main():
@@ -78,15 +81,24 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    res = {}
+    res, tables = {}, {}
     for sparse in (False, True):
-        ms, head = run(sparse, a.V, a.E, a.touched, a.steps, dev)
+        ms, tab, touched = run(sparse, a.V, a.E, a.touched, a.steps, dev)
         res["sparse" if sparse else "dense_lazy"] = round(ms, 3)
-        res["head_" + ("sparse" if sparse else "dense")] = head
+        tables[sparse] = tab
         torch.cuda.empty_cache()
-    same = torch.equal(res.pop("head_sparse"), res.pop("head_dense"))
+    d, s_ = tables[False], tables[True]
+    torch.manual_seed(0)  # run()'s initial table
+    init = _M(a.V, a.E).embedding.detach().to(dev) if a.V * a.E <= 2_000_000_000 else None
     print(json.dumps({"V": a.V, "E": a.E, "touched_frac": a.touched, "ms_per_step": res,
-                      "speedup": round(res["dense_lazy"] / res["sparse"], 2), "rows_equal": same}))
+                      "speedup": round(res["dense_lazy"] / res["sparse"], 2),
+                      # every row of the table, and the touched rows on their own
+                      "table_equal": bool(torch.equal(d, s_)),
+                      "touched_rows": int(touched.numel()),
+                      "touched_rows_equal": bool(torch.equal(d[touched], s_[touched])),
+                      "touched_rows_changed": None if init is None else
+                      bool((s_[touched] != init[touched]).any(dim=1).all()),
+                      "max_abs_diff": float((d - s_).abs().max())}))
 
 
 if __name__ == "__main__":
