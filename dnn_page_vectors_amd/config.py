@@ -130,6 +130,9 @@ class Configuration:
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
     grad_bucket_mb: float = 32.0
+    # graph mode on a data-parallel run captures the whole step INCLUDING its RCCL collectives
+    # (page / query gathers, bucketed gradient all-reduces) in the hipGraph; False = eager there
+    graph_distributed: bool = True
     query_stream: bool = True             # query tower (fwd, hence bwd) on a side HIP stream
     deterministic: bool = False           # order-free (fixed-point) GPU reductions, one stream (ops/determinism.py)
     placement: str = "dp"                # dp (data parallel) | tower (slots over ranks, cnn_dssm_tf.py:139-158)

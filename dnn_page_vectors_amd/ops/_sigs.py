@@ -115,13 +115,18 @@ SIGS = {
     "pv_cast_pad_bf16": "pp" "lii" "p",
     "pv_sumsq": "p" "l" "p" "p",
     "pv_scale": "p" "lf" "p",
-    # gemm.hip
-    "pv_gemm_bf16": "p" "l" "i" "p" "l" "i" "p" "l" "iii" "i" "l" "p" "f" "iii" "p",
-    "pv_gemm_set_group": "i",
+    # gemm_mx8.hip
     "pv_mx_probe": "ppppp" "p",
     "pv_gemm_mx8": "p" "l" "p" "l" "p" "l" "iii" "i" "l" "p" "f" "p" "ii" "p",
     "pv_amax_quant_fp8_t": "p" "ii" "ppp" "i" "p",
     "pv_bag_counts8": "p" "p" "i" "p" "i" "p" "iiii" "p",
+    # bag_gemm.hip (long-bag products with on-the-fly counts)
+    "pv_bag_segments": "i",
+    "pv_bag_set_dbg": "i",
+    "pv_bag_groups": "i",
+    "pv_bag_rle": "pppppppp" "iiii" "p",
+    "pv_bag_mm_fwd": "pppp" "iii" "i" "p",
+    "pv_bag_mm_wgrad": "pppp" "ii" "iii" "p",
 }
 
 _RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,

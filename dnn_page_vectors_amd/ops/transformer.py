@@ -15,7 +15,6 @@ import torch
 import torch.nn.functional as F
 
 from . import dense as dops
-from . import gemm as gops
 from . import grad_sink
 from . import reference as ref
 from ._common import P, check, lib, stream, use_hip
@@ -384,9 +383,7 @@ class _Linear16Fn(torch.autograd.Function):
     def forward(ctx, x, w, b, w16, res=None):
         x = x.to(torch.bfloat16)
         x2 = x.reshape(-1, x.shape[-1])
-        if gops.use("fwd", x2, w16):  # gemm.hip: bias in the epilogue, bf16 out
-            y = gops.gemm(x2, w16, bias=b, out_dtype=torch.bfloat16)
-        elif b is not None:
+        if b is not None:
             y = torch.addmm(b.to(torch.bfloat16), x2, w16.t())
         else:
             y = x2 @ w16.t()
@@ -404,30 +401,20 @@ class _Linear16Fn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             rg = ctx.res.grad if ctx.res is not None else None
-            eng = gops.use("dgrad", dy2, w16, b_col=True)
             if rg is not None:  # + the residual branch's gradient of the same x (ResidualLink)
                 ctx.res.grad = None
-                if eng and rg.dtype == dy2.dtype and rg.is_contiguous():
-                    # gemm.hip: C += dY W in the epilogue (bf16 read-add-write)
-                    dx = gops.gemm(dy2, w16, b_col=True, out=rg.view(-1, rg.shape[-1]), accumulate=True)
-                    dx = dx.view(ctx.shape)
-                elif rg.dtype == dy2.dtype and rg.is_contiguous():
+                if rg.dtype == dy2.dtype and rg.is_contiguous():
                     # in place: C += dY W in the GEMM epilogue (out-of-place addmm copies C first)
                     dx = rg.view(-1, rg.shape[-1]).addmm_(dy2, w16).view(ctx.shape)
                 else:
                     dx = torch.addmm(rg.reshape(-1, rg.shape[-1]).to(dy2.dtype), dy2, w16).view(ctx.shape)
-            elif eng:
-                dx = gops.gemm(dy2, w16, b_col=True, out_dtype=torch.bfloat16).view(ctx.shape)
             else:
                 dx = (dy2 @ w16).view(ctx.shape)
         pw, pb = ctx.params
         dw = db = None
         if ctx.needs_input_grad[1]:
             tw = grad_sink.write_target(pw)
-            if gops.use("wgrad", dy2, x2, a_col=True, b_col=True):  # dW = dY^T X, split-K fp32
-                dw = gops.gemm(dy2, x2, a_col=True, b_col=True, out=tw)
-            else:
-                dw = wgrad_f32(dy2, x2, out=tw)
+            dw = wgrad_f32(dy2, x2, out=tw)
             if tw is not None:
                 grad_sink.done(pw)
                 dw = None

@@ -152,7 +152,13 @@ class Trainer:
             self._det_fin = weakref.finalize(self, _restore_det, self._det_prev)
         else:
             determinism.ensure(False)
-        self.graph_mode = (bool(graph) and self.device.type == "cuda" and not self.info.enabled
+        # data parallel: the collectives are captured with the step (RCCL supports stream
+        # capture; the bucket hooks, the page gather and the loss gathers all enqueue on
+        # streams that fork from and join back into the capture stream); not with the sparse
+        # tables (their exchange sizes itself with a host sync) or tower placement
+        self.graph_mode = (bool(graph) and self.device.type == "cuda"
+                           and (not self.info.enabled or (bool(getattr(cfg, "graph_distributed", True))
+                                                          and self.placement == "dp"))
                            and not self.deterministic and self.sparse is None)
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
         # Round 1 needed it: replays interleaved with eager allocating work faulted after ~97

@@ -40,7 +40,7 @@ KNOBS: Dict[str, tuple] = {
     # bags, dense, loss, optimizer
     "PAGEVEC_BAG_SPARSE_BWD": ("ab", "1", "short-bag backward by sorted token runs"),
     "PAGEVEC_BAG_COUNTS16": ("ab", "1", "16-bit packed LDS counts histogram"),
-    "PAGEVEC_BAG_GEMM": ("ab", "auto", "long-bag GEMMs: in-tree on-the-fly-counts kernels or hipBLASLt"),
+    "PAGEVEC_BAG_GEMM": ("ab", "lib", "long-bag GEMMs: hipBLASLt on the count matrix (lib) or bag_gemm.hip (hip)"),
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),

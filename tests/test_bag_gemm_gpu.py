@@ -1,0 +1,142 @@
+"""bag_gemm.hip (K1 long bags: segment lists + on-the-fly-count MFMA products) against plain
+PyTorch fp32 / fp64 references of the same op (C = per-bag token counts):
+
+    forward  C @ W        (split-K partial slabs, summed here as the colsum kernel would)
+    backward C^T @ Gs     (dW rows stored or accumulated into a strided target)
+"""
+import pytest
+import torch
+
+from dnn_page_vectors_amd.ops import embedding as eops
+from dnn_page_vectors_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ids(N, L, V, seed, zipf=True):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    if zipf:  # Zipf over a permuted vocabulary: hot ids repeat inside a page
+        r = torch.arange(1, V, dtype=torch.float64)
+        p = r.pow(-1.05)
+        ids = torch.multinomial(p / p.sum(), N * L, replacement=True, generator=g) + 1
+        ids = torch.randperm(V, generator=g)[ids.clamp(max=V - 1)]
+    else:
+        ids = torch.randint(0, V, (N * L,), generator=g)
+    ids = ids.view(N, L).to(torch.int32)
+    ids[:, L - L // 5:] = 0  # padding tail (pad = 0 is not counted)
+    ids[0, :] = 5            # a page of ONE token: count L - L // 5 (> 256 when L is long)
+    if N > 1 and V > 200:    # a page whose first segment holds 64 distinct ids (> the 4 in registers)
+        ids[1, :64] = torch.arange(64, dtype=torch.int32) + 64
+    return ids.to(DEV)
+
+
+def _dense_counts(ids, V, pad=0):
+    N, L = ids.shape
+    C = torch.zeros(N, V, dtype=torch.float64, device=ids.device)
+    ok = ids != pad
+    C.scatter_add_(1, torch.where(ok, ids, torch.zeros_like(ids)).long(), ok.double())
+    return C
+
+
+@pytest.mark.parametrize("N,L,V,E", [(4096, 2000, 30000, 512), (300, 130, 1000, 72), (37, 512, 65000, 128),
+                                     (513, 300, 30000, 256)])
+def test_bag_rle_and_products_match_fp64(N, L, V, E):
+    """The in-tree arm (PAGEVEC_BAG_GEMM=hip) directly: atom lists, forward partials, dW."""
+    torch.manual_seed(0)
+    ids = _ids(N, L, V, seed=N + V)
+    rle = eops._Rle(ids, V, 0)
+    C = _dense_counts(ids, V)
+    # the atom lists decode to the exact counts (bf16 of the count: exact below 257)
+    S, Q = (V + 63) // 64, (N + 63) // 64
+    ao = rle.ao.to(torch.int64)
+    assert int(ao[-1]) == int((C != 0).sum())
+    torch.testing.assert_close(rle.lens, C.sum(1).float(), rtol=0, atol=0)
+    ent = rle.ent[:int(ao[-1])].to(torch.int64) & 0xFFFFFFFF
+    atom = torch.searchsorted(ao[:S * Q + 1].contiguous(), torch.arange(ent.numel(), device=DEV), right=True) - 1
+    seg, grp = atom // Q, atom % Q
+    page = grp * 64 + ((ent >> 6) & 63)
+    idv = seg * 64 + (ent & 63)
+    cnt = ((ent >> 16).to(torch.int32) << 16).view(torch.float32).double()
+    dec = torch.zeros_like(C)
+    dec[page, idv] = cnt
+    torch.testing.assert_close(dec, C.float().bfloat16().double(), rtol=0, atol=0)
+    Cb = C.float().bfloat16().double()  # the operand the kernel multiplies
+
+    def close(got, want):  # fp32 accumulation of long sums: error relative to the largest value
+        err = float((got.double() - want).abs().max())
+        assert err <= 2e-6 * float(want.abs().max()) + 1e-5, (err, float(want.abs().max()))
+
+    W = torch.randn(V, E, device=DEV).bfloat16()
+    part = rle.forward_partials(W)
+    ref_fwd = Cb @ W.double()
+    close(part.double().sum(0), ref_fwd)
+    gs = torch.randn(N, E, device=DEV).bfloat16()
+    ref_dw = Cb.t() @ gs.double()
+    out = torch.full((V, E + 8), 7.0, device=DEV)[:, :E]  # strided target, padding untouched
+    rle.weight_grad(gs, out, accumulate=False)
+    close(out, ref_dw)
+    base = torch.randn(V, E, device=DEV)
+    acc = base.clone()
+    rle.weight_grad(gs, acc, accumulate=True)
+    close(acc, base.double() + ref_dw)
+
+
+def test_bag_hip_matches_library_plan_end_to_end(monkeypatch):
+    """The MLP page bag (mean, bias, tanh) with its W / bias gradients: in-tree kernels vs the
+    hipBLASLt counts plan vs fp32 torch."""
+    V, N, L, E = 30000, 512, 2000, 512
+    ids = _ids(N, L, V, seed=9)
+    W0 = torch.randn(V, E, device=DEV).bfloat16().float()
+    b0 = torch.randn(E, device=DEV) * 0.3
+    gy = torch.randn(N, E, device=DEV)
+    res = {}
+    for arm in ("hip", "lib"):
+        monkeypatch.setattr(eops, "BAG_GEMM", arm)
+        W = W0.clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        y = eops.embedding_bag(ids, W, pad=0, mean=True, plan="counts", bias=b, act="tanh")
+        (y * gy).sum().backward()
+        res[arm] = (y.detach(), W.grad, b.grad)
+    Wr = W0.clone().requires_grad_(True)
+    br = b0.clone().requires_grad_(True)
+    cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
+    yr = torch.tanh(ref.embedding_bag_sum(ids, Wr, 0) / cnt + br)
+    (yr * gy).sum().backward()
+    for arm in ("hip", "lib"):
+        y, gW, gb = res[arm]
+        torch.testing.assert_close(y, yr, rtol=2e-2, atol=2e-2)
+        for got, want in ((gW, Wr.grad), (gb, br.grad)):
+            err = float((got - want).abs().max() / want.abs().max())
+            assert err < 2e-2, (arm, err)
+    # the two device arms agree far tighter than either does with fp32 (same bf16 operands)
+    torch.testing.assert_close(res["hip"][0], res["lib"][0], rtol=1e-4, atol=1e-4)
+
+
+def test_chunked_fp8_bag_backward_uses_segment_lists(monkeypatch):
+    """Config 5's fp8 bag keeps the MX fp8 forward; its weight gradient now comes from the
+    segment lists (no bf16 count matrix): equal to the library arm's exact C^T G."""
+    V, N, L, E = 30000, 256, 512, 512
+    ids = _ids(N, L, V, seed=4)
+    W0 = torch.randn(V, E, device=DEV).bfloat16().float() * 0.1
+    gy = torch.randn(N, E, device=DEV)
+    grads = {}
+    for arm in ("hip", "lib"):
+        monkeypatch.setattr(eops, "BAG_GEMM", arm)
+        W = W0.clone().requires_grad_(True)
+        y = eops.embedding_bag(ids, W, pad=0, mean=True, plan="counts", act="tanh", fp8=True)
+        (y * gy).sum().backward()
+        grads[arm] = W.grad
+    # the exact weight gradient: C^T (dz / len) with dz from the (fp8) forward's activation
+    C = _dense_counts(ids, V)
+    lens = C.sum(1, keepdim=True).clamp(min=1)
+    monkeypatch.setattr(eops, "BAG_GEMM", "hip")
+    W = W0.clone().requires_grad_(True)
+    y = eops.embedding_bag(ids, W, pad=0, mean=True, plan="counts", act="tanh", fp8=True).detach()
+    gs = ((gy * (1 - y * y)).double() / lens).float().bfloat16().double()
+    want = C.float().bfloat16().double().t() @ gs
+    scale = float(want.abs().max())
+    err_hip = float((grads["hip"].double() - want).abs().max()) / scale
+    err_lib = float((grads["lib"].double() - want).abs().max()) / scale
+    # fp32 output here; the library arm of this path returns the bf16 GEMM result (2^-8)
+    assert err_hip < 1e-5 and err_lib < 8e-3, (err_hip, err_lib)

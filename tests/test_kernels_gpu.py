@@ -1610,62 +1610,6 @@ def test_new_config_training_curve_hip_matches_torch(preset, overrides, steps, l
     assert abs(rh - rt) < 0.08, (rh, rt)
 
 
-@pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 136, 128), (1000, 520, 768), (64, 1032, 2048),
-                                   (8, 256, 4096)])
-def test_gemm_engine_layouts(a_col, b_col, M, N, K):
-    """gemm.hip: C = A . B^T for every operand storage (row = K contiguous, col = M / N
-    contiguous), edge tiles, and split-K, against fp32 torch on the same bf16 operands."""
-    from dnn_page_vectors_amd.ops import gemm as gops
-
-    g = torch.Generator().manual_seed(M * 7 + N + K)
-    A = torch.randn(M, K, generator=g).bfloat16()
-    B = torch.randn(N, K, generator=g).bfloat16()
-    ref_c = A.float() @ B.float().t()
-    a = (A.t().contiguous() if a_col else A).to(DEV)
-    b = (B.t().contiguous() if b_col else B).to(DEV)
-    L = _native.hip()
-    for group in (4, 0):  # grouped tile order (default) and the panel order
-        L.pv_gemm_set_group(group)
-        try:
-            for ks in (1, 0, 4):
-                if ks == 4 and K < 4 * 64:
-                    continue
-                c = gops.gemm(a, b, a_col, b_col, ksplit=ks)
-                torch.cuda.synchronize()
-                err = float((c.cpu() - ref_c).abs().max() / ref_c.abs().max())
-                assert err < 1e-5, (group, ks, err)
-        finally:
-            L.pv_gemm_set_group(4)
-
-
-def test_gemm_engine_epilogues():
-    """Fused epilogue: alpha, bias, relu / gelu / tanh, bf16 output, beta = 1 accumulation;
-    split-K with the same epilogue through the column-sum reduce."""
-    from dnn_page_vectors_amd.ops import gemm as gops
-
-    g = torch.Generator().manual_seed(9)
-    M, N, K = 520, 384, 512
-    A = torch.randn(M, K, generator=g).bfloat16().to(DEV)
-    B = torch.randn(N, K, generator=g).bfloat16().to(DEV)
-    bias = torch.randn(N, generator=g).to(DEV)
-    pre = 0.5 * (A.float() @ B.float().t()) + bias
-    acts = {"none": pre, "relu": torch.relu(pre), "tanh": torch.tanh(pre),
-            "gelu": torch.nn.functional.gelu(pre, approximate="tanh")}
-    for act, want in acts.items():
-        for ks in (1, 2):
-            c = gops.gemm(A, B, bias=bias, act=act, alpha=0.5, ksplit=ks)
-            torch.testing.assert_close(c, want, rtol=2e-4, atol=2e-3)
-        c16 = gops.gemm(A, B, bias=bias, act=act, alpha=0.5, out_dtype=torch.bfloat16)
-        assert c16.dtype == torch.bfloat16
-        torch.testing.assert_close(c16.float(), want, rtol=1e-2, atol=2e-2)
-    base = torch.randn(M, N, generator=g).to(DEV)
-    for ks in (1, 2):
-        c = base.clone()
-        gops.gemm(A, B, out=c, accumulate=True, ksplit=ks)
-        torch.testing.assert_close(c, base + A.float() @ B.float().t(), rtol=2e-4, atol=2e-3)
-
-
 def _mx_k_of(hyp: str, l: int, j: int) -> int:
     """k index of byte j (0..31) of lane l's 32-byte operand under a layout hypothesis."""
     g = l >> 4

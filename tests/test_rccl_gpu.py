@@ -134,3 +134,65 @@ def test_rccl_world1_forced_collectives_match_single_process():
         assert i["all_gather_into_tensor"] == 0 and i["page_gather"] == 0 and i["cross_gpu_fn"] == 0, r
         assert abs(r["loss_d"] - r["loss_s"]) <= 2e-3 * max(1.0, abs(r["loss_s"])), r
         assert r["grad_rel"] < 2e-2, r
+
+
+def _graph_worker(port, models, steps, out):
+    """Eager vs captured data-parallel step on a world-1 RCCL group with every collective path
+    forced on: the same init, the same fresh batch each step."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      PAGEVEC_FORCE_DIST="1")
+    os.environ.pop("PAGEVEC_DIST_BACKEND", None)
+    try:
+        from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+        from dnn_page_vectors_amd.models import build_model
+        from dnn_page_vectors_amd.parallel import dist as pdist
+        from dnn_page_vectors_amd.train.trainer import Trainer
+
+        info = pdist.init_distributed()
+        assert info.backend == "nccl" and pdist.active(), info
+        dev = info.device
+        res = {}
+        for model in models:
+            cfg = _cfg(model)
+            data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=1024), dev, seed=3)
+            batches = [data.batch(cfg.batch_size) for _ in range(steps)]
+            runs = {}
+            for graph in (False, True):
+                torch.manual_seed(1234)
+                tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), dev, graph=graph)
+                assert tr.buckets is not None and tr.graph_mode == graph
+                losses, grads = [], []
+                for q, d in batches:
+                    m = tr.train_step(q, d)
+                    losses.append(float(m["loss"]))
+                    grads.append(tr.flat.grad.detach().clone())
+                torch.cuda.synchronize()
+                runs[graph] = (losses, grads, tr.flat.data.detach().clone(), tr._graph is not None)
+            (le, ge, pe, _), (lg, gg, pg, captured) = runs[False], runs[True]
+            dl = max(abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lg))
+            dg = max(float((a - b).abs().max() / a.abs().max().clamp(min=1e-30)) for a, b in zip(ge, gg))
+            dp = float((pe - pg).abs().max())
+            res[model] = dict(captured=captured, loss_rel=dl, grad_rel=dg, param_abs=dp, steps=len(le))
+        out.put(("ok", res))
+        pdist.destroy()
+    except Exception as e:
+        import traceback
+
+        out.put(("err", repr(e) + "\n" + traceback.format_exc()))
+
+
+def test_rccl_world1_graph_captured_dp_step_matches_eager():
+    """the data-parallel step captured in a hipGraph WITH its RCCL collectives
+    (page gather, query / scale gathers, bucketed all-reduce) gives the eager trajectory over
+    20 replays with fresh batches (CDSSM: dropout seeds from the per-replay device seed)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_worker, args=(_port(), ("mlp", "cdssm"), 22, q))
+    p.start()
+    status, res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", res
+    for model, r in res.items():
+        print(model, r)
+        assert r["captured"], r
+        assert r["loss_rel"] < 2e-3 and r["grad_rel"] < 2e-2, r

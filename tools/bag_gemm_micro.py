@@ -1,11 +1,19 @@
-"""Counts-GEMM embedding bag (MLP config): C (N x V bf16 counts) @ W (V x E) forward and
-C^T @ G backward on hipBLASLt, plain vs split over V (fwd) / N (bwd) into batched GEMMs.
+"""Long-bag products of the MLP / chunked towers: in-tree bag_gemm.hip (segment lists +
+on-the-fly-count MFMA products) against the library plan (dense bf16 count matrix + hipBLASLt),
+on synthetic Zipf pages of the bench distribution.  CUDA-event timed, same process.
 
-    python tools/bag_gemm_micro.py
+    python tools/bag_gemm_micro.py [--N 4096] [--L 2000] [--V 30000] [--E 512]
+
+Reported per call (ms): rle (segment lists), hip_fwd (partials), hip_wgrad, lib_counts (dense
+count matrix), lib_fwd (split-K bmm), lib_wgrad (C^T G); plus max relative differences.
 """
+import argparse
 import json
+import os
+import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
 
 def ev(fn, it=20):
@@ -22,26 +30,47 @@ def ev(fn, it=20):
 
 
 def main():
-    N, V, E, ldc = 4096, 30000, 512, 30016
-    C = torch.zeros(N, ldc, device="cuda", dtype=torch.bfloat16)
-    C[:, :V] = (torch.rand(N, V, device="cuda") < 0.05).to(torch.bfloat16)
-    W = torch.randn(V, E, device="cuda").to(torch.bfloat16)
-    G = torch.randn(N, E, device="cuda").to(torch.bfloat16)
-    r = {"fwd_plain": ev(lambda: (C[:, :V] @ W).float())}
-    ref = (C[:, :V] @ W).float()
-    for sk in (4, 8, 16):
-        Vk = V // sk
-        Cb = C[:, :V].unflatten(1, (sk, Vk)).transpose(0, 1)
-        Wb = W.view(sk, Vk, E)
-        f = lambda: torch.bmm(Cb, Wb, out_dtype=torch.float32).sum(0)
-        r[f"fwd_sk{sk}"] = ev(f)
-        r[f"fwd_sk{sk}_err"] = float((f() - ref).abs().max() / ref.abs().max())
-    r["bwd_plain"] = ev(lambda: (C[:, :V].t() @ G).float())
-    for sk in (2, 4):
-        Nk = N // sk
-        Cb = C[:, :V].view(sk, Nk, V).transpose(1, 2)
-        Gb = G.view(sk, Nk, E)
-        r[f"bwd_sk{sk}"] = ev(lambda: torch.bmm(Cb, Gb, out_dtype=torch.float32).sum(0))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=4096)
+    ap.add_argument("--L", type=int, default=2000)
+    ap.add_argument("--V", type=int, default=30000)
+    ap.add_argument("--E", type=int, default=512)
+    a = ap.parse_args()
+    from dnn_page_vectors_amd.config import Configuration
+    from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
+    from dnn_page_vectors_amd.ops import embedding as eops
+
+    dev = torch.device("cuda")
+    cfg = Configuration(feature_level="ngram", vocab_hash_size=a.V, query_length=45, document_length=a.L, J=0)
+    data = SyntheticPairs(spec_from_config(cfg, a.V, num_pages=a.N), dev, seed=5)
+    ids = data.pages[:a.N].contiguous()
+    W16 = torch.randn(a.V, a.E, device=dev).bfloat16()
+    G16 = torch.randn(a.N, a.E, device=dev).bfloat16()
+    r = {"shape": [a.N, a.L, a.V, a.E]}
+    rle = eops._Rle(ids, a.V, 0)
+    r["rle"] = ev(lambda: eops._Rle(ids, a.V, 0))
+    part = rle.forward_partials(W16)
+    r["hip_fwd"] = ev(lambda: rle.forward_partials(W16))
+    dW = torch.empty(a.V, a.E, device=dev)
+    r["hip_wgrad"] = ev(lambda: rle.weight_grad(G16, dW, False))
+    C, lens = eops._counts(ids, a.V, 0)
+    r["lib_counts"] = ev(lambda: eops._counts(ids, a.V, 0))
+    ref = eops._counts_gemm(C[:, :a.V], W16)
+    r["lib_fwd"] = ev(lambda: eops._counts_gemm(C[:, :a.V], W16))
+    Ct = C[:, :a.V].t()
+    out = torch.empty(a.V, a.E, device=dev)
+    r["lib_wgrad"] = ev(lambda: torch.mm(Ct, G16, out_dtype=torch.float32, out=out))
+    r["fwd_rel_diff"] = float((part.sum(0) - ref).abs().max() / ref.abs().max())
+    from dnn_page_vectors_amd.ops._common import lib
+    for d in (1, 2, 3, 4, 8, 12, 15):  # timing ablations (bag_gemm.hip DBG bits)
+        lib().pv_bag_set_dbg(d)
+        r[f"fwd_dbg{d}"] = ev(lambda: rle.forward_partials(W16))
+    lib().pv_bag_set_dbg(0)
+    r["wgrad_rel_diff"] = float((dW - out).abs().max() / out.abs().max())
+    flops = 2.0 * a.N * a.V * a.E
+    r["hip_fwd_tflops"] = round(flops / r["hip_fwd"] / 1e9, 1)
+    r["hip_wgrad_tflops"] = round(flops / r["hip_wgrad"] / 1e9, 1)
+    r["nnz_per_page"] = float(rle.ao[-1]) / a.N
     print(json.dumps(r), flush=True)
 
 

@@ -90,7 +90,7 @@ void run(const char* name, double flop_per_mfma, int waves_per_simd) {
 }
 
 int main() {
-  for (int w = 1; w <= 2; ++w) {
+  for (int w = 1; w <= 4; ++w) {
     run<0>("16x16x32_bf16", 2.0 * 16 * 16 * 32, w);
     run<1>("16x16x16_bf16", 2.0 * 16 * 16 * 16, w);
     run<2>("32x32x16_bf16", 2.0 * 32 * 32 * 16, w);

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--preset", default="cdssm_ngram_bf16")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--setter", default="", help="a libpagevec_hip setter (e.g. pv_conv_r7_set_occ) instead of a flag")
+    ap.add_argument("--env", default="", help="an environment variable read at call time (e.g. PAGEVEC_QUERY_STREAM): "
+                                              "the two values are its string values")
     a = ap.parse_args()
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
@@ -44,12 +46,14 @@ def main():
 
     mod = importlib.import_module(a.module)
     va, vb = (ast.literal_eval(v) for v in a.vals.split(","))
-    if a.vals == "0,1" and not a.setter:
+    if a.vals == "0,1" and not a.setter and not a.env:
         va, vb = False, True
     from dnn_page_vectors_amd.ops._common import lib
 
     def setv(v):
-        if a.setter:
+        if a.env:
+            os.environ[a.env] = str(v)
+        elif a.setter:
             getattr(lib(), a.setter)(int(v))
         else:
             setattr(mod, a.flag, v)
@@ -71,7 +75,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             res[val].append(e0.elapsed_time(e1) / a.steps)
-    print(json.dumps({"preset": a.preset, "flag": a.setter or a.flag, "a": str(va), "b": str(vb),
+    print(json.dumps({"preset": a.preset, "flag": a.env or a.setter or a.flag, "a": str(va), "b": str(vb),
                       "a_ms": [round(x, 3) for x in res[va]], "b_ms": [round(x, 3) for x in res[vb]],
                       "a_median": round(statistics.median(res[va]), 3),
                       "b_median": round(statistics.median(res[vb]), 3)}), flush=True)
