@@ -130,6 +130,7 @@ class Configuration:
     seed: int = 1337                      # np.random.seed(1337), cnn_dssm_th.py:20
     backend: str = "auto"                 # auto | hip | torch  (op implementation)
     grad_bucket_mb: float = 32.0
+    lr_warmup_steps: int = 0              # linear learning-rate warmup (0 = none; Keras had none)
     # graph mode on a data-parallel run captures the whole step INCLUDING its RCCL collectives
     # (page / query gathers, bucketed gradient all-reduces) in the hipGraph; False = eager there
     graph_distributed: bool = True

@@ -20,6 +20,13 @@ __device__ __forceinline__ void store_bf16x4(unsigned short* dst, const f32x4& v
   *reinterpret_cast<uint2*>(dst) = uint2{lo, hi};
 }
 
+// tdev = {step, warmup steps}: the learning rate ramps linearly over the first warmup steps
+// (0 = none), read on the device so a captured step replays the schedule
+__device__ __forceinline__ float warmup_scale(const float* tdev) {
+  const float w = tdev[1];
+  return w > 0.f ? fminf(1.f, tdev[0] / w) : 1.f;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
                                                    float b1, float b2, float eps, float wd, int torch_style,
@@ -28,7 +35,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    unsigned short* __restrict__ p16) {
   if (skip && *skip != 0.f) return;  // non-finite guard: skip the whole step
   if (tdev) {  // step count on the device (hipGraph replays): bias corrections computed here
-    const float t = *tdev, lr = lr_t;
+    const float t = tdev[0], lr = lr_t * warmup_scale(tdev);
     const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
     if (torch_style) {
       lr_t = lr / bc1;
@@ -116,7 +123,8 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
   constexpr int NJ = LPR == 64 ? 4 : 1;  // column groups per lane
   constexpr int RPW = 64 / LPR;          // rows per wave and trip
   if (skip && *skip != 0.f) return;
-  const float t = *tdev;
+  const float t = tdev[0];
+  lr *= warmup_scale(tdev);
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
   const float lr_t = torch_style ? lr / bc1 : lr * sqrtf(bc2) / bc1;
   const float bc2_sqrt_inv = torch_style ? rsqrtf(bc2) : 1.f;

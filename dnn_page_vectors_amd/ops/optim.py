@@ -91,7 +91,7 @@ class FlatParams:
 class FlatAdam:
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, torch_style: bool = False, lazy: Optional[Iterable[str]] = None,
-                 mirror: Optional[Iterable[str]] = None, sparse=None):
+                 mirror: Optional[Iterable[str]] = None, sparse=None, warmup: int = 0):
         """lazy: names of 2-D embedding tables updated LazyAdam-style — a row whose gradient is
         all zero this step (none of its tokens in the batch) keeps its weights and moments
         (optim.hip::adam_lazy_rows_kernel; the step then streams ~4 B instead of 28 B per
@@ -134,12 +134,15 @@ class FlatAdam:
         self.step_count = 0
         # the step count also lives on the device: the HIP update reads (and advances) it,
         # so a captured training step replays with the right bias corrections
-        self.t_dev = torch.zeros(1, dtype=torch.float32, device=flat.data.device)
+        # t_dev = {step, linear warmup steps} (optim.hip warmup_scale)
+        self.warmup = int(warmup)
+        self.t_dev = torch.tensor([0.0, float(self.warmup)], dtype=torch.float32, device=flat.data.device)
 
     def step(self, skip_flag: Optional[torch.Tensor] = None) -> None:
         """One update. ``skip_flag``: device scalar; non-zero => the kernel skips (NaN guard)."""
         self.step_count += 1
         t = self.step_count
+        lr = self.lr * (min(1.0, t / self.warmup) if self.warmup > 0 else 1.0)  # host paths
         if use_hip(self.flat.data):
             if self.lazy or self.mirrors or self.sparse is not None:
                 self._step_segments(skip_flag)
@@ -166,9 +169,9 @@ class FlatAdam:
                 self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
                 bc1 = 1 - self.b1 ** t
                 bc2 = 1 - self.b2 ** t
-                self.flat.data.addcdiv_(self.m, (self.v.sqrt() / math.sqrt(bc2)).add_(self.eps), value=-self.lr / bc1)
+                self.flat.data.addcdiv_(self.m, (self.v.sqrt() / math.sqrt(bc2)).add_(self.eps), value=-lr / bc1)
             else:
-                ref.adam_keras_([self.flat.data], [g], [self.m], [self.v], t, self.lr, self.b1, self.b2, self.eps)
+                ref.adam_keras_([self.flat.data], [g], [self.m], [self.v], t, lr, self.b1, self.b2, self.eps)
             for o, k, rl, untouched, saved in keep:
                 for tt, sv in zip((self.flat.data, self.m, self.v), saved):
                     tt[o:o + k].view(-1, rl)[untouched] = sv
@@ -224,7 +227,7 @@ class FlatAdam:
         self.m.copy_(d["m"])
         self.v.copy_(d["v"])
         self.step_count = int(d["step"])
-        self.t_dev.fill_(float(self.step_count))
+        self.t_dev[0] = float(self.step_count)
 
 
 def _generation() -> int:

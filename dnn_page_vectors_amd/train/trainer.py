@@ -114,7 +114,8 @@ class Trainer:
         self.sparse = (SparseTables(self.flat, sparse_rows.table_names(self.model))
                        if getattr(cfg, "sparse_embedding_grad", False) else None)
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
-                            torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror, sparse=self.sparse)
+                            torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror, sparse=self.sparse,
+                            warmup=int(getattr(cfg, "lr_warmup_steps", 0)))
         self.placement = getattr(cfg, "placement", "dp")
         if self.placement not in ("dp", "tower"):
             raise ValueError(f"unknown placement {self.placement!r}")
@@ -301,7 +302,12 @@ class Trainer:
         self._gq.copy_(q_ids, non_blocking=True)
         self._gd.copy_(d_ids, non_blocking=True)
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
-        self._seed_dev.fill_(seed)
+        # the captured step ran with seed 0, so every kernel seed was its tower's constant
+        # (models/base.py: query 2 s + 1, pages 2 s + 2 + 1000 slot); the kernels add the
+        # device value, so 2 s (mod 2^32) replays exactly the eager step's conv-tower dropout
+        # masks (BERT derives its layer seeds multiplicatively: fresh, but different, masks)
+        d = (2 * seed) & 0xFFFFFFFF
+        self._seed_dev.fill_(d - (1 << 32) if d >= (1 << 31) else d)
         self._graph.replay()
         if self.graph_fence:
             torch.cuda.synchronize(self.device)
@@ -479,6 +485,6 @@ class Trainer:
         self.opt.step_count = int(st.get("opt_step", self.step))
         # the HIP Adam reads its bias corrections from the DEVICE step counter (captured
         # steps replay without the host): it must resume at the same count as the host one
-        self.opt.t_dev.fill_(float(self.opt.step_count))
+        self.opt.t_dev[0] = float(self.opt.step_count)
         bump_generation()
         self.opt.refresh_mirrors()

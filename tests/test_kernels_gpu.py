@@ -1047,13 +1047,13 @@ def test_resume_restores_device_adam_step(tmp_path):
     ck.save_epoch(tb, str(tmp_path / "ck"), 1)
     tc = Trainer(cfg, CDSSM(cfg, 500), torch.device(DEV))
     assert ck.resume(tc, str(tmp_path / "ck"))
-    assert tc.opt.step_count == 2 and float(tc.opt.t_dev) == 2.0
+    assert tc.opt.step_count == 2 and float(tc.opt.t_dev[0]) == 2.0
     tc.train_step(*data[2])
     before_c = tc.flat.data.clone()
     tc.train_step(*data[3])
     delta_c = tc.flat.data - before_c
     torch.cuda.synchronize()
-    assert float(tc.opt.t_dev) == 4.0
+    assert float(tc.opt.t_dev[0]) == 4.0
     rel = float((delta_c - delta_a).norm() / delta_a.norm())
     assert rel < 0.05, rel
     torch.testing.assert_close(tc.flat.data, ta.flat.data, rtol=1e-3, atol=2e-4)

@@ -39,7 +39,7 @@ def lazy(a):
     g = torch.zeros(R, C, device="cuda")
     rows = torch.randperm(R, device="cuda")[:max(1, int(R * a.touched))]
     g[rows] = torch.randn(rows.numel(), C, device="cuda")
-    t = torch.ones(1, device="cuda")
+    t = torch.tensor([1.0, 0.0], device="cuda")  # {step, warmup steps}
     L = lib()
     res = {}
     for name, rl in (("dense", 0), ("lazy", C)):
