@@ -121,6 +121,9 @@ class Configuration:
     # exchanged between data-parallel ranks (all-gather of ids + rows, not a dense all-reduce)
     # and updated (LazyAdam) — for million-row word vocabularies
     sparse_embedding_grad: bool = False
+    # padding of the row exchange: -1 = min(V, noted ids) agreed once (no per-step host sync:
+    # capturable), 0 = exact per-step maximum (a host sync per table and step), > 0 = rows
+    sparse_rows_capacity: int = -1
     optimizer_bf16_mirror: bool = True   # the Adam kernel also writes the bf16 compute copies of big weights
     # compute precision (ops/_common.py::precision_scope): bf16 = the HIP kernels (bf16 MFMA
     # operands, fp32 accumulation / master weights); fp32 = the reference's precision, no bf16

@@ -15,17 +15,26 @@ table registered here instead:
 * only the previous step's rows are zeroed (the rest of the table gradient stays zero by
   construction), ``FlatParams.zero_grad`` skips the table;
 * data parallel: in place of the table's dense bucket all-reduce, every rank all-gathers
-  (row ids, gradient rows) padded to the largest rank's count (one 4-byte MAX all-reduce
-  to size them), zeroes its own rows and index-adds everyone's rows scaled by 1/W — the
-  average, exactly what the dense all-reduce would have left in those rows, every other
-  row being zero on every rank;
+  (row ids, gradient rows) padded to a capacity every rank agrees on, zeroes its own rows
+  and index-adds everyone's rows scaled by 1/W — the average, exactly what the dense
+  all-reduce would have left in those rows, every other row being zero on every rank;
 * the optimizer runs LazyAdam over the union rows only (``pv_adam_rows``: the lazy kernel
   over a row list, rows whose gradient is all zero keep weights and moments — the
   ``lazy_embedding_adam`` semantics, so a sparse run equals a lazy dense run);
 * the gradient norm / non-finite check reads the union rows, not the table.
 
-Cost per step: O(touched rows x E) instead of O(V x E); the host learns the gathered row
-count once per table and step (a sync, so these tables rule out hipGraph capture).
+Cost per step: O(touched rows x E) instead of O(V x E).
+
+Row lists are FIXED-SIZE device tensors (sorted unique rows, then -1 padding): the union is a
+sort + first-of-run flags + a scatter to the run's rank, never ``torch.unique`` or a boolean
+mask (both size their output on the host).  ``Configuration.sparse_rows_capacity`` picks the
+exchange's padding: -1 (default) = min(V, the largest rank's noted-id count), agreed by one
+MAX all-reduce the first time a table is exchanged — no host sync afterwards, so the step is
+capturable in a hipGraph; 0 = the exact per-step maximum of distinct rows (a host sync per
+table and step: the smallest exchange, not capturable); > 0 = that many rows.  A step whose
+distinct rows exceed the capacity counts into ``overflow`` (device); ``check()`` raises on it
+(the trainer calls it where it reads metrics anyway).  The Adam row kernel and the gradient
+statistics skip -1 entries.
 """
 from __future__ import annotations
 
@@ -49,11 +58,38 @@ class _Table:
     rows: Optional[torch.Tensor] = None      # int32 candidate rows of the current step (after exchange)
     prev: Optional[torch.Tensor] = None      # rows written last step (zeroed before the next)
     pending: Optional[Tuple] = None          # in-flight all-gathers
+    prev_buf: Optional[torch.Tensor] = None  # persistent copy of ``prev`` (stable address under capture)
+    cap: int = 0                             # agreed exchange capacity (rows), 0 = not yet agreed
+
+
+def unique_rows(ids: torch.Tensor, V: int, cap: int,
+                overflow: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sorted distinct ids in [0, V) of ``ids`` in a fixed-size int32 tensor of ``cap`` entries,
+    padded with -1 — without a host sync.  Distinct ids beyond ``cap`` are dropped and counted
+    into ``overflow`` (int64 device scalar) when given."""
+    dev = ids.device
+    if ids.numel() == 0 or cap <= 0:
+        return torch.full((max(cap, 0),), -1, dtype=torch.int32, device=dev)
+    x = ids.reshape(-1).to(torch.int64)
+    x = torch.where((x >= 0) & (x < V), x, torch.full_like(x, V))  # invalid -> V (sorts last)
+    s, _ = torch.sort(x)
+    first = torch.ones_like(s, dtype=torch.bool)
+    first[1:] = s[1:] != s[:-1]
+    first &= s < V
+    pos = torch.cumsum(first, 0) - 1
+    keep = first & (pos < cap)
+    out = torch.full((cap + 1,), -1, dtype=torch.int32, device=dev)
+    out.scatter_(0, torch.where(keep, pos, torch.full_like(pos, cap)), torch.where(keep, s, -1).to(torch.int32))
+    if overflow is not None:
+        overflow += (first & ~keep).sum()
+    return out[:cap]
 
 
 class SparseTables:
-    def __init__(self, flat, names: Sequence[str]):
+    def __init__(self, flat, names: Sequence[str], capacity: int = -1):
         self.flat = flat
+        self.capacity = int(capacity)
+        self.overflow = torch.zeros((), dtype=torch.int64, device=flat.grad.device)
         named = dict(flat.named)
         self.tables: Dict[str, _Table] = {}
         self._by_id: Dict[int, _Table] = {}
@@ -76,7 +112,8 @@ class SparseTables:
         """Before the forward: zero the rows written last step (the dense zero skips tables)."""
         for t in self.tables.values():
             if t.prev is not None and t.prev.numel():
-                self.grad2d(t).index_fill_(0, t.prev.long(), 0.0)
+                # -1 padding -> row 0: every untouched row of the table gradient is zero
+                self.grad2d(t).index_fill_(0, t.prev.clamp(min=0).long(), 0.0)
             t.prev = None
             t.rows = None
             t.notes = []
@@ -90,36 +127,48 @@ class SparseTables:
     def grad2d(self, t: _Table) -> torch.Tensor:
         return self.flat.grad[t.off:t.off + t.V * t.E].view(t.V, t.E)
 
-    def _local_rows(self, t: _Table) -> torch.Tensor:
+    def _noted(self, t: _Table) -> torch.Tensor:
         if not t.notes:
-            return torch.empty(0, dtype=torch.int32, device=self.flat.grad.device)
-        ids = torch.cat([x.to(torch.int64) for x in t.notes]) if len(t.notes) > 1 else t.notes[0].to(torch.int64)
-        u = torch.unique(ids)  # sorted
-        u = u[(u >= 0) & (u < t.V)]
-        return u.to(torch.int32)
+            return torch.empty(0, dtype=torch.int64, device=self.flat.grad.device)
+        return torch.cat([x.to(torch.int64) for x in t.notes]) if len(t.notes) > 1 else t.notes[0]
+
+    def _local_rows(self, t: _Table) -> torch.Tensor:
+        ids = self._noted(t)
+        return unique_rows(ids, t.V, min(t.V, ids.numel()), self.overflow)
+
+    def _agree_cap(self, t: _Table, ids: torch.Tensor, group) -> int:
+        if self.capacity > 0:
+            return min(t.V, self.capacity)
+        if self.capacity == 0:  # exact: this step's largest distinct-row count (host sync)
+            u = unique_rows(ids, t.V, min(t.V, ids.numel()))
+            cnt = (u >= 0).sum().reshape(1)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+            return max(1, int(cnt.item()))
+        if t.cap == 0:  # auto: agreed once, from the noted-id counts (no per-step sync)
+            cnt = torch.tensor([min(t.V, ids.numel())], dtype=torch.int64, device=ids.device)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
+            t.cap = max(1, int(cnt.item()))
+        return t.cap
 
     def launch(self, t: _Table, group=None) -> None:
         """The table's gradient is complete: start its row exchange (or just fix its rows)."""
-        u = self._local_rows(t)
+        ids = self._noted(t)
         t.notes = []
         if not active(group):
-            t.rows = u
+            t.rows = unique_rows(ids, t.V, min(t.V, ids.numel()), self.overflow)
             return
         W = dist.get_world_size(group)
-        cnt = torch.tensor([u.numel()], dtype=torch.int64, device=u.device)
-        dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
-        cap = int(cnt.item())  # host sync: the gathered buffers' size
-        rows = torch.full((cap,), -1, dtype=torch.int32, device=u.device)
-        rows[:u.numel()] = u
+        cap = self._agree_cap(t, ids, group)
+        rows = unique_rows(ids, t.V, cap, self.overflow)
         g2 = self.grad2d(t)
-        vals = torch.zeros(cap, t.E, dtype=g2.dtype, device=g2.device)
-        if u.numel():
-            vals[:u.numel()] = g2.index_select(0, u.long())
-        all_rows = torch.empty(W * cap, dtype=torch.int32, device=u.device)
+        ok = (rows >= 0).unsqueeze(1)
+        vals = torch.where(ok, g2.index_select(0, rows.clamp(min=0).long()), torch.zeros((), dtype=g2.dtype,
+                                                                                       device=g2.device))
+        all_rows = torch.empty(W * cap, dtype=torch.int32, device=rows.device)
         all_vals = torch.empty(W * cap, t.E, dtype=g2.dtype, device=g2.device)
         h1 = dist.all_gather_into_tensor(all_rows, rows, group=group, async_op=True)
         h2 = dist.all_gather_into_tensor(all_vals, vals, group=group, async_op=True)
-        t.pending = (u, all_rows, all_vals, h1, h2, W)
+        t.pending = (rows, all_rows, all_vals, h1, h2, W)
 
     def complete(self, t: _Table) -> None:
         """Wait for the exchange; the table gradient rows := the mean over ranks."""
@@ -130,17 +179,28 @@ class SparseTables:
         h1.wait()
         h2.wait()
         g2 = self.grad2d(t)
-        if u.numel():
-            g2.index_fill_(0, u.long(), 0.0)
-        ok = all_rows >= 0
-        r = all_rows[ok].long()
-        g2.index_add_(0, r, all_vals[ok], alpha=1.0 / W)
-        t.rows = torch.unique(r).to(torch.int32)
+        # padding entries name row 0 with zero values: zeroing / adding zero to an untouched
+        # row (zero by construction) changes nothing
+        g2.index_fill_(0, u.clamp(min=0).long(), 0.0)
+        g2.index_add_(0, all_rows.clamp(min=0).long(), all_vals, alpha=1.0 / W)
+        t.rows = unique_rows(all_rows, t.V, min(t.V, all_rows.numel()))
 
     def finish_step(self) -> None:
         """After the optimizer: the rows written this step are the next step's zero list."""
         for t in self.tables.values():
-            t.prev = t.rows
+            r = t.rows
+            if r is not None and (t.prev_buf is None or t.prev_buf.shape != r.shape):
+                t.prev_buf = torch.empty_like(r)
+            if r is not None:  # a copy at a fixed address: a captured step reads the last replay's
+                t.prev_buf.copy_(r)
+            t.prev = t.prev_buf if r is not None else None
+
+    def check(self) -> None:
+        """Raise if a step's distinct rows ever exceeded the exchange capacity (a host read)."""
+        n = int(self.overflow.item())
+        if n:
+            raise RuntimeError(f"sparse embedding gradients: {n} distinct rows beyond the exchange capacity were "
+                               f"dropped (sparse_rows_capacity={self.capacity}); raise it or use 0 (exact)")
 
     def candidate_rows(self, t: _Table) -> torch.Tensor:
         if t.rows is None:  # never launched (no data parallel hook): local rows
@@ -162,8 +222,9 @@ class SparseTables:
         for t in self.tables.values():
             rows = self.candidate_rows(t)
             if rows.numel():
-                g = self.grad2d(t).index_select(0, rows.long())
-                fin = torch.isfinite(g)
+                g = self.grad2d(t).index_select(0, rows.clamp(min=0).long())
+                fin = torch.isfinite(g) | (rows < 0).unsqueeze(1)  # padding rows: ignored
+                g = torch.where(rows.unsqueeze(1) >= 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
                 out[0] += torch.where(fin, g, torch.zeros_like(g)).pow(2).sum()
                 out[1] = torch.maximum(out[1], (~fin).any().float())
         out[1] = (out[1] > 0).float()

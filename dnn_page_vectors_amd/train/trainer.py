@@ -111,7 +111,8 @@ class Trainer:
                 and getattr(cfg, "dtype", "bf16") != "fp32"
                 and os.environ.get("PAGEVEC_NO_MIRROR", "0") != "1") else None
         # row-sparse embedding gradients for large vocabularies (parallel/sparse_rows.py)
-        self.sparse = (SparseTables(self.flat, sparse_rows.table_names(self.model))
+        self.sparse = (SparseTables(self.flat, sparse_rows.table_names(self.model),
+                                    capacity=int(getattr(cfg, "sparse_rows_capacity", -1)))
                        if getattr(cfg, "sparse_embedding_grad", False) else None)
         self.opt = FlatAdam(self.flat, lr=cfg.lr, betas=(cfg.beta1, cfg.beta2), eps=cfg.adam_eps,
                             torch_style=(cfg.model == "bert"), lazy=lazy, mirror=mirror, sparse=self.sparse,
@@ -155,12 +156,14 @@ class Trainer:
             determinism.ensure(False)
         # data parallel: the collectives are captured with the step (RCCL supports stream
         # capture; the bucket hooks, the page gather and the loss gathers all enqueue on
-        # streams that fork from and join back into the capture stream); not with the sparse
-        # tables (their exchange sizes itself with a host sync) or tower placement
+        # streams that fork from and join back into the capture stream); the sparse tables'
+        # fixed-capacity row exchange too, not the exact one (sparse_rows_capacity 0 sizes
+        # itself with a host sync); not tower placement
         self.graph_mode = (bool(graph) and self.device.type == "cuda"
                            and (not self.info.enabled or (bool(getattr(cfg, "graph_distributed", True))
                                                           and self.placement == "dp"))
-                           and not self.deterministic and self.sparse is None)
+                           and not self.deterministic
+                           and (self.sparse is None or self.sparse.capacity != 0))
         # graph_fence: optional device sync after every replay (debugging aid, off by default).
         # Round 1 needed it: replays interleaved with eager allocating work faulted after ~97
         # CDSSM steps inside rocPRIM's onesweep radix sort (the dTable gradient's bucketing),
@@ -422,6 +425,8 @@ class Trainer:
             n += 1
         if n == 0:
             return {}
+        if train and self.sparse is not None:
+            self.sparse.check()
         out = {k: float(v) / n for k, v in tot.items() if k != "nonfinite"}
         if train and "nonfinite" in tot:
             self.skipped_steps += int(round(float(tot["nonfinite"])))

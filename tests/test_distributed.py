@@ -292,7 +292,7 @@ def _sparse_data(B, V):
              torch.randint(1, V, (B, 4, 16), generator=g, dtype=torch.int32)) for _ in range(3)]
 
 
-def _sparse_worker(rank, world, port, q, V, sparse):
+def _sparse_worker(rank, world, port, q, V, sparse, cap=-1):
     _env(rank, world, port)
     from dnn_page_vectors_amd.models.cdssm import CDSSM
     from dnn_page_vectors_amd.parallel import dist as pdist
@@ -300,15 +300,33 @@ def _sparse_worker(rank, world, port, q, V, sparse):
 
     pdist.init_distributed(device="cpu")
     B = 8
-    cfg = _cfg("cross_gpu", B // world).replace(sparse_embedding_grad=sparse, lazy_embedding_adam=True)
+    cfg = _cfg("cross_gpu", B // world).replace(sparse_embedding_grad=sparse, lazy_embedding_adam=True,
+                                                sparse_rows_capacity=cap)
     tr = Trainer(cfg, CDSSM(cfg, V))
     if sparse:
         assert tr.buckets.sparse_bucket  # the tables' buckets are row exchanges
     for qa, da in _sparse_data(B, V):
         sl = slice(rank * B // world, (rank + 1) * B // world)
         tr.train_step(qa[sl], da[sl])
-    q.put((rank, tr.flat.data.detach().numpy().copy()))
+    err = ""
+    if sparse:
+        try:
+            tr.sparse.check()
+        except RuntimeError as e:
+            err = str(e)
+    q.put((rank, tr.flat.data.detach().numpy().copy(), err))
     pdist.destroy()
+
+
+def _run_sparse(world, V, sparse, cap=-1):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sparse_worker, args=(r, world, port, q, V, sparse, cap)) for r in range(world)]
+    [p.start() for p in ps]
+    res = {r: (torch.from_numpy(v), e) for r, v, e in (q.get(timeout=300) for _ in ps)}
+    [p.join(timeout=60) for p in ps]
+    return res
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -323,16 +341,11 @@ def test_sparse_embedding_grad_dp_equals_dense(world):
     V = 200_000
     out = {}
     for sparse in (True, False):
-        port = _port()
-        ctx = mp.get_context("spawn")
-        q = ctx.Queue()
-        ps = [ctx.Process(target=_sparse_worker, args=(r, world, port, q, V, sparse)) for r in range(world)]
-        [p.start() for p in ps]
-        res = {r: torch.from_numpy(v) for r, v in (q.get(timeout=300) for _ in ps)}
-        [p.join(timeout=60) for p in ps]
+        res = _run_sparse(world, V, sparse)
         for r in range(1, world):
-            torch.testing.assert_close(res[0], res[r], rtol=0, atol=0)
-        out[sparse] = res[0]
+            torch.testing.assert_close(res[0][0], res[r][0], rtol=0, atol=0)
+        assert all(not e for _, e in res.values())
+        out[sparse] = res[0][0]
     torch.testing.assert_close(out[True], out[False], rtol=1e-5, atol=1e-6)
     pdist.set_info(pdist.DistInfo())
     cfg = _cfg("in_batch", 8).replace(sparse_embedding_grad=True, lazy_embedding_adam=True)
@@ -340,3 +353,34 @@ def test_sparse_embedding_grad_dp_equals_dense(world):
     for qa, da in _sparse_data(8, V):
         tr.train_step(qa, da)
     torch.testing.assert_close(out[True], tr.flat.data, rtol=1e-4, atol=3e-5)
+
+
+def test_sparse_rows_capacity_modes():
+    """The exchange's padding (Configuration.sparse_rows_capacity): exact per-step sizing (0,
+    host sync) and a fixed capacity with room give the auto mode's parameters; a capacity below
+    the distinct-row count drops rows and every rank's check() says so."""
+    V, world = 200_000, 2
+    auto = _run_sparse(world, V, True, -1)[0][0]
+    for cap in (0, 4096):
+        res = _run_sparse(world, V, True, cap)
+        assert all(not e for _, e in res.values()), cap
+        torch.testing.assert_close(res[0][0], auto, rtol=1e-6, atol=1e-7)
+    res = _run_sparse(world, V, True, 8)
+    assert all("beyond the exchange capacity" in e for _, e in res.values())
+
+
+def test_unique_rows_fixed_size():
+    from dnn_page_vectors_amd.parallel.sparse_rows import unique_rows
+
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(-3, 60, (500,), generator=g)
+    want = torch.unique(ids[(ids >= 0) & (ids < 50)]).to(torch.int32)
+    ov = torch.zeros((), dtype=torch.int64)
+    got = unique_rows(ids, 50, 64, ov)
+    assert got.shape == (64,) and int(ov) == 0
+    torch.testing.assert_close(got[:want.numel()], want)
+    assert bool((got[want.numel():] == -1).all())
+    got = unique_rows(ids, 50, 10, ov)  # capacity below the distinct count: first 10, rest counted
+    torch.testing.assert_close(got, want[:10])
+    assert int(ov) == want.numel() - 10
+    assert unique_rows(ids[:0], 50, 4).tolist() == [-1] * 4

@@ -39,6 +39,9 @@ def _cfg(model):
 
     if model == "cdssm":
         return preset_config("cdssm_ngram_bf16").replace(batch_size=64, document_length=256, grad_bucket_mb=1.0)
+    if model == "cdssm_sparse":  # row-sparse table gradients: the fixed-capacity row exchange
+        return preset_config("cdssm_ngram_bf16").replace(batch_size=64, document_length=256, grad_bucket_mb=1.0,
+                                                         sparse_embedding_grad=True, lazy_embedding_adam=True)
     return preset_config("mlp_xgpu").replace(batch_size=64, document_length=256, grad_bucket_mb=8.0)
 
 
@@ -167,6 +170,9 @@ def _graph_worker(port, models, steps, out):
                     losses.append(float(m["loss"]))
                     grads.append(tr.flat.grad.detach().clone())
                 torch.cuda.synchronize()
+                if tr.sparse is not None:
+                    assert tr.buckets.sparse_bucket
+                    tr.sparse.check()  # no row dropped by the fixed-capacity exchange
                 runs[graph] = (losses, grads, tr.flat.data.detach().clone(), tr._graph is not None)
             (le, ge, pe, _), (lg, gg, pg, captured) = runs[False], runs[True]
             dl = max(abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lg))
@@ -184,10 +190,11 @@ def _graph_worker(port, models, steps, out):
 def test_rccl_world1_graph_captured_dp_step_matches_eager():
     """the data-parallel step captured in a hipGraph WITH its RCCL collectives
     (page gather, query / scale gathers, bucketed all-reduce) gives the eager trajectory over
-    20 replays with fresh batches (CDSSM: dropout seeds from the per-replay device seed)."""
+    20 replays with fresh batches (CDSSM: dropout seeds from the per-replay device seed; with
+    row-sparse table gradients the fixed-capacity row exchange is captured too)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_graph_worker, args=(_port(), ("mlp", "cdssm"), 22, q))
+    p = ctx.Process(target=_graph_worker, args=(_port(), ("mlp", "cdssm", "cdssm_sparse"), 22, q))
     p.start()
     status, res = q.get(timeout=300)
     p.join(timeout=60)
