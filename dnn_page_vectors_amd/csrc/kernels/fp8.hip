@@ -40,6 +40,32 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   }
 }
 
+// Byte transpose for the fp8 weight gradient (ops/embedding.py, config 5): dst (C x ldd) with
+// dst[c][r] = src[r][c] for r < R, 0 for R <= r < ldd (the MX GEMM's K padding).  64 x 64 byte
+// tiles through LDS: one 16-byte load per thread, 16 column bytes gathered per thread, one
+// 16-byte store per thread.
+__global__ __launch_bounds__(256) void transpose_u8_kernel(const unsigned char* __restrict__ src, long lds, int R,
+                                                           int C, unsigned char* __restrict__ dst, long ldd) {
+  __shared__ unsigned char tile[64][80];
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  {
+    const int r = threadIdx.x >> 2, c16 = (threadIdx.x & 3) * 16;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (r0 + r < R && c0 + c16 < lds) v = *reinterpret_cast<const uint4*>(src + (size_t)(r0 + r) * lds + c0 + c16);
+    *reinterpret_cast<uint4*>(&tile[r][c16]) = v;
+  }
+  __syncthreads();
+  const int c = threadIdx.x >> 2, rb = (threadIdx.x & 3) * 16;
+  if (c0 + c >= C || r0 + rb >= ldd) return;
+  unsigned w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w[q] = (unsigned)tile[rb + 4 * q][c] | ((unsigned)tile[rb + 4 * q + 1][c] << 8) |
+           ((unsigned)tile[rb + 4 * q + 2][c] << 16) | ((unsigned)tile[rb + 4 * q + 3][c] << 24);
+  }
+  *reinterpret_cast<uint4*>(dst + (size_t)(c0 + c) * ldd + r0 + rb) = uint4{w[0], w[1], w[2], w[3]};
+}
+
 // out: n bytes (n % 4 == 0); scale = 448 / max(amax, tiny)
 __global__ void quant_fp8_kernel(const float* __restrict__ x, const float* __restrict__ amax,
                                  unsigned* __restrict__ out, long n4) {
@@ -333,6 +359,18 @@ PV_API int pv_amax_quant_fp8_t(const float* W, int V, int E, float* ws, float* a
   PV_LAUNCH_CHECK();
   hipLaunchKernelGGL(quant_t_kernel, dim3(ldo / 64, (E + 63) / 64), dim3(256), 0, st, W, V, E, (const float*)ws,
                      (int)blocks, amax_out, (unsigned char*)out, ldo);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// src (R x lds bytes, lds % 16 == 0, lds >= C) -> dst (C x ldd bytes), dst[c][r] = src[r][c],
+// zero for R <= r < ldd (ldd % 64 == 0, ldd >= R); 16-byte aligned rows.
+PV_API int pv_transpose_u8(const void* src, long lds, int R, int C, void* dst, long ldd, void* stream) {
+  using namespace pv::fp8;
+  if (R <= 0 || C <= 0 || lds % 16 || ldd % 64 || ldd < R || lds < C) return -1;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return -2;
+  hipLaunchKernelGGL(transpose_u8_kernel, dim3((unsigned)(ldd / 64), (unsigned)((C + 63) / 64)), dim3(256), 0,
+                     (hipStream_t)stream, (const unsigned char*)src, lds, R, C, (unsigned char*)dst, ldd);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -21,6 +21,7 @@
 //                     the gradient, -gscale*g*clip' * {d_pos, q}.
 #include "common.h"
 #include <stdlib.h>
+#include <algorithm>
 #include <type_traits>
 
 namespace pv {
@@ -696,6 +697,135 @@ __global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __res
   }
 }
 
+// ---- ibw: wide vectors (D = 768 BERT towers, DP % 128 == 0) ----------------------------------
+// The flash structure of ib3 / ib5 for vectors too wide to keep a query row's D accumulators
+// in one wave: the S tile's reduction over D AND the gradient product's output columns are
+// split across the workgroup's 4 waves (wave w owns the d-slice [w DP/4, (w+1) DP/4)).
+//   * a workgroup owns 16 "owner" rows (their bf16 d-slice fragments in registers) and walks
+//     32-row tiles of the "iterated" matrix (staged once in LDS, shared by the 4 waves);
+//   * each wave computes its d-slice's partial S^T (32 iter rows x 16 owner rows, 2 KS
+//     MFMAs), the partials meet in LDS and every wave sums the full tile;
+//   * FWD : per owner row sum_j exp(g (clip(S) - 1)) -> part[split][row] (ib_rowsum);
+//     ROW : out_owner += sum_j G_oj It_j with G = scale[owner] exp(..) clip'  (dQ);
+//     COL : out_owner += sum_j G_jo It_j with G = scale[iter row] exp(..) clip' (dD);
+//     G^T stays in registers as the B operand of out^T += It^T G^T (the S^T C-layout is the
+//     B layout with the k order of pack_b), It^T through ds_read_b64_tr_b16 (ib3's trick);
+//   * no S / dS block reaches HBM and no library GEMM runs (the round-4 path materialised
+//     fp32 S blocks through torch.mm and ran two more GEMMs on a bf16 dS per block).
+// Partial outputs per split go to ws[split][owner][DP] (ib_split_reduce), part[split][owner].
+constexpr int IBW_T = 32;  // iterated rows per staged tile
+
+template <int KS, int MODE, int CLIPV>  // KS = DP / 128 k-steps of 32 per wave; MODE 0 FWD, 1 ROW, 2 COL
+__global__ __launch_bounds__(256, 2) void ibw_kernel(const unsigned short* __restrict__ O, int no,
+                                                     const unsigned short* __restrict__ It, int ni,
+                                                     const float* __restrict__ scale, float gamma,
+                                                     float* __restrict__ out, int tiles_per_split) {
+  constexpr int DP = KS * 128, LDW = DP + 8;  // LDS row stride (elements): 16-B aligned, staggered banks
+  extern __shared__ __attribute__((aligned(16))) unsigned short ibw_lds[];
+  unsigned short* it = ibw_lds;                                      // [IBW_T][LDW]
+  f32x4* sp = reinterpret_cast<f32x4*>(ibw_lds + IBW_T * LDW);       // [4 waves][2][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int o0 = blockIdx.x * 16, split = blockIdx.y;
+  const int orow = o0 + (lane & 15);
+  const int dw = wave * KS * 32;  // this wave's d-slice
+  bf16x8 ob[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+    ob[k] = orow < no ? *reinterpret_cast<const bf16x8*>(O + (size_t)orow * DP + dw + k * 32 + g * 8)
+                      : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const float osc = (MODE == 1 && orow < no) ? scale[orow] : 0.f;
+  f32x4 acc[MODE == 0 ? 1 : 2 * KS];
+#pragma unroll
+  for (int i = 0; i < (MODE == 0 ? 1 : 2 * KS); ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rsum = 0.f;
+  const int ntiles = (ni + IBW_T - 1) / IBW_T;
+  const int t_lo = split * tiles_per_split, t_hi = min(ntiles, t_lo + tiles_per_split);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int i0 = t * IBW_T;
+    // stage the tile: IBW_T x DP bf16, 16-byte pieces
+    for (int q = threadIdx.x; q < IBW_T * (DP / 8); q += 256) {
+      const int r = q / (DP / 8), c = (q % (DP / 8)) * 8;
+      *reinterpret_cast<u32x4*>(it + r * LDW + c) =
+          i0 + r < ni ? *reinterpret_cast<const u32x4*>(It + (size_t)(i0 + r) * DP + c) : u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    // this wave's d-slice of S^T: rows = iter rows (2 subtiles of 16), cols = owner rows
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(it + (c * 16 + (lane & 15)) * LDW + dw + k * 32 + g * 8);
+        s4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ob[k], s4, 0, 0, 0);
+      }
+      sp[(wave * 2 + c) * 64 + lane] = s4;
+    }
+    __syncthreads();
+    f32x4 sv[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      sv[c] = sp[c * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) sv[c] += sp[(w * 2 + c) * 64 + lane];
+    }
+    // epilogue: element (iter row i0 + 16c + 4g + r, owner row orow)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ir = i0 + c * 16 + 4 * g + r;
+        const float raw = sv[c][r];
+        const float x = CLIPV ? fminf(fmaxf(raw, 0.f), 1.f) : raw;
+        const float e = ir < ni ? __expf(gamma * (x - 1.f)) : 0.f;
+        if (MODE == 0) {
+          rsum += e;
+        } else {
+          const bool pass = !CLIPV || (raw >= 0.f && raw <= 1.f);
+          const float sc = MODE == 1 ? osc : (ir < ni ? scale[ir] : 0.f);
+          sv[c][r] = pass ? sc * e : 0.f;
+        }
+      }
+    if (MODE != 0) {
+      // G^T as the B operand of one k-step of 32 iter rows (k order 16 (j >> 2) + 4g + (j & 3))
+      u32x4 w4;
+      w4[0] = pack_bf16x2(sv[0][0], sv[0][1]);
+      w4[1] = pack_bf16x2(sv[0][2], sv[0][3]);
+      w4[2] = pack_bf16x2(sv[1][0], sv[1][1]);
+      w4[3] = pack_bf16x2(sv[1][2], sv[1][3]);
+      const bf16x8 gb = __builtin_bit_cast(bf16x8, w4);
+#pragma unroll
+      for (int i = 0; i < 2 * KS; ++i) {
+        // It^T fragment: A[m = d (dw + 16 i + lane & 15)][k = the permuted iter rows]
+        const unsigned short* p = it + (4 * g + ((lane & 15) >> 2)) * LDW + dw + i * 16 + 4 * (lane & 3);
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p + 16 * LDW));
+        const bf16x8 a = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, gb, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the tile and the partials are rewritten next iteration
+  }
+  if (MODE == 0) {
+    rsum += __shfl_xor(rsum, 16, 64);
+    rsum += __shfl_xor(rsum, 32, 64);
+    if (wave == 0 && g == 0 && orow < no) out[(size_t)split * no + orow] = rsum;
+    return;
+  }
+  if (orow >= no) return;
+  // acc[i] C layout: lane holds out^T[d = dw + 16 i + 4g + r][owner = orow]
+  float* dst = out + ((size_t)split * no + orow) * DP + dw;
+#pragma unroll
+  for (int i = 0; i < 2 * KS; ++i) *reinterpret_cast<f32x4*>(dst + i * 16 + 4 * g) = acc[i];
+}
+
+// tiles per split so that (owner blocks x splits) >= ~512 workgroups (2 per CU)
+inline void ibw_plan(int no, int ni, int& ns, int& per) {
+  const int ob = (no + 15) / 16, nt = (ni + IBW_T - 1) / IBW_T;
+  ns = std::max(1, std::min(nt, (512 + ob - 1) / ob));
+  per = (nt + ns - 1) / ns;
+  ns = (nt + per - 1) / per;
+}
+
 // Positive logit + one-hot gradient term; one wave per query row.
 // spos[i] = g*clip(qn_i . dn_pos), and when gscale != null:
 //   h = -gscale_i*g*clip'; dQ_i += h*dn_pos ; dD_pos += h*qn_i
@@ -725,9 +855,9 @@ __global__ __launch_bounds__(256) void ib_pos_kernel(const unsigned short* __res
   }
 }
 
-// Wide vectors (D > 192, e.g. BERT's 768): the flash kernels above keep a query row's D
-// accumulators in registers, which D = 768 does not fit, so the logits are tiled at the
-// GEMM level instead — S is produced one column block (B x Mb, bounded memory) at a time by
+// Wide vectors, fallback path (D > 192 that ibw_kernel does not cover, or PAGEVEC_IB_WIDE=0):
+// the narrow flash kernels keep a query row's D accumulators in registers, which D = 768 does
+// not fit, so the logits are tiled at the GEMM level instead — S is produced one column block (B x Mb, bounded memory) at a time by
 // a bf16 x bf16 -> fp32 library GEMM and never exists whole.  Per block, one wave per row:
 //  * forward (scale == nullptr): part[row] = sum_c exp(g * (clip(S_rc) - 1)) (the logits are
 //    shifted by the largest possible one, as in the flash kernels, so block partial sums
@@ -1071,5 +1201,66 @@ PV_API int pv_ib_grad_scale(const float* gl, int scalar, float invB, const float
   hipLaunchKernelGGL(pv::loss::ib_grad_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, gl, scalar, invB, sumexp, B, gamma, U, DP, dq, scale, grow);
   PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Wide-vector in-batch loss passes (ibw_kernel), DP % 128 == 0, 256 <= DP <= 1024.
+// mode 0: part (ns x no) row partial sums of exp(g (clip(S) - 1)), S = O . It^T;
+// mode 1 / 2: out (no x DP) fp32 = sum_j G . It_j with the scale indexed by the owner row (1) or
+// the iterated row (2); ws >= pv_ibw_ws(no, ni, DP) floats when ns > 1.  pv_ibw_splits -> ns.
+PV_API int pv_ibw_splits(int no, int ni) {
+  int ns, per;
+  pv::loss::ibw_plan(no, ni, ns, per);
+  return ns;
+}
+
+PV_API long pv_ibw_ws(int no, int ni, int DP) {
+  int ns, per;
+  pv::loss::ibw_plan(no, ni, ns, per);
+  return ns > 1 ? (long)ns * no * DP : 0;
+}
+
+PV_API int pv_ibw(const void* O, int no, const void* It, int ni, int DP, const float* scale, float gamma, int clip,
+                  int mode, float* out, float* ws, void* stream) {
+  using namespace pv::loss;
+  if (no <= 0 || ni <= 0 || DP % 128 || DP < 256 || DP > 1024 || mode < 0 || mode > 2) return -1;
+  if (mode > 0 && !scale) return -2;
+  int ns, per;
+  ibw_plan(no, ni, ns, per);
+  if (mode > 0 && ns > 1 && !ws) return -3;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((no + 15) / 16, ns);
+  float* dst = (mode == 0 || ns == 1) ? out : ws;
+  const size_t lds = (size_t)IBW_T * (DP + 8) * 2 + 4 * 2 * 64 * sizeof(f32x4);
+  const unsigned short* o16 = (const unsigned short*)O;
+  const unsigned short* i16 = (const unsigned short*)It;
+  bool done = false;
+#define PV_IBW(KSV, MODEV, CLIPV)                                                                          \
+  if (!done && DP == KSV * 128 && mode == MODEV && clip == CLIPV) {                                       \
+    static bool attr = false;                                                                              \
+    if (!attr) {                                                                                           \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&ibw_kernel<KSV, MODEV, CLIPV>),               \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)         \
+        return -5;                                                                                         \
+      attr = true;                                                                                         \
+    }                                                                                                      \
+    hipLaunchKernelGGL((ibw_kernel<KSV, MODEV, CLIPV>), grid, dim3(256), lds, s, o16, no, i16, ni, scale,  \
+                       gamma, dst, per);                                                                   \
+    done = true;                                                                                           \
+  }
+#define PV_IBW_KS(KSV) \
+  PV_IBW(KSV, 0, 0) PV_IBW(KSV, 0, 1) PV_IBW(KSV, 1, 0) PV_IBW(KSV, 1, 1) PV_IBW(KSV, 2, 0) PV_IBW(KSV, 2, 1)
+  PV_IBW_KS(2) PV_IBW_KS(3) PV_IBW_KS(4) PV_IBW_KS(6) PV_IBW_KS(8)
+#undef PV_IBW_KS
+#undef PV_IBW
+  if (!done) return -4;  // DP = 640, 896: no instantiation
+  PV_LAUNCH_CHECK();
+  if (mode > 0 && ns > 1) {
+    const long n4 = (long)no * DP / 4;
+    long blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(ib_split_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, out, n4, ns);
+    PV_LAUNCH_CHECK();
+  }
   return 0;
 }

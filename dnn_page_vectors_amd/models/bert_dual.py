@@ -56,8 +56,7 @@ class BertLayer(nn.Module):
         # output bias + hidden dropout fused into the residual add + LayerNorm (counter-hash
         # masks; the bias gradient is reduced in the LayerNorm backward)
         x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo, res=r1)
-        f = tops.bias_gelu(tops.linear(x, self.w1, res=r2), self.b1)
-        f2 = tops.linear(f, self.w2)
+        f2 = tops.ffn(x, self.w1, self.b1, self.w2, res=r2)  # GELU in the GEMM epilogues
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
                                   bias=self.b2, res=r2)
 
@@ -72,8 +71,7 @@ class BertLayer(nn.Module):
         a = tops.packed_attention(qkv, masks, shapes, self.heads)
         o = tops.linear(a, self.wo)
         x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo, res=r1)
-        f = tops.bias_gelu(tops.linear(x, self.w1, res=r2), self.b1)
-        f2 = tops.linear(f, self.w2)
+        f2 = tops.ffn(x, self.w1, self.b1, self.w2, res=r2)  # GELU in the GEMM epilogues
         return tops.add_layernorm(f2, x, self.ln2_g, self.ln2_b, p=p, seed=(seed + 0x5BD1E995) & 0xFFFFFFFF,
                                   bias=self.b2, res=r2)
 

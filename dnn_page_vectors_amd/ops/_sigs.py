@@ -94,6 +94,14 @@ SIGS = {
     "pv_layernorm_bwd_ws": "ii",
     "pv_layernorm_bwd": "ppppppppp" "ii" "p",
     "pv_bias_gelu_fwd": "ppp" "li" "p",
+    # lt_gemm.hip (hipBLASLt with fused epilogues)
+    "pv_lt_gemm": "ii" "iii" "pi" "pi" "pi" "i" "f" "pi" "p" "i" "pl" "p",
+    "pv_lt_set_tune": "i",
+    "pv_transpose_u8": "pl" "ii" "pl" "p",
+    # loss.hip wide-vector (D = 768) flash passes
+    "pv_ibw_splits": "ii",
+    "pv_ibw_ws": "iii",
+    "pv_ibw": "pi" "pi" "i" "p" "f" "i" "i" "pp" "p",
     "pv_bias_gelu_bwd": "pppppp" "ii" "p",
     "pv_bias_gelu_bwd_ws": "ii",
     "pv_softmax_fwd": "pp" "liif" "p",
@@ -130,7 +138,8 @@ SIGS = {
 }
 
 _RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,
-            "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long}
+            "pv_bias_gelu_bwd_ws": ctypes.c_long, "pv_layernorm_bwd_ws": ctypes.c_long,
+            "pv_ibw_ws": ctypes.c_long}
 
 
 def declare(lib) -> None:

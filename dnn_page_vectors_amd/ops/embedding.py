@@ -144,6 +144,9 @@ SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
 _BAG_SPLITK = int(os.environ.get("PAGEVEC_BAG_SPLITK", "0"))  # override of the vocabulary split (A/B)
 BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
 FP8_BAG = os.environ.get("PAGEVEC_FP8_BAG", "1") != "0"  # 0: fp8 towers keep the bf16 counts GEMM (A/B)
+# fp8 bag weight gradient: C^T G on the MX fp8 MFMA too (e4m3 counts transposed, G per-tensor
+# scaled e4m3) instead of the exact bf16 counts + hipBLASLt
+FP8_BWD = os.environ.get("PAGEVEC_FP8_BWD", "1") != "0"
 
 
 _BAG_ACT = {"none": 0, "relu": 1, "tanh": 3}
@@ -187,10 +190,14 @@ class _BagFn(torch.autograd.Function):
 
             W8t, amax = w8
             want = ctx.needs_input_grad[1]
-            use_rle = want and _rle_ok(N, L, V, E)
-            C8, C, lens = _counts8(ids, V, pad, want and not use_rle)
+            fp8_bwd = want and FP8_BWD and E % 4 == 0
+            use_rle = want and not fp8_bwd and _rle_ok(N, L, V, E)
+            C8, C, lens = _counts8(ids, V, pad, want and not use_rle and not fp8_bwd)
             if use_rle:  # the weight gradient's counts as segment lists (bag_gemm.hip), not bf16 C
                 rle = _Rle(ids, V, pad)
+            if fp8_bwd:  # the e4m3 counts serve the weight gradient too (no bf16 N x V matrix)
+                C = C8
+                ctx.fp8_bwd = True
             part = fops.gemm_mx8(C8, W8t, 1.0 / fops.FP8_MAX, amax)
             if part.dim() == 2:
                 part = part.unsqueeze(0)
@@ -272,7 +279,8 @@ def _counts_backward(ctx, g, C, lens, y, rle=None):
     W, V, bias = ctx.W, ctx.V, ctx.bias
     N, E = g.shape
     want_db = bias is not None and ctx.needs_input_grad[6]
-    dz = torch.empty_like(g) if want_db else None
+    fp8_bwd = getattr(ctx, "fp8_bwd", False)
+    dz = torch.empty_like(g) if want_db or fp8_bwd else None
     gs = torch.empty(N, E, dtype=torch.bfloat16, device=g.device)
     check(lib().pv_act_bwd_rowscale(P(y), P(g), P(dz), P(gs), P(lens) if ctx.mean else None, E, g.numel(),
                                     _BAG_ACT[ctx.act] if y is not None else 0, stream(g.device)),
@@ -286,6 +294,14 @@ def _counts_backward(ctx, g, C, lens, y, rle=None):
             db = None
         elif db.dtype != bias.dtype:
             db = db.to(bias.dtype)
+    if fp8_bwd:  # e4m3 C^T x e4m3 G on the MX fp8 MFMA
+        tw = grad_sink.write_target(W)
+        dW = tw if tw is not None else torch.empty(V, E, dtype=torch.float32, device=g.device)
+        _fp8_weight_grad(C, dz, V, dW, lens if ctx.mean else None)
+        if tw is not None:
+            grad_sink.done(W)
+            dW = None
+        return None, dW, None, None, None, None, db, None, None
     if rle is not None:  # bag_gemm.hip weight gradient: count tiles built in LDS, dW rows stored
         tw = grad_sink.write_target(W)
         if tw is not None:
@@ -305,6 +321,24 @@ def _counts_backward(ctx, g, C, lens, y, rle=None):
         grad_sink.done(W)
         return None, None, None, None, None, None, db, None, None
     return None, (Ct @ gs).float(), None, None, None, None, db, None, None
+
+
+def _fp8_weight_grad(C8, dz, V, out, lens=None):
+    """out (V, E) fp32 = C8[:, :V]^T (dz / len) on the MX fp8 MFMA: the counts (exact e4m3 up to
+    16, the forward's own operand) transposed to K(page)-contiguous rows, the row-scaled fp32
+    gradient quantised per tensor to e4m3 and transposed, one gemm_mx8 with the dequant scale
+    amax_g / 448 in its epilogue.  Reference: the exact bf16 C^T G of _counts_backward."""
+    from . import fp8 as fops
+
+    N, E = dz.shape
+    dev = dz.device
+    gs32 = dz / lens.clamp(min=1.0)[:, None] if lens is not None else dz
+    Np = -(-N // fops.MX_BK) * fops.MX_BK
+    g8t, amax_g = fops.quantize_t(gs32, Np)           # (E, Np) e4m3, scale 448 / amax_g
+    ct = torch.empty(V, Np, dtype=torch.uint8, device=dev)
+    check(lib().pv_transpose_u8(P(C8), C8.stride(0), N, V, P(ct), Np, stream(dev)), "pv_transpose_u8")
+    check(lib().pv_gemm_mx8(P(ct), Np, P(g8t), Np, P(out), out.stride(0), V, E, Np, 1, 0, None,
+                            1.0 / fops.FP8_MAX, P(amax_g), 0, 0, stream(dev)), "pv_gemm_mx8(wgrad)")
 
 
 def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor] = None, pad: int = 0,

@@ -194,8 +194,11 @@ def _col_blocks(B: int, M: int):
 
 
 class _InBatchRowsFn(torch.autograd.Function):
-    """Wide vectors (D > 192, e.g. BERT's 768; the flash kernels hold D accumulators per query
-    row in registers): the logits are tiled over page-column blocks at the GEMM level — each
+    """Wide vectors (D > 192, e.g. BERT's 768; the narrow flash kernels hold D accumulators per
+    query row in registers).  Default: the wide flash kernel (loss.hip::ibw_kernel, _wide_ok):
+    S reduced over D across a workgroup's 4 waves, the gradient products on the same tile, no
+    S block in HBM and no library GEMM.  Fallback (other D, PAGEVEC_IB_WIDE=0): the logits are
+    tiled over page-column blocks at the GEMM level — each
     (B x Mb) block of S comes from a bf16 x bf16 -> fp32 library GEMM, is reduced by
     loss.hip::ib_rows_blk_kernel and dropped, so memory stays O(B * Mb) for any M; the
     backward recomputes each block (flash-style) and turns it into the block's dS in place.
@@ -235,12 +238,41 @@ class _InBatchRowsFn(torch.autograd.Function):
         return dq[:, :D], dd[:, :D], None, None, None, None
 
 
+# Wide vectors on the flash kernel (loss.hip::ibw_kernel, DP % 128 == 0, 256..1024): no S block
+# in HBM, no library GEMM; "0" = the column-block path below (fp32 S blocks + hipBLASLt)
+IB_WIDE = os.environ.get("PAGEVEC_IB_WIDE", "1") != "0"
+
+
+def _wide_ok(DP: int) -> bool:
+    return IB_WIDE and DP % 128 == 0 and 256 <= DP <= 1024 and DP not in (640, 896)
+
+
+def _ibw(o, it, DP, scale, gamma, clip, mode, out):
+    """loss.hip::pv_ibw: mode 0 row partial sums of o against it -> (splits, no) part; 1 / 2:
+    out (no, DP) fp32 = the G-weighted sums of it rows (scale by o row / by it row)."""
+    no, ni = o.shape[0], it.shape[0]
+    L_ = lib()
+    ws_n = L_.pv_ibw_ws(no, ni, DP) if mode else 0
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=o.device) if ws_n else None
+    check(L_.pv_ibw(P(o), no, P(it), ni, DP, P(scale), float(gamma), int(clip), mode, P(out), P(ws),
+                    stream(o.device)), f"pv_ibw(mode {mode})")
+    return out
+
+
 def _rows_forward(qb, db, pos, B, M, DP, gamma, clip):
     """Wide-vector forward over page-column blocks -> (per-row loss, P+, sumexp)."""
     dev, s, L_ = qb.device, stream(qb.device), lib()
     spos = torch.empty(B, dtype=torch.float32, device=dev)
     check(L_.pv_ib_pos(P(qb), P(db), P(pos), P(spos), None, None, None, B, DP, float(gamma), int(clip), s),
           "pv_ib_pos")
+    if _wide_ok(DP):
+        ns = int(L_.pv_ibw_splits(B, M))
+        part = _ibw(qb, db, DP, None, gamma, clip, 0, torch.empty(ns, B, dtype=torch.float32, device=dev))
+        sumexp = torch.empty(B, dtype=torch.float32, device=dev)
+        loss = torch.empty(B, dtype=torch.float32, device=dev)
+        prob = torch.empty(B, dtype=torch.float32, device=dev)
+        check(L_.pv_ib_rowsum(P(part), P(sumexp), B, ns, P(spos), P(loss), P(prob), float(gamma), s), "pv_ib_rowsum")
+        return loss, prob, sumexp
     blocks = _col_blocks(B, M)
     part = torch.empty(len(blocks), B, dtype=torch.float32, device=dev)
     for k, (c0, c1) in enumerate(blocks):
@@ -261,6 +293,13 @@ def _rows_backward(xb, yb, scale, gamma, clip, dq=None, dd=None):
     accumulated), dd[block] = dS^T xb (columns' gradient, written)."""
     R, C = xb.shape[0], yb.shape[0]
     s, L_ = stream(xb.device), lib()
+    DP = xb.shape[1]
+    if _wide_ok(DP):  # flash passes: dq rows own, walk the columns; dd columns own, walk the rows
+        if dq is not None:  # written, not accumulated: every caller passes a zeroed dq
+            _ibw(xb, yb, DP, scale, gamma, clip, 1, dq)
+        if dd is not None:
+            _ibw(yb, xb, DP, scale, gamma, clip, 2, dd)
+        return
     for c0, c1 in _col_blocks(R, C):
         S = torch.mm(xb, yb[c0:c1].t(), out_dtype=torch.float32)
         check(L_.pv_ib_rows_blk(P(S), c1 - c0, R, c1 - c0, P(scale), None, float(gamma), int(clip), s),

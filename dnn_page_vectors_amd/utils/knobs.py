@@ -41,10 +41,16 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_BAG_SPARSE_BWD": ("ab", "1", "short-bag backward by sorted token runs"),
     "PAGEVEC_BAG_COUNTS16": ("ab", "1", "16-bit packed LDS counts histogram"),
     "PAGEVEC_BAG_GEMM": ("ab", "lib", "long-bag GEMMs: hipBLASLt on the count matrix (lib) or bag_gemm.hip (hip)"),
+    "PAGEVEC_FP8_BAG": ("ab", "1", "fp8 towers: page bag on the MX fp8 MFMA"),
+    "PAGEVEC_FP8_BWD": ("ab", "1", "fp8 towers: bag weight gradient on the MX fp8 MFMA (e4m3 counts^T x e4m3 G)"),
+    "PAGEVEC_LT_TUNE": ("ab", "0", "time hipBLASLt's top candidates once per problem (lt_gemm.hip)"),
+    "PAGEVEC_LINEAR_LT": ("ab", "0", "BERT linear layers on lt_gemm.hip instead of torch mm / addmm"),
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),
+    "PAGEVEC_FFN_LT": ("ab", "1", "BERT FFN bias + GELU (and its backward) in hipBLASLt GEMM epilogues"),
     "PAGEVEC_IB": ("ab", "5", "in-batch loss kernel generation"),
+    "PAGEVEC_IB_WIDE": ("ab", "1", "wide-vector (D = 768) loss on the ibw flash kernel (0: fp32 S blocks + GEMMs)"),
     "PAGEVEC_IB_ROWS_BLOCK": ("ab", str(1 << 25), "wide-vector loss column block (elements)"),
     "PAGEVEC_NO_MIRROR": ("ab", "0", "no bf16 mirror written by the Adam kernel"),
     "PAGEVEC_QUERY_FIRST": ("ab", "0", "query tower before the page tower on one rank"),

@@ -117,6 +117,7 @@ def test_chunked_fp8_bag_backward_uses_segment_lists(monkeypatch):
     """Config 5's fp8 bag keeps the MX fp8 forward; its weight gradient now comes from the
     segment lists (no bf16 count matrix): equal to the library arm's exact C^T G."""
     V, N, L, E = 30000, 256, 512, 512
+    monkeypatch.setattr(eops, "FP8_BWD", False)
     ids = _ids(N, L, V, seed=4)
     W0 = torch.randn(V, E, device=DEV).bfloat16().float() * 0.1
     gy = torch.randn(N, E, device=DEV)
@@ -140,3 +141,41 @@ def test_chunked_fp8_bag_backward_uses_segment_lists(monkeypatch):
     err_lib = float((grads["lib"].double() - want).abs().max()) / scale
     # fp32 output here; the library arm of this path returns the bf16 GEMM result (2^-8)
     assert err_hip < 1e-5 and err_lib < 8e-3, (err_hip, err_lib)
+
+
+@pytest.mark.parametrize("N,L", [(256, 512), (4096, 512), (300, 700)])
+def test_chunked_fp8_bag_backward_on_mx_fp8(N, L, monkeypatch):
+    """PAGEVEC_FP8_BWD (config 5 default): the bag weight gradient as e4m3 counts^T x e4m3
+    (per-tensor scaled) dz / len on the MX fp8 MFMA, against an fp64 reference of exactly that
+    quantised product (emulate_e4m3 = the device's RNE saturating conversion), and within fp8
+    rounding of the exact gradient."""
+    from dnn_page_vectors_amd.ops import fp8 as fops
+
+    V, E = 30000, 512
+    monkeypatch.setattr(eops, "FP8_BWD", True)
+    ids = _ids(N, L, V, seed=N + L)
+    W0 = torch.randn(V, E, device=DEV).bfloat16().float() * 0.1
+    b0 = torch.randn(E, device=DEV) * 0.1
+    gy = torch.randn(N, E, device=DEV)
+    W = W0.clone().requires_grad_(True)
+    b = b0.clone().requires_grad_(True)
+    y = eops.embedding_bag(ids, W, pad=0, mean=True, plan="counts", act="tanh", fp8=True, bias=b)
+    (y * gy).sum().backward()
+    C = _dense_counts(ids, V)
+    lens = C.sum(1, keepdim=True).clamp(min=1)
+    yd = y.detach().double()
+    dz = gy.double() * (1 - yd * yd)
+    gs = (gy * (1 - y.detach() * y.detach())) / lens.float()  # fp32, as on the device
+    amax = float(gs.abs().max())
+    g8 = fops.emulate_e4m3(gs * (448.0 / amax)).double() * (amax / 448.0)
+    c8 = fops.emulate_e4m3(C.float()).double()
+    want = c8.t() @ g8
+    scale = float(want.abs().max())
+    err = float((W.grad.double() - want).abs().max()) / scale
+    # fp32 summation order + the odd e4m3 rounding tie of dz computed with / without an FMA
+    assert err < 3e-3, err
+    # within fp8 rounding of the exact gradient; counts above 448 saturate in e4m3 (as in the
+    # forward: _ids' page 0 repeats one token L - L // 5 times), so that reference clamps them
+    exact = C.clamp(max=448.0).t() @ (dz / lens)
+    assert float((W.grad.double() - exact).abs().max()) / float(exact.abs().max()) < 0.08
+    torch.testing.assert_close(b.grad.double(), dz.sum(0), rtol=1e-4, atol=1e-4)

@@ -654,14 +654,21 @@ def test_big_model_train_steps_gpu(preset):
     assert losses[-1] < 0.7 * losses[0], losses
 
 
-@pytest.mark.parametrize("B,M,clip,block", [(40, 160, False, 1 << 25), (40, 1000, True, 40 * 256),
-                                            (300, 3000, False, 300 * 700), (64, 5000, True, 64 * 256)])
-def test_inbatch_loss_wide_rows_path(B, M, clip, block, monkeypatch):
-    """D = 768 (BERT): logits tiled over page-column blocks at the GEMM level (one block, or
-    several with a partial last one), never materialised whole."""
-    monkeypatch.setattr(lops, "ROWS_BLOCK_ELEMS", block)
+@pytest.mark.parametrize("B,M,clip,block,wide,D", [(40, 160, False, 1 << 25, 0, 768), (40, 1000, True, 40 * 256, 0, 768),
+                                                   (300, 3000, False, 300 * 700, 0, 768),
+                                                   (64, 5000, True, 64 * 256, 0, 768),
+                                                   (40, 160, False, 1 << 25, 1, 768), (40, 1000, True, 0, 1, 768),
+                                                   (300, 3000, False, 0, 1, 768), (256, 2048, True, 0, 1, 768),
+                                                   (33, 77, False, 0, 1, 256), (70, 300, True, 0, 1, 1024),
+                                                   (50, 500, False, 0, 1, 384)])
+def test_inbatch_loss_wide_rows_path(B, M, clip, block, wide, D, monkeypatch):
+    """D = 768 (BERT): wide = 1, the flash kernels (loss.hip::ibw_kernel: S reduced over D
+    across the workgroup's waves, never in HBM, no library GEMM); wide = 0, logits tiled over
+    page-column blocks at the GEMM level (one block, or several with a partial last one)."""
+    monkeypatch.setattr(lops, "IB_WIDE", bool(wide))
+    if not wide:
+        monkeypatch.setattr(lops, "ROWS_BLOCK_ELEMS", block)
     torch.manual_seed(4)
-    D = 768
     qn = torch.randn(B, D, device=DEV)
     dn = torch.randn(M, D, device=DEV)
     pos = (torch.arange(B, device=DEV, dtype=torch.int32) * 3) % M
@@ -670,7 +677,10 @@ def test_inbatch_loss_wide_rows_path(B, M, clip, block, monkeypatch):
         qn, dn = qn.abs(), dn.abs()
     qn = bf(ref.l2_normalize(qn)).requires_grad_(True)
     dn = bf(ref.l2_normalize(dn)).requires_grad_(True)
-    assert len(lops._col_blocks(B, M)) == (1 if block >= B * M else -(-M // max(256, block // B)))
+    if not wide:
+        assert len(lops._col_blocks(B, M)) == (1 if block >= B * M else -(-M // max(256, block // B)))
+    else:
+        assert lops._wide_ok(D)
     loss, _ = lops.inbatch_loss(qn, dn, pos, 10.0, clip)
     q2, d2 = qn.detach().clone().requires_grad_(True), dn.detach().clone().requires_grad_(True)
     lr, _ = ref.inbatch_softmax_loss(q2, d2, pos, 10.0, clip)
