@@ -93,28 +93,37 @@ __device__ __forceinline__ void pack_b(const f32x4 (&x)[4], bf16x8 (&b)[2]) {
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 // ---------------------------------------------------------------------------- forward
-// grid (ceil(L/64), H, N), 256 threads; wave w owns queries q0 + 16w .. +15
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const unsigned short* __restrict__ qkv,
-                                                          const int* __restrict__ mask,
-                                                          unsigned short* __restrict__ out, float* __restrict__ lse,
-                                                          int L, int H, float scale) {
+// QG = 16-query groups per wave: every staged K / V fragment feeds QG MFMAs (LDS reads and
+// tile stores per FLOP / QG).  grid (ceil(L / (64 QG)), H, N), 256 threads; wave w owns
+// queries q0 + 16 (w QG + j) .. +15, j < QG.
+template <int QG>
+__global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_fwd_kernel(const unsigned short* __restrict__ qkv,
+                                                                        const int* __restrict__ mask,
+                                                                        unsigned short* __restrict__ out,
+                                                                        float* __restrict__ lse, int L, int H,
+                                                                        float scale) {
   __shared__ __attribute__((aligned(16))) unsigned short kt[2][TB * LDT];
   __shared__ __attribute__((aligned(16))) unsigned short vt[2][TB * LDT];
   __shared__ float mk[2][TB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int n = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TB + wave * 16;
+  const int n = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TB * QG + wave * 16 * QG;
   const size_t ld = (size_t)3 * H * HD;
   const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
   const unsigned short* K = Q + (size_t)H * HD;
   const unsigned short* V = Q + (size_t)2 * H * HD;
   const int* mrow = mask ? mask + (size_t)n * L : nullptr;
   const float sl = scale * LOG2E;
-  bf16x8 qb[2];
-  glob_frag(Q, ld, q0 + (lane & 15), L, qb);
-  f32x4 o[4];
+  bf16x8 qb[QG][2];
+  f32x4 o[QG][4];
+  float m[QG], l[QG];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < QG; ++j) {
+    glob_frag(Q, ld, q0 + 16 * j + (lane & 15), L, qb[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
   u32x4 sk[2], sv[2];
   float smk = 0.f;
   load_tile(K, ld, 0, L, sk);
@@ -135,45 +144,57 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const unsigned short* 
         smk = (kk < L && (!mrow || mrow[kk])) ? 1.f : 0.f;
       }
     }
-    // S^T (keys x queries), 4 key subtiles
-    f32x4 s[4];
+    // S^T (keys x queries), 4 key subtiles per query group; one K fragment read per QG MFMAs
+    f32x4 s[QG][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      s[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int st = 0; st < 2; ++st) s[c] = MFMA(row_frag(kt[buf], c * 16, st), qb[st], s[c]);
+      for (int j = 0; j < QG; ++j) s[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 a = row_frag(kt[buf], c * 16, st);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) s[j][c] = MFMA(a, qb[j][st], s[j][c]);
+      }
     }
-    float bm = -INFINITY;
+    bf16x8 pb[QG][2];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int j = 0; j < QG; ++j) {
+      float bm = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float keep = mk[buf][c * 16 + 4 * g + r];
-        s[c][r] = keep != 0.f ? s[c][r] * sl : -INFINITY;
-        bm = fmaxf(bm, s[c][r]);
-      }
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    const float mn = fmaxf(m, bm);
-    const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m - mn);
-    m = mn;
-    l *= corr;
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] *= corr;
+        for (int r = 0; r < 4; ++r) {
+          const float keep = mk[buf][c * 16 + 4 * g + r];
+          s[j][c][r] = keep != 0.f ? s[j][c][r] * sl : -INFINITY;
+          bm = fmaxf(bm, s[j][c][r]);
+        }
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m[j], bm);
+      const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m[j] - mn);
+      m[j] = mn;
+      l[j] *= corr;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int i = 0; i < 4; ++i) o[j][i] *= corr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = s[c][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[c][r] - mn);
-        s[c][r] = pv;
-        l += pv;
-      }
-    bf16x8 pb[2];
-    pack_b(s, pb);
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = s[j][c][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[j][c][r] - mn);
+          s[j][c][r] = pv;
+          l[j] += pv;
+        }
+      pack_b(s[j], pb[j]);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = MFMA(tr_frag(vt[buf], s2, i * 16), pb[s2], o[i]);
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 a = tr_frag(vt[buf], s2, i * 16);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) o[j][i] = MFMA(a, pb[j][s2], o[j][i]);
+      }
     if (more) {
       store_tile(kt[buf ^ 1], sk);
       store_tile(vt[buf ^ 1], sv);
@@ -181,17 +202,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const unsigned short* 
     }
     __syncthreads();
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  const int q = q0 + (lane & 15);
-  if (q < L) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    unsigned short* orow = out + ((size_t)n * L + q) * H * HD + (size_t)h * HD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<uint2*>(orow + i * 16 + 4 * g) =
-          uint2{pack_bf16x2(o[i][0] * inv, o[i][1] * inv), pack_bf16x2(o[i][2] * inv, o[i][3] * inv)};
-    if (g == 0) lse[((size_t)n * H + h) * L + q] = m + __log2f(l);  // log2 domain, includes scale
+  for (int j = 0; j < QG; ++j) {
+    float lj = l[j];
+    lj += __shfl_xor(lj, 16, 64);
+    lj += __shfl_xor(lj, 32, 64);
+    const int q = q0 + 16 * j + (lane & 15);
+    if (q < L) {
+      const float inv = lj > 0.f ? 1.f / lj : 0.f;
+      unsigned short* orow = out + ((size_t)n * L + q) * H * HD + (size_t)h * HD;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint2*>(orow + i * 16 + 4 * g) =
+            uint2{pack_bf16x2(o[j][i][0] * inv, o[j][i][1] * inv), pack_bf16x2(o[j][i][2] * inv, o[j][i][3] * inv)};
+      if (g == 0) lse[((size_t)n * H + h) * L + q] = m[j] + __log2f(lj);  // log2 domain, includes scale
+    }
   }
 }
 
@@ -247,8 +272,10 @@ __global__ __launch_bounds__(256) void attn_bwd_prep4_kernel(const unsigned shor
   }
 }
 
-// grid (ceil(L/64) key blocks, H, N); wave w owns keys k0 + 16w .. +15 (lane column)
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned short* __restrict__ qkv,
+// grid (ceil(L / (64 QG)) key blocks, H, N); wave w owns keys kw + 16 j .. +15 (lane column),
+// kw = block + 16 QG w, j < QG
+template <int QG>
+__global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dkdv_kernel(const unsigned short* __restrict__ qkv,
                                                                const int* __restrict__ mask,
                                                                const unsigned short* __restrict__ dout,
                                                                const float* __restrict__ lse,
@@ -259,7 +286,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned sh
   __shared__ __attribute__((aligned(16))) unsigned short dt[2][TB * LDT];
   __shared__ float sl_[2][TB], sd_[2][TB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int n = blockIdx.z, h = blockIdx.y, kw = blockIdx.x * TB + wave * 16;
+  const int n = blockIdx.z, h = blockIdx.y, kw = blockIdx.x * TB * QG + wave * 16 * QG;
   const size_t ld = (size_t)3 * H * HD, ldo = (size_t)H * HD;
   const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
   const unsigned short* K = Q + (size_t)H * HD;
@@ -267,15 +294,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned sh
   const unsigned short* dO = dout + (size_t)n * L * ldo + (size_t)h * HD;
   const float* LS = lse + ((size_t)n * H + h) * L;
   const float* DD = Dv + ((size_t)n * H + h) * L;
-  const int key = kw + (lane & 15);
-  const bool kvalid = key < L && (!mask || mask[(size_t)n * L + key]);
   const float sl = scale * LOG2E;
-  bf16x8 kb[2], vb[2];
-  glob_frag(K, ld, key, L, kb);
-  glob_frag(V, ld, key, L, vb);
-  f32x4 dk[4], dv[4];
+  bf16x8 kb[QG][2], vb[QG][2];
+  bool kvalid[QG];
+  f32x4 dk[QG][4], dv[QG][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < QG; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+    kvalid[j] = key < L && (!mask || mask[(size_t)n * L + key]);
+    glob_frag(K, ld, key, L, kb[j]);
+    glob_frag(V, ld, key, L, vb[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dk[j][i] = dv[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   u32x4 sq[2], sdo[2];
   float slv = 0.f, sdv = 0.f;
   load_tile(Q, ld, 0, L, sq);
@@ -304,35 +335,49 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned sh
       }
     }
     // S (queries x keys) and dP = dO . V^T, 4 query subtiles: rows q = c*16 + 4g + r, col = key
-    f32x4 p[4], dp[4];
+    f32x4 p[QG][4], dp[QG][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      p[c] = dp[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < QG; ++j) p[j][c] = dp[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        p[c] = MFMA(row_frag(qt[buf], c * 16, st), kb[st], p[c]);
-        dp[c] = MFMA(row_frag(dt[buf], c * 16, st), vb[st], dp[c]);
+        const bf16x8 aq = row_frag(qt[buf], c * 16, st);
+        const bf16x8 ad = row_frag(dt[buf], c * 16, st);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) {
+          p[j][c] = MFMA(aq, kb[j][st], p[j][c]);
+          dp[j][c] = MFMA(ad, vb[j][st], dp[j][c]);
+        }
       }
     }
+    bf16x8 pb[QG][2], db[QG][2];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int j = 0; j < QG; ++j) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qi = c * 16 + 4 * g + r;
-        const bool ok = kvalid && q0 + qi < L;
-        const float pv = ok ? __builtin_amdgcn_exp2f(p[c][r] * sl - sl_[buf][qi]) : 0.f;
-        p[c][r] = pv;
-        dp[c][r] = pv * (dp[c][r] - sd_[buf][qi]);  // dS (without the softmax scale)
-      }
-    bf16x8 pb[2], db[2];
-    pack_b(p, pb);
-    pack_b(dp, db);
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = c * 16 + 4 * g + r;
+          const bool ok = kvalid[j] && q0 + qi < L;
+          const float pv = ok ? __builtin_amdgcn_exp2f(p[j][c][r] * sl - sl_[buf][qi]) : 0.f;
+          p[j][c][r] = pv;
+          dp[j][c][r] = pv * (dp[j][c][r] - sd_[buf][qi]);  // dS (without the softmax scale)
+        }
+      pack_b(p[j], pb[j]);
+      pack_b(dp[j], db[j]);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        dv[i] = MFMA(tr_frag(dt[buf], s2, i * 16), pb[s2], dv[i]);
-        dk[i] = MFMA(tr_frag(qt[buf], s2, i * 16), db[s2], dk[i]);
+        const bf16x8 ad = tr_frag(dt[buf], s2, i * 16);
+        const bf16x8 aq = tr_frag(qt[buf], s2, i * 16);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) {
+          dv[j][i] = MFMA(ad, pb[j][s2], dv[j][i]);
+          dk[j][i] = MFMA(aq, db[j][s2], dk[j][i]);
+        }
       }
     if (more) {
       store_tile(qt[buf ^ 1], sq);
@@ -344,20 +389,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const unsigned sh
     }
     __syncthreads();
   }
-  if (key < L) {
-    unsigned short* row = dqkv + ((size_t)n * L + key) * ld + (size_t)h * HD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint2*>(row + (size_t)H * HD + i * 16 + 4 * g) =
-          uint2{pack_bf16x2(dk[i][0] * scale, dk[i][1] * scale), pack_bf16x2(dk[i][2] * scale, dk[i][3] * scale)};
-      *reinterpret_cast<uint2*>(row + (size_t)2 * H * HD + i * 16 + 4 * g) =
-          uint2{pack_bf16x2(dv[i][0], dv[i][1]), pack_bf16x2(dv[i][2], dv[i][3])};
+  for (int j = 0; j < QG; ++j) {
+    const int key = kw + 16 * j + (lane & 15);
+    if (key < L) {
+      unsigned short* row = dqkv + ((size_t)n * L + key) * ld + (size_t)h * HD;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        *reinterpret_cast<uint2*>(row + (size_t)H * HD + i * 16 + 4 * g) =
+            uint2{pack_bf16x2(dk[j][i][0] * scale, dk[j][i][1] * scale),
+                  pack_bf16x2(dk[j][i][2] * scale, dk[j][i][3] * scale)};
+        *reinterpret_cast<uint2*>(row + (size_t)2 * H * HD + i * 16 + 4 * g) =
+            uint2{pack_bf16x2(dv[j][i][0], dv[j][i][1]), pack_bf16x2(dv[j][i][2], dv[j][i][3])};
+      }
     }
   }
 }
 
-// grid (ceil(L/64) query blocks, H, N); wave w owns queries q0 + 16w .. +15
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned short* __restrict__ qkv,
+// grid (ceil(L / (64 QG)) query blocks, H, N); wave w owns queries qw + 16 j .. +15, j < QG
+template <int QG>
+__global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dq_kernel(const unsigned short* __restrict__ qkv,
                                                              const int* __restrict__ mask,
                                                              const unsigned short* __restrict__ dout,
                                                              const float* __restrict__ lse,
@@ -368,7 +419,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned shor
   __shared__ __attribute__((aligned(16))) unsigned short vt[2][TB * LDT];
   __shared__ float mk[2][TB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int n = blockIdx.z, h = blockIdx.y, q = blockIdx.x * TB + wave * 16 + (lane & 15);
+  const int n = blockIdx.z, h = blockIdx.y, qw = blockIdx.x * TB * QG + wave * 16 * QG;
   const size_t ld = (size_t)3 * H * HD, ldo = (size_t)H * HD;
   const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
   const unsigned short* K = Q + (size_t)H * HD;
@@ -376,14 +427,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned shor
   const unsigned short* dO = dout + (size_t)n * L * ldo + (size_t)h * HD;
   const int* mrow = mask ? mask + (size_t)n * L : nullptr;
   const float sl = scale * LOG2E;
-  const float lq = q < L ? lse[((size_t)n * H + h) * L + q] : 0.f;
-  const float dq_ = q < L ? Dv[((size_t)n * H + h) * L + q] : 0.f;
-  bf16x8 qb[2], ob[2];
-  glob_frag(Q, ld, q, L, qb);
-  glob_frag(dO, ldo, q, L, ob);
-  f32x4 acc[4];
+  float lq[QG], dq_[QG];
+  bf16x8 qb[QG][2], ob[QG][2];
+  f32x4 acc[QG][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < QG; ++j) {
+    const int q = qw + 16 * j + (lane & 15);
+    lq[j] = q < L ? lse[((size_t)n * H + h) * L + q] : 0.f;
+    dq_[j] = q < L ? Dv[((size_t)n * H + h) * L + q] : 0.f;
+    glob_frag(Q, ld, q, L, qb[j]);
+    glob_frag(dO, ldo, q, L, ob[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   u32x4 sk[2], sv[2];
   float smk = 0.f;
   load_tile(K, ld, 0, L, sk);
@@ -404,30 +460,43 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned shor
         smk = (kk < L && (!mrow || mrow[kk])) ? 1.f : 0.f;
       }
     }
-    f32x4 s[4], dp[4];
+    f32x4 s[QG][4], dp[QG][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      s[c] = dp[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < QG; ++j) s[j][c] = dp[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        s[c] = MFMA(row_frag(kt[buf], c * 16, st), qb[st], s[c]);
-        dp[c] = MFMA(row_frag(vt[buf], c * 16, st), ob[st], dp[c]);
+        const bf16x8 ak = row_frag(kt[buf], c * 16, st);
+        const bf16x8 av = row_frag(vt[buf], c * 16, st);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) {
+          s[j][c] = MFMA(ak, qb[j][st], s[j][c]);
+          dp[j][c] = MFMA(av, ob[j][st], dp[j][c]);
+        }
       }
     }
+    bf16x8 db[QG][2];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int j = 0; j < QG; ++j) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float keep = mk[buf][c * 16 + 4 * g + r];
-        const float pv = keep != 0.f ? __builtin_amdgcn_exp2f(s[c][r] * sl - lq) : 0.f;
-        s[c][r] = pv * (dp[c][r] - dq_);  // dS^T
-      }
-    bf16x8 db[2];
-    pack_b(s, db);
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float keep = mk[buf][c * 16 + 4 * g + r];
+          const float pv = keep != 0.f ? __builtin_amdgcn_exp2f(s[j][c][r] * sl - lq[j]) : 0.f;
+          s[j][c][r] = pv * (dp[j][c][r] - dq_[j]);  // dS^T
+        }
+      pack_b(s[j], db[j]);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = MFMA(tr_frag(kt[buf], s2, i * 16), db[s2], acc[i]);
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 a = tr_frag(kt[buf], s2, i * 16);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) acc[j][i] = MFMA(a, db[j][s2], acc[j][i]);
+      }
     if (more) {
       store_tile(kt[buf ^ 1], sk);
       store_tile(vt[buf ^ 1], sv);
@@ -435,12 +504,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned shor
     }
     __syncthreads();
   }
-  if (q < L) {
-    unsigned short* row = dqkv + ((size_t)n * L + q) * ld + (size_t)h * HD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<uint2*>(row + i * 16 + 4 * g) =
-          uint2{pack_bf16x2(acc[i][0] * scale, acc[i][1] * scale), pack_bf16x2(acc[i][2] * scale, acc[i][3] * scale)};
+  for (int j = 0; j < QG; ++j) {
+    const int q = qw + 16 * j + (lane & 15);
+    if (q < L) {
+      unsigned short* row = dqkv + ((size_t)n * L + q) * ld + (size_t)h * HD;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint2*>(row + i * 16 + 4 * g) =
+            uint2{pack_bf16x2(acc[j][i][0] * scale, acc[j][i][1] * scale),
+                  pack_bf16x2(acc[j][i][2] * scale, acc[j][i][3] * scale)};
+    }
   }
 }
 
@@ -451,13 +525,30 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const unsigned shor
 
 using namespace pv;
 
+namespace {
+// 16-row groups per wave (template QG) of the forward / dQ and of the dK dV kernels;
+// pv_attn_set_qg for the A/B (0 = the measured default per kernel)
+int g_qg_fwd = 0, g_qg_dq = 0, g_qg_dkdv = 0;
+int qg_or(int v, int def) { return (v == 1 || v == 2 || v == 4) ? v : def; }
+}  // namespace
+
+PV_API void pv_attn_set_qg(int fwd, int dq, int dkdv) {
+  g_qg_fwd = fwd;
+  g_qg_dq = dq;
+  g_qg_dkdv = dkdv;
+}
+
 // qkv (N, L, 3, H, 64) bf16; mask (N, L) int32 or null; out (N, L, H, 64) bf16; lse (N, H, L) f32
 PV_API int pv_attn_fwd(const void* qkv, const int* mask, void* out, float* lse, int N, int L, int H, float scale,
                        void* stream) {
+  using namespace pv::attn;
   if (N <= 0 || L <= 0 || H <= 0) return -1;
-  dim3 grid((L + pv::attn::TB - 1) / pv::attn::TB, H, N);
-  hipLaunchKernelGGL(pv::attn::attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const unsigned short*)qkv, mask, (unsigned short*)out, lse, L, H, scale);
+  const int qg = qg_or(g_qg_fwd, 1);
+#define PV_AFWD(QGV)                                                                                            hipLaunchKernelGGL(attn_fwd_kernel<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0,                            (hipStream_t)stream, (const unsigned short*)qkv, mask, (unsigned short*)out, lse, L, H, scale)
+  if (qg == 4) PV_AFWD(4);
+  else if (qg == 2) PV_AFWD(2);
+  else PV_AFWD(1);
+#undef PV_AFWD
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -476,12 +567,16 @@ PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const 
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
                        (const unsigned short*)out, D, NL, L, H);
   PV_LAUNCH_CHECK();
-  dim3 grid((L + TB - 1) / TB, H, N);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, s, (const unsigned short*)qkv, mask,
-                     (const unsigned short*)dout, lse, D, (unsigned short*)dqkv, L, H, scale);
+  const int qk = qg_or(g_qg_dkdv, 1), qq = qg_or(g_qg_dq, 1);
+#define PV_ABWD(KERN, QGV)                                                                                       hipLaunchKernelGGL(KERN<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0, s,                                     (const unsigned short*)qkv, mask, (const unsigned short*)dout, lse, D, (unsigned short*)dqkv,                      L, H, scale)
+  if (qk == 4) PV_ABWD(attn_bwd_dkdv_kernel, 4);
+  else if (qk == 2) PV_ABWD(attn_bwd_dkdv_kernel, 2);
+  else PV_ABWD(attn_bwd_dkdv_kernel, 1);
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, s, (const unsigned short*)qkv, mask,
-                     (const unsigned short*)dout, lse, D, (unsigned short*)dqkv, L, H, scale);
+  if (qq == 4) PV_ABWD(attn_bwd_dq_kernel, 4);
+  else if (qq == 2) PV_ABWD(attn_bwd_dq_kernel, 2);
+  else PV_ABWD(attn_bwd_dq_kernel, 1);
+#undef PV_ABWD
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -97,6 +97,7 @@ SIGS = {
     # lt_gemm.hip (hipBLASLt with fused epilogues)
     "pv_lt_gemm": "ii" "iii" "pi" "pi" "pi" "i" "f" "pi" "p" "i" "pl" "p",
     "pv_lt_set_tune": "i",
+    "pv_attn_set_qg": "iii",
     "pv_transpose_u8": "pl" "ii" "pl" "p",
     # loss.hip wide-vector (D = 768) flash passes
     "pv_ibw_splits": "ii",

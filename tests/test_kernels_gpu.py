@@ -732,11 +732,22 @@ def test_debug_kernels_flag_bad_ids_without_faulting():
 
 
 @pytest.mark.parametrize("L,H", [(32, 4), (37, 4), (64, 12), (65, 4), (200, 4), (256, 12), (300, 6)])
-def test_fused_attention_packed_qkv(L, H):
+@pytest.mark.parametrize("qg", [1, 2, 4])
+def test_fused_attention_packed_qkv(L, H, qg):
     """attention.hip (online softmax fwd, dK/dV + dQ bwd) vs an fp32 reference on the same
-    bf16 packed QKV, with key padding."""
+    bf16 packed QKV, with key padding; qg = 16-row groups per wave of every kernel (the
+    workgroup owns 64 qg rows; partial blocks at L = 37 / 65 / 200 / 300)."""
     from dnn_page_vectors_amd.ops import transformer as tops
+    from dnn_page_vectors_amd.ops._common import lib
 
+    lib().pv_attn_set_qg(qg, qg, qg)
+    try:
+        _attention_case(L, H, tops)
+    finally:
+        lib().pv_attn_set_qg(0, 0, 0)
+
+
+def _attention_case(L, H, tops):
     torch.manual_seed(L)
     N, d = 3, 64
     qkv = (torch.randn(N, L, 3 * H * d, device=DEV) * 0.5).bfloat16().requires_grad_(True)

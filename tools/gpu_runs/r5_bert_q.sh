@@ -11,11 +11,15 @@ run() {  # name, timeout, command...
   echo "$n rc=$rc $(tail -1 $out/$n.log | cut -c1-600)"
   case $rc in 0) ;; *) exit $rc ;; esac
 }
-run parity12 400 python -u tools/bert_parity.py --layers 12 --batch 64 --steps 200
 B="python -u bench.py --model bert --steps 3 --warmup 3 --eager-compare 0"
-run base 240 $B
-run lr1e4_w50 240 $B --set lr=1e-4 --set lr_warmup_steps=50
-run lr1e4_w50_noclip_g20 240 $B --set lr=1e-4 --set lr_warmup_steps=50 --set cos_clip=False --set inbatch_gamma=20
-run lr3e4_w50_noclip_g20 240 $B --set lr=3e-4 --set lr_warmup_steps=50 --set cos_clip=False --set inbatch_gamma=20
-run lr3e4_w50_noclip_g40 240 $B --set lr=3e-4 --set lr_warmup_steps=50 --set cos_clip=False --set inbatch_gamma=40
-run lr1e3_w50_noclip_g20 240 $B --set lr=1e-3 --set lr_warmup_steps=50 --set cos_clip=False --set inbatch_gamma=20
+if [ "$1" = "a" ]; then
+run parity12 400 python -u tools/bert_parity.py --layers 12 --batch 64 --steps 200
+run base 200 $B
+run lr1e4_w50 200 $B --set lr=1e-4 --set lr_warmup_steps=50
+run lr1e4_w50_noclip_g20 200 $B --set lr=1e-4 --set lr_warmup_steps=50 --set cos_clip=False --set inbatch_gamma=20
+else
+run lr3e5_w20 200 $B --set lr=3e-5 --set lr_warmup_steps=20
+run lr5e5_w50 200 $B --set lr=5e-5 --set lr_warmup_steps=50
+run lr2e5_noclip_g20 200 $B --set cos_clip=False --set inbatch_gamma=20
+run lr2e5_g20 200 $B --set inbatch_gamma=20
+fi
