@@ -527,7 +527,10 @@ using namespace pv;
 
 namespace {
 // 16-row groups per wave (template QG) of the forward / dQ and of the dK dV kernels;
-// pv_attn_set_qg for the A/B (0 = the measured default per kernel)
+// pv_attn_set_qg for the A/B (0 = the measured default: tools/attn_micro.py at the BERT
+// shapes, profiles/r5_attn/: L 256 fwd 157-173 -> 124-128 us with QG 2, bwd 453 -> 435 us with
+// QG 2 for dQ only (dK dV with 2: 473; QG 4: 1 wave per SIMD, slower everywhere); L 32 (the
+// query segments) stays at QG 1 — a 128-row workgroup would be mostly empty)
 int g_qg_fwd = 0, g_qg_dq = 0, g_qg_dkdv = 0;
 int qg_or(int v, int def) { return (v == 1 || v == 2 || v == 4) ? v : def; }
 }  // namespace
@@ -543,7 +546,7 @@ PV_API int pv_attn_fwd(const void* qkv, const int* mask, void* out, float* lse, 
                        void* stream) {
   using namespace pv::attn;
   if (N <= 0 || L <= 0 || H <= 0) return -1;
-  const int qg = qg_or(g_qg_fwd, 1);
+  const int qg = qg_or(g_qg_fwd, L >= 128 ? 2 : 1);
 #define PV_AFWD(QGV)                                                                                            hipLaunchKernelGGL(attn_fwd_kernel<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0,                            (hipStream_t)stream, (const unsigned short*)qkv, mask, (unsigned short*)out, lse, L, H, scale)
   if (qg == 4) PV_AFWD(4);
   else if (qg == 2) PV_AFWD(2);
@@ -567,7 +570,7 @@ PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const 
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((NL + 3) / 4), dim3(256), 0, s, (const unsigned short*)dout,
                        (const unsigned short*)out, D, NL, L, H);
   PV_LAUNCH_CHECK();
-  const int qk = qg_or(g_qg_dkdv, 1), qq = qg_or(g_qg_dq, 1);
+  const int qk = qg_or(g_qg_dkdv, 1), qq = qg_or(g_qg_dq, L >= 128 ? 2 : 1);
 #define PV_ABWD(KERN, QGV)                                                                                       hipLaunchKernelGGL(KERN<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0, s,                                     (const unsigned short*)qkv, mask, (const unsigned short*)dout, lse, D, (unsigned short*)dqkv,                      L, H, scale)
   if (qk == 4) PV_ABWD(attn_bwd_dkdv_kernel, 4);
   else if (qk == 2) PV_ABWD(attn_bwd_dkdv_kernel, 2);
