@@ -391,6 +391,53 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_vec_kernel(const unsigned s
   *reinterpret_cast<f32x4*>(pr + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
+// v2 of the two vector kernels: 128-thread blocks (D = 3072 is 384 column octets = 3 full
+// blocks; the 256-thread v1 left half of its second block idle) and U rows' loads issued
+// before any of their math (v1 kept 2 loads in flight per thread, ~4.5 TB/s at the BERT shape)
+template <int U>
+__global__ __launch_bounds__(128) void bias_gelu_bwd_vec2_kernel(const unsigned short* __restrict__ x,
+                                                                 const float* __restrict__ b,
+                                                                 const unsigned short* __restrict__ dy,
+                                                                 unsigned short* __restrict__ dx,
+                                                                 float* __restrict__ part, int M, int D, int rpb) {
+  const int c8 = (blockIdx.x * 128 + threadIdx.x) * 8;
+  if (c8 >= D) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + c8), b1 = *reinterpret_cast<const f32x4*>(b + c8 + 4);
+  const float bc[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int row = r0; row < r1; row += U) {
+    u32x4 xv[U], gv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t o = (size_t)min(row + u, r1 - 1) * D + c8;  // clamped: a re-read, never stored twice
+      xv[u] = *reinterpret_cast<const u32x4*>(x + o);
+      gv[u] = *reinterpret_cast<const u32x4*>(dy + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (row + u >= r1) break;
+      u32x4 out;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float x0 = __uint_as_float(xv[u][w] << 16) + bc[2 * w];
+        const float x1 = __uint_as_float(xv[u][w] & 0xFFFF0000u) + bc[2 * w + 1];
+        const float g0 = __uint_as_float(gv[u][w] << 16) * gelu_tanh_grad_fast(x0);
+        const float g1 = __uint_as_float(gv[u][w] & 0xFFFF0000u) * gelu_tanh_grad_fast(x1);
+        acc[2 * w] += g0;
+        acc[2 * w + 1] += g1;
+        out[w] = pack_bf16x2(g0, g1);
+      }
+      *reinterpret_cast<u32x4*>(dx + (size_t)(row + u) * D + c8) = out;
+    }
+  }
+  float* pr = part + (size_t)blockIdx.y * D + c8;
+  *reinterpret_cast<f32x4*>(pr) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<f32x4*>(pr + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+}
+
 // Column sums in a fixed order, two stages: colsum_part (grid (ceil(D/64), S)) reduces
 // a 1/S slice of the rows of 64 columns with 4 row lanes + LDS into part2[S][D];
 // colsum_final adds the S partials.
@@ -476,6 +523,35 @@ __global__ __launch_bounds__(128) void bias_gelu_fwd_vec_kernel(const unsigned s
       w[k] = pack_bf16x2(gelu_tanh_fast(a0), gelu_tanh_fast(a1));
     }
     *reinterpret_cast<u32x4*>(y + o) = w;
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(128) void bias_gelu_fwd_vec2_kernel(const unsigned short* __restrict__ x,
+                                                                 const float* __restrict__ b,
+                                                                 unsigned short* __restrict__ y, int M, int D,
+                                                                 int rpb) {
+  const int col = (blockIdx.x * 128 + threadIdx.x) * 8;
+  if (col >= D) return;
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(b + col), b1 = *reinterpret_cast<const f32x4*>(b + col + 4);
+  const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  for (int r = r0; r < r1; r += U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const u32x4*>(x + (size_t)min(r + u, r1 - 1) * D + col);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r + u >= r1) break;
+      u32x4 w;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float a0 = __uint_as_float(v[u][k] << 16) + bb[2 * k];
+        const float a1 = __uint_as_float(v[u][k] & 0xFFFF0000u) + bb[2 * k + 1];
+        w[k] = pack_bf16x2(gelu_tanh_fast(a0), gelu_tanh_fast(a1));
+      }
+      *reinterpret_cast<u32x4*>(y + (size_t)(r + u) * D + col) = w;
+    }
   }
 }
 
@@ -753,8 +829,23 @@ PV_API int pv_add_ln_drop_fwd(const void* x, const float* xb, const void* r, con
   return 0;
 }
 
+namespace {
+int g_gelu_v = 2;  // pv_gelu_set_v: 1 = the round-2 vector kernels, 2 = the 128-thread unrolled ones
+constexpr int kGelu2Rpb = 32;
+}  // namespace
+
+PV_API void pv_gelu_set_v(int v) { g_gelu_v = v; }
+
 PV_API int pv_bias_gelu_fwd(const void* x, const float* b, void* y, long n, int D, void* stream) {
   if (D % 2) return -1;
+  if (g_gelu_v == 2 && D % 8 == 0 && n / D <= 0x7FFFFFFFL) {
+    const int M = (int)(n / D);
+    dim3 grid((D / 8 + 127) / 128, (M + kGelu2Rpb - 1) / kGelu2Rpb);
+    hipLaunchKernelGGL(pv::tfm::bias_gelu_fwd_vec2_kernel<4>, grid, dim3(128), 0, (hipStream_t)stream,
+                       (const unsigned short*)x, b, (unsigned short*)y, M, D, kGelu2Rpb);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
   if (D % 8 == 0 && n / D <= 0x7FFFFFFFL) {
     const int M = (int)(n / D);
     dim3 grid((D / 8 + 127) / 128, (M + pv::tfm::kGeluFwdRpb - 1) / pv::tfm::kGeluFwdRpb);
@@ -782,10 +873,16 @@ PV_API long pv_bias_gelu_bwd_ws(int M, int D) {
 PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void* dx, float* db, float* ws, int M,
                             int D, void* stream) {
   if (D % 8 == 0 && ws) {
-    const int rpb = kGeluRpb, R = (M + rpb - 1) / rpb;
-    dim3 grid((D / 8 + 255) / 256, R);
-    hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_vec_kernel, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, ws, M, D, rpb);
+    const int rpb = g_gelu_v == 2 ? kGelu2Rpb : kGeluRpb, R = (M + rpb - 1) / rpb;  // kGelu2Rpb >= kGeluRpb
+    if (g_gelu_v == 2) {
+      dim3 grid((D / 8 + 127) / 128, R);
+      hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_vec2_kernel<4>, grid, dim3(128), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, ws, M, D, rpb);
+    } else {
+      dim3 grid((D / 8 + 255) / 256, R);
+      hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_vec_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, ws, M, D, rpb);
+    }
     PV_LAUNCH_CHECK();
     float* ws2 = ws + (size_t)R * D;
     hipLaunchKernelGGL(pv::tfm::colsum_part_kernel, dim3((D + 63) / 64, pv::tfm::kColSplits), dim3(256), 0,

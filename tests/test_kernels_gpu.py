@@ -545,16 +545,28 @@ def test_add_layernorm_and_bias_gelu(D):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
     torch.testing.assert_close(g.grad, gr.grad, rtol=3e-2, atol=1e-1)
     torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=1e-1)
-    u = torch.randn(M, 3072, device=DEV).bfloat16().requires_grad_(True)
-    bb = torch.randn(3072, device=DEV).requires_grad_(True)
-    o = tops.bias_gelu(u, bb)
-    ur, bbr = u.detach().float().requires_grad_(True), bb.detach().clone().requires_grad_(True)
+    from dnn_page_vectors_amd.ops._common import lib
+
+    u0 = torch.randn(M, 3072, device=DEV).bfloat16()
+    bb0 = torch.randn(3072, device=DEV)
+    do = torch.randn(M, 3072, device=DEV)
+    ur, bbr = u0.float().requires_grad_(True), bb0.clone().requires_grad_(True)
     orf = torch.nn.functional.gelu(ur + bbr, approximate="tanh")
-    torch.testing.assert_close(o.float(), orf, rtol=2e-2, atol=2e-2)
-    do = torch.randn_like(orf)
-    (o.float() * do).sum().backward()
     (orf * do).sum().backward()
-    torch.testing.assert_close(bb.grad, bbr.grad, rtol=3e-2, atol=2e-1)
+    outs = {}
+    for gv in (1, 2):  # round-2 vector kernels / 128-thread unrolled ones (pv_gelu_set_v)
+        lib().pv_gelu_set_v(gv)
+        try:
+            u, bb = u0.clone().requires_grad_(True), bb0.clone().requires_grad_(True)
+            o = tops.bias_gelu(u, bb)
+            torch.testing.assert_close(o.float(), orf, rtol=2e-2, atol=2e-2)
+            (o.float() * do).sum().backward()
+            torch.testing.assert_close(bb.grad, bbr.grad, rtol=3e-2, atol=2e-1)
+            torch.testing.assert_close(u.grad.float(), ur.grad, rtol=3e-2, atol=5e-2)
+            outs[gv] = (o, u.grad)
+        finally:
+            lib().pv_gelu_set_v(2)
+    assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])  # same per-element math
 
 
 @pytest.mark.parametrize("L", [37, 64, 300])  # generic / register (<=256) / register (<=512) softmax
