@@ -234,6 +234,99 @@ __global__ __launch_bounds__(256) void add_ln_drop_fwd_kernel(const unsigned sho
   }
 }
 
+// v2: RPW rows per wave with every row's x / r loads issued before any row's math (v1: one
+// row per wave, 2 VPT loads in flight per lane, ~4.6 TB/s at the BERT shape); same per-row
+// arithmetic, so the outputs are bit-identical to v1.
+template <int VPT, int RPW>
+__global__ __launch_bounds__(256) void add_ln_drop_fwd2_kernel(const unsigned short* __restrict__ x,
+                                                               const unsigned short* __restrict__ r,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               unsigned short* __restrict__ y,
+                                                               unsigned short* __restrict__ h,
+                                                               float* __restrict__ mean_out,
+                                                               float* __restrict__ rstd_out, int M, float eps,
+                                                               int thr, float scale, unsigned seed,
+                                                               const unsigned* __restrict__ seed_ptr,
+                                                               const float* __restrict__ xb) {
+  constexpr int D = 256 * VPT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row0 = (blockIdx.x * 4 + wave) * RPW;
+  if (row0 >= M) return;
+  if (seed_ptr) seed += *seed_ptr;
+  uint2 xa[RPW][VPT], ra[RPW][VPT];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = min(row0 + q, M - 1);  // clamped re-read; only rows < M are stored
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const size_t o = (size_t)row * D + (i * 64 + lane) * 4;
+      xa[q][i] = *reinterpret_cast<const uint2*>(x + o);
+      if (r) ra[q][i] = *reinterpret_cast<const uint2*>(r + o);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = row0 + q;
+    if (row >= M) break;
+    const unsigned hrow = thr > 0 ? dropout_row_hash(seed, (unsigned)row) : 0u;
+    float v[VPT][4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      const uint2 a = xa[q][i];
+      v[i][0] = __uint_as_float(a.x << 16);
+      v[i][1] = __uint_as_float(a.x & 0xFFFF0000u);
+      v[i][2] = __uint_as_float(a.y << 16);
+      v[i][3] = __uint_as_float(a.y & 0xFFFF0000u);
+      if (xb) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(xb + c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += b4[k];
+      }
+      if (thr > 0) {
+        const unsigned kb = keep4(hrow, c, thr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] = ((kb >> k) & 1u) ? v[i][k] * scale : 0.f;
+      }
+      if (r) {
+        const uint2 b = ra[q][i];
+        v[i][0] += __uint_as_float(b.x << 16);
+        v[i][1] += __uint_as_float(b.x & 0xFFFF0000u);
+        v[i][2] += __uint_as_float(b.y << 16);
+        v[i][3] += __uint_as_float(b.y & 0xFFFF0000u);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[i][k] = bf16_to_f32(f32_to_bf16(v[i][k]));
+      s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    }
+    const float mu = wave_sum(s) * (1.f / D);
+    float qv = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qv += (v[i][k] - mu) * (v[i][k] - mu);
+    const float rstd = rsqrtf(wave_sum(qv) * (1.f / D) + eps);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      const size_t o = (size_t)row * D + c;
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(gamma + c);
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(beta + c);
+      float out[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) out[k] = (v[i][k] - mu) * rstd * g4[k] + b4[k];
+      *reinterpret_cast<uint2*>(y + o) = uint2{pack_bf16x2(out[0], out[1]), pack_bf16x2(out[2], out[3])};
+      if (h) *reinterpret_cast<uint2*>(h + o) = uint2{pack_bf16x2(v[i][0], v[i][1]), pack_bf16x2(v[i][2], v[i][3])};
+    }
+    if (lane == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
 // Wave-per-row LayerNorm backward for D = 256 * VPT: each lane holds VPT 4-element
 // vectors of dy and x_hat in registers (one read of each), the two row means are wave
 // reductions (no barriers), and dgamma/dbeta accumulate in registers over the rows this
@@ -807,13 +900,30 @@ PV_API int pv_layernorm_bwd_drop(const void* dy, const void* hsum, const float* 
                             seed_ptr, dxb, stream);
 }
 
+namespace {
+int g_ln_rpw = 2;  // pv_ln_set_rpw: rows per wave of the add + LN forward (1 = the v1 kernel)
+}  // namespace
+
+PV_API void pv_ln_set_rpw(int rpw) { g_ln_rpw = rpw; }
+
 // Wave-per-row residual add (+ optional dropout on x) + LayerNorm, D in {256, 512, 768, 1024}.
 PV_API int pv_add_ln_drop_fwd(const void* x, const float* xb, const void* r, const float* gamma, const float* beta,
                               void* y, void* h, float* mean, float* rstd, int M, int D, float eps, int thr, float scale,
                               unsigned seed, const unsigned* seed_ptr, void* stream) {
   if (!ln_rows_ok(D) || thr < 0 || thr > 255) return -1;
-  const dim3 grid((M + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
+  if (g_ln_rpw == 2 || g_ln_rpw == 4) {
+    const int rpw = g_ln_rpw;
+    const dim3 g2((M + 4 * rpw - 1) / (4 * rpw));
+#define PV_ADDLN2(VPT, RPWV)                                                                                        hipLaunchKernelGGL((pv::tfm::add_ln_drop_fwd2_kernel<VPT, RPWV>), g2, dim3(256), 0, st,                                              (const unsigned short*)x, (const unsigned short*)r, gamma, beta, (unsigned short*)y,                               (unsigned short*)h, mean, rstd, M, eps, thr, scale, seed, seed_ptr, xb)
+#define PV_ADDLN2_D(RPWV)                   switch (D) {                                case 256: PV_ADDLN2(1, RPWV); break;      case 512: PV_ADDLN2(2, RPWV); break;      case 768: PV_ADDLN2(3, RPWV); break;      default: PV_ADDLN2(4, RPWV); break;     }
+    if (rpw == 2) { PV_ADDLN2_D(2) } else { PV_ADDLN2_D(4) }
+#undef PV_ADDLN2_D
+#undef PV_ADDLN2
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
+  const dim3 grid((M + 3) / 4);
 #define PV_ADDLN(VPT)                                                                                          \
   hipLaunchKernelGGL(pv::tfm::add_ln_drop_fwd_kernel<VPT>, grid, dim3(256), 0, st, (const unsigned short*)x,  \
                      (const unsigned short*)r, gamma, beta, (unsigned short*)y, (unsigned short*)h, mean, rstd, \

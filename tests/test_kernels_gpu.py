@@ -547,6 +547,20 @@ def test_add_layernorm_and_bias_gelu(D):
     torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=1e-1)
     from dnn_page_vectors_amd.ops._common import lib
 
+    # rows per wave of the add + LN forward (pv_ln_set_rpw): same per-row math, bit-identical,
+    # with and without the dropout branch (M = 70: partial last waves)
+    if D in (256, 512, 768, 1024):
+        ys = []
+        for rpw in (1, 2, 4):
+            lib().pv_ln_set_rpw(rpw)
+            try:
+                with torch.no_grad():
+                    ys.append((tops.add_layernorm(x, r, g, b), tops.add_layernorm(x, r, g, b, p=0.1, seed=7)))
+            finally:
+                lib().pv_ln_set_rpw(2)
+        for a_, b_ in ys[1:]:
+            assert torch.equal(a_, ys[0][0]) and torch.equal(b_, ys[0][1])
+
     u0 = torch.randn(M, 3072, device=DEV).bfloat16()
     bb0 = torch.randn(3072, device=DEV)
     do = torch.randn(M, 3072, device=DEV)

@@ -41,6 +41,20 @@ def main():
             r[f"fwd_v{v}_r{rnd}"] = ev(lambda: lib().pv_bias_gelu_fwd(P(x), P(b), P(y), M * D, D, s))
             r[f"bwd_v{v}_r{rnd}"] = ev(lambda: lib().pv_bias_gelu_bwd(P(x), P(b), P(dy), P(dx), P(db), P(ws), M, D, s))
     lib().pv_gelu_set_v(2)
+    # add + LayerNorm forward (dropout 0.1, branch bias) at T x 768: rows per wave 1 / 2 / 4
+    H = 768
+    xa = torch.randn(M, H, device=dev).bfloat16()
+    ra = torch.randn(M, H, device=dev).bfloat16()
+    g_, b_, xb_ = torch.ones(H, device=dev), torch.zeros(H, device=dev), torch.zeros(H, device=dev)
+    ya, ha = torch.empty_like(xa), torch.empty_like(xa)
+    mu, rs = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    for rnd in range(2):
+        for rpw in (1, 2, 4):
+            lib().pv_ln_set_rpw(rpw)
+            r[f"addln_rpw{rpw}_r{rnd}"] = ev(lambda: lib().pv_add_ln_drop_fwd(
+                P(xa), P(xb_), P(ra), P(g_), P(b_), P(ya), P(ha), P(mu), P(rs), M, H, 1e-12, 26, 256.0 / 230, 7, None, s))
+    lib().pv_ln_set_rpw(2)
+    r["addln_best_TBps"] = round(4 * M * H * 2 / 1e9 / min(v for k, v in r.items() if k.startswith("addln")) * 1e3, 2)
     gb = M * D * 2 / 1e9
     r["fwd_v2_TBps"] = round(2 * gb / min(r["fwd_v2_r0"], r["fwd_v2_r1"]) * 1e6 / 1e3, 2)
     r["bwd_v2_TBps"] = round(3 * gb / min(r["bwd_v2_r0"], r["bwd_v2_r1"]) * 1e6 / 1e3, 2)
