@@ -1,4 +1,4 @@
-"""Render a rocprofv3 --kernel-trace --stats CSV directory into a markdown table.
+"""Render a rocprofv3 --kernel-trace --stats CSV (or its rocpd SQLite .db) into a markdown table.
 
     python tools/prof_summary.py gpurun_out/prof_all/cdssm/cdssm_kernel_stats.csv --steps 13 \
         --title "..." --cmd "..." > profiles/x.md
@@ -22,7 +22,14 @@ def main():
     ap.add_argument("--note", default="")
     ap.add_argument("--top", type=int, default=25)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.csv)))
+    if a.csv.endswith(".db"):  # rocprofv3's default rocpd (SQLite) output: the top_kernels view (us)
+        import sqlite3
+
+        con = sqlite3.connect(a.csv)
+        rows = [{"Name": n, "Calls": c, "TotalDurationNs": t * 1e3, "Percentage": p}
+                for n, c, t, _, p in con.execute("select * from top_kernels order by total_duration desc")]
+    else:
+        rows = list(csv.DictReader(open(a.csv)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     print(f"# {a.title}\n")
     if a.cmd:
