@@ -121,13 +121,17 @@ int make_plan(hipblasLtHandle_t h, Plan& p, int ta, int tb, int m, int n, int k,
 }
 
 // Time every candidate (1 warm-up + 3 runs each, events on the caller's stream) and keep the
-// fastest.  Only for beta = 0 (each run rewrites D / AUX / the bias gradient with the same
-// values) and outside stream capture; a host sync, once per problem.
-void autotune(hipblasLtHandle_t h, Plan& p, const void* A, const void* B, void* D, void* ws, hipStream_t st) {
+// fastest; outside stream capture only, a host sync once per problem.  beta = 0 problems time
+// in place (each run rewrites D / AUX / the bias gradient with the same values); beta != 0
+// ones (D += A B, the residual dX) time with beta = 0 into a scratch D, so D keeps its input.
+void autotune(hipblasLtHandle_t h, Plan& p, const void* A, const void* B, void* D, bool acc, size_t dbytes, void* ws,
+              hipStream_t st) {
   p.tuned = true;
   if (p.ncand < 2) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  void* dst = D;
+  if (acc && hipMalloc(&dst, dbytes) != hipSuccess) return;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return;
   if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return; }
@@ -136,7 +140,7 @@ void autotune(hipblasLtHandle_t h, Plan& p, const void* A, const void* B, void* 
   int besti = p.pick;
   for (int c = 0; c < p.ncand; ++c) {
     auto run = [&]() {
-      return hipblasLtMatmul(h, p.op, &alpha, A, p.a, B, p.b, &beta, D, p.d, D, p.d, &p.cand[c].algo, ws,
+      return hipblasLtMatmul(h, p.op, &alpha, A, p.a, B, p.b, &beta, dst, p.d, dst, p.d, &p.cand[c].algo, ws,
                              p.cand[c].workspaceSize, st);
     };
     if (run() != HIPBLAS_STATUS_SUCCESS) continue;
@@ -150,6 +154,10 @@ void autotune(hipblasLtHandle_t h, Plan& p, const void* A, const void* B, void* 
     if (ms < best) { best = ms; besti = c; }
   }
   p.pick = besti;
+  if (acc) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(dst);
+  }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
 }
@@ -188,7 +196,8 @@ PV_API int pv_lt_gemm(int ta, int tb, int m, int n, int k, const void* A, int ld
   if (!p.ok) return -3;
   if (bias) LT_TRY(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
   if (aux) LT_TRY(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
-  if (g_tune && !p.tuned && beta == 0.f) autotune(hit->second, p, A, B, D, ws, (hipStream_t)stream);
+  if (g_tune && !p.tuned)
+    autotune(hit->second, p, A, B, D, beta != 0.f, (size_t)ldd * n * (d_f32 ? 4 : 2), ws, (hipStream_t)stream);
   const float alpha = 1.f;
   const hipblasLtMatmulHeuristicResult_t& c = p.cand[p.pick];
   LT_TRY(hipblasLtMatmul(hit->second, p.op, &alpha, A, p.a, B, p.b, &beta, D, p.d, D, p.d, &c.algo, ws,

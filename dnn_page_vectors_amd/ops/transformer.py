@@ -364,7 +364,7 @@ def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] =
     ``out``: fp32 destination (a flat-gradient view, ops/grad_sink.py), overwritten.
     """
     T = dy2.shape[0]
-    if LINEAR_LT and dy2.is_cuda:
+    if WGRAD_LT and dy2.is_cuda:
         o = out if out is not None else torch.empty(dy2.shape[1], x2.shape[1], dtype=torch.float32,
                                                     device=dy2.device)
         check(lt_mm(dy2, x2, o, ta=True), "pv_lt_gemm(wgrad)")
@@ -444,9 +444,11 @@ FFN_LT = os.environ.get("PAGEVEC_FFN_LT", "1") != "0"
 # hipBLASLt candidate autotuning (lt_gemm.hip): time the heuristic's top 16 once per problem
 LT_TUNE = os.environ.get("PAGEVEC_LT_TUNE", "0") != "0"
 _LT_TUNE_SET = [None]
-# the linear layers' own GEMMs through lt_gemm.hip too (bias epilogue, in-place residual dX,
-# fp32 weight gradient in one library GEMM) instead of torch.addmm / mm / split-K bmm
+# the linear layers' forward / dX GEMMs through lt_gemm.hip too (bias epilogue, in-place
+# residual dX) instead of torch.addmm / mm; WGRAD_LT: the fp32 weight gradient as one lt GEMM
+# instead of the split-K bmm (measured slower: profiles/r5_lt/)
 LINEAR_LT = os.environ.get("PAGEVEC_LINEAR_LT", "0") != "0"
+WGRAD_LT = os.environ.get("PAGEVEC_WGRAD_LT", "0") != "0"
 _LT_WS = {}
 _LT_BAD = set()  # (shape, epilogue) keys hipBLASLt has no solution for
 LT_WS_BYTES = 64 << 20

@@ -44,7 +44,8 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_FP8_BAG": ("ab", "1", "fp8 towers: page bag on the MX fp8 MFMA"),
     "PAGEVEC_FP8_BWD": ("ab", "1", "fp8 towers: bag weight gradient on the MX fp8 MFMA (e4m3 counts^T x e4m3 G)"),
     "PAGEVEC_LT_TUNE": ("ab", "0", "time hipBLASLt's top candidates once per problem (lt_gemm.hip)"),
-    "PAGEVEC_LINEAR_LT": ("ab", "0", "BERT linear layers on lt_gemm.hip instead of torch mm / addmm"),
+    "PAGEVEC_LINEAR_LT": ("ab", "0", "BERT linear forward / dX GEMMs on lt_gemm.hip instead of torch mm / addmm"),
+    "PAGEVEC_WGRAD_LT": ("ab", "0", "BERT weight gradients as one lt_gemm.hip GEMM instead of the split-K bmm"),
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),

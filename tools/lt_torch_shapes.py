@@ -27,8 +27,8 @@ def main():
              ("ffn1_dw  3072 x 768 x T (fp32)", (T, 3072), (T, 768), "tn", True),
              ("square 8192", (8192, 8192), (8192, 8192), "nt", False)]
     for name, sa, sb, mode, f32 in cases:
-        a = torch.randn(*sa, device=dev).to(bf)
-        b = torch.randn(*sb, device=dev).to(bf)
+        a = (torch.rand(*sa, device=dev) * 2 - 1).to(bf)  # uniform [-1, 1) as the C++ tool
+        b = (torch.rand(*sb, device=dev) * 2 - 1).to(bf)
         if mode == "nt":
             fn = lambda: a @ b.t()  # noqa: E731
             fl = 2.0 * sa[0] * sa[1] * sb[0]

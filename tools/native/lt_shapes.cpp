@@ -6,8 +6,25 @@
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <random>
 #include <vector>
+
+// random bf16 in [-1, 1) (constant operands draw less power and clock higher: not comparable)
+static int fill_random(void* dst, size_t n, unsigned seed) {
+  std::vector<uint16_t> h(n);
+  std::mt19937 g(seed);
+  std::uniform_real_distribution<float> u(-1.f, 1.f);
+  for (size_t i = 0; i < n; ++i) {
+    const float f = u(g);
+    uint32_t b;
+    std::memcpy(&b, &f, 4);
+    h[i] = (uint16_t)(b >> 16);
+  }
+  return (int)hipMemcpy(dst, h.data(), n * 2, hipMemcpyHostToDevice);
+}
 
 #define CK(x)                                                             \
   do {                                                                    \
@@ -48,8 +65,8 @@ int main() {
     CK(hipMalloc(&A, (size_t)rowsA * colsA * 2));
     CK(hipMalloc(&B, (size_t)rowsB * colsB * 2));
     CK(hipMalloc(&D, (size_t)s.m * s.n * (s.d32 ? 4 : 2)));
-    CK(hipMemset(A, 0x3c, (size_t)rowsA * colsA * 2));
-    CK(hipMemset(B, 0x3c, (size_t)rowsB * colsB * 2));
+    CK(fill_random(A, (size_t)rowsA * colsA, 1));
+    CK(fill_random(B, (size_t)rowsB * colsB, 2));
     hipblasLtMatmulDesc_t op;
     CK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
     hipblasOperation_t oa = s.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, ob = s.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
