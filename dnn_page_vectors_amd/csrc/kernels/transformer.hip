@@ -434,14 +434,29 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 }
 
 // tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp instead of libm tanhf
+// tanh / sigmoid through v_exp_f32 and v_rcp_f32 (1 ulp): an IEEE fdiv / __frcp_rn is a
+// ~10-instruction div_scale / div_fmas / div_fixup sequence per element, and these kernels
+// are VALU-bound (~20 VALU per element) at the BERT shape; the results are rounded to bf16.
 __device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - 2.f / (__expf(2.f * u) + 1.f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
+}
+
+// tanh-GELU through s = sigmoid(2u), u = k (x + c x^3): gelu = x s, 1 + t = 2 s,
+// 1 - t^2 = 4 s (1 - s), so gelu' = s + x s (1 - s) (2k + 6kc x^2) — one exp2 and one rcp
+// (v_exp_f32 / v_rcp_f32) and six FMA-class ops per element.
+constexpr float kGeluK = 0.7978845608028654f, kGeluC = 0.044715f, kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float gelu_sig2u(float x, float x2) {
+  // sigmoid(2u) = 1 / (1 + 2^(-2 k log2e (x + c x^3)))
+  const float e = __builtin_amdgcn_exp2f(x * fmaf(x2, -2.f * kGeluK * kGeluC * kLog2e, -2.f * kGeluK * kLog2e));
+  return __builtin_amdgcn_rcpf(1.f + e);
 }
 
 __device__ __forceinline__ float gelu_tanh_grad_fast(float x) {
   const float x2 = x * x;
-  const float t = fast_tanh(0.7978845608028654f * (x + 0.044715f * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x2);
+  const float sg = gelu_sig2u(x, x2);
+  const float q = x * fmaf(x2, 6.f * kGeluK * kGeluC, 2.f * kGeluK);
+  return fmaf(q, fmaf(-sg, sg, sg), sg);
 }
 
 // Vectorised bias-GELU backward: a thread owns 8 consecutive columns (16-byte loads and
@@ -586,10 +601,7 @@ __global__ void bias_gelu_fwd_kernel(const unsigned short* __restrict__ x, const
 }
 
 // x * sigmoid(2u) == 0.5 x (1 + tanh u): one v_exp + one v_rcp, no libm tanhf
-__device__ __forceinline__ float gelu_tanh_fast(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return x * __frcp_rn(1.f + __expf(-2.f * u));
-}
+__device__ __forceinline__ float gelu_tanh_fast(float x) { return x * gelu_sig2u(x, x * x); }
 
 // Vectorised bias + GELU forward (D % 8 == 0): a thread owns 8 consecutive columns
 // (16-byte loads / stores, its 8 bias values in registers) for RPB rows.  The scalar kernel

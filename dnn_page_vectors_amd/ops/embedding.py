@@ -348,7 +348,8 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
     ``act`` in {none, relu, tanh}; bias / act are fused into the producing kernel on the GPU.
     ``fp8``: long bags (the counts plan) multiply e4m3 counts by the per-tensor-scaled e4m3
     table on the block-scaled fp8 MFMA (``w8`` = ops.fp8.quantize_t(W) of this step, else
-    quantised here); the weight gradient stays the exact bf16 C^T G (straight-through)."""
+    quantised here); the weight gradient is e4m3 C^T x the per-tensor e4m3 gradient on the same
+    MFMA (PAGEVEC_FP8_BWD, default), or the exact bf16 C^T G (straight-through)."""
     note_rows(W, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
     if use_hip(ids, W) and act in _BAG_ACT:
         if W16 is None:
@@ -374,6 +375,30 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
     return dops._torch_act(out, act)
 
 
+class _Fp8BagRef(torch.autograd.Function):
+    """CPU reference of the fp8 bag product: forward e4m3(C) @ e4m3(W) (per-tensor scaled);
+    backward as the GPU's: with FP8_BWD the e4m3 counts^T times the per-tensor e4m3 quantised
+    gradient (_fp8_weight_grad), else the exact C^T G (straight-through)."""
+
+    @staticmethod
+    def forward(ctx, C, W):
+        from . import fp8 as fops
+
+        ctx.save_for_backward(C)
+        return fops.emulate_e4m3(C) @ fops._emulate(W.detach())
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import fp8 as fops
+
+        C, = ctx.saved_tensors
+        if not FP8_BWD:
+            return None, C.t() @ g
+        amax = float(g.abs().max())
+        gq = fops.emulate_e4m3(g * (fops.FP8_MAX / max(amax, 1e-12))) * (max(amax, 1e-12) / fops.FP8_MAX)
+        return None, fops.emulate_e4m3(C).t() @ gq
+
+
 def _bag_fp8_reference(ids, W, pad, mean, bias, act):
     from . import fp8 as fops
 
@@ -382,10 +407,11 @@ def _bag_fp8_reference(ids, W, pad, mean, bias, act):
     C = torch.zeros(ids.shape[0], V, dtype=torch.float32, device=ids.device)
     C.scatter_add_(1, torch.where(valid, ids, torch.zeros_like(ids)).long(), valid.float())
     lens = valid.sum(dim=1).float()
-    exact = C @ W  # the GPU backward's exact C^T G: straight-through for counts AND table
-    with torch.no_grad():
-        q = fops.emulate_e4m3(C) @ fops._emulate(W.detach())
-    out = exact + (q - exact).detach() if exact.requires_grad else q
+    if W.requires_grad and torch.is_grad_enabled():
+        out = _Fp8BagRef.apply(C, W)
+    else:
+        with torch.no_grad():
+            out = fops.emulate_e4m3(C) @ fops._emulate(W.detach())
     if mean:
         out = out / lens.clamp(min=1.0)[:, None]
     if bias is not None:

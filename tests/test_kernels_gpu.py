@@ -1777,7 +1777,7 @@ def test_quant_fp8_t_and_counts8():
 def test_fp8_bag_matches_reference():
     """embedding_bag(fp8=True) on the GPU (e4m3 counts x e4m3 W^T on the MX MFMA + split-K
     column-sum epilogue: mean, bias, tanh) against the CPU reference with the same
-    quantisation; the weight gradient is the exact bf16 C^T G on both (straight-through)."""
+    quantisation, forward and weight gradient (e4m3 C^T x e4m3 G, PAGEVEC_FP8_BWD)."""
     from dnn_page_vectors_amd.ops import embedding as eops
 
     g = torch.Generator().manual_seed(2)
@@ -1804,7 +1804,10 @@ def test_fp8_bag_matches_reference():
     print(f"fp8 bag vs reference-quantised {err:.2e}, vs exact fp32 (quantisation) {qerr:.3f}")
     assert qerr < 0.08
     gw = float((Wd.grad.cpu() - W.grad).abs().max() / W.grad.abs().max())
-    assert gw < 1e-2, gw  # bf16 dz on the GPU
+    # FP8_BWD (default): both sides quantise the gradient to e4m3 per tensor — the odd
+    # rounding tie differs (fp32 dz computed with / without FMAs); else the exact C^T G with
+    # bf16 dz on the GPU
+    assert gw < (5e-3 if eops.FP8_BWD else 1e-2), gw
     torch.testing.assert_close(bd.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
 
 
