@@ -952,7 +952,10 @@ PV_API int pv_add_ln_drop_fwd(const void* x, const float* xb, const void* r, con
 }
 
 namespace {
-int g_gelu_v = 2;  // pv_gelu_set_v: 1 = the round-2 vector kernels, 2 = the 128-thread unrolled ones
+// pv_gelu_set_v: 1 = the round-2 vector kernels; 2 (default) = the 128-thread unrolled backward
+// (296 vs 316 us per BERT layer call) with the v1 forward; 3 = the unrolled forward too
+// (183 vs 174 us: slower; tools/gelu_micro.py, profiles/r5_final/gelu_micro.log)
+int g_gelu_v = 2;
 constexpr int kGelu2Rpb = 32;
 }  // namespace
 
@@ -960,7 +963,7 @@ PV_API void pv_gelu_set_v(int v) { g_gelu_v = v; }
 
 PV_API int pv_bias_gelu_fwd(const void* x, const float* b, void* y, long n, int D, void* stream) {
   if (D % 2) return -1;
-  if (g_gelu_v == 2 && D % 8 == 0 && n / D <= 0x7FFFFFFFL) {
+  if (g_gelu_v == 3 && D % 8 == 0 && n / D <= 0x7FFFFFFFL) {  // measured slower than v1 (183 vs 174 us)
     const int M = (int)(n / D);
     dim3 grid((D / 8 + 127) / 128, (M + kGelu2Rpb - 1) / kGelu2Rpb);
     hipLaunchKernelGGL(pv::tfm::bias_gelu_fwd_vec2_kernel<4>, grid, dim3(128), 0, (hipStream_t)stream,
@@ -995,8 +998,8 @@ PV_API long pv_bias_gelu_bwd_ws(int M, int D) {
 PV_API int pv_bias_gelu_bwd(const void* x, const float* b, const void* dy, void* dx, float* db, float* ws, int M,
                             int D, void* stream) {
   if (D % 8 == 0 && ws) {
-    const int rpb = g_gelu_v == 2 ? kGelu2Rpb : kGeluRpb, R = (M + rpb - 1) / rpb;  // kGelu2Rpb >= kGeluRpb
-    if (g_gelu_v == 2) {
+    const int rpb = g_gelu_v >= 2 ? kGelu2Rpb : kGeluRpb, R = (M + rpb - 1) / rpb;  // kGelu2Rpb >= kGeluRpb
+    if (g_gelu_v >= 2) {
       dim3 grid((D / 8 + 127) / 128, R);
       hipLaunchKernelGGL(pv::tfm::bias_gelu_bwd_vec2_kernel<4>, grid, dim3(128), 0, (hipStream_t)stream,
                          (const unsigned short*)x, b, (const unsigned short*)dy, (unsigned short*)dx, ws, M, D, rpb);

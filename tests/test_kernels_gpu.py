@@ -568,7 +568,7 @@ def test_add_layernorm_and_bias_gelu(D):
     orf = torch.nn.functional.gelu(ur + bbr, approximate="tanh")
     (orf * do).sum().backward()
     outs = {}
-    for gv in (1, 2):  # round-2 vector kernels / 128-thread unrolled ones (pv_gelu_set_v)
+    for gv in (1, 2, 3):  # round-2 vector kernels / unrolled backward / unrolled both (pv_gelu_set_v)
         lib().pv_gelu_set_v(gv)
         try:
             u, bb = u0.clone().requires_grad_(True), bb0.clone().requires_grad_(True)
@@ -580,7 +580,8 @@ def test_add_layernorm_and_bias_gelu(D):
             outs[gv] = (o, u.grad)
         finally:
             lib().pv_gelu_set_v(2)
-    assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])  # same per-element math
+    for gv in (2, 3):  # same per-element math
+        assert torch.equal(outs[1][0], outs[gv][0]) and torch.equal(outs[1][1], outs[gv][1])
 
 
 @pytest.mark.parametrize("L", [37, 64, 300])  # generic / register (<=256) / register (<=512) softmax
