@@ -57,6 +57,15 @@ def test_bench_spawns_ranks_for_gpus_n():
     assert out["config"]["dist_backend"] == "gloo" and out["config"]["launch"] == "bench-spawn"
     assert out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
     assert out["recall_candidates"] == 2 * 64 and out["dry_run"] is True
+    # the driver's JSON contract
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["higher_is_better"] is True and out["scaling"] == "weak"
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in out["config"], k
+    knobs = out["runtime_knobs"]  # every PAGEVEC_* and HIP knob in effect, with the HIP defaults
+    assert "GPU_MAX_HW_QUEUES" in knobs and "HSA_ENABLE_IPC_MODE_LEGACY" in knobs
 
 
 def test_bench_rejects_world_size_mismatch():
