@@ -350,14 +350,15 @@ def preset_config(name: str) -> Configuration:
                              embedding_dim=512, mlp_dims=(512, 512, 128), batch_size=4096,
                              dtype="bf16", loss_mode="cross_gpu", J=0, cos_clip=False, lr=3e-3)
     if name in ("bert_dp8", "config4"):
-        # recipe (round-5 sweep, profiles/r5_bert/, Recall@10 after the 200-step bench
-        # protocol): lr 2e-5 with the reference's softmax scale 10 and [0, 1] cosine clip 0.25;
-        # scale 20: 0.34 (clip) / 0.38 (no clip); lr 1e-4 + warmup collapses (loss stays ln B),
-        # 3e-5 / 5e-5 0.27 / 0.19.  The fp32 parity arm at full depth (12 layers, B 64) agrees
-        # with the HIP step (tail loss 0.2 %, Recall@10 0.002 apart: tools/bert_parity.py)
+        # recipe (round-5 sweeps, profiles/r5_bert/ + r5_bq2/, Recall@10 after the 200-step
+        # bench protocol): lr 2e-5 with the reference's softmax scale 10 and [0, 1] cosine clip
+        # 0.25; scale 20 without the clip: lr 2e-5 0.25-0.38 (five runs), 3e-5 0.42 / 0.42,
+        # 5e-5 (20 warmup steps) 0.19 / 0.09, 1e-4 collapses (loss stays ln B); scale 30 0.31,
+        # 40 0.06.  The fp32 parity arm at full depth (12 layers, B 64) agrees with the HIP step
+        # (tail loss 0.2 %, Recall@10 0.002 apart: tools/bert_parity.py)
         return Configuration(model="bert", feature_level="word", vocab_hash_size=30522,
                              query_length=32, document_length=256, batch_size=256,
-                             dtype="bf16", loss_mode="cross_gpu", J=0, lr=2e-5,
+                             dtype="bf16", loss_mode="cross_gpu", J=0, lr=3e-5,
                              inbatch_gamma=20.0, cos_clip=False)
     if name in ("longpage_fp8", "config5"):
         return Configuration(model="chunked", feature_level="ngram", vocab_hash_size=30000,
