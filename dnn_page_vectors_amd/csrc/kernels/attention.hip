@@ -220,6 +220,149 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_fwd_kernel(const un
   }
 }
 
+// DMA variant of the forward (pv_attn_set_fwd_dma): K / V tiles land in LDS by
+// global_load_lds_dwordx4 instead of global loads into staging VGPRs + ds_write_b128.  The
+// [64][LDT] tile image is 576 consecutive 16-byte chunks (LDT = 72 elements = 9 chunks), so
+// piece p (one wave-instruction, 1 KB) writes chunks 64p .. 64p + 63: chunk q -> row q / 9,
+// column chunk q % 9 (the pad chunk 8 re-reads chunk 0); rows >= L re-read row L - 1 (finite
+// data, masked by mk).  Tile k + 1's pieces are issued before tile k's math and waited for
+// (own vmcnt) + one barrier after it.
+__device__ __forceinline__ void attn_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void dma_tile(const unsigned short* __restrict__ base, size_t ld, int r0, int L,
+                                         unsigned short* t) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int pc = wave + 4 * u;  // pieces 0..8
+    if (pc < 9) {
+      const int q = pc * 64 + lane;
+      const int r = q / 9, c = q - 9 * (q / 9);
+      const int row = min(r0 + r, L - 1);
+      attn_glds16(base + (size_t)row * ld + (c < 8 ? c : 0) * 8, reinterpret_cast<char*>(t) + pc * 1024);
+    }
+  }
+}
+
+template <int QG>
+__global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_fwd_dma_kernel(const unsigned short* __restrict__ qkv,
+                                                                            const int* __restrict__ mask,
+                                                                            unsigned short* __restrict__ out,
+                                                                            float* __restrict__ lse, int L, int H,
+                                                                            float scale) {
+  __shared__ __attribute__((aligned(1024))) unsigned short kt[2][TB * LDT];
+  __shared__ __attribute__((aligned(1024))) unsigned short vt[2][TB * LDT];
+  __shared__ float mk[2][TB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int n = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * TB * QG + wave * 16 * QG;
+  const size_t ld = (size_t)3 * H * HD;
+  const unsigned short* Q = qkv + (size_t)n * L * ld + (size_t)h * HD;
+  const unsigned short* K = Q + (size_t)H * HD;
+  const unsigned short* V = Q + (size_t)2 * H * HD;
+  const int* mrow = mask ? mask + (size_t)n * L : nullptr;
+  const float sl = scale * LOG2E;
+  bf16x8 qb[QG][2];
+  f32x4 o[QG][4];
+  float m[QG], l[QG];
+#pragma unroll
+  for (int j = 0; j < QG; ++j) {
+    glob_frag(Q, ld, q0 + 16 * j + (lane & 15), L, qb[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
+  dma_tile(K, ld, 0, L, kt[0]);
+  dma_tile(V, ld, 0, L, vt[0]);
+  float smk = 0.f;
+  if (threadIdx.x < TB) mk[0][threadIdx.x] = (threadIdx.x < L && (!mrow || mrow[threadIdx.x])) ? 1.f : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < L; k0 += TB, buf ^= 1) {
+    const bool more = k0 + TB < L;
+    if (more) {  // the other buffer was released by the previous iteration's barrier
+      dma_tile(K, ld, k0 + TB, L, kt[buf ^ 1]);
+      dma_tile(V, ld, k0 + TB, L, vt[buf ^ 1]);
+      if (threadIdx.x < TB) {
+        const int kk = k0 + TB + threadIdx.x;
+        smk = (kk < L && (!mrow || mrow[kk])) ? 1.f : 0.f;
+      }
+    }
+    f32x4 s[QG][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int j = 0; j < QG; ++j) s[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 a = row_frag(kt[buf], c * 16, st);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) s[j][c] = MFMA(a, qb[j][st], s[j][c]);
+      }
+    }
+    bf16x8 pb[QG][2];
+#pragma unroll
+    for (int j = 0; j < QG; ++j) {
+      float bm = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float keep = mk[buf][c * 16 + 4 * g + r];
+          s[j][c][r] = keep != 0.f ? s[j][c][r] * sl : -INFINITY;
+          bm = fmaxf(bm, s[j][c][r]);
+        }
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m[j], bm);
+      const float corr = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(m[j] - mn);
+      m[j] = mn;
+      l[j] *= corr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[j][i] *= corr;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = s[j][c][r] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[j][c][r] - mn);
+          s[j][c][r] = pv;
+          l[j] += pv;
+        }
+      pack_b(s[j], pb[j]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 a = tr_frag(vt[buf], s2, i * 16);
+#pragma unroll
+        for (int j = 0; j < QG; ++j) o[j][i] = MFMA(a, pb[j][s2], o[j][i]);
+      }
+    if (more && threadIdx.x < TB) mk[buf ^ 1][threadIdx.x] = smk;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of the next tile
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < QG; ++j) {
+    float lj = l[j];
+    lj += __shfl_xor(lj, 16, 64);
+    lj += __shfl_xor(lj, 32, 64);
+    const int q = q0 + 16 * j + (lane & 15);
+    if (q < L) {
+      const float inv = lj > 0.f ? 1.f / lj : 0.f;
+      unsigned short* orow = out + ((size_t)n * L + q) * H * HD + (size_t)h * HD;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint2*>(orow + i * 16 + 4 * g) =
+            uint2{pack_bf16x2(o[j][i][0] * inv, o[j][i][1] * inv), pack_bf16x2(o[j][i][2] * inv, o[j][i][3] * inv)};
+      if (g == 0) lse[((size_t)n * H + h) * L + q] = m[j] + __log2f(lj);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- backward
 // D[n,h,q] = sum_d dO * O ; one wave per (n, q), lanes over heads x 16 pieces
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const unsigned short* __restrict__ dout,
@@ -532,8 +675,11 @@ namespace {
 // QG 2 for dQ only (dK dV with 2: 473; QG 4: 1 wave per SIMD, slower everywhere); L 32 (the
 // query segments) stays at QG 1 — a 128-row workgroup would be mostly empty)
 int g_qg_fwd = 0, g_qg_dq = 0, g_qg_dkdv = 0;
+int g_fwd_dma = 0;  // pv_attn_set_fwd_dma: K / V tiles by LDS-DMA in the forward (A/B)
 int qg_or(int v, int def) { return (v == 1 || v == 2 || v == 4) ? v : def; }
 }  // namespace
+
+PV_API void pv_attn_set_fwd_dma(int on) { g_fwd_dma = on; }
 
 PV_API void pv_attn_set_qg(int fwd, int dq, int dkdv) {
   g_qg_fwd = fwd;
@@ -548,9 +694,13 @@ PV_API int pv_attn_fwd(const void* qkv, const int* mask, void* out, float* lse, 
   if (N <= 0 || L <= 0 || H <= 0) return -1;
   const int qg = qg_or(g_qg_fwd, L >= 128 ? 2 : 1);
 #define PV_AFWD(QGV)                                                                                            hipLaunchKernelGGL(attn_fwd_kernel<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0,                            (hipStream_t)stream, (const unsigned short*)qkv, mask, (unsigned short*)out, lse, L, H, scale)
-  if (qg == 4) PV_AFWD(4);
-  else if (qg == 2) PV_AFWD(2);
-  else PV_AFWD(1);
+  if (qg == 4) {
+    PV_AFWD(4);
+  } else if (qg == 2) {
+    PV_AFWD(2);
+  } else {
+    PV_AFWD(1);
+  }
 #undef PV_AFWD
   PV_LAUNCH_CHECK();
   return 0;

@@ -98,6 +98,7 @@ SIGS = {
     "pv_lt_gemm": "ii" "iii" "pi" "pi" "pi" "i" "f" "pi" "p" "i" "pl" "p",
     "pv_lt_set_tune": "i",
     "pv_attn_set_qg": "iii",
+    "pv_attn_set_fwd_dma": "i",
     "pv_gelu_set_v": "i",
     "pv_ln_set_rpw": "i",
     "pv_transpose_u8": "pl" "ii" "pl" "p",

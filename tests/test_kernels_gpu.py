@@ -759,8 +759,8 @@ def test_debug_kernels_flag_bad_ids_without_faulting():
 
 
 @pytest.mark.parametrize("L,H", [(32, 4), (37, 4), (64, 12), (65, 4), (200, 4), (256, 12), (300, 6)])
-@pytest.mark.parametrize("qg", [1, 2, 4])
-def test_fused_attention_packed_qkv(L, H, qg):
+@pytest.mark.parametrize("qg,dma", [(1, 0), (2, 0), (4, 0), (1, 1), (2, 1)])
+def test_fused_attention_packed_qkv(L, H, qg, dma):
     """attention.hip (online softmax fwd, dK/dV + dQ bwd) vs an fp32 reference on the same
     bf16 packed QKV, with key padding; qg = 16-row groups per wave of every kernel (the
     workgroup owns 64 qg rows; partial blocks at L = 37 / 65 / 200 / 300)."""
@@ -768,10 +768,12 @@ def test_fused_attention_packed_qkv(L, H, qg):
     from dnn_page_vectors_amd.ops._common import lib
 
     lib().pv_attn_set_qg(qg, qg, qg)
+    lib().pv_attn_set_fwd_dma(dma)  # forward K / V tiles by LDS-DMA
     try:
         _attention_case(L, H, tops)
     finally:
         lib().pv_attn_set_qg(0, 0, 0)
+        lib().pv_attn_set_fwd_dma(0)
 
 
 def _attention_case(L, H, tops):

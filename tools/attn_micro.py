@@ -46,6 +46,12 @@ def main():
                 lib().pv_attn_set_qg(qg, qg, qg)
                 res[f"L{L}_qg{qg}_fwd_r{rnd}"] = ev(fwd)
                 res[f"L{L}_qg{qg}_bwd_r{rnd}"] = ev(bwd)
+        for qg in (1, 2):
+            for rnd in range(2):
+                lib().pv_attn_set_qg(qg, qg, qg)
+                lib().pv_attn_set_fwd_dma(1)
+                res[f"L{L}_qg{qg}_fwd_dma_r{rnd}"] = ev(fwd)
+            lib().pv_attn_set_fwd_dma(0)
         for qf, qq, qk in ((1, 1, 2), (1, 2, 1), (2, 1, 1), (4, 1, 1), (1, 4, 1), (1, 1, 4)):
             lib().pv_attn_set_qg(qf, qq, qk)
             res[f"L{L}_bwd_dq{qq}_dkdv{qk}"] = ev(bwd)
