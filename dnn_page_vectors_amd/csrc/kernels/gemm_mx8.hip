@@ -92,8 +92,15 @@ __device__ __forceinline__ float act_f(float x, int act) {
   return x;
 }
 
+// NS staging buffers: NS = 2 (round 3) stages tile kt + 2 after tile kt's barrier, i.e. one
+// tile (~1000 MFMA cycles per SIMD, ~0.4 us) ahead — less than the HBM latency under load,
+// and the round-5 PMC pass showed 55 % of wave-cycles waiting (35 % MFMA busy,
+// profiles/r5_mx8/).  NS = 3 (144 KB of LDS) keeps two tiles in flight: tile kt + 3 is staged
+// into tile kt's buffer, and the switch waits only for tile kt + 1 (vmcnt(6): the 6 DMA
+// pieces a wave issues per tile for kt + 2 may still be in flight).
+template <int NS>
 __global__ __launch_bounds__(NTH, 1) void gemm_mx8_kernel(Params p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][A | B]
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [NS][A | B]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -120,11 +127,20 @@ __global__ __launch_bounds__(NTH, 1) void gemm_mx8_kernel(Params p) {
     stage_ptrs<BN>(p.B, p.ldb, n0, p.N - 1, wave, sb);
     stage<BM>(sa, kt0 * BK, smem, wave);
     stage<BN>(sb, kt0 * BK, smem + A_BYTES, wave);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (NS == 3) {  // tile kt0 + 1 in flight behind tile kt0 (clamped: never read past kt1)
+      const int k1 = min(kt0 + 1, kt1 - 1) * BK;
+      stage<BM>(sa, k1, smem + STAGE, wave);
+      stage<BN>(sb, k1, smem + STAGE + A_BYTES, wave);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    if (kt0 + 1 < kt1) {
-      stage<BM>(sa, (kt0 + 1) * BK, smem + STAGE, wave);
-      stage<BN>(sb, (kt0 + 1) * BK, smem + STAGE + A_BYTES, wave);
+    {
+      const int k2 = min(kt0 + NS - 1, kt1 - 1) * BK;  // NS = 2: kt0 + 1; NS = 3: kt0 + 2
+      char* st = smem + (NS - 1) * STAGE;
+      stage<BM>(sa, k2, st, wave);
+      stage<BN>(sb, k2, st + A_BYTES, wave);
     }
     // B fragments of a whole K tile (4) double-buffered across tiles; A fragments streamed
     // one 16-row block at a time (read block i + 1 while block i's 4 MFMAs run): 64 acc +
@@ -151,13 +167,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_mx8_kernel(Params p) {
       for (int j = 0; j < 4; ++j) acc[2][j] = mx(a0, bc[j], acc[2][j]);
       __builtin_amdgcn_sched_barrier(0);
       // branch-free tile switch (one basic block, so the sched_barriers hold): the reads of
-      // the next tile's first fragments and the staging of the tile after next are issued
-      // unconditionally — past the split's end they re-read / re-load a clamped tile into the
+      // the next tile's first fragments and the staging of the tile NS - 1 ahead are issued
+      // unconditionally — past the split's end they re-read / re-load a clamped tile into a
       // buffer nobody reads again
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __syncthreads();
+      const int nbuf = buf + 1 == NS ? 0 : buf + 1;
       {
-        const char* nt = smem + (buf ^ 1) * STAGE;
+        const char* nt = smem + nbuf * STAGE;
 #pragma unroll
         for (int j = 0; j < 4; ++j) bn[j] = frag(nt + A_BYTES, brb + 16 * j);
         a0 = frag(nt, arb);
@@ -168,16 +186,18 @@ __global__ __launch_bounds__(NTH, 1) void gemm_mx8_kernel(Params p) {
       __builtin_amdgcn_sched_barrier(0);
       {
         char* st = smem + buf * STAGE;
-        const int k2 = min(kt + 2, kt1 - 1) * BK;
+        const int k2 = min(kt + NS, kt1 - 1) * BK;
         stage<BM>(sa, k2, st, wave);
         stage<BN>(sb, k2, st + A_BYTES, wave);
       }
+      return nbuf;
     };
+    int buf = 0;
 #pragma unroll 1
     for (int kt = kt0; kt < kt1; kt += 2) {
-      tile(kt, 0, b[0], b[1]);
+      buf = tile(kt, buf, b[0], b[1]);
       if (kt + 1 >= kt1) break;
-      tile(kt + 1, 1, b[1], b[0]);
+      buf = tile(kt + 1, buf, b[1], b[0]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped extra loads land before exit
   }
@@ -227,6 +247,15 @@ PV_DEBUG_EXPORT(gemm8)
 
 using namespace pv;
 
+namespace {
+// pv_gemm_mx8_set_stages: staging buffers (2 = round 3, 3 = two tiles in flight); measured equal
+// (bag forward 68-76 vs 74-78 us, weight gradient 90-94 vs 91-93, square 8192 1.69-1.71 PF/s
+// both; profiles/r5_mx8/): the waits the PMC pass counts are not the DMA latency
+int g_mx8_stages = 2;
+}  // namespace
+
+PV_API void pv_gemm_mx8_set_stages(int n) { g_mx8_stages = n; }
+
 // C = epi(alpha * (*alpha_ptr) * A8 . B8^T); A8 (M x K) and B8 (N x K) e4m3 bytes, K % 128 == 0,
 // 16-byte aligned rows.  ksplit > 1: C is a workspace of ksplit fp32 slabs (slab = elements
 // per slab) the caller reduces; bias / act / bf16 then belong to the caller's reduction.
@@ -241,15 +270,20 @@ PV_API int pv_gemm_mx8(const void* A, long lda, const void* B, long ldb, void* C
   if (act != 0 && act != 1 && act != 3) return -4;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mx8_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mx8_kernel<2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mx8_kernel<3>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 3 * STAGE) != hipSuccess)
       return -5;
     attr = true;
   }
   Params p{(const unsigned char*)A, (const unsigned char*)B, lda, ldb, C, ldc, M, N, K, ksplit, slab, bias, alpha,
            alpha_ptr, act, out_bf16, (M + BM - 1) / BM, (N + BN - 1) / BN, N <= M ? 1 : 0};
   const int grid = p.tiles_m * p.tiles_n * ksplit;
-  hipLaunchKernelGGL(gemm_mx8_kernel, dim3(grid), dim3(NTH), 2 * STAGE, (hipStream_t)stream, p);
+  if (g_mx8_stages == 3)
+    hipLaunchKernelGGL(gemm_mx8_kernel<3>, dim3(grid), dim3(NTH), 3 * STAGE, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(gemm_mx8_kernel<2>, dim3(grid), dim3(NTH), 2 * STAGE, (hipStream_t)stream, p);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -99,6 +99,7 @@ SIGS = {
     "pv_lt_set_tune": "i",
     "pv_attn_set_qg": "iii",
     "pv_attn_set_fwd_dma": "i",
+    "pv_gemm_mx8_set_stages": "i",
     "pv_gelu_set_v": "i",
     "pv_ln_set_rpw": "i",
     "pv_transpose_u8": "pl" "ii" "pl" "p",

@@ -1738,8 +1738,18 @@ def test_gemm_mx8(M, N, K, ks):
     a8 = A.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
     b8 = B.to(torch.float8_e4m3fn).view(torch.uint8).to(DEV)
     amax = torch.tensor([3.0], device=DEV)
-    out = fops.gemm_mx8(a8, b8, 0.25, amax, ksplit=ks)
+    from dnn_page_vectors_amd.ops._common import lib
+
+    outs = []
+    for ns in (2, 3):  # staging buffers: same MFMA order, bit-identical results
+        lib().pv_gemm_mx8_set_stages(ns)
+        try:
+            outs.append(fops.gemm_mx8(a8, b8, 0.25, amax, ksplit=ks))
+        finally:
+            lib().pv_gemm_mx8_set_stages(2)
     torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    out = outs[1]
     c = out.sum(0) if out.dim() == 3 else out
     want = 0.75 * (A.double() @ B.double().t())
     err = float((c.cpu().double() - want).abs().max() / want.abs().max())
