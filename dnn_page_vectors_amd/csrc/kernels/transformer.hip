@@ -331,7 +331,10 @@ __global__ __launch_bounds__(256) void add_ln_drop_fwd2_kernel(const unsigned sh
 // vectors of dy and x_hat in registers (one read of each), the two row means are wave
 // reductions (no barriers), and dgamma/dbeta accumulate in registers over the rows this
 // wave owns; the 4 waves of a block combine through LDS and issue one atomic per column.
-template <int VPT>
+// PF = 1: the next row's dy / h / statistics are loaded before this row's math (the rows of a
+// wave are gridDim.x * 4 apart, so without it each row's loads start only after the previous
+// row's stores); same per-row arithmetic and accumulation order: bit-identical to PF = 0.
+template <int VPT, int PF = 0>
 __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned short* __restrict__ dy,
                                                                  const unsigned short* __restrict__ hsum,
                                                                  const float* __restrict__ gamma,
@@ -359,15 +362,58 @@ __global__ __launch_bounds__(256) void layernorm_bwd_rows_kernel(const unsigned 
       gc[i][k] = 0.f;
     }
   }
-  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
+  const int rstride = gridDim.x * 4;
+  uint2 gvn[VPT], hvn[VPT];
+  float mun = 0.f, rsn = 0.f;
+  if (PF && blockIdx.x * 4 + wave < M) {
+    const int r = blockIdx.x * 4 + wave;
+    mun = mean[r];
+    rsn = rstd[r];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const size_t o = (size_t)r * D + (i * 64 + lane) * 4;
+      gvn[i] = *reinterpret_cast<const uint2*>(dy + o);
+      hvn[i] = *reinterpret_cast<const uint2*>(hsum + o);
+    }
+  }
+  for (int row = blockIdx.x * 4 + wave; row < M; row += rstride) {
+    float mu, rs;
+    uint2 gvc[VPT], hvc[VPT];
+    if (PF) {
+      mu = mun;
+      rs = rsn;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        gvc[i] = gvn[i];
+        hvc[i] = hvn[i];
+      }
+      const int nr = row + rstride;
+      if (nr < M) {
+        mun = mean[nr];
+        rsn = rstd[nr];
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+          const size_t o = (size_t)nr * D + (i * 64 + lane) * 4;
+          gvn[i] = *reinterpret_cast<const uint2*>(dy + o);
+          hvn[i] = *reinterpret_cast<const uint2*>(hsum + o);
+        }
+      }
+    } else {
+      mu = mean[row];
+      rs = rstd[row];
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const size_t o = (size_t)row * D + (i * 64 + lane) * 4;
+        gvc[i] = *reinterpret_cast<const uint2*>(dy + o);
+        hvc[i] = *reinterpret_cast<const uint2*>(hsum + o);
+      }
+    }
     float g[VPT][4], xh[VPT][4];
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
-      const size_t o = (size_t)row * D + (i * 64 + lane) * 4;
-      const uint2 gv = *reinterpret_cast<const uint2*>(dy + o);
-      const uint2 hv = *reinterpret_cast<const uint2*>(hsum + o);
+      const uint2 gv = gvc[i];
+      const uint2 hv = hvc[i];
       const unsigned gw[2] = {gv.x, gv.y}, hw[2] = {hv.x, hv.y};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -844,6 +890,11 @@ PV_API long pv_layernorm_bwd_ws(int M, int D) {
   return ln_rows_ok(D) ? (long)ln_blocks(M) * 3 * D + 3L * pv::tfm::kColSplits * D : 0;  // room for dbias
 }
 
+namespace {
+int g_ln_rpw = 2;     // pv_ln_set_rpw: rows per wave of the add + LN forward (1 = the v1 kernel)
+int g_ln_bwd_pf = 1;  // pv_ln_bwd_set_pf: next-row prefetch in the LN backward (0 = round-3 kernel)
+}  // namespace
+
 // dgamma/dbeta are overwritten on the wave-per-row path (D in {256,512,768,1024}, ws given)
 static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gamma, const float* mean,
                               const float* rstd, void* dx, float* dgamma, float* dbeta, float* ws, int M, int D,
@@ -854,6 +905,11 @@ static int layernorm_bwd_impl(const void* dy, const void* hsum, const float* gam
 #define PV_LN_ROWS(VPT)                                                                                          \
   {                                                                                                              \
     const int np = dxb ? 3 : 2;                                                                                  \
+    if (g_ln_bwd_pf)                                                                                             \
+      hipLaunchKernelGGL((pv::tfm::layernorm_bwd_rows_kernel<VPT, 1>), dim3(blocks), dim3(256), 0, st,             \
+                         (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,              \
+                         (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr, np);      \
+    else                                                                                                         \
     hipLaunchKernelGGL(pv::tfm::layernorm_bwd_rows_kernel<VPT>, dim3(blocks), dim3(256), 0, st,                  \
                        (const unsigned short*)dy, (const unsigned short*)hsum, gamma, mean, rstd,                \
                        (unsigned short*)dx, ws, M, (unsigned short*)dxm, thr, scale, seed, seed_ptr, np);        \
@@ -912,9 +968,7 @@ PV_API int pv_layernorm_bwd_drop(const void* dy, const void* hsum, const float* 
                             seed_ptr, dxb, stream);
 }
 
-namespace {
-int g_ln_rpw = 2;  // pv_ln_set_rpw: rows per wave of the add + LN forward (1 = the v1 kernel)
-}  // namespace
+PV_API void pv_ln_bwd_set_pf(int on) { g_ln_bwd_pf = on; }
 
 PV_API void pv_ln_set_rpw(int rpw) { g_ln_rpw = rpw; }
 

@@ -102,6 +102,7 @@ SIGS = {
     "pv_gemm_mx8_set_stages": "i",
     "pv_gelu_set_v": "i",
     "pv_ln_set_rpw": "i",
+    "pv_ln_bwd_set_pf": "i",
     "pv_transpose_u8": "pl" "ii" "pl" "p",
     # loss.hip wide-vector (D = 768) flash passes
     "pv_ibw_splits": "ii",

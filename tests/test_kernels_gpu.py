@@ -560,6 +560,19 @@ def test_add_layernorm_and_bias_gelu(D):
                 lib().pv_ln_set_rpw(2)
         for a_, b_ in ys[1:]:
             assert torch.equal(a_, ys[0][0]) and torch.equal(b_, ys[0][1])
+        # LN backward with / without the next-row prefetch (pv_ln_bwd_set_pf): bit-identical
+        grads = []
+        for pf in (0, 1):
+            lib().pv_ln_bwd_set_pf(pf)
+            try:
+                xx, rr_ = x.detach().clone().requires_grad_(True), r.detach().clone().requires_grad_(True)
+                gg, bb_ = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+                (tops.add_layernorm(xx, rr_, gg, bb_, p=0.1, seed=7).float() * dy).sum().backward()
+                grads.append((xx.grad, rr_.grad, gg.grad, bb_.grad))
+            finally:
+                lib().pv_ln_bwd_set_pf(1)
+        for u_, v_ in zip(*grads):
+            assert torch.equal(u_, v_)
 
     u0 = torch.randn(M, 3072, device=DEV).bfloat16()
     bb0 = torch.randn(3072, device=DEV)

@@ -54,6 +54,18 @@ def main():
             r[f"addln_rpw{rpw}_r{rnd}"] = ev(lambda: lib().pv_add_ln_drop_fwd(
                 P(xa), P(xb_), P(ra), P(g_), P(b_), P(ya), P(ha), P(mu), P(rs), M, H, 1e-12, 26, 256.0 / 230, 7, None, s))
     lib().pv_ln_set_rpw(2)
+    # LN backward (with the dropout-branch output) with / without the next-row prefetch
+    dya = torch.randn(M, H, device=dev).bfloat16()
+    dxa, dxm = torch.empty_like(xa), torch.empty_like(xa)
+    dgam, dbet, dxb = torch.empty(H, device=dev), torch.empty(H, device=dev), torch.empty(H, device=dev)
+    wsl = torch.empty(lib().pv_layernorm_bwd_ws(M, H), device=dev)
+    for rnd in range(2):
+        for pf in (0, 1):
+            lib().pv_ln_bwd_set_pf(pf)
+            r[f"lnbwd_pf{pf}_r{rnd}"] = ev(lambda: lib().pv_layernorm_bwd_drop(
+                P(dya), P(ha), P(g_), P(mu), P(rs), P(dxa), P(dxm), P(dgam), P(dbet), P(dxb), P(wsl), M, H, 26,
+                256.0 / 230, 7, None, s))
+    lib().pv_ln_bwd_set_pf(1)
     r["addln_best_TBps"] = round(4 * M * H * 2 / 1e9 / min(v for k, v in r.items() if k.startswith("addln")) * 1e3, 2)
     gb = M * D * 2 / 1e9
     r["fwd_v1_TBps"] = round(2 * gb / min(r["fwd_v1_r0"], r["fwd_v1_r1"]) * 1e6 / 1e3, 2)
