@@ -39,6 +39,11 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_F32_MASK": ("ab", "1", "fp32 forward dropout keep-bit plane"),
     # bags, dense, loss, optimizer
     "PAGEVEC_BAG_SPARSE_BWD": ("ab", "1", "short-bag backward by sorted token runs"),
+    "PAGEVEC_BAG_EPW": ("ab", "64", "sorted entries per wave of the short-bag backward"),
+    "PAGEVEC_BAG_SPLITK": ("ab", "0", "vocabulary split of the counts GEMM (0 = auto)"),
+    "PAGEVEC_COLSUM": ("ab", "1", "column sums on the HIP kernel (0: torch reductions)"),
+    "PAGEVEC_WGRAD_WG": ("ab", "512", "dense-layer weight-gradient workgroup target"),
+    "PAGEVEC_QUERY_STREAM": ("ab", "1", "query tower on its own stream beside the page tower"),
     "PAGEVEC_BAG_COUNTS16": ("ab", "1", "16-bit packed LDS counts histogram"),
     "PAGEVEC_BAG_GEMM": ("ab", "lib", "long-bag GEMMs: hipBLASLt on the count matrix (lib) or bag_gemm.hip (hip)"),
     "PAGEVEC_FP8_BAG": ("ab", "1", "fp8 towers: page bag on the MX fp8 MFMA"),
