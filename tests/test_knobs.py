@@ -17,6 +17,9 @@ def test_every_env_knob_is_registered():
         with open(f) as fh:
             for m in _READ.finditer(fh.read()):
                 names.add(m.group(1) or m.group(2))
+    for f in glob.glob(os.path.join(REPO, "dnn_page_vectors_amd", "csrc", "**", "*.hip"), recursive=True):
+        with open(f) as fh:  # the kernels' own getenv() knobs
+            names.update(re.findall(r'getenv\("(PAGEVEC_[A-Z0-9_]+)"\)', fh.read()))
     assert names, "no knob reads found (pattern out of date?)"
     missing = sorted(names - set(knobs.KNOBS))
     assert not missing, f"register these in utils/knobs.py: {missing}"
