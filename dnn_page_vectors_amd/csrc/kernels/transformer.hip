@@ -592,6 +592,63 @@ __global__ __launch_bounds__(128) void bias_gelu_bwd_vec2_kernel(const unsigned 
   *reinterpret_cast<f32x4*>(pr + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
+// BERT embedding front end over the packed token batch (ops/transformer.py::bert_embed): token
+// t of group g (rows off_g .. off_g + N_g L_g, position (t - off_g) mod L_g) gets
+// bf16(word[id] + pos[l] + typ0) — one pass instead of the fp32 gather, two broadcast adds, a
+// cast and a cat.  A thread owns 8 columns of a row.
+struct EmbedGroups {
+  int off[4], L[4], n;
+};
+
+__global__ __launch_bounds__(256) void bert_embed_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ word,
+                                                             const float* __restrict__ pos,
+                                                             const float* __restrict__ typ0,
+                                                             unsigned short* __restrict__ out, long T, int H,
+                                                             EmbedGroups gr) {
+  const int c8n = H / 8;
+  const long total = T * c8n;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long t = i / c8n;
+    const int c = (int)(i - t * c8n) * 8;
+    int g = 0;
+    while (g + 1 < gr.n && t >= gr.off[g + 1]) ++g;
+    const int l = (int)((t - gr.off[g]) % gr.L[g]);
+    const float* w = word + (size_t)ids[t] * H + c;
+    const float* pp = pos + (size_t)l * H + c;
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(w), w1 = *reinterpret_cast<const f32x4*>(w + 4);
+    const f32x4 p0 = *reinterpret_cast<const f32x4*>(pp), p1 = *reinterpret_cast<const f32x4*>(pp + 4);
+    const f32x4 y0 = *reinterpret_cast<const f32x4*>(typ0 + c), y1 = *reinterpret_cast<const f32x4*>(typ0 + c + 4);
+    u32x4 o;
+    o[0] = pack_bf16x2(w0[0] + p0[0] + y0[0], w0[1] + p0[1] + y0[1]);
+    o[1] = pack_bf16x2(w0[2] + p0[2] + y0[2], w0[3] + p0[3] + y0[3]);
+    o[2] = pack_bf16x2(w1[0] + p1[0] + y1[0], w1[1] + p1[1] + y1[1]);
+    o[3] = pack_bf16x2(w1[2] + p1[2] + y1[2], w1[3] + p1[3] + y1[3]);
+    *reinterpret_cast<u32x4*>(out + (size_t)t * H + c) = o;
+  }
+}
+
+// word-table gradient: out[id[t]] += g[t] (fp32 atomics from the bf16 rows); an all-zero
+// 8-column piece (padding tokens: masked keys and unused queries carry exactly zero
+// gradient) issues no atomics, so the padding row is not a contention hot spot
+__global__ __launch_bounds__(256) void bert_embed_wgrad_kernel(const int* __restrict__ ids,
+                                                               const unsigned short* __restrict__ g,
+                                                               float* __restrict__ out, long T, int H) {
+  const int c8n = H / 8;
+  const long total = T * c8n;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long t = i / c8n;
+    const int c = (int)(i - t * c8n) * 8;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(g + (size_t)t * H + c);
+    if ((v[0] | v[1] | v[2] | v[3]) == 0u) continue;
+    float* o = out + (size_t)ids[t] * H + c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      atomicAdd(o + 2 * k, __uint_as_float(v[k] << 16));
+      atomicAdd(o + 2 * k + 1, __uint_as_float(v[k] & 0xFFFF0000u));
+    }
+  }
+}
+
 // Column sums in a fixed order, two stages: colsum_part (grid (ceil(D/64), S)) reduces
 // a 1/S slice of the rows of 64 columns with 4 row lanes + LDS into part2[S][D];
 // colsum_final adds the S partials.
@@ -1111,6 +1168,40 @@ PV_API int pv_softmax_bwd(const void* P, void* dP, long R, int L, float scale, v
   }
   hipLaunchKernelGGL(pv::tfm::softmax_bwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned short*)P, (unsigned short*)dP, R, L, scale);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Packed BERT embedding front end (bert_embed_fwd_kernel): ids (T) int32, word (V, H) / pos
+// (Lmax, H) / typ0 (H) fp32, out (T, H) bf16; groups: ng <= 4 (offset, L) pairs, offsets
+// ascending from 0.  H % 8 == 0.
+PV_API int pv_bert_embed_fwd(const int* ids, const float* word, const float* pos, const float* typ0, void* out, long T,
+                             int H, const int* offs, const int* lens, int ng, void* stream) {
+  if (T <= 0 || H % 8 || ng < 1 || ng > 4) return -1;
+  pv::tfm::EmbedGroups gr{};
+  for (int i = 0; i < ng; ++i) {
+    gr.off[i] = offs[i];
+    gr.L[i] = lens[i];
+    if (lens[i] <= 0) return -2;
+  }
+  gr.n = ng;
+  const long total = T * (H / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pv::tfm::bert_embed_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ids,
+                     word, pos, typ0, (unsigned short*)out, T, H, gr);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// out (V, H) fp32 += rows of g (T, H) bf16 at ids (atomics; all-zero pieces skipped)
+PV_API int pv_bert_embed_wgrad(const int* ids, const void* g, float* out, long T, int H, void* stream) {
+  if (T <= 0 || H % 8) return -1;
+  const long total = T * (H / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pv::tfm::bert_embed_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ids,
+                     (const unsigned short*)g, out, T, H);
   PV_LAUNCH_CHECK();
   return 0;
 }

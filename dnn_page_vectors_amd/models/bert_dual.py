@@ -153,15 +153,20 @@ class BertEncoder(nn.Module):
         dt = torch.bfloat16 if ids_list[0].is_cuda else torch.float32
         xs, masks, shapes = [], [], []
         for ids in ids_list:
-            ids = ids.long()
             N, L = ids.shape
             mask = (ids != 0)
             mask[:, 0] = True
-            xs.append((_row_gather(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
-                      .reshape(N * L, -1))
             masks.append(mask)
             shapes.append((N, L))
-        x = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
+        # one fused gather + position / type add + cast over every group (ops/transformer.py)
+        x = tops.bert_embed(self.word, self.pos, self.typ, ids_list)
+        if x is None:
+            for ids in ids_list:
+                ids = ids.long()
+                N, L = ids.shape
+                xs.append((_row_gather(ids, self.word) + self.pos[:L].unsqueeze(0) + self.typ[0]).to(dt)
+                          .reshape(N * L, -1))
+            x = torch.cat(xs, 0) if len(xs) > 1 else xs[0]
         x = tops.add_layernorm(x, None, self.ln_g, self.ln_b)
         if training and p_drop > 0:
             x = F.dropout(x, p_drop, True)

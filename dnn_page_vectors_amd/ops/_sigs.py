@@ -103,6 +103,8 @@ SIGS = {
     "pv_gelu_set_v": "i",
     "pv_ln_set_rpw": "i",
     "pv_ln_bwd_set_pf": "i",
+    "pv_bert_embed_fwd": "ppppp" "li" "ppi" "p",
+    "pv_bert_embed_wgrad": "ppp" "li" "p",
     "pv_transpose_u8": "pl" "ii" "pl" "p",
     # loss.hip wide-vector (D = 768) flash passes
     "pv_ibw_splits": "ii",

@@ -324,6 +324,83 @@ def packed_attention(qkv: torch.Tensor, masks, shapes, heads: int) -> torch.Tens
     return torch.cat(outs, 0)
 
 
+class _BertEmbedFn(torch.autograd.Function):
+    """BERT's embedding front end over the packed token batch: bf16(word[id] + pos[l] + typ[0])
+    in one kernel (transformer.hip::bert_embed_fwd_kernel) instead of an fp32 gather, two
+    broadcast adds, a cast and a cat per group.  Backward: the word-table rows by fp32 atomics
+    straight from the bf16 gradient into the flat gradient (all-zero padding pieces skipped),
+    the position rows as per-group sums over sequences, the type row as their total — each
+    table receives ONE gradient (the per-group lookups of the old path made the word table a
+    multi-use parameter: two zero-filled V x H temporaries, an add and a copy per step)."""
+
+    @staticmethod
+    def forward(ctx, word, pos, typ, ids_flat, groups):
+        import ctypes
+
+        T = ids_flat.numel()
+        H = word.shape[1]
+        out = torch.empty(T, H, dtype=torch.bfloat16, device=word.device)
+        offs, lens = [], []
+        off = 0
+        for N, L in groups:
+            offs.append(off)
+            lens.append(L)
+            off += N * L
+        if off != T:
+            raise ValueError("group shapes do not cover the packed ids")
+        oa, la = (ctypes.c_int * 4)(*offs), (ctypes.c_int * 4)(*lens)
+        check(lib().pv_bert_embed_fwd(P(ids_flat), P(word), P(pos), P(typ[0]), P(out), T, H,
+                                      ctypes.cast(oa, ctypes.c_void_p), ctypes.cast(la, ctypes.c_void_p), len(groups),
+                                      stream(word.device)), "pv_bert_embed_fwd")
+        ctx.save_for_backward(ids_flat)
+        ctx.groups = list(groups)
+        ctx.params = (word, pos, typ)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids_flat,) = ctx.saved_tensors
+        word, pos, typ = ctx.params
+        g = g.to(torch.bfloat16).contiguous()
+        T, H = g.shape
+        dword = dpos = dtyp = None
+        if ctx.needs_input_grad[0]:
+            tw = grad_sink.accum_target(word)
+            dst = tw if tw is not None else torch.zeros(word.shape, dtype=torch.float32, device=g.device)
+            check(lib().pv_bert_embed_wgrad(P(ids_flat), P(g), P(dst), T, H, stream(g.device)), "pv_bert_embed_wgrad")
+            if tw is not None:
+                grad_sink.done(word)
+            else:
+                dword = dst
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dpos = torch.zeros(pos.shape, dtype=torch.float32, device=g.device)
+            off = 0
+            for N, L in ctx.groups:
+                dpos[:L] += torch.sum(g[off:off + N * L].view(N, L, H), dim=0, dtype=torch.float32)
+                off += N * L
+            if ctx.needs_input_grad[2]:
+                dtyp = torch.zeros(typ.shape, dtype=torch.float32, device=g.device)
+                dtyp[0] = dpos.sum(0)
+            if not ctx.needs_input_grad[1]:
+                dpos = None
+        return dword, dpos, dtyp, None, None
+
+
+def bert_embed(word: torch.Tensor, pos: torch.Tensor, typ: torch.Tensor, ids_list) -> Optional[torch.Tensor]:
+    """Packed (T, H) bf16 embeddings of several id batches, or None off the HIP path."""
+    if not (use_hip(word) and word.shape[1] % 8 == 0 and len(ids_list) <= 4 and BERT_EMBED):
+        return None
+    from ..parallel.sparse_rows import note_rows
+
+    flat = torch.cat([i.reshape(-1) for i in ids_list]).to(torch.int32) if len(ids_list) > 1 \
+        else ids_list[0].reshape(-1).to(torch.int32)
+    note_rows(word, flat)  # row-sparse table gradients (parallel/sparse_rows.py) record the rows
+    return _BertEmbedFn.apply(word, pos, typ, flat.contiguous(), [tuple(i.shape) for i in ids_list])
+
+
+BERT_EMBED = os.environ.get("PAGEVEC_BERT_EMBED", "1") != "0"
+
+
 # bf16 copies of fp32 master weights, refreshed once per optimizer step (generation counter
 # of models.base: bump_generation() after every update)
 _W16 = {}

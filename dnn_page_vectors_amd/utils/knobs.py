@@ -54,6 +54,7 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),
+    "PAGEVEC_BERT_EMBED": ("ab", "1", "BERT embedding front end as one fused gather + add kernel"),
     "PAGEVEC_FFN_LT": ("ab", "1", "BERT FFN bias + GELU (and its backward) in hipBLASLt GEMM epilogues"),
     "PAGEVEC_IB": ("ab", "5", "in-batch loss kernel generation"),
     "PAGEVEC_IB_WIDE": ("ab", "1", "wide-vector (D = 768) loss on the ibw flash kernel (0: fp32 S blocks + GEMMs)"),

@@ -1857,3 +1857,36 @@ def test_conv_pool_backward_dw_stream_placement(side, monkeypatch):
         grads.append([t.grad, w3.grad, w4.grad, b3.grad, b4.grad])
     for u, v in zip(*grads):
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5)
+
+
+def test_bert_embed_fused_matches_unfused(monkeypatch):
+    """transformer.hip::bert_embed_* (the packed front end: one gather + position / type add +
+    bf16 cast; word rows by atomics, position / type rows by per-group sums) against the
+    per-group torch path of BertEncoder.forward_multi: forward bit-identical, gradients equal up
+    to the summation order."""
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    torch.manual_seed(3)
+    V, H, Lmax = 500, 64, 40
+    word0 = torch.randn(V, H, device=DEV) * 0.1
+    pos0 = torch.randn(Lmax, H, device=DEV) * 0.1
+    typ0 = torch.randn(2, H, device=DEV) * 0.1
+    q = torch.randint(1, V, (7, 12), device=DEV)
+    d = torch.randint(0, V, (5, 33), device=DEV)
+    d[:, 20:] = 0  # padding tail
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(tops, "BERT_EMBED", fused)
+        word, pos, typ = (t.clone().requires_grad_(True) for t in (word0, pos0, typ0))
+        x = tops.bert_embed(word, pos, typ, [q, d])
+        if x is None:
+            xs = [(word[i.long()] + pos[:i.shape[1]].unsqueeze(0) + typ[0]).to(torch.bfloat16).reshape(-1, H)
+                  for i in (q, d)]
+            x = torch.cat(xs, 0)
+        gy = torch.randn(x.shape, device=DEV)
+        gy[7 * 12:].view(5, 33, H)[:, 20:] = 0  # padding rows carry no gradient, as in the model
+        (x.float() * gy).sum().backward()
+        out[fused] = (x, word.grad, pos.grad, typ.grad)
+    assert torch.equal(out[True][0], out[False][0])
+    for a, b in zip(out[True][1:], out[False][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)

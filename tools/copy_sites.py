@@ -4,7 +4,6 @@ with their GPU time.   python tools/copy_sites.py [--preset bert_dp8]"""
 import argparse
 import os
 import sys
-from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -29,21 +28,42 @@ def main():
     for q, d in batches[:2]:
         tr.train_step(q, d)
     torch.cuda.synchronize()
-    from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    import traceback
+
+    sites = {}
+
+    def site():
+        for fr in reversed(traceback.extract_stack()[:-2]):
+            if "dnn_page_vectors_amd" in fr.filename:
+                return f"{os.path.relpath(fr.filename, os.path.dirname(os.path.dirname(__file__)))}:{fr.lineno}"
+        return "?"
+
+    def wrap(owner, name):
+        orig = getattr(owner, name)
+
+        def w(*args, **kw):
+            out = orig(*args, **kw)
+            t = out if isinstance(out, torch.Tensor) else None
+            src = args[0] if args and isinstance(args[0], torch.Tensor) else None
+            if t is not None and t.is_cuda and (src is None or t.data_ptr() != src.data_ptr()):
+                k = (name, site())
+                n, b = sites.get(k, (0, 0))
+                sites[k] = (n + 1, b + t.numel() * t.element_size())
+            return out
+        setattr(owner, name, w)
+        return orig
+
+    saved = [(torch.Tensor, n, wrap(torch.Tensor, n)) for n in ("to", "contiguous", "clone", "float", "bfloat16")]
+    saved += [(torch, n, wrap(torch, n)) for n in ("cat", "zeros", "zeros_like", "stack")]
+    saved += [(torch.Tensor, n, wrap(torch.Tensor, n)) for n in ("zero_", "fill_", "copy_")]
+    try:
         tr.train_step(*batches[2])
         torch.cuda.synchronize()
-    sites = defaultdict(lambda: [0, 0.0])
-    for ev in prof.events():
-        if ev.name in ("aten::copy_", "aten::to", "aten::_to_copy", "aten::contiguous", "aten::cat", "aten::clone",
-                       "aten::zeros", "aten::fill_", "aten::zero_"):
-            stack = [f for f in (ev.stack or []) if "dnn_page_vectors_amd" in f or "bench" in f]
-            key = (ev.name, stack[0] if stack else "?")
-            sites[key][0] += 1
-            sites[key][1] += ev.device_time_total if hasattr(ev, "device_time_total") else ev.cuda_time_total
-    rows = sorted(sites.items(), key=lambda kv: -kv[1][1])
-    for (name, site), (n, us) in rows[:40]:
-        print(f"{us:9.1f} us  {n:4d}x  {name:16s} {site}", flush=True)
+    finally:
+        for owner, n, orig in saved:
+            setattr(owner, n, orig)
+    for (name, where), (n, b) in sorted(sites.items(), key=lambda kv: -kv[1][1])[:40]:
+        print(f"{b / 1e6:9.1f} MB {n:4d}x {name:11s} {where}", flush=True)
 
 
 if __name__ == "__main__":
