@@ -154,8 +154,8 @@ class BertEncoder(nn.Module):
         xs, masks, shapes = [], [], []
         for ids in ids_list:
             N, L = ids.shape
-            mask = (ids != 0)
-            mask[:, 0] = True
+            mask = (ids != 0).to(torch.int32)  # int32 once: the attention kernels' layout (no per-layer cast)
+            mask[:, 0] = 1
             masks.append(mask)
             shapes.append((N, L))
         # one fused gather + position / type add + cast over every group (ops/transformer.py)
