@@ -92,6 +92,26 @@ __device__ __forceinline__ void pack_b(const f32x4 (&x)[4], bf16x8 (&b)[2]) {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
+// Column sums of a wave's QG x 4 output accumulators (rows d = 16 i + 4 g + r, columns = the
+// wave's 16 QG tokens) over its tokens: the sum of rows 16 i + 4 g + r lands in every lane of
+// lane group g (xor shuffles inside the 16-lane groups).
+template <int QG>
+__device__ __forceinline__ void token_colsum(const f32x4 (&a)[QG][4], float (&out)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < QG; ++j) v += a[j][i][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      out[i][r] = v;
+    }
+}
+
+
+
 // ---------------------------------------------------------------------------- forward
 // QG = 16-query groups per wave: every staged K / V fragment feeds QG MFMAs (LDS reads and
 // tile stores per FLOP / QG).  grid (ceil(L / (64 QG)), H, N), 256 threads; wave w owns
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dkdv_kernel(con
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ Dv,
                                                                unsigned short* __restrict__ dqkv, int L, int H,
-                                                               float scale) {
+                                                               float scale, float* __restrict__ bpart, int nb64) {
   __shared__ __attribute__((aligned(16))) unsigned short qt[2][TB * LDT];
   __shared__ __attribute__((aligned(16))) unsigned short dt[2][TB * LDT];
   __shared__ float sl_[2][TB], sd_[2][TB];
@@ -547,6 +567,27 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dkdv_kernel(con
       }
     }
   }
+  if (bpart) {  // the qkv bias gradient's K / V parts: this workgroup's column sums over its keys
+    float sk[4][4], sv[4][4];
+    token_colsum<QG>(dk, sk);
+    token_colsum<QG>(dv, sv);
+    __shared__ float bred[4][2 * HD];
+    if ((lane & 15) == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bred[wave][i * 16 + 4 * g + r] = sk[i][r] * scale;
+          bred[wave][HD + i * 16 + 4 * g + r] = sv[i][r];
+        }
+    __syncthreads();
+    if (threadIdx.x < 2 * HD) {
+      const int c = threadIdx.x;
+      const float v = bred[0][c] + bred[1][c] + bred[2][c] + bred[3][c];
+      const int slot = 1 + c / HD, d = c % HD;
+      bpart[((size_t)n * nb64 + blockIdx.x) * (3 * H * HD) + (size_t)slot * H * HD + (size_t)h * HD + d] = v;
+    }
+  }
 }
 
 // grid (ceil(L / (64 QG)) query blocks, H, N); wave w owns queries qw + 16 j .. +15, j < QG
@@ -557,7 +598,7 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dq_kernel(const
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ Dv,
                                                              unsigned short* __restrict__ dqkv, int L, int H,
-                                                             float scale) {
+                                                             float scale, float* __restrict__ bpart, int nb64) {
   __shared__ __attribute__((aligned(16))) unsigned short kt[2][TB * LDT];
   __shared__ __attribute__((aligned(16))) unsigned short vt[2][TB * LDT];
   __shared__ float mk[2][TB];
@@ -659,6 +700,22 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dq_kernel(const
                   pack_bf16x2(acc[j][i][2] * scale, acc[j][i][3] * scale)};
     }
   }
+  if (bpart) {  // the qkv bias gradient's Q part: column sums over this workgroup's queries
+    float sq[4][4];
+    token_colsum<QG>(acc, sq);
+    __shared__ float bred[4][HD];
+    if ((lane & 15) == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bred[wave][i * 16 + 4 * g + r] = sq[i][r] * scale;
+    __syncthreads();
+    if (threadIdx.x < HD) {
+      const int d = threadIdx.x;
+      bpart[((size_t)n * nb64 + blockIdx.x) * (3 * H * HD) + (size_t)h * HD + d] =
+          bred[0][d] + bred[1][d] + bred[2][d] + bred[3][d];
+    }
+  }
 }
 
 #undef MFMA
@@ -706,9 +763,12 @@ PV_API int pv_attn_fwd(const void* qkv, const int* mask, void* out, float* lse, 
   return 0;
 }
 
-// dout, out (N, L, H, 64) bf16; lse (N, H, L); D workspace (N, H, L) f32; dqkv (N, L, 3, H, 64) bf16
-PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const void* dout, const float* lse,
-                       float* D, void* dqkv, int N, int L, int H, float scale, void* stream) {
+// dout, out (N, L, H, 64) bf16; lse (N, H, L); D workspace (N, H, L) f32; dqkv (N, L, 3, H, 64) bf16.
+// bpart (optional, zero-filled by the caller): (N * ceil(L / 64), 3 * H * 64) fp32 rows of per-
+// workgroup column sums of dQ / dK / dV — their column sum is the qkv bias gradient
+// (ops/transformer.py: no separate pass over dqkv).
+PV_API int pv_attn_bwd2(const void* qkv, const int* mask, const void* out, const void* dout, const float* lse,
+                        float* D, void* dqkv, int N, int L, int H, float scale, float* bpart, void* stream) {
   using namespace pv::attn;
   if (N <= 0 || L <= 0 || H <= 0) return -1;
   hipStream_t s = (hipStream_t)stream;
@@ -721,7 +781,7 @@ PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const 
                        (const unsigned short*)out, D, NL, L, H);
   PV_LAUNCH_CHECK();
   const int qk = qg_or(g_qg_dkdv, 1), qq = qg_or(g_qg_dq, L >= 128 ? 2 : 1);
-#define PV_ABWD(KERN, QGV)                                                                                       hipLaunchKernelGGL(KERN<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0, s,                                     (const unsigned short*)qkv, mask, (const unsigned short*)dout, lse, D, (unsigned short*)dqkv,                      L, H, scale)
+#define PV_ABWD(KERN, QGV)                                                                                       hipLaunchKernelGGL(KERN<QGV>, dim3((L + TB * QGV - 1) / (TB * QGV), H, N), dim3(256), 0, s,                                     (const unsigned short*)qkv, mask, (const unsigned short*)dout, lse, D, (unsigned short*)dqkv,                      L, H, scale, bpart, (L + TB - 1) / TB)
   if (qk == 4) PV_ABWD(attn_bwd_dkdv_kernel, 4);
   else if (qk == 2) PV_ABWD(attn_bwd_dkdv_kernel, 2);
   else PV_ABWD(attn_bwd_dkdv_kernel, 1);
@@ -732,4 +792,9 @@ PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const 
 #undef PV_ABWD
   PV_LAUNCH_CHECK();
   return 0;
+}
+
+PV_API int pv_attn_bwd(const void* qkv, const int* mask, const void* out, const void* dout, const float* lse,
+                       float* D, void* dqkv, int N, int L, int H, float scale, void* stream) {
+  return pv_attn_bwd2(qkv, mask, out, dout, lse, D, dqkv, N, L, H, scale, nullptr, stream);
 }

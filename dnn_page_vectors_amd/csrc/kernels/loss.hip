@@ -686,6 +686,222 @@ __global__ __launch_bounds__(NW * 64, 2) void ib5_kernel(const unsigned short* _
   }
 }
 
+// ---- ib7: ib5 software-pipelined ------------------------------------------------------------
+// ib5 runs each tile as S product -> epilogue -> out product, and the one-barrier-per-tile ring
+// keeps the 8 waves of a workgroup in phase: both waves of a SIMD sit in their MFMA phase or in
+// their VALU epilogue (~27 issue cycles per S element: clamp, compare, fma, select, v_exp,
+// scale, cvt) at the same time, so matrix and vector work barely co-execute (~1.0 PF/s on the
+// 344 GFLOP passes at the W = 8 shape, docs/PERF.md).  ib7 computes the NEXT tile's S product
+// in the same basic block as this tile's epilogue (independent instructions the scheduler
+// interleaves: each 32x32x16 MFMA holds vector issue for 8 of its 32 cycles), so one wave's
+// epilogue hides behind its own matrix work.  The next tile must be resident one iteration
+// earlier: a 4-slot ring (80 KB at DP = 160) staged three tiles ahead, each iteration waiting for
+// tile t + 2.  Per tile, three phases keep the live registers at ib5's: (1) S rows 32..63
+// beside the epilogue of rows 0..31, (2) the next tile's S rows 0..31 and the out product over
+// rows 0..31 beside the epilogue of rows 32..63, (3) the out product over rows 32..63 —
+// scheduling barriers hold that order.  Same arithmetic as ib5 (the out product's k-steps in
+// the same order): bit-identical results.
+template <int KS, bool ROW, bool CLIP, bool FWD = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 2) void ib7_kernel(const unsigned short* __restrict__ X,
+                                                      const unsigned short* __restrict__ Y,
+                                                      const float* __restrict__ scale, float* __restrict__ out,
+                                                      float* __restrict__ ws, int nx, int ny, int per_split,
+                                                      int nrb, float gamma, float* __restrict__ part = nullptr) {
+  static_assert(!FWD || ROW, "the fused forward runs over query rows");
+  static_assert(KS == 4 || KS == 5, "ib7: chunk swizzles exist for DP = 128 and 160");
+  static_assert(Ib5<KS>::K16 >= 8, "ib7: one epilogue group per S k-step");
+  using T = Ib5<KS>;
+  constexpr int NB = 4;
+  __shared__ __attribute__((aligned(1024))) char ring[NB * T::TILE_B];
+  __shared__ __attribute__((aligned(16))) float ysc[NB][TD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / nrb, rb = bid - split * nrb;
+  const int r0 = rb * (NW * 32) + wave * 32;
+  const int x = r0 + l32;
+  const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
+  const int ntiles = (c_end - c_begin + TD - 1) / TD;
+  const float gl = gamma * 1.4426950408889634f;
+  const int np = ib5_pieces<KS, ROW, NW>(wave);
+  bf16x8 xb[T::K16];
+#pragma unroll
+  for (int ks = 0; ks < T::K16; ++ks)
+    xb[ks] = x < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)x * T::DP + 16 * ks + 8 * h)
+                    : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const float rsc = (ROW && !FWD && x < nx) ? scale[x] : 0.f;
+  float rs = 0.f;
+  f32x16 o[T::FT];
+#pragma unroll
+  for (int f = 0; f < T::FT; ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[f][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < ntiles) ib5_stage<KS, ROW, NW>(Y, scale, c_begin + i * TD, c_end, ring + i * T::TILE_B, ysc[i]);
+  // tiles 0 and 1 landed; tile 2's pieces may stay in flight
+  wait_vm(ntiles > 2 ? np : 0);
+  __builtin_amdgcn_s_barrier();
+  const int tq = (lane & 15) >> 2, tf = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  // Fragment addresses (DP = 160) as a lane base + compile-time offsets (ds_read immediates).  S product,
+  // A = Y row y = 32 yt + l32, 16-byte chunk c = 2 ks + h stored at c ^ swz(y); swz(y) =
+  // ib5_swz(l32) for both yt (32 yt keeps y >> 2 & 3 and y & 3), and it flips only the chunk's
+  // low two bits: c ^ swz = 4 (ks >> 1) + ((2 (ks & 1) + h) ^ swz) -> two lane bases (ks parity)
+  // plus 64 (ks >> 1) + 32 yt * ROWB.  Out product, A = rows ylo = 32 yt + 16 s2 + 4 h + tq and
+  // ylo + 8, feature fe = 32 f + tf: chunk (fe >> 3) ^ swz(ylo) = 4 f + ((tf >> 3) ^ swz(ylo)),
+  // and swz(ylo) = swz(4 h + tq), swz(ylo + 8) = swz(4 h + tq + 8) -> two lane bases plus
+  // (32 yt + 16 s2) * ROWB + 64 f.
+  const int swzA = ib5_swz<KS>(l32);
+  const int offA0 = l32 * T::ROWB + ((h ^ swzA) << 4), offA1 = l32 * T::ROWB + (((2 + h) ^ swzA) << 4);
+  const int ylo0 = 4 * h + tq;
+  const int offTlo = ylo0 * T::ROWB + (((tf >> 3) ^ ib5_swz<KS>(ylo0)) << 4) + (tf & 7) * 2;
+  const int offThi = (ylo0 + 8) * T::ROWB + (((tf >> 3) ^ ib5_swz<KS>(ylo0 + 8)) << 4) + (tf & 7) * 2;
+  // (DP = 128: the swizzle is 4 bits wide and permutes whole rows of chunks — the generic
+  // per-fragment address, as in ib5)
+  auto ldA = [&](const char* base, int ks, int yt) {
+    if constexpr (KS == 5) {
+      const char* p = base + ((ks & 1) ? offA1 : offA0) + 64 * (ks >> 1) + 32 * yt * T::ROWB;
+      return *reinterpret_cast<const bf16x8*>(p);
+    } else {
+      const int y = 32 * yt + l32, c = 2 * ks + h;
+      return *reinterpret_cast<const bf16x8*>(base + y * T::ROWB + ((c ^ ib5_swz<KS>(y)) << 4));
+    }
+  };
+  auto ldT = [&](const char* base, int yt, int s2, int f) {
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const char *plo, *phi;
+    if constexpr (KS == 5) {
+      const int c = (32 * yt + 16 * s2) * T::ROWB + 64 * f;
+      plo = base + offTlo + c;
+      phi = base + offThi + c;
+    } else {
+      const int ylo = 32 * yt + 16 * s2 + 4 * h + tq, yhi = ylo + 8;
+      const int fe = 32 * f + tf;
+      plo = base + ylo * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(ylo))) << 4) + (fe & 7) * 2;
+      phi = base + yhi * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(yhi))) << 4) + (fe & 7) * 2;
+    }
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plo));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(phi));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  // acc[yt][r] = S^T[y = 32 yt + 8 (r >> 2) + 4 h + (r & 3)][x] of the current tile
+  f32x16 acc[2];
+  {
+    bf16x8 a = ldA(ring, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < T::K16; ++ks) {
+      const bf16x8 b = a;
+      if (ks + 1 < T::K16) a = ldA(ring, ks + 1, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[ks], ks == 0 ? f32x16{} : acc[0], 0, 0, 0);
+    }
+  }
+  // one tile; FULL (compile time): every Y row of the tile is inside the split (all tiles but
+  // possibly the last, which is peeled off so the steady-state loop body is one basic block)
+  auto tile = [&](int t, auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
+    const int c0 = c_begin + t * TD;
+    const int sb = t & (NB - 1);
+    const bool ahead = t + 3 < ntiles;
+    if (ahead) {  // slot (t + 3) % 4 = (t - 1) % 4: every wave left it at the last barrier
+      const int nb = (t + 3) & (NB - 1);
+      ib5_stage<KS, ROW, NW>(Y, scale, c0 + 3 * TD, c_end, ring + nb * T::TILE_B, ysc[nb]);
+    }
+    const char* cb = ring + sb * T::TILE_B;
+    const char* nbp = ring + ((t + 1) & (NB - 1)) * T::TILE_B;
+    u32x4 gp[2][2];
+    // epilogue of the 4 S^T rows y = 32 yt + 8 j + 4 h + (0..3) of this tile -> G^T fragment
+    auto epi4 = [&](int yt, int j) {
+      f32x4 ysv;
+      if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[sb][32 * yt + 8 * j + 4 * h]);
+      float gv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int yr = 32 * yt + 8 * j + 4 * h + r;
+        const float v = acc[yt][4 * j + r];
+        float xx;
+        if constexpr (FWD) {
+          const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
+          xx = __builtin_fmaf(vc, gl, -gl);
+          if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
+          const float e = __builtin_amdgcn_exp2f(xx);
+          rs += e;
+          gv[r] = (!CLIP || vc == v) ? e : 0.f;
+          continue;
+        }
+        if constexpr (CLIP) {
+          const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
+          xx = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
+        } else {
+          xx = __builtin_fmaf(v, gl, -gl);
+        }
+        if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
+        gv[r] = (ROW ? rsc : ysv[r]) * __builtin_amdgcn_exp2f(xx);
+      }
+      gp[yt][j >> 1][(j & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
+      gp[yt][j >> 1][(j & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
+    };
+    // phase 1: this tile's S rows 32..63 (acc[1]) beside the epilogue of rows 0..31
+    {
+      bf16x8 a = ldA(cb, 0, 1);
+#pragma unroll
+      for (int ks = 0; ks < T::K16; ++ks) {
+        const bf16x8 b = a;
+        if (ks + 1 < T::K16) a = ldA(cb, ks + 1, 1);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[ks], ks == 0 ? f32x16{} : acc[1], 0, 0, 0);
+        if ((ks & 1) == 0 && ks < 8) epi4(0, ks >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // phase 2: the NEXT tile's S rows 0..31 (acc[0], slot t + 1: stale rows past the last tile
+    // are computed and unused) and out^T += Y^T G^T over rows 0..31, beside the epilogue of
+    // rows 32..63
+    {
+      bf16x8 a = ldA(nbp, 0, 0);
+      bf16x8 at = ldT(cb, 0, 0, 0);
+#pragma unroll
+      for (int ks = 0; ks < T::K16; ++ks) {
+        const bf16x8 b = a, bt = at;
+        if (ks + 1 < T::K16) {
+          a = ldA(nbp, ks + 1, 0);
+          at = ldT(cb, 0, (ks + 1) / T::FT, (ks + 1) % T::FT);
+        }
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[ks], ks == 0 ? f32x16{} : acc[0], 0, 0, 0);
+        const int s2 = ks / T::FT, f = ks % T::FT;  // 2 FT = K16 out-product steps over rows 0..31
+        o[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bt, __builtin_bit_cast(bf16x8, gp[0][s2]), o[f], 0, 0, 0);
+        if ((ks & 1) == 0 && ks < 8) epi4(1, ks >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // phase 3: out^T += Y^T G^T over rows 32..63
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int f = 0; f < T::FT; ++f)
+        o[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ldT(cb, 1, s2, f), __builtin_bit_cast(bf16x8, gp[1][s2]), o[f],
+                                                       0, 0, 0);
+    // tile t + 2 landed (this wave's pieces; the barrier covers the others'); t + 3 may stay in flight
+    wait_vm(ahead ? np : 0);
+    __builtin_amdgcn_s_barrier();
+  };
+  const int nfull = (c_end - c_begin) / TD;
+#pragma unroll 1
+  for (int t = 0; t < nfull; ++t) tile(t, std::true_type{});
+  if (nfull < ntiles) tile(nfull, std::false_type{});
+  if constexpr (FWD) {
+    rs += __shfl_xor(rs, 32, 64);
+    if (h == 0 && x < nx) part[(size_t)split * nx + x] = rs;
+  }
+  float* dst = (gridDim.x == (unsigned)nrb) ? out : ws + (size_t)split * nx * T::DP;
+  if (x < nx) {
+    float* orow = dst + (size_t)x * T::DP;
+#pragma unroll
+    for (int f = 0; f < T::FT; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(orow + 32 * f + 8 * j + 4 * h) =
+            f32x4{o[f][4 * j], o[f][4 * j + 1], o[f][4 * j + 2], o[f][4 * j + 3]};
+  }
+}
+
 // out[i] = sum_s ws[s][i], n4 = nx*DP/4
 __global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                               long n4, int ns) {
@@ -1029,11 +1245,13 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
 //   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for
 //                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
 //   3: ib3 everywhere (A/B and the ib5-vs-ib3 numerics test)
+//   7: ib7 (ib5 software-pipelined) for every pass at DP = 160 / 128, ib3 for the rest
 static int g_ib_version = -1;
 static int ib_version() {
   if (g_ib_version < 0) {
     const char* e = getenv("PAGEVEC_IB");
-    g_ib_version = (e && atoi(e) == 3) ? 3 : 5;
+    const int v = e ? atoi(e) : 5;
+    g_ib_version = (v == 3 || v == 7) ? v : 5;
   }
   return g_ib_version;
 }
@@ -1041,7 +1259,7 @@ static int ib_version() {
 PV_API int pv_ib_version() { return ib_version(); }
 // A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)
 PV_API int pv_ib_set_version(int v) {
-  if (v != 3 && v != 5) return -1;
+  if (v != 3 && v != 5 && v != 7) return -1;
   g_ib_version = v;
   return 0;
 }
@@ -1081,7 +1299,13 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   const int nrb = (nx + 255) / 256;
   const dim3 grid3(nrb * ns);
 #define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
-  if (ib_version() == 5 && ROWV && DP == 160) {                                                                 \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib7_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else if (ib_version() == 7 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib7_kernel<4, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else if (ib_version() == 5 && ROWV && DP == 160) {                                                                 \
     hipLaunchKernelGGL((ib5_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
                        (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
   } else if (ib_version() == 5 && ROWV && DP == 128) {                                                          \
@@ -1129,7 +1353,13 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   const int nrb = (nx + 255) / 256;
   const dim3 grid3(nrb * ns);
 #define PV_IB_FWDDQ(CLIPV)                                                                                      \
-  if (ib_version() == 5 && DP == 160) {                                                                         \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib7_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 7 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib7_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 5 && DP == 160) {                                                                         \
     hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
                        (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
   } else if (ib_version() == 5 && DP == 128) {                                                                  \

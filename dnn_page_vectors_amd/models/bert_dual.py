@@ -49,9 +49,9 @@ class BertLayer(nn.Module):
                 seed: int = 0):
         N, L, H = x.shape
         p = p_drop if training else 0.0
-        r1, r2 = tops.ResidualLink(), tops.ResidualLink()
-        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1)    # (N, L, 3H) packed [slot][head][d]
-        a = tops.fused_attention(qkv, mask, self.heads)       # (N, L, H), no permute copies
+        r1, r2, bl = tops.ResidualLink(), tops.ResidualLink(), tops.BiasGradLink()
+        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1, bias_link=bl)  # (N, L, 3H) [slot][head][d]
+        a = tops.fused_attention(qkv, mask, self.heads, bias_link=bl)     # (N, L, H), no permute copies
         o = tops.linear(a, self.wo)
         # output bias + hidden dropout fused into the residual add + LayerNorm (counter-hash
         # masks; the bias gradient is reduced in the LayerNorm backward)
@@ -66,9 +66,9 @@ class BertLayer(nn.Module):
         p = p_drop if training else 0.0
         # each x feeds a linear layer and a residual add: their gradients meet in the
         # linear's dX GEMM (tops.ResidualLink) instead of an autograd add
-        r1, r2 = tops.ResidualLink(), tops.ResidualLink()
-        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1)    # (T, 3H): one GEMM for every group
-        a = tops.packed_attention(qkv, masks, shapes, self.heads)
+        r1, r2, bl = tops.ResidualLink(), tops.ResidualLink(), tops.BiasGradLink()
+        qkv = tops.linear(x, self.wqkv, self.bqkv, res=r1, bias_link=bl)  # (T, 3H): one GEMM, all groups
+        a = tops.packed_attention(qkv, masks, shapes, self.heads, bias_link=bl)
         o = tops.linear(a, self.wo)
         x = tops.add_layernorm(o, x, self.ln1_g, self.ln1_b, p=p, seed=seed, bias=self.bo, res=r1)
         f2 = tops.ffn(x, self.w1, self.b1, self.w2, res=r2)  # GELU in the GEMM epilogues

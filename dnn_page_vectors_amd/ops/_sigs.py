@@ -72,6 +72,7 @@ SIGS = {
     "pv_ib_bwd_ws": "iii",
     "pv_attn_fwd": "pppp" "iii" "f" "p",
     "pv_attn_bwd": "ppppppp" "iii" "f" "p",
+    "pv_attn_bwd2": "ppppppp" "iii" "f" "p" "p",
     "pv_ib_fwd_dq_parts": "ii",
     "pv_ib_fwd_dq": "pppppp" "iiif" "i" "ppp" "p",
     "pv_ib_pos": "ppppppp" "ii" "fi" "p",

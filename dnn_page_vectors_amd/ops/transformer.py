@@ -45,6 +45,25 @@ class ResidualLink:
         self.grad = None
 
 
+class BiasGradLink:
+    """Pairs the qkv projection (``linear(x, w, b, bias_link=link)``) with the attention that
+    consumes its output (``packed_attention(..., bias_link=link)``).  The qkv bias gradient is
+    the column sum of dqkv over every token (T x 3H bf16, re-read from HBM by a colsum pass); the
+    attention backward kernels already hold dQ / dK / dV in registers and emit per-workgroup
+    column sums instead (attention.hip::pv_attn_bwd2, ``part``: (sum N_i ceil(L_i / 64), 3H)
+    fp32, ~50x fewer rows), which the linear's backward reduces into the bias gradient.  The
+    attention backward always runs first: the linear's output gradient is its dqkv."""
+
+    __slots__ = ("part",)
+
+    def __init__(self):
+        self.part = None
+
+
+# qkv bias gradient from the attention backward's partial column sums (BiasGradLink)
+ATTN_BGRAD = os.environ.get("PAGEVEC_ATTN_BGRAD", "1") != "0"
+
+
 class _AddLNFn(torch.autograd.Function):
     """y = LayerNorm(dropout(x + xb) + r).  D in {256, 512, 768, 1024}: one wave per row
     (``pv_add_ln_drop_fwd``); the dropout mask is a counter hash of (seed, row, column)
@@ -221,7 +240,7 @@ class _FusedAttnFn(torch.autograd.Function):
     """qkv (N, L, 3*H*64) bf16 packed [slot][head][d] -> (N, L, H*64); csrc/kernels/attention.hip."""
 
     @staticmethod
-    def forward(ctx, qkv, mask, heads, scale):
+    def forward(ctx, qkv, mask, heads, scale, blink=None):
         qkv = qkv.to(torch.bfloat16).contiguous()
         N, L, C = qkv.shape
         H = heads
@@ -233,6 +252,7 @@ class _FusedAttnFn(torch.autograd.Function):
               "pv_attn_fwd")
         ctx.save_for_backward(qkv, mask, out, lse)
         ctx.meta = (H, float(scale))
+        ctx.blink = blink
         return out
 
     @staticmethod
@@ -243,19 +263,25 @@ class _FusedAttnFn(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         D = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
-        check(lib().pv_attn_bwd(P(qkv), P(mask), P(out), P(dout), P(lse), P(D), P(dqkv), N, L, H, scale,
-                                stream(qkv.device)), "pv_attn_bwd")
-        return dqkv, None, None, None
+        part = None
+        if ctx.blink is not None:
+            part = torch.zeros(N * ((L + 63) // 64), 3 * H * 64, dtype=torch.float32, device=qkv.device)
+            ctx.blink.part = part
+        check(lib().pv_attn_bwd2(P(qkv), P(mask), P(out), P(dout), P(lse), P(D), P(dqkv), N, L, H, scale,
+                                 P(part), stream(qkv.device)), "pv_attn_bwd2")
+        return dqkv, None, None, None, None
 
 
-def fused_attention(qkv: torch.Tensor, mask: Optional[torch.Tensor], heads: int) -> torch.Tensor:
-    """qkv (N, L, 3*H*d) packed projection output -> attention output (N, L, H*d), mask (N, L)."""
+def fused_attention(qkv: torch.Tensor, mask: Optional[torch.Tensor], heads: int,
+                    bias_link: Optional[BiasGradLink] = None) -> torch.Tensor:
+    """qkv (N, L, 3*H*d) packed projection output -> attention output (N, L, H*d), mask (N, L).
+    ``bias_link``: shared with the qkv ``linear`` (BiasGradLink)."""
     N, L, C = qkv.shape
     d = C // (3 * heads)
     scale = 1.0 / math.sqrt(d)
     if use_hip(qkv) and d == 64:
         m = mask.to(torch.int32).contiguous() if mask is not None else None
-        return _FusedAttnFn.apply(qkv, m, heads, scale)
+        return _FusedAttnFn.apply(qkv, m, heads, scale, bias_link if ATTN_BGRAD else None)
     q, k, v = qkv.view(N, L, 3, heads, d).permute(2, 0, 3, 1, 4)
     return attention(q, k, v, mask).transpose(1, 2).reshape(N, L, heads * d)
 
@@ -267,7 +293,7 @@ class _PackedAttnFn(torch.autograd.Function):
     shared input / output / gradient buffers — no per-tower copies, slices or gradient adds."""
 
     @staticmethod
-    def forward(ctx, qkv, masks, shapes, heads, scale):
+    def forward(ctx, qkv, masks, shapes, heads, scale, blink=None):
         qkv = qkv.to(torch.bfloat16).contiguous()
         T, C = qkv.shape
         H = heads
@@ -288,6 +314,7 @@ class _PackedAttnFn(torch.autograd.Function):
             raise ValueError("segment shapes do not cover the packed tensor")
         ctx.save_for_backward(qkv, out, *masks, *lses)
         ctx.meta = (H, float(scale), list(shapes), len(masks))
+        ctx.blink = blink
         return out
 
     @staticmethod
@@ -300,23 +327,33 @@ class _PackedAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         esz = qkv.element_size()
         s = stream(qkv.device)
+        part, prow = None, 0
+        if ctx.blink is not None:
+            part = torch.zeros(sum(N * ((L + 63) // 64) for N, L in shapes), C, dtype=torch.float32,
+                               device=qkv.device)
+            ctx.blink.part = part
         off = 0
         for (N, L), m, lse in zip(shapes, masks, lses):
             D = torch.empty(N, H, L, dtype=torch.float32, device=qkv.device)
-            check(lib().pv_attn_bwd(qkv.data_ptr() + off * C * esz, P(m), out.data_ptr() + off * H * 64 * esz,
-                                    dout.data_ptr() + off * H * 64 * esz, P(lse), P(D),
-                                    dqkv.data_ptr() + off * C * esz, N, L, H, scale, s), "pv_attn_bwd")
+            check(lib().pv_attn_bwd2(qkv.data_ptr() + off * C * esz, P(m), out.data_ptr() + off * H * 64 * esz,
+                                     dout.data_ptr() + off * H * 64 * esz, P(lse), P(D),
+                                     dqkv.data_ptr() + off * C * esz, N, L, H, scale,
+                                     part.data_ptr() + prow * C * 4 if part is not None else None, s),
+                  "pv_attn_bwd2")
             off += N * L
-        return dqkv, None, None, None, None
+            prow += N * ((L + 63) // 64)
+        return dqkv, None, None, None, None, None
 
 
-def packed_attention(qkv: torch.Tensor, masks, shapes, heads: int) -> torch.Tensor:
+def packed_attention(qkv: torch.Tensor, masks, shapes, heads: int,
+                     bias_link: Optional[BiasGradLink] = None) -> torch.Tensor:
     """qkv (T, 3*H*d) token-major with segments of shapes [(N_i, L_i)] back to back, masks
-    [(N_i, L_i)] -> (T, H*d)."""
+    [(N_i, L_i)] -> (T, H*d).  ``bias_link``: shared with the qkv ``linear`` (BiasGradLink)."""
     d = qkv.shape[1] // (3 * heads)
     if use_hip(qkv) and d == 64:
         ms = [m.to(torch.int32).contiguous() for m in masks]
-        return _PackedAttnFn.apply(qkv, ms, [tuple(x) for x in shapes], heads, 1.0 / math.sqrt(d))
+        return _PackedAttnFn.apply(qkv, ms, [tuple(x) for x in shapes], heads, 1.0 / math.sqrt(d),
+                                   bias_link if ATTN_BGRAD else None)
     outs, off = [], 0
     for (N, L), m in zip(shapes, masks):
         outs.append(fused_attention(qkv[off:off + N * L].view(N, L, -1), m, heads).reshape(N * L, -1))
@@ -462,7 +499,7 @@ class _Linear16Fn(torch.autograd.Function):
     """y = x @ W^T (+ b) in bf16 on hipBLASLt over a cached bf16 W; fp32 weight/bias grads."""
 
     @staticmethod
-    def forward(ctx, x, w, b, w16, res=None):
+    def forward(ctx, x, w, b, w16, res=None, blink=None):
         x = x.to(torch.bfloat16)
         x2 = x.reshape(-1, x.shape[-1])
         if LINEAR_LT and x2.is_cuda and x2.is_contiguous():
@@ -478,6 +515,7 @@ class _Linear16Fn(torch.autograd.Function):
         ctx.shape = x.shape
         ctx.params = (w, b)  # flat-gradient direct-write targets (ops/grad_sink.py)
         ctx.res = res
+        ctx.blink = blink
         return y.view(*x.shape[:-1], w16.shape[0])
 
     @staticmethod
@@ -499,17 +537,23 @@ class _Linear16Fn(torch.autograd.Function):
                 dw = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             tb = grad_sink.write_target(pb)
-            db = dops.colsum(dy2, out=tb, accumulate=tb is not None)  # a first contribution's region is zero
+            # a first contribution's region is zero; the attention backward's partial column
+            # sums stand in for dY when linked (BiasGradLink)
+            blink = ctx.blink
+            src = blink.part if blink is not None and blink.part is not None else dy2
+            db = dops.colsum(src, out=tb, accumulate=tb is not None)
+            if blink is not None:
+                blink.part = None
             if tb is not None:
                 grad_sink.done(pb)
                 db = None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
-           res: Optional[ResidualLink] = None) -> torch.Tensor:
+           res: Optional[ResidualLink] = None, bias_link: Optional[BiasGradLink] = None) -> torch.Tensor:
     if use_hip(x):
-        return _Linear16Fn.apply(x, w, b, weight_bf16(w), res)
+        return _Linear16Fn.apply(x, w, b, weight_bf16(w), res, bias_link)
     return F.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
 
 

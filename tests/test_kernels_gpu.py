@@ -324,13 +324,14 @@ def test_inbatch_loss(B, M, D, clip):
     torch.testing.assert_close(dn.grad, dn2.grad, rtol=3e-2, atol=3e-3)
 
 
-@pytest.mark.parametrize("ver", [5, 3])
+@pytest.mark.parametrize("ver", [5, 3, 7])
 @pytest.mark.parametrize("B,M,clip,D", [(700, 5000, True, 150), (4096, 16384, False, 150), (300, 20000, True, 150),
                                         (700, 5000, True, 128), (2048, 9000, False, 128)])
 def test_inbatch_loss_split_shapes(ver, B, M, clip, D):
     """Shapes with several Y splits, >= 3 tiles per split (the ib3 LDS ring wraps), a
-    partial last tile and row blocks past nx, for both kernel generations (5: ib5 on 32x32x16
-    MFMAs for the query-row passes; 3: ib3, 16x16x32, everywhere) vs the fp32 reference."""
+    partial last tile and row blocks past nx, for the kernel generations (5: ib5 on 32x32x16
+    MFMAs for the query-row passes; 3: ib3, 16x16x32, everywhere; 7: the software-pipelined
+    ib7 for every pass) vs the fp32 reference."""
     from dnn_page_vectors_amd.ops._common import lib as _lib
 
     L_ = _lib()
@@ -1874,6 +1875,8 @@ def test_bert_embed_fused_matches_unfused(monkeypatch):
     q = torch.randint(1, V, (7, 12), device=DEV)
     d = torch.randint(0, V, (5, 33), device=DEV)
     d[:, 20:] = 0  # padding tail
+    gy = torch.randn(7 * 12 + 5 * 33, H, device=DEV)  # one upstream gradient for both arms
+    gy[7 * 12:].view(5, 33, H)[:, 20:] = 0  # padding rows carry no gradient, as in the model
     out = {}
     for fused in (True, False):
         monkeypatch.setattr(tops, "BERT_EMBED", fused)
@@ -1883,10 +1886,88 @@ def test_bert_embed_fused_matches_unfused(monkeypatch):
             xs = [(word[i.long()] + pos[:i.shape[1]].unsqueeze(0) + typ[0]).to(torch.bfloat16).reshape(-1, H)
                   for i in (q, d)]
             x = torch.cat(xs, 0)
-        gy = torch.randn(x.shape, device=DEV)
-        gy[7 * 12:].view(5, 33, H)[:, 20:] = 0  # padding rows carry no gradient, as in the model
         (x.float() * gy).sum().backward()
         out[fused] = (x, word.grad, pos.grad, typ.grad)
     assert torch.equal(out[True][0], out[False][0])
     for a, b in zip(out[True][1:], out[False][1:]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("fused_shapes", [False, True])
+def test_attention_bias_grad_link(monkeypatch, fused_shapes):
+    """attention.hip::pv_attn_bwd2's per-workgroup dQ / dK / dV column sums (BiasGradLink) give
+    the qkv bias gradient of the linear feeding the attention: against the colsum of dqkv (the
+    unlinked path) — equal up to bf16 rounding of dqkv before the sum; every other gradient
+    bit-identical."""
+    from dnn_page_vectors_amd.ops import transformer as tops
+
+    torch.manual_seed(5)
+    H, Hd = 4, 256
+    shapes = [(6, 32), (5, 100)] if fused_shapes else [(3, 77)]
+    T = sum(n * l for n, l in shapes)
+    x0 = torch.randn(T, Hd, device=DEV)
+    w0 = torch.randn(3 * Hd, Hd, device=DEV) * 0.05
+    b0 = torch.randn(3 * Hd, device=DEV) * 0.1
+    masks = []
+    for n, l in shapes:
+        m = torch.ones(n, l, dtype=torch.int32, device=DEV)
+        m[0, l // 2:] = 0
+        masks.append(m)
+    gy = torch.randn(T, Hd, device=DEV)
+    out = {}
+    for linked in (True, False):
+        monkeypatch.setattr(tops, "ATTN_BGRAD", linked)
+        x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        bl = tops.BiasGradLink()
+        qkv = tops.linear(x, w, b, bias_link=bl)
+        if fused_shapes:
+            a = tops.packed_attention(qkv, masks, shapes, H, bias_link=bl)
+        else:
+            n, l = shapes[0]
+            a = tops.fused_attention(qkv.view(n, l, -1), masks[0], H, bias_link=bl).reshape(T, -1)
+        (a.float() * gy).sum().backward()
+        assert bl.part is None  # consumed by the linear's backward
+        out[linked] = (x.grad, w.grad, b.grad)
+    assert torch.equal(out[True][0], out[False][0])
+    assert torch.equal(out[True][1], out[False][1])
+    ref = out[False][2]
+    err = (out[True][2] - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-4, err
+
+
+@pytest.mark.parametrize("B,M,clip,D", [(700, 5000, True, 150), (2048, 9000, False, 128), (300, 20000, True, 150),
+                                        (513, 4097, True, 150)])
+def test_inbatch_loss_ib7_matches_ib5(B, M, clip, D):
+    """loss.hip::ib7_kernel (next tile's S product beside this tile's epilogue, 4-slot ring,
+    peeled partial tile) does ib5's arithmetic in ib5's order: the loss and the query-side
+    gradient (ib5 in generation 5) bit-identical; the page-side gradient (ib3 in generation 5,
+    a different summation order) against generation 5 to fp32 rounding."""
+    from dnn_page_vectors_amd.ops._common import lib as _lib
+
+    L_ = _lib()
+    old = L_.pv_ib_version()
+    torch.manual_seed(11)
+    q = torch.randn(B, D, device=DEV)
+    dd = torch.randn(M, D, device=DEV)
+    dd[:B] = q + 2.0 * dd[:B]
+    if clip:
+        q, dd = q.abs(), dd.abs()
+    qn0 = bf(ref.l2_normalize(q))
+    dn0 = bf(ref.l2_normalize(dd))
+    pos = torch.arange(B, device=DEV, dtype=torch.int32)
+    w = torch.rand(B, device=DEV)
+    res = {}
+    try:
+        for ver in (5, 7):
+            assert L_.pv_ib_set_version(ver) == 0
+            qn = qn0.clone().requires_grad_(True)
+            dn = dn0.clone().requires_grad_(True)
+            loss, P = lops.inbatch_loss(qn, dn, pos, 10.0, clip)
+            (loss * w).sum().backward()
+            torch.cuda.synchronize()
+            res[ver] = (loss.detach(), qn.grad, dn.grad)
+    finally:
+        L_.pv_ib_set_version(old)
+    assert torch.equal(res[5][0], res[7][0])
+    assert torch.equal(res[5][1], res[7][1])
+    torch.testing.assert_close(res[7][2], res[5][2], rtol=1e-4, atol=1e-6)
