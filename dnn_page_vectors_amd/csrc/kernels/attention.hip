@@ -93,8 +93,13 @@ __device__ __forceinline__ void pack_b(const f32x4 (&x)[4], bf16x8 (&b)[2]) {
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 // Column sums of a wave's QG x 4 output accumulators (rows d = 16 i + 4 g + r, columns = the
-// wave's 16 QG tokens) over its tokens: the sum of rows 16 i + 4 g + r lands in every lane of
-// lane group g (xor shuffles inside the 16-lane groups).
+// wave's 16 QG tokens) over its tokens: the sum of rows 16 i + 4 g + r lands in lane 15 of
+// lane group g (an inclusive row_shr 1 / 2 / 4 / 8 DPP scan inside each 16-lane row: four
+// VALU adds per value, no LDS traffic).
+template <int CTRL>
+__device__ __forceinline__ float row_shr_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 template <int QG>
 __device__ __forceinline__ void token_colsum(const f32x4 (&a)[QG][4], float (&out)[4][4]) {
 #pragma unroll
@@ -104,8 +109,10 @@ __device__ __forceinline__ void token_colsum(const f32x4 (&a)[QG][4], float (&ou
       float v = 0.f;
 #pragma unroll
       for (int j = 0; j < QG; ++j) v += a[j][i][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      v = row_shr_add<0x111>(v);
+      v = row_shr_add<0x112>(v);
+      v = row_shr_add<0x114>(v);
+      v = row_shr_add<0x118>(v);
       out[i][r] = v;
     }
 }
@@ -431,7 +438,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep4_kernel(const unsigned shor
                 __uint_as_float(x.y & 0xFFFF0000u) * __uint_as_float(y.y & 0xFFFF0000u);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    if ((lane & 15) == 0) Dv[((size_t)n * H + 4 * c + (lane >> 4)) * L + q] = acc;
+    if ((lane & 15) == 15) Dv[((size_t)n * H + 4 * c + (lane >> 4)) * L + q] = acc;
   }
 }
 
@@ -572,7 +579,7 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dkdv_kernel(con
     token_colsum<QG>(dk, sk);
     token_colsum<QG>(dv, sv);
     __shared__ float bred[4][2 * HD];
-    if ((lane & 15) == 0)
+    if ((lane & 15) == 15)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -704,7 +711,7 @@ __global__ __launch_bounds__(256, QG >= 4 ? 1 : 2) void attn_bwd_dq_kernel(const
     float sq[4][4];
     token_colsum<QG>(acc, sq);
     __shared__ float bred[4][HD];
-    if ((lane & 15) == 0)
+    if ((lane & 15) == 15)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -633,18 +633,17 @@ __global__ __launch_bounds__(256) void bert_embed_fwd_kernel(const int* __restri
 __global__ __launch_bounds__(256) void bert_embed_wgrad_kernel(const int* __restrict__ ids,
                                                                const unsigned short* __restrict__ g,
                                                                float* __restrict__ out, long T, int H) {
-  const int c8n = H / 8;
-  const long total = T * c8n;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long t = i / c8n;
-    const int c = (int)(i - t * c8n) * 8;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(g + (size_t)t * H + c);
-    if ((v[0] | v[1] | v[2] | v[3]) == 0u) continue;
-    float* o = out + (size_t)ids[t] * H + c;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      atomicAdd(o + 2 * k, __uint_as_float(v[k] << 16));
-      atomicAdd(o + 2 * k + 1, __uint_as_float(v[k] & 0xFFFF0000u));
+  // one wave per token row, lanes on consecutive columns: each atomic instruction covers 64
+  // consecutive floats (2 cache lines; an 8-columns-per-lane layout spreads one instruction
+  // over 16 lines and measured 1.5 ms slower per BERT step)
+  const int lane = threadIdx.x & 63;
+  const long nw = (long)gridDim.x * (blockDim.x >> 6);
+  for (long t = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < T; t += nw) {
+    const unsigned short* gr = g + (size_t)t * H;
+    float* o = out + (size_t)ids[t] * H;
+    for (int c = lane; c < H; c += 64) {
+      const unsigned short b = gr[c];
+      if (b & 0x7FFF) atomicAdd(o + c, __uint_as_float((unsigned)b << 16));
     }
   }
 }
@@ -1197,8 +1196,7 @@ PV_API int pv_bert_embed_fwd(const int* ids, const float* word, const float* pos
 // out (V, H) fp32 += rows of g (T, H) bf16 at ids (atomics; all-zero pieces skipped)
 PV_API int pv_bert_embed_wgrad(const int* ids, const void* g, float* out, long T, int H, void* stream) {
   if (T <= 0 || H % 8) return -1;
-  const long total = T * (H / 8);
-  long blocks = (total + 255) / 256;
+  long blocks = (T + 3) / 4;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pv::tfm::bert_embed_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ids,
                      (const unsigned short*)g, out, T, H);
