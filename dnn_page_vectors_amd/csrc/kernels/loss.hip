@@ -686,12 +686,6 @@ __global__ __launch_bounds__(NW * 64, 2) void ib5_kernel(const unsigned short* _
   }
 }
 
-__device__ __forceinline__ float mul_f32_scalar(float a, float b) {
-  float r;
-  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
 // ---- ib7: ib5 software-pipelined ------------------------------------------------------------
 // ib5 runs each tile as S product -> epilogue -> out product, and the one-barrier-per-tile ring
 // keeps the 8 waves of a workgroup in phase: both waves of a SIMD sit in their MFMA phase or in
@@ -840,21 +834,18 @@ __global__ __launch_bounds__(NW * 64, 2) void ib7_kernel(const unsigned short* _
           xx = __builtin_fmaf(v, gl, -gl);
         }
         if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
-        // a scalar v_mul_f32 the compiler cannot SLP-pack into v_pk_mul_f32 (a packed f32 op
-        // beside MFMAs costs ~22 cycles: MI355X_MICROARCH.md)
-        gv[r] = mul_f32_scalar(ROW ? rsc : ysv[r], __builtin_amdgcn_exp2f(xx));
+        gv[r] = (ROW ? rsc : ysv[r]) * __builtin_amdgcn_exp2f(xx);
       }
       gp[yt][j >> 1][(j & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
       gp[yt][j >> 1][(j & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
     };
     // phase 1: this tile's S rows 32..63 (acc[1]) beside the epilogue of rows 0..31
-    {  // A fragments two k-steps ahead (LDS latency under 8 waves' load)
-      bf16x8 a = ldA(cb, 0, 1), a2 = ldA(cb, 1, 1);
+    {
+      bf16x8 a = ldA(cb, 0, 1);
 #pragma unroll
       for (int ks = 0; ks < T::K16; ++ks) {
         const bf16x8 b = a;
-        a = a2;
-        if (ks + 2 < T::K16) a2 = ldA(cb, ks + 2, 1);
+        if (ks + 1 < T::K16) a = ldA(cb, ks + 1, 1);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[ks], ks == 0 ? f32x16{} : acc[1], 0, 0, 0);
         if ((ks & 1) == 0 && ks < 8) epi4(0, ks >> 1);
         __builtin_amdgcn_sched_barrier(0);
@@ -864,16 +855,14 @@ __global__ __launch_bounds__(NW * 64, 2) void ib7_kernel(const unsigned short* _
     // are computed and unused) and out^T += Y^T G^T over rows 0..31, beside the epilogue of
     // rows 32..63
     {
-      bf16x8 a = ldA(nbp, 0, 0), a2 = ldA(nbp, 1, 0);
-      bf16x8 at = ldT(cb, 0, 0, 0), at2 = ldT(cb, 0, 1 / T::FT, 1 % T::FT);
+      bf16x8 a = ldA(nbp, 0, 0);
+      bf16x8 at = ldT(cb, 0, 0, 0);
 #pragma unroll
       for (int ks = 0; ks < T::K16; ++ks) {
         const bf16x8 b = a, bt = at;
-        a = a2;
-        at = at2;
-        if (ks + 2 < T::K16) {
-          a2 = ldA(nbp, ks + 2, 0);
-          at2 = ldT(cb, 0, (ks + 2) / T::FT, (ks + 2) % T::FT);
+        if (ks + 1 < T::K16) {
+          a = ldA(nbp, ks + 1, 0);
+          at = ldT(cb, 0, (ks + 1) / T::FT, (ks + 1) % T::FT);
         }
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[ks], ks == 0 ? f32x16{} : acc[0], 0, 0, 0);
         const int s2 = ks / T::FT, f = ks % T::FT;  // 2 FT = K16 out-product steps over rows 0..31
@@ -1253,16 +1242,16 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
 
 // Kernel generation (PAGEVEC_IB / pv_ib_set_version), read once per process so the
 // workspace queries and the launches always agree:
-//   5 (default): ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for
-//                the rest (the dD pass measured equal or faster on ib3: docs/PERF.md)
+//   7 (default): ib7 (ib5 software-pipelined) for every pass at DP = 160 / 128, ib3 for the rest
+//                (fused forward -15 %, dD pass -3 % vs gens 5 / 3: profiles/r5_ib7/)
+//   5: ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for the rest
 //   3: ib3 everywhere (A/B and the ib5-vs-ib3 numerics test)
-//   7: ib7 (ib5 software-pipelined) for every pass at DP = 160 / 128, ib3 for the rest
 static int g_ib_version = -1;
 static int ib_version() {
   if (g_ib_version < 0) {
     const char* e = getenv("PAGEVEC_IB");
-    const int v = e ? atoi(e) : 5;
-    g_ib_version = (v == 3 || v == 7) ? v : 5;
+    const int v = e ? atoi(e) : 7;
+    g_ib_version = (v == 3 || v == 5) ? v : 7;
   }
   return g_ib_version;
 }

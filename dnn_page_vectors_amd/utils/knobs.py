@@ -57,7 +57,7 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_ATTN_BGRAD": ("ab", "1", "qkv bias gradient from the attention backward's partial column sums"),
     "PAGEVEC_BERT_EMBED": ("ab", "1", "BERT embedding front end as one fused gather + add kernel"),
     "PAGEVEC_FFN_LT": ("ab", "1", "BERT FFN bias + GELU (and its backward) in hipBLASLt GEMM epilogues"),
-    "PAGEVEC_IB": ("ab", "5", "in-batch loss kernel generation"),
+    "PAGEVEC_IB": ("ab", "7", "in-batch loss kernel generation (7 pipelined ib7, 5 ib5 + ib3, 3 ib3)"),
     "PAGEVEC_IB_WIDE": ("ab", "1", "wide-vector (D = 768) loss on the ibw flash kernel (0: fp32 S blocks + GEMMs)"),
     "PAGEVEC_IB_ROWS_BLOCK": ("ab", str(1 << 25), "wide-vector loss column block (elements)"),
     "PAGEVEC_NO_MIRROR": ("ab", "0", "no bf16 mirror written by the Adam kernel"),
