@@ -424,8 +424,13 @@ class _BertEmbedFn(torch.autograd.Function):
 
 
 def bert_embed(word: torch.Tensor, pos: torch.Tensor, typ: torch.Tensor, ids_list) -> Optional[torch.Tensor]:
-    """Packed (T, H) bf16 embeddings of several id batches, or None off the HIP path."""
-    if not (use_hip(word) and word.shape[1] % 8 == 0 and len(ids_list) <= 4 and BERT_EMBED):
+    """Packed (T, H) bf16 embeddings of several id batches, or None off the HIP path and in the
+    deterministic mode (the word-table gradient here is float atomics; the per-group path's
+    index_add_ is deterministic there)."""
+    from . import determinism
+
+    if not (use_hip(word) and word.shape[1] % 8 == 0 and len(ids_list) <= 4 and BERT_EMBED) \
+            or determinism.enabled():
         return None
     from ..parallel.sparse_rows import note_rows
 

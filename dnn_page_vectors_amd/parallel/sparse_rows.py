@@ -179,6 +179,14 @@ class SparseTables:
         h1.wait()
         h2.wait()
         g2 = self.grad2d(t)
+        if g2.is_cuda:
+            # launch() ran on the stream of the table's gradient hook (the query tower's side
+            # stream when that tower owns the table): these blocks belong to that stream's
+            # allocator pool, and without this the next step's side-stream allocations could
+            # reuse them before the index_fill_ / index_add_ below have run on this stream
+            cur = torch.cuda.current_stream(g2.device)
+            for x in (u, all_rows, all_vals):
+                x.record_stream(cur)
         # padding entries name row 0 with zero values: zeroing / adding zero to an untouched
         # row (zero by construction) changes nothing
         g2.index_fill_(0, u.clamp(min=0).long(), 0.0)
