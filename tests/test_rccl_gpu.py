@@ -139,6 +139,9 @@ def test_rccl_world1_forced_collectives_match_single_process():
         assert r["grad_rel"] < 2e-2, r
 
 
+GRAD_STEPS = 5
+
+
 def _graph_worker(port, models, steps, out):
     """Eager vs captured data-parallel step on a world-1 RCCL group with every collective path
     forced on: the same init, the same fresh batch each step."""
@@ -176,7 +179,12 @@ def _graph_worker(port, models, steps, out):
                 runs[graph] = (losses, grads, tr.flat.data.detach().clone(), tr._graph is not None)
             (le, ge, pe, _), (lg, gg, pg, captured) = runs[False], runs[True]
             dl = max(abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lg))
-            dg = max(float((a - b).abs().max() / a.abs().max().clamp(min=1e-30)) for a, b in zip(ge, gg))
+            # gradients over the first GRAD_STEPS steps: float-atomic sums make two EAGER runs of
+            # the row-sparse CDSSM differ by ~1e-7, and a later step whose cosine clip / max-pool
+            # argmax flips on that difference jumps by O(0.1) (eager vs eager: 0.245 at step 6,
+            # profiles/r5_sparse_diag/); the loss is compared over every step
+            dg = max(float((a - b).abs().max() / a.abs().max().clamp(min=1e-30))
+                     for a, b in list(zip(ge, gg))[:GRAD_STEPS])
             dp = float((pe - pg).abs().max())
             res[model] = dict(captured=captured, loss_rel=dl, grad_rel=dg, param_abs=dp, steps=len(le))
         out.put(("ok", res))
