@@ -27,6 +27,20 @@ __device__ __forceinline__ float warmup_scale(const float* tdev) {
   return w > 0.f ? fminf(1.f, tdev[0] / w) : 1.f;
 }
 
+// NT: non-temporal loads / stores (the update streams 28-30 B per parameter once per step,
+// far beyond the L2 / Infinity Cache: no reuse to keep); A/B via pv_adam_set_nt
+template <int NT>
+__device__ __forceinline__ f32x4 ld4(const float* b, long i) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(b) + i);
+  else return reinterpret_cast<const f32x4*>(b)[i];
+}
+template <int NT>
+__device__ __forceinline__ void st4(float* b, long i, const f32x4& x) {
+  if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(b) + i);
+  else reinterpret_cast<f32x4*>(b)[i] = x;
+}
+
+template <int NT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
                                                    float b1, float b2, float eps, float wd, int torch_style,
@@ -62,33 +76,33 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   long i = i4;
   for (; i + stride < n4; i += 2 * stride) {
     const long j = i + stride;
-    f32x4 p0 = reinterpret_cast<f32x4*>(p)[i], p1 = reinterpret_cast<f32x4*>(p)[j];
-    f32x4 g0 = reinterpret_cast<const f32x4*>(g)[i], g1 = reinterpret_cast<const f32x4*>(g)[j];
-    f32x4 m0 = reinterpret_cast<f32x4*>(m)[i], m1 = reinterpret_cast<f32x4*>(m)[j];
-    f32x4 v0 = reinterpret_cast<f32x4*>(v)[i], v1 = reinterpret_cast<f32x4*>(v)[j];
+    f32x4 p0 = ld4<NT>(p, i), p1 = ld4<NT>(p, j);
+    f32x4 g0 = ld4<NT>(g, i), g1 = ld4<NT>(g, j);
+    f32x4 m0 = ld4<NT>(m, i), m1 = ld4<NT>(m, j);
+    f32x4 v0 = ld4<NT>(v, i), v1 = ld4<NT>(v, j);
     upd(p0, g0, m0, v0);
     upd(p1, g1, m1, v1);
     if (p16) {  // bf16 compute copy of the updated weights (consumers skip their cast kernel)
       store_bf16x4(p16 + 4 * i, p0);
       store_bf16x4(p16 + 4 * j, p1);
     }
-    reinterpret_cast<f32x4*>(p)[i] = p0;
-    reinterpret_cast<f32x4*>(m)[i] = m0;
-    reinterpret_cast<f32x4*>(v)[i] = v0;
-    reinterpret_cast<f32x4*>(p)[j] = p1;
-    reinterpret_cast<f32x4*>(m)[j] = m1;
-    reinterpret_cast<f32x4*>(v)[j] = v1;
+    st4<NT>(p, i, p0);
+    st4<NT>(m, i, m0);
+    st4<NT>(v, i, v0);
+    st4<NT>(p, j, p1);
+    st4<NT>(m, j, m1);
+    st4<NT>(v, j, v1);
   }
   for (; i < n4; i += stride) {
-    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
-    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+    f32x4 pp = ld4<NT>(p, i);
+    f32x4 gg = ld4<NT>(g, i);
+    f32x4 mm = ld4<NT>(m, i);
+    f32x4 vv = ld4<NT>(v, i);
     upd(pp, gg, mm, vv);
     if (p16) store_bf16x4(p16 + 4 * i, pp);
-    reinterpret_cast<f32x4*>(p)[i] = pp;
-    reinterpret_cast<f32x4*>(m)[i] = mm;
-    reinterpret_cast<f32x4*>(v)[i] = vv;
+    st4<NT>(p, i, pp);
+    st4<NT>(m, i, mm);
+    st4<NT>(v, i, vv);
   }
   for (long i = n4 * 4 + i4; i < n; i += stride) {
     float gk = g[i] + wd * p[i];
@@ -252,9 +266,29 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
 
 using namespace pv;
 
+static int g_adam_nt = -1, g_adam_grid = 4096;
+static int adam_nt() {
+  if (g_adam_nt < 0) {
+    const char* e = getenv("PAGEVEC_ADAM_NT");
+    g_adam_nt = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  return g_adam_nt;
+}
+// dense Adam launch (plain / non-temporal streams)
+static void launch_adam(dim3 grid, hipStream_t st, float* p, const float* g, float* m, float* v, long n, float lr,
+                        float b1, float b2, float eps, float wd, int torch_style, float bc2i, const float* skip,
+                        const float* tdev, unsigned short* p16) {
+  if (adam_nt())
+    hipLaunchKernelGGL(pv::optim::adam_kernel<1>, grid, dim3(256), 0, st, p, g, m, v, n, lr, b1, b2, eps, wd,
+                       torch_style, bc2i, skip, tdev, p16);
+  else
+    hipLaunchKernelGGL(pv::optim::adam_kernel<0>, grid, dim3(256), 0, st, p, g, m, v, n, lr, b1, b2, eps, wd,
+                       torch_style, bc2i, skip, tdev, p16);
+}
+
 static unsigned grid_for(long n, int per_thread) {
   long b = (n / per_thread + 255) / 256;
-  if (b > 4096) b = 4096;
+  if (b > g_adam_grid) b = g_adam_grid;
   if (b < 1) b = 1;
   return (unsigned)b;
 }
@@ -266,8 +300,8 @@ PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
   hipLaunchKernelGGL(pv::optim::step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, tdev);
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                     lr, b1, b2, eps, wd, torch_style, 1.f, skip, (const float*)tdev, (unsigned short*)nullptr);
+  launch_adam(dim3(grid_for(n, 4)), (hipStream_t)stream, p, g, m, v, n, lr, b1, b2, eps, wd, torch_style, 1.f, skip,
+              (const float*)tdev, (unsigned short*)nullptr);
   PV_LAUNCH_CHECK();
   return 0;
 }
@@ -275,6 +309,13 @@ PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
 // Segmented step (lazy embedding rows): pv_step_inc once, then one pv_adam_seg per range of
 // the flat buffer — row_len 0: dense update of n elements; row_len > 0: lazy rows of an
 // (n / row_len, row_len) table.
+// A/B: non-temporal Adam streams (nt 0 / 1) and the dense launch's workgroup cap
+PV_API int pv_adam_set_nt(int nt, int grid_cap) {
+  g_adam_nt = nt ? 1 : 0;
+  if (grid_cap >= 256 && grid_cap <= 65536) g_adam_grid = grid_cap;
+  return 0;
+}
+
 PV_API int pv_step_inc(float* tdev, void* stream) {
   hipLaunchKernelGGL(pv::optim::step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, tdev);
   PV_LAUNCH_CHECK();
@@ -289,8 +330,8 @@ PV_API int pv_adam_seg(float* p, const float* g, float* m, float* v, long n, int
   if (n <= 0) return 0;
   unsigned short* h = (unsigned short*)p16;
   if (row_len == 0) {
-    hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                       lr, b1, b2, eps, wd, torch_style, 1.f, skip, tdev, h);
+    launch_adam(dim3(grid_for(n, 4)), (hipStream_t)stream, p, g, m, v, n, lr, b1, b2, eps, wd, torch_style, 1.f, skip,
+                tdev, h);
   } else {
     if (row_len % 4 || row_len > 1024 || n % row_len) return -2;
     const long rows = n / row_len;
@@ -350,8 +391,8 @@ PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int ste
   } else {
     lr_t = (float)(lr * sqrt(bc2) / bc1);
   }
-  hipLaunchKernelGGL(pv::optim::adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                     lr_t, b1, b2, eps, wd, torch_style, bc2i, skip, (const float*)nullptr, (unsigned short*)nullptr);
+  launch_adam(dim3(grid_for(n, 4)), (hipStream_t)stream, p, g, m, v, n, lr_t, b1, b2, eps, wd, torch_style, bc2i, skip,
+              (const float*)nullptr, (unsigned short*)nullptr);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -125,6 +125,7 @@ SIGS = {
     "pv_loss_stats": "pp" "i" "pp" "p",
     "pv_ib_grad_scale": "p" "i" "f" "p" "i" "f" "p" "i" "ppp" "p",
     "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
+    "pv_adam_set_nt": "ii",
     "pv_step_inc": "p" "p",
     "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "pp" "p",
     "pv_adam_rows": "pppp" "i" "pl" "p" "fffff" "i" "pp" "p",

@@ -1974,3 +1974,31 @@ def test_inbatch_loss_ib7_matches_ib5(B, M, clip, D, ver):
     assert torch.equal(res[5][0], res[ver][0])
     assert torch.equal(res[5][1], res[ver][1])
     torch.testing.assert_close(res[ver][2], res[5][2], rtol=1e-4, atol=1e-6)
+
+
+def test_adam_nontemporal_bit_identical():
+    """optim.hip::adam_kernel<1> (non-temporal loads / stores) and a larger workgroup cap
+    change only the memory path: the update is bit-identical to the default kernel."""
+    from dnn_page_vectors_amd.ops._common import P, lib, stream
+
+    L_ = lib()
+    torch.manual_seed(2)
+    n = 1_000_003
+    base = [torch.randn(n, device=DEV) * 0.01 for _ in range(4)]
+    base[3].abs_()
+    outs = []
+    try:
+        for nt, cap in ((0, 4096), (1, 4096), (1, 16384)):
+            L_.pv_adam_set_nt(nt, cap)
+            p, g, m, v = (x.clone() for x in base)
+            t = torch.zeros(1, device=DEV)
+            for _ in range(3):
+                assert L_.pv_adam_dev(P(p), P(g), P(m), P(v), n, P(t), 1e-3, 0.9, 0.999, 1e-7, 0.0, 0, None,
+                                      stream(p.device)) == 0
+            torch.cuda.synchronize()
+            outs.append((p, m, v))
+    finally:
+        L_.pv_adam_set_nt(0, 4096)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
