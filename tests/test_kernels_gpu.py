@@ -1998,7 +1998,7 @@ def test_adam_nontemporal_bit_identical():
             torch.cuda.synchronize()
             outs.append((p, m, v))
     finally:
-        L_.pv_adam_set_nt(0, 4096)
+        L_.pv_adam_set_nt(0, 16384)  # the defaults
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)

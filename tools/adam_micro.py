@@ -46,7 +46,7 @@ def main():
         for (nt, cap), xs in res.items():
             us = statistics.median(xs)
             out[f"n{n}_nt{nt}_cap{cap}"] = {"us": round(us, 1), "TBps": round(28 * n / us / 1e6, 2)}
-    L.pv_adam_set_nt(0, 4096)
+    L.pv_adam_set_nt(0, 16384)  # the defaults
     print(json.dumps(out))
 
 
