@@ -42,6 +42,9 @@ def _cfg(model):
     if model == "cdssm_sparse":  # row-sparse table gradients: the fixed-capacity row exchange
         return preset_config("cdssm_ngram_bf16").replace(batch_size=64, document_length=256, grad_bucket_mb=1.0,
                                                          sparse_embedding_grad=True, lazy_embedding_adam=True)
+    if model == "bert":  # D = 768: the wide-vector cross-GPU path (_CrossGpuRowsFn + the ibw kernel)
+        return preset_config("bert_dp8").replace(bert_layers=2, batch_size=16, document_length=64, query_length=16,
+                                                 grad_bucket_mb=32.0)
     return preset_config("mlp_xgpu").replace(batch_size=64, document_length=256, grad_bucket_mb=8.0)
 
 
@@ -84,12 +87,11 @@ def _worker(port, models, out):
             calls["page_gather"] += 1
             orig_pg(self, *a, **k)
         lops.PageGather.__init__ = pg_init
-        orig_fn = lops._CrossGpuFn.forward
-
-        def fn_fwd(*a, **k):
-            calls["cross_gpu_fn"] += 1
-            return orig_fn(*a, **k)
-        lops._CrossGpuFn.forward = staticmethod(fn_fwd)
+        for cls in (lops._CrossGpuFn, lops._CrossGpuRowsFn):  # D <= 192 / the wide-vector path
+            def fn_fwd(*a, _f=cls.forward, **k):
+                calls["cross_gpu_fn"] += 1
+                return _f(*a, **k)
+            cls.forward = staticmethod(fn_fwd)
         res = {}
         for model in models:
             cfg = _cfg(model)
@@ -211,3 +213,24 @@ def test_rccl_world1_graph_captured_dp_step_matches_eager():
         print(model, r)
         assert r["captured"], r
         assert r["loss_rel"] < 2e-3 and r["grad_rel"] < 2e-2, r
+
+
+def test_rccl_world1_bert_wide_loss_matches_single_process():
+    """The D = 768 cross-GPU loss (BERT) with RCCL collectives: page gather, query / scale
+    gathers and bucketed all-reduce on a world-1 nccl group (round 4 covered this path only
+    over gloo) — loss and flat gradient equal to the collectives-off step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), ("bert",), q))
+    p.start()
+    status, res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert status == "ok", res
+    r = res["bert"]
+    print(r)
+    u, i = r["used"], r["idle"]
+    assert u["page_gather"] == 1 and u["cross_gpu_fn"] == 1, r
+    assert u["all_gather_into_tensor"] >= 2 and u["all_reduce"] >= r["nbuckets"] >= 1, r
+    assert i["all_gather_into_tensor"] == 0 and i["page_gather"] == 0 and i["cross_gpu_fn"] == 0, r
+    assert abs(r["loss_d"] - r["loss_s"]) <= 2e-3 * max(1.0, abs(r["loss_s"])), r
+    assert r["grad_rel"] < 2e-2, r
