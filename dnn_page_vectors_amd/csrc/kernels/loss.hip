@@ -902,279 +902,6 @@ __global__ __launch_bounds__(NW * 64, 2) void ib7_kernel(const unsigned short* _
   }
 }
 
-// ---- ib8: 64 X rows per wave, one wave per SIMD --------------------------------------------
-// ib7 reads every staged Y fragment from LDS once per 32-row wave; at 8 waves per CU the LDS
-// reads and the two waves' VALU epilogues share one issue port per SIMD.  ib8 gives each of 4
-// waves (one per SIMD, 512 registers: the out accumulators live in AGPRs) 64 X rows as two
-// 32-row halves: every S-product A fragment and every out-product A^T fragment feeds two
-// MFMAs (half the LDS bytes per FLOP).  Per tile two balanced phases of 40 MFMAs each:
-//   P1: this tile's S rows 32..63 (20) + the PREVIOUS tile's out product over its rows 32..63
-//       (20), beside the epilogue of this tile's rows 0..31 (32 S elements per lane)
-//   P2: the NEXT tile's S rows 0..31 (20) + this tile's out product over rows 0..31 (20),
-//       beside the epilogue of this tile's rows 32..63
-// so the previous tile stays resident one more iteration: a 5-slot ring (100 KB at DP = 160),
-// staged three tiles ahead.  Same per-element arithmetic and the same out-product k-order as
-// ib5 / ib7: bit-identical results.
-template <int KS, bool ROW, bool CLIP, bool FWD = false>
-__global__ __launch_bounds__(256, 1) void ib8_kernel(const unsigned short* __restrict__ X,
-                                                  const unsigned short* __restrict__ Y,
-                                                  const float* __restrict__ scale, float* __restrict__ out,
-                                                  float* __restrict__ ws, int nx, int ny, int per_split,
-                                                  int nrb, float gamma, float* __restrict__ part = nullptr) {
-  static_assert(!FWD || ROW, "the fused forward runs over query rows");
-  static_assert(KS == 4 || KS == 5, "ib8: chunk swizzles exist for DP = 128 and 160");
-  static_assert(Ib5<KS>::K16 >= 8, "ib8: one epilogue group per S k-step");
-  constexpr int NW = 4;
-  using T = Ib5<KS>;
-  constexpr int NB = 5;
-  __shared__ __attribute__((aligned(1024))) char ring[NB * T::TILE_B];
-  __shared__ __attribute__((aligned(16))) float ysc[NB][TD];
-  // the wave index as a scalar the compiler knows is < NW: the staging loop's piece guards and the
-  // waits below compile to straight-line code (per-lane branches there split the tile loop into
-  // blocks, and machine sinking then moved half the epilogue past the barrier)
-  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  __builtin_assume(wave >= 0 && wave < NW);
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = bid / nrb, rb = bid - split * nrb;
-  const int r0 = rb * (NW * 64) + wave * 64;
-  const int c_begin = split * per_split, c_end = min(ny, c_begin + per_split);
-  const int ntiles = (c_end - c_begin + TD - 1) / TD;
-  const float gl = gamma * 1.4426950408889634f;
-  // staging: PIECES / NW 1 KB DMA instructions per wave (+ the tile's 64 row scales, !ROW,
-  // issued by every wave so the per-wave op count is uniform)
-  static_assert(T::PIECES % NW == 0, "ib8: whole DMA pieces per wave");
-  constexpr int NPW = T::PIECES / NW + (ROW ? 0 : 1);
-  auto stage = [&](int c0s, int sbi) {
-    char* dst = ring + sbi * T::TILE_B;
-#pragma unroll
-    for (int u = 0; u < T::PIECES / NW; ++u) {
-      const int p = wave + NW * u;
-      const int q = p * 64 + lane;
-      const int r = q / T::CPR, pc = q - r * T::CPR;
-      const int c = pc ^ ib5_swz<KS>(r);
-      const int row = min(c0s + r, c_end - 1);
-      glds16(Y + (size_t)row * T::DP + c * 8, dst + p * 1024);
-    }
-    if constexpr (!ROW) glds4(scale + min(c0s + lane, c_end - 1), ysc[sbi]);
-  };
-  bf16x8 xb[2][T::K16];
-  float rsc[2], rs[2] = {0.f, 0.f};
-#pragma unroll
-  for (int xh = 0; xh < 2; ++xh) {
-    const int x = r0 + 32 * xh + l32;
-#pragma unroll
-    for (int ks = 0; ks < T::K16; ++ks)
-      xb[xh][ks] = x < nx ? *reinterpret_cast<const bf16x8*>(X + (size_t)x * T::DP + 16 * ks + 8 * h)
-                          : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    rsc[xh] = (ROW && !FWD && x < nx) ? scale[x] : 0.f;
-  }
-  f32x16 o[2][T::FT];
-#pragma unroll
-  for (int xh = 0; xh < 2; ++xh)
-#pragma unroll
-    for (int f = 0; f < T::FT; ++f)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[xh][f][r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    if (i < ntiles) stage(c_begin + i * TD, i);
-  wait_vm(ntiles > 2 ? NPW : 0);
-  __builtin_amdgcn_s_barrier();
-  const int tq = (lane & 15) >> 2, tf = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  // fragment addresses: see ib7
-  const int swzA = ib5_swz<KS>(l32);
-  const int offA0 = l32 * T::ROWB + ((h ^ swzA) << 4), offA1 = l32 * T::ROWB + (((2 + h) ^ swzA) << 4);
-  const int ylo0 = 4 * h + tq;
-  const int offTlo = ylo0 * T::ROWB + (((tf >> 3) ^ ib5_swz<KS>(ylo0)) << 4) + (tf & 7) * 2;
-  const int offThi = (ylo0 + 8) * T::ROWB + (((tf >> 3) ^ ib5_swz<KS>(ylo0 + 8)) << 4) + (tf & 7) * 2;
-  auto ldA = [&](const char* base, int ks, int yt) {
-    if constexpr (KS == 5) {
-      const char* p = base + ((ks & 1) ? offA1 : offA0) + 64 * (ks >> 1) + 32 * yt * T::ROWB;
-      return *reinterpret_cast<const bf16x8*>(p);
-    } else {
-      const int y = 32 * yt + l32, c = 2 * ks + h;
-      return *reinterpret_cast<const bf16x8*>(base + y * T::ROWB + ((c ^ ib5_swz<KS>(y)) << 4));
-    }
-  };
-  auto ldT = [&](const char* base, int yt, int s2, int f) {
-    typedef __attribute__((address_space(3))) v4s lds_v4s;
-    const char *plo, *phi;
-    if constexpr (KS == 5) {
-      const int c = (32 * yt + 16 * s2) * T::ROWB + 64 * f;
-      plo = base + offTlo + c;
-      phi = base + offThi + c;
-    } else {
-      const int ylo = 32 * yt + 16 * s2 + 4 * h + tq, yhi = ylo + 8;
-      const int fe = 32 * f + tf;
-      plo = base + ylo * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(ylo))) << 4) + (fe & 7) * 2;
-      phi = base + yhi * T::ROWB + ((((fe >> 3) ^ ib5_swz<KS>(yhi))) << 4) + (fe & 7) * 2;
-    }
-    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(plo));
-    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(phi));
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  // acc[yt][xh][r] = S^T[y = 32 yt + 8 (r >> 2) + 4 h + (r & 3)][x = r0 + 32 xh + l32]
-  f32x16 acc[2][2];
-  u32x4 gp[2][2][2];  // G^T fragments [yt][xh][s2]; gp[1] carries into the next tile's P1
-  {
-    bf16x8 a = ldA(ring, 0, 0);
-#pragma unroll
-    for (int ks = 0; ks < T::K16; ++ks) {
-      const bf16x8 b = a;
-      if (ks + 1 < T::K16) a = ldA(ring, ks + 1, 0);
-#pragma unroll
-      for (int xh = 0; xh < 2; ++xh)
-        acc[0][xh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[xh][ks], ks == 0 ? f32x16{} : acc[0][xh], 0, 0, 0);
-    }
-  }
-  auto slot = [&](int t) { return t % NB; };
-  auto tile = [&](int t, auto full_c, auto first_c) {
-    constexpr bool FULL = decltype(full_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value;
-    const int c0 = c_begin + t * TD;
-    const int sb = slot(t);
-    const bool ahead = t + 3 < ntiles;
-    if (ahead) stage(c0 + 3 * TD, slot(t + 3));  // slot (t + 3) % 5 = (t - 2) % 5: free since the last barrier
-    const char* cb = ring + sb * T::TILE_B;
-    const char* pb = ring + slot(t + NB - 1) * T::TILE_B;  // previous tile (P1 out product)
-    const char* nbp = ring + slot(t + 1) * T::TILE_B;
-    auto epi4 = [&](int yt, int xh, int j) {
-      f32x4 ysv;
-      if constexpr (!ROW) ysv = *reinterpret_cast<const f32x4*>(&ysc[sb][32 * yt + 8 * j + 4 * h]);
-      float gv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int yr = 32 * yt + 8 * j + 4 * h + r;
-        const float v = acc[yt][xh][4 * j + r];
-        float xx;
-        if constexpr (FWD) {
-          const float vc = CLIP ? __builtin_amdgcn_fmed3f(v, 0.f, 1.f) : v;
-          xx = __builtin_fmaf(vc, gl, -gl);
-          if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
-          const float e = __builtin_amdgcn_exp2f(xx);
-          rs[xh] += e;
-          gv[r] = (!CLIP || vc == v) ? e : 0.f;
-          continue;
-        }
-        if constexpr (CLIP) {
-          const float vc = __builtin_amdgcn_fmed3f(v, 0.f, 1.f);
-          xx = vc == v ? __builtin_fmaf(vc, gl, -gl) : -INFINITY;
-        } else {
-          xx = __builtin_fmaf(v, gl, -gl);
-        }
-        if constexpr (!FULL) xx = c0 + yr < c_end ? xx : -INFINITY;
-        gv[r] = (ROW ? rsc[xh] : ysv[r]) * __builtin_amdgcn_exp2f(xx);
-      }
-      gp[yt][xh][j >> 1][(j & 1) * 2] = pack_bf16x2(gv[0], gv[1]);
-      gp[yt][xh][j >> 1][(j & 1) * 2 + 1] = pack_bf16x2(gv[2], gv[3]);
-    };
-    // P1: S rows 32..63 of this tile + out product of the previous tile over its rows 32..63,
-    // beside the epilogue of rows 0..31 (group ks: rows 8 (ks & 3) + .., half ks >> 2)
-    {
-      bf16x8 a = ldA(cb, 0, 1);
-      bf16x8 at;
-      if constexpr (!FIRST) at = ldT(pb, 1, 0, 0);
-#pragma unroll
-      for (int ks = 0; ks < T::K16; ++ks) {
-        const bf16x8 b = a, bt = at;
-        if (ks + 1 < T::K16) {
-          a = ldA(cb, ks + 1, 1);
-          if constexpr (!FIRST) at = ldT(pb, 1, (ks + 1) / T::FT, (ks + 1) % T::FT);
-        }
-#pragma unroll
-        for (int xh = 0; xh < 2; ++xh)
-          acc[1][xh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[xh][ks], ks == 0 ? f32x16{} : acc[1][xh], 0, 0, 0);
-        if constexpr (!FIRST) {
-          const int s2 = ks / T::FT, f = ks % T::FT;
-#pragma unroll
-          for (int xh = 0; xh < 2; ++xh)
-            o[xh][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bt, __builtin_bit_cast(bf16x8, gp[1][xh][s2]), o[xh][f],
-                                                               0, 0, 0);
-        }
-        if (ks < 8) epi4(0, ks >> 2, ks & 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // P2: the next tile's S rows 0..31 (slot t + 1: stale rows past the last tile, computed and
-    // unused) + this tile's out product over rows 0..31, beside the epilogue of rows 32..63
-    {
-      bf16x8 a = ldA(nbp, 0, 0);
-      bf16x8 at = ldT(cb, 0, 0, 0);
-#pragma unroll
-      for (int ks = 0; ks < T::K16; ++ks) {
-        const bf16x8 b = a, bt = at;
-        if (ks + 1 < T::K16) {
-          a = ldA(nbp, ks + 1, 0);
-          at = ldT(cb, 0, (ks + 1) / T::FT, (ks + 1) % T::FT);
-        }
-#pragma unroll
-        for (int xh = 0; xh < 2; ++xh)
-          acc[0][xh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, xb[xh][ks], ks == 0 ? f32x16{} : acc[0][xh], 0, 0, 0);
-        const int s2 = ks / T::FT, f = ks % T::FT;
-#pragma unroll
-        for (int xh = 0; xh < 2; ++xh)
-          o[xh][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bt, __builtin_bit_cast(bf16x8, gp[0][xh][s2]), o[xh][f], 0,
-                                                             0, 0);
-        if (ks < 8) epi4(1, ks >> 2, ks & 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // the G^T fragments of rows 32..63 (used by the next tile's P1) materialise here, before the
-    // wait branches: otherwise machine sinking moves their epilogue past the barrier
-#pragma unroll
-    for (int xh = 0; xh < 2; ++xh)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) asm volatile("" : "+v"(gp[1][xh][s2]));
-    // tile t + 2 landed (this wave's NPW ops; the barrier covers the others'); t + 3 may stay in flight
-    if (ahead) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  const int nfull = (c_end - c_begin) / TD;
-  if (nfull >= 1) {
-    tile(0, std::true_type{}, std::true_type{});
-#pragma unroll 1
-    for (int t = 1; t < nfull; ++t) tile(t, std::true_type{}, std::false_type{});
-    if (nfull < ntiles) tile(nfull, std::false_type{}, std::false_type{});
-  } else if (ntiles > 0) {
-    tile(0, std::false_type{}, std::true_type{});
-  }
-  // drain: the last tile's out product over its rows 32..63
-  if (ntiles > 0) {
-    const char* lb = ring + slot(ntiles - 1) * T::TILE_B;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int f = 0; f < T::FT; ++f) {
-        const bf16x8 at = ldT(lb, 1, s2, f);
-#pragma unroll
-        for (int xh = 0; xh < 2; ++xh)
-          o[xh][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(at, __builtin_bit_cast(bf16x8, gp[1][xh][s2]), o[xh][f], 0,
-                                                             0, 0);
-      }
-  }
-  float* dst = (gridDim.x == (unsigned)nrb) ? out : ws + (size_t)split * nx * T::DP;
-#pragma unroll
-  for (int xh = 0; xh < 2; ++xh) {
-    const int x = r0 + 32 * xh + l32;
-    if constexpr (FWD) {
-      float v = rs[xh];
-      v += __shfl_xor(v, 32, 64);
-      if (h == 0 && x < nx) part[(size_t)split * nx + x] = v;
-    }
-    if (x < nx) {
-      float* orow = dst + (size_t)x * T::DP;
-#pragma unroll
-      for (int f = 0; f < T::FT; ++f)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4*>(orow + 32 * f + 8 * j + 4 * h) =
-              f32x4{o[xh][f][4 * j], o[xh][f][4 * j + 1], o[xh][f][4 * j + 2], o[xh][f][4 * j + 3]};
-    }
-  }
-}
-
 // out[i] = sum_s ws[s][i], n4 = nx*DP/4
 __global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                               long n4, int ns) {
@@ -1519,13 +1246,12 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
 //                (fused forward -15 %, dD pass -3 % vs gens 5 / 3: profiles/r5_ib7/)
 //   5: ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for the rest
 //   3: ib3 everywhere (A/B and the ib5-vs-ib3 numerics test)
-//   8: ib8 (64 X rows per wave, one wave per SIMD) for every pass at DP = 160 / 128
 static int g_ib_version = -1;
 static int ib_version() {
   if (g_ib_version < 0) {
     const char* e = getenv("PAGEVEC_IB");
     const int v = e ? atoi(e) : 7;
-    g_ib_version = (v == 3 || v == 5 || v == 8) ? v : 7;
+    g_ib_version = (v == 3 || v == 5) ? v : 7;
   }
   return g_ib_version;
 }
@@ -1533,7 +1259,7 @@ static int ib_version() {
 PV_API int pv_ib_version() { return ib_version(); }
 // A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)
 PV_API int pv_ib_set_version(int v) {
-  if (v != 3 && v != 5 && v != 7 && v != 8) return -1;
+  if (v != 3 && v != 5 && v != 7) return -1;
   g_ib_version = v;
   return 0;
 }
@@ -1573,13 +1299,7 @@ PV_API int pv_ib_bwd(const void* X, const void* Y, const float* scale, float* ou
   const int nrb = (nx + 255) / 256;
   const dim3 grid3(nrb * ns);
 #define PV_IB_BWD(ROWV, CLIPV)                                                                                  \
-  if (ib_version() == 8 && DP == 160) {                                                                         \
-    hipLaunchKernelGGL((ib8_kernel<5, ROWV, CLIPV>), grid3, dim3(256), 0, s, (const unsigned short*)X,          \
-                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
-  } else if (ib_version() == 8 && DP == 128) {                                                                  \
-    hipLaunchKernelGGL((ib8_kernel<4, ROWV, CLIPV>), grid3, dim3(256), 0, s, (const unsigned short*)X,          \
-                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
-  } else if (ib_version() == 7 && DP == 160) {                                                                         \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
     hipLaunchKernelGGL((ib7_kernel<5, ROWV, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,          \
                        (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
   } else if (ib_version() == 7 && DP == 128) {                                                                  \
@@ -1633,13 +1353,7 @@ PV_API int pv_ib_fwd_dq(const void* X, const void* Y, float* sumexp, float* U, f
   const int nrb = (nx + 255) / 256;
   const dim3 grid3(nrb * ns);
 #define PV_IB_FWDDQ(CLIPV)                                                                                      \
-  if (ib_version() == 8 && DP == 160) {                                                                         \
-    hipLaunchKernelGGL((ib8_kernel<5, true, CLIPV, true>), grid3, dim3(256), 0, s, (const unsigned short*)X,    \
-                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
-  } else if (ib_version() == 8 && DP == 128) {                                                                  \
-    hipLaunchKernelGGL((ib8_kernel<4, true, CLIPV, true>), grid3, dim3(256), 0, s, (const unsigned short*)X,    \
-                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
-  } else if (ib_version() == 7 && DP == 160) {                                                                         \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
     hipLaunchKernelGGL((ib7_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
                        (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
   } else if (ib_version() == 7 && DP == 128) {                                                                  \
