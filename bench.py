@@ -88,8 +88,8 @@ def parse():
                          "single GPU only) and report the speedup")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the training step in a hipGraph after 2 eager steps (single process only); "
-                         "-1 = auto: on for the launch-bound mlp / chunked / bert steps, off for cdssm (its "
-                         "step is kernel-bound: eager 9.76 vs graph 9.89 ms measured)")
+                         "-1 = auto: on for the mlp / chunked / chunked_cdssm / bert steps, off for cdssm (its "
+                         "graph serialises the side streams: eager 6.74-6.82 vs graph 7.24 ms)")
     ap.add_argument("--quality-steps", type=int, default=-1,
                     help="after the timed steps, keep training (untimed, fresh synthetic batches, eager) until "
                          "this many optimizer steps in total, then measure Recall@10 on held-out pairs; "
@@ -213,7 +213,10 @@ def main():
     model = build_model(cfg, V)
     # the capture happens after 2 eager steps: only inside the untimed warmup
     if a.graph < 0:
-        a.graph = 0 if a.model in ("cdssm", "cdssm_char", "chunked_cdssm") else 1
+        # cdssm: a graph serialises the query tower / dW side streams (6.74-6.82 eager vs 7.24 ms
+        # graph, profiles/r5_graph_ab/); chunked_cdssm's eager step is bimodal (1.08 / 1.41 ms),
+        # its graph step steady at 1.13-1.14 ms
+        a.graph = 0 if a.model in ("cdssm", "cdssm_char") else 1
     if a.quality_steps < 0:
         a.quality_steps = {"cdssm": 1000, "mlp": 1000, "chunked": 500, "chunked_cdssm": 500, "cdssm_char": 500,
                            "bert": 200}[a.model]
