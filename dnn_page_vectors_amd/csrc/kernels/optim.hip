@@ -266,7 +266,7 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
 
 using namespace pv;
 
-static int g_adam_nt = -1, g_adam_grid = 16384;  // 16384: -2..4 % vs 4096 (tools/adam_micro.py)
+static int g_adam_nt = -1, g_adam_grid = 16384;  // 16384: -2..4 % vs 4096 (tools/adam_stream_micro.py)
 static int adam_nt() {
   if (g_adam_nt < 0) {
     const char* e = getenv("PAGEVEC_ADAM_NT");

@@ -1,53 +1,79 @@
-"""Dense Adam step (optim.hip::adam_kernel through pv_adam_dev) at the MLP (16 M) and BERT
-(110 M) parameter counts: plain vs non-temporal streams, workgroup caps; interleaved rounds,
-CUDA-event timed; effective HBM rate at 28 B / parameter.
+"""Flat-buffer Adam bandwidth: pv_adam (HIP) vs torch.optim.Adam(fused=True) on the same
+16 M fp32 parameters (28 bytes moved per parameter).
 
-    python tools/adam_micro.py [--n 16e6,110e6] [--rounds 5]
+    python tools/adam_micro.py [--n 16777216] [--lazy-rows 7500000 --lazy-cols 100 --touched 0.01]
+
+--lazy-rows: also time the lazy embedding-row update (pv_adam_seg row_len > 0) on a
+(rows, cols) table with a fraction ``--touched`` of rows carrying a gradient, against the
+dense update of the same table (a word-level vocabulary of millions of rows).
 """
 import argparse
 import json
 import os
-import statistics
 import sys
 
+import torch
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch  # noqa: E402
+
+
+def ev(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def lazy(a):
+    from dnn_page_vectors_amd.ops._common import P, check, lib, stream
+
+    R, C = a.lazy_rows, a.lazy_cols
+    n = R * C
+    p, m, v = (torch.zeros(n, device="cuda") for _ in range(3))
+    g = torch.zeros(R, C, device="cuda")
+    rows = torch.randperm(R, device="cuda")[:max(1, int(R * a.touched))]
+    g[rows] = torch.randn(rows.numel(), C, device="cuda")
+    t = torch.tensor([1.0, 0.0], device="cuda")  # {step, warmup steps}
+    L = lib()
+    res = {}
+    for name, rl in (("dense", 0), ("lazy", C)):
+        res[name + "_ms"] = round(ev(lambda: check(L.pv_adam_seg(P(p), P(g), P(m), P(v), n, rl, P(t), 1e-3, 0.9, 0.999,
+                                                                  1e-8, 0.0, 0, None, stream()), "seg")), 4)
+    print(json.dumps({"rows": R, "cols": C, "touched": a.touched, **res}), flush=True)
 
 
 def main():
+    from dnn_page_vectors_amd.ops._common import P, check, lib, stream
+
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", default="16e6,110e6")
-    ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--n", type=int, default=16 * 1024 * 1024)
+    ap.add_argument("--lazy-rows", type=int, default=0)
+    ap.add_argument("--lazy-cols", type=int, default=100)
+    ap.add_argument("--touched", type=float, default=0.01)
     a = ap.parse_args()
-    from dnn_page_vectors_amd.ops._common import lib, P, stream
+    if a.lazy_rows:
+        lazy(a)
+    n = a.n
+    p, g, m, v = (torch.randn(n, device="cuda") for _ in range(4))
+    v.abs_()
     L = lib()
-    dev = torch.device("cuda")
-    arms = [(0, 4096), (1, 4096), (0, 16384), (1, 16384)]
-    out = {}
-    for n in [int(float(x)) for x in a.n.split(",")]:
-        p, g, m, v = (torch.randn(n, device=dev) * 0.01 for _ in range(4))
-        v.abs_()
-        t = torch.zeros(1, device=dev)
-        s = stream(dev)
-        res = {arm: [] for arm in arms}
-        for _ in range(a.rounds):
-            for nt, cap in arms:
-                L.pv_adam_set_nt(nt, cap)
-                for _ in range(3):
-                    L.pv_adam_dev(P(p), P(g), P(m), P(v), n, P(t), 1e-4, 0.9, 0.999, 1e-7, 0.0, 0, None, s)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    L.pv_adam_dev(P(p), P(g), P(m), P(v), n, P(t), 1e-4, 0.9, 0.999, 1e-7, 0.0, 0, None, s)
-                e1.record()
-                torch.cuda.synchronize()
-                res[(nt, cap)].append(e0.elapsed_time(e1) / a.iters * 1e3)
-        for (nt, cap), xs in res.items():
-            us = statistics.median(xs)
-            out[f"n{n}_nt{nt}_cap{cap}"] = {"us": round(us, 1), "TBps": round(28 * n / us / 1e6, 2)}
-    L.pv_adam_set_nt(0, 16384)  # the defaults
-    print(json.dumps(out))
+    t_hip = ev(lambda: check(L.pv_adam(P(p), P(g), P(m), P(v), n, 5, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None,
+                                       stream()), "adam"))
+    t_sq = ev(lambda: check(L.pv_sumsq(P(g), n, P(m[:2]), stream()), "sumsq"))
+    pt = torch.nn.Parameter(torch.randn(n, device="cuda"))
+    pt.grad = torch.randn(n, device="cuda")
+    opt = torch.optim.Adam([pt], lr=1e-3, fused=True)
+    t_torch = ev(opt.step)
+    gb = 28.0 * n / 1e9
+    print(json.dumps({"n": n, "pv_adam_ms": round(t_hip, 4), "pv_adam_TBps": round(gb / t_hip, 2),
+                      "torch_fused_adam_ms": round(t_torch, 4), "torch_TBps": round(gb / t_torch, 2),
+                      "pv_sumsq_ms": round(t_sq, 4), "sumsq_TBps": round(4.0 * n / 1e9 / t_sq, 2)}), flush=True)
 
 
 if __name__ == "__main__":
