@@ -2000,3 +2000,15 @@ def test_adam_nontemporal_bit_identical():
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
+
+
+def test_loss_generation_default_matches_knob_registry():
+    """The loss-kernel generation in effect by default is the one utils/knobs.py records in
+    the bench JSON (7: ib7), unless PAGEVEC_IB overrides it."""
+    import os
+
+    from dnn_page_vectors_amd.ops._common import lib as _lib
+    from dnn_page_vectors_amd.utils.knobs import KNOBS
+
+    want = int(os.environ.get("PAGEVEC_IB", KNOBS["PAGEVEC_IB"][1]))
+    assert _lib().pv_ib_version() == (want if want in (3, 5, 7) else 7)
