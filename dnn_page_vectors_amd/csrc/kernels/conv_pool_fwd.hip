@@ -866,6 +866,12 @@ PV_API int pv_conv_packed_size() {
 static int g_conv_dbg = getenv("PAGEVEC_CONV_DBG") ? atoi(getenv("PAGEVEC_CONV_DBG")) : 0;
 PV_API void pv_conv_set_dbg(int d) { g_conv_dbg = d; }
 PV_API int pv_conv_get_dbg() { return g_conv_dbg; }
+// Short sequences (the query tower, L = 45): one chunk of 48 window rows (3 blocks of 16)
+// instead of 112 — a 45-token query filled 43 of 112 rows (62 % of the MFMA blocks padding).
+// Same per-window arithmetic and block order: bit-identical (test_conv_short_chunk_bit_identical).
+static int g_conv_short = getenv("PAGEVEC_CONV_SHORT") ? atoi(getenv("PAGEVEC_CONV_SHORT")) : 1;
+PV_API void pv_conv_set_short(int on) { g_conv_short = on; }
+constexpr int SHORT_RR = 48;
 
 // bias3 / bias4: the two widths' biases (FW floats each, e.g. the parameters themselves)
 PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpack, const float* bias3,
@@ -907,6 +913,11 @@ PV_API int pv_conv_pool_fwd2(const int* ids, const void* table, const void* wpac
     // v7: role-split workgroup (8 MFMA waves + 4 loader waves), 16384 + 64 * PF + OPT
     case 0:  // production: v7, A prefetch depth 1, pinned K-step order (same process at the bench shape:
              // 4.858 vs 5.025 ms unpinned; v4 5.349 vs unpinned v7 4.838 on another box)
+      if (g_conv_short && L - 2 <= SHORT_RR) {  // every window of both widths in one 48-row chunk
+        PV_CONV_DM(conv_pool_fwd7_kernel, NTH7, 1, 5 + 1024, SHORT_RR)
+        break;
+      }
+      [[fallthrough]];
     case 16384 + 64 + 5 + 1024: PV_CONV_DM(conv_pool_fwd7_kernel, NTH7, 1, 5 + 1024, 112) break;
     case 16384 + 64 + 5: hipLaunchKernelGGL((conv_pool_fwd7_kernel<1, 5, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;
     case 16384 + 128 + 5: hipLaunchKernelGGL((conv_pool_fwd7_kernel<2, 5, 112, 1>), dim3(grid), dim3(NTH7), 0, st, p); break;

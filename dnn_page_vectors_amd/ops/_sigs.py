@@ -13,6 +13,7 @@ SIGS = {
     "pv_conv_weight_rows": "ppipp",
     "pv_conv_packed_size": "",
     "pv_conv_set_dbg": "i",
+    "pv_conv_set_short": "i",
     "pv_conv_get_dbg": "",
     # chunkpool.hip (chunked long-page encoder, models/chunked.py)
     "pv_chunk_mean_fwd": "pp" "iiii" "pp" "p",

@@ -55,6 +55,7 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),
     "PAGEVEC_ADAM_NT": ("ab", "0", "dense Adam with non-temporal loads / stores"),
+    "PAGEVEC_CONV_SHORT": ("ab", "1", "conv forward: one 48-row chunk for sequences up to 50 tokens (query tower)"),
     "PAGEVEC_ATTN_BGRAD": ("ab", "1", "qkv bias gradient from the attention backward's partial column sums"),
     "PAGEVEC_BERT_EMBED": ("ab", "1", "BERT embedding front end as one fused gather + add kernel"),
     "PAGEVEC_FFN_LT": ("ab", "1", "BERT FFN bias + GELU (and its backward) in hipBLASLt GEMM epilogues"),

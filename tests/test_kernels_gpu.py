@@ -2012,3 +2012,38 @@ def test_loss_generation_default_matches_knob_registry():
 
     want = int(os.environ.get("PAGEVEC_IB", KNOBS["PAGEVEC_IB"][1]))
     assert _lib().pv_ib_version() == (want if want in (3, 5, 7) else 7)
+
+
+@pytest.mark.parametrize("L", [45, 50, 20, 4])
+@pytest.mark.parametrize("p,mode", [(0.25, "element"), (0.0, "element"), (0.3, "token")])
+def test_conv_short_chunk_bit_identical(L, p, mode):
+    """conv_pool_fwd.hip: sequences of <= 50 tokens (the query tower) run the v7 kernel with one
+    48-row chunk instead of 112 rows — pooled values and argmax windows bit-identical, and the
+    training step's gradients (sort keys emitted by the same loader waves) equal up to the
+    backward's float-atomic summation order."""
+    from dnn_page_vectors_amd.ops._common import lib as _lib
+
+    torch.manual_seed(7)
+    V, E, F, N = 700, 100, 150, 300
+    ids = torch.randint(1, V, (N, L), dtype=torch.int32, device=DEV)
+    table0 = torch.randn(V, E, device=DEV) * 0.3
+    w30, w40 = torch.randn(F, 3, E, device=DEV) * 0.1, torch.randn(F, 4, E, device=DEV) * 0.1
+    b0 = [torch.randn(F, device=DEV) * 0.1, torch.randn(F, device=DEV) * 0.1]
+    gy = torch.randn(N, 2 * F, device=DEV)
+    lib = _lib()
+    outs = []
+    try:
+        for short in (0, 1):
+            lib.pv_conv_set_short(short)
+            table, w3, w4 = (t.clone().requires_grad_(True) for t in (table0, w30, w40))
+            b = [t.clone().requires_grad_(True) for t in b0]
+            pooled, arg = cops.conv_relu_maxpool_fused(ids, table, [w3, w4], b, p, 11, True, mode)
+            (pooled * gy).sum().backward()
+            torch.cuda.synchronize()
+            outs.append((pooled.detach(), arg, table.grad, w3.grad, w4.grad, b[0].grad, b[1].grad))
+    finally:
+        lib.pv_conv_set_short(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    for a, c in zip(outs[0][2:], outs[1][2:]):
+        torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-6)
