@@ -129,10 +129,7 @@ def build_hip(verbose: bool = False, jobs: int = 4, debug: bool = False) -> str:
     out = HIP_DEBUG_LIB if debug else HIP_LIB
     objs = _compile_all(srcs, HIPCC, flags, os.path.join(CSRC, "kernels"), "hipdbg" if debug else "hip", jobs,
                         verbose)
-    # hipBLASLt (lt_gemm.hip: fused-epilogue library GEMMs); at run time the soname resolves to
-    # torch's already-loaded copy
-    _link(objs, out, [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lhipblaslt",
-                      "-Wl,-rpath,/opt/rocm/lib"], verbose)
+    _link(objs, out, [HIPCC, f"--offload-arch={ARCH}", "-fPIC"], verbose)
     return out
 
 

@@ -42,37 +42,89 @@ __host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
 }
 
 // One lowbias32 round per row: mix32(seed) is loop-invariant in every caller (hoisted), so
-// a row costs one finaliser (two 32-bit multiplies) — the sparse backward kernels recompute
-// it for every gradient entry and are VALU-bound.
+// a row costs one finaliser (two 32-bit multiplies).
 __device__ __forceinline__ unsigned dropout_row_hash(unsigned seed, unsigned row) {
   return mix32(row ^ mix32(seed));
 }
 
-// Keep-bits for columns 4g..4g+3 of a row (byte b of the group hash >= thr).
-__device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
+// 24-bit multiply (v_mul_u32_u24 / v_mad_u32_u24: full rate; v_mul_lo_u32 is quarter rate):
+// low 32 bits of (a mod 2^24) * (b mod 2^24).
+// (the masks make both operands provably 24-bit, so the backend selects the u24 forms)
+__host__ __device__ __forceinline__ unsigned umul24(unsigned a, unsigned b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+
+// Group hash of a dropout row (round 6): the row hash is already a full lowbias32 round, so the
+// 8- or 4-column groups of the row only need to be decorrelated from each other — two
+// xorshift / 24-bit-multiply rounds, six full-rate VALU ops, instead of mix32's two quarter-rate
+// 32-bit multiplies (the sparse backward kernels regenerate this hash for every gathered
+// 16-byte piece and were VALU-bound on it: dW 1.10 -> 0.61 ms per step with dropout off,
+// profiles/r6_first/).  Quality: keep rate, all pairwise correlations of a row's 104 decisions,
+// and the per-piece / per-row / adjacent-piece count distributions at the statistical floor
+// (tests/test_dropout_mask.py).  ops/reference.py::dropout_keep_mask is the specification.
+constexpr unsigned DROP_GROUP_STEP = 0x9E3779u;  // 24-bit golden-ratio step between groups
+__host__ __device__ __forceinline__ unsigned mix24(unsigned x) {
+  x ^= x >> 16;
+  x = umul24(x, 0xED5AD5u);
+  x ^= x >> 15;
+  return umul24(x, 0x9E3779u);
+}
+#ifdef PV_DROP_HASH_LEGACY  // quality A/B build only (tools/conv_variant_build.py): the round-5 mask stream
+__host__ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
   return mix32(hrow + g * 0x9E3779B9u);
 }
+#else
+__host__ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
+  return mix24(hrow + umul24(g, DROP_GROUP_STEP));
+}
+#endif
 
-// Bytes in {0, 1} -> bytes in {0, 0xFF}: x * 255 as (x << 8) - x (two full-rate ops instead
-// of a quarter-rate v_mul_lo_u32; the sparse-backward kernels are VALU-bound).
+// Nibble mode (thr % 16 == 0, p = k/16 — the reference's 0.25 is k = 4): element j (column
+// 8g + j) of a group reads the 4-bit value  h[P] h[P-8] h[P-4] h[P-12]  (MSB first) with
+// P = 15 - (j >> 1) + 16 (j & 1), and is kept iff that value >= thr / 16.  The bit positions are
+// chosen so the fast path below needs no per-element extraction: "value >= t" for t = 2, 4, 8,
+// 12 is a bitwise function of h, h << 8, h << 4 landing on bit P, and v_perm_b32's sign-
+// replicating selectors (8 -> bit 15, 9 -> bit 31, 10 -> bit 47, 11 -> bit 63 of {S0, S1})
+// turn bits 15 / 31 of a word into the two 16-bit halves of a bf16-pair AND mask.
+__host__ __device__ __forceinline__ int dropout_nib_pos(int j) { return 15 - (j >> 1) + 16 * (j & 1); }
+__host__ __device__ __forceinline__ unsigned dropout_nibble(unsigned h, int j) {
+#ifdef PV_DROP_HASH_LEGACY
+  return (h >> (4 * j)) & 0xFu;
+#endif
+  const int P = dropout_nib_pos(j);
+  return (((h >> P) & 1u) << 3) | (((h >> (P - 8)) & 1u) << 2) | (((h >> (P - 4)) & 1u) << 1) | ((h >> (P - 12)) & 1u);
+}
+// rotate left by r (v_alignbit_b32); at the bit positions P the result equals h << r for
+// r <= 12, and a rotate keeps the backend from folding the shift into the preceding 24-bit
+// multiply (h * K << 8 became one quarter-rate v_mul_lo_u32 by K << 8)
+__device__ __forceinline__ unsigned rotl32(unsigned h, int r) { return __builtin_amdgcn_alignbit(h, h, 32 - r); }
+// word whose bit P_j is the keep decision of element j (other bits: don't care)
+__device__ __forceinline__ unsigned dropout_keep_word(unsigned h, int t) {
+#ifdef PV_DROP_HASH_LEGACY
+  unsigned lw = 0u;
+  for (int j = 0; j < 8; ++j) lw |= (dropout_nibble(h, j) >= (unsigned)t ? 1u : 0u) << dropout_nib_pos(j);
+  return lw;
+#endif
+  if (t == 4) return h | rotl32(h, 8);                   // value >= 4: either of the two top bits
+  if (t == 2) return h | rotl32(h, 8) | rotl32(h, 4);    // value >= 2: any of the three top bits
+  if (t == 8) return h;                                  // value >= 8: the top bit
+  if (t == 12) return h & rotl32(h, 8);                  // value >= 12: both top bits
+  unsigned w = 0u;
+  for (int j = 0; j < 8; ++j) w |= (dropout_nibble(h, j) >= (unsigned)t ? 1u : 0u) << dropout_nib_pos(j);
+  return w;
+}
+// keep decisions of the group's 8 columns as bits 0..7 (bit j = column 8g + j kept)
+__device__ __forceinline__ unsigned dropout_keep_bits8(unsigned h, int t) {
+  const unsigned w = dropout_keep_word(h, t);
+  unsigned b = 0u;
+  for (int j = 0; j < 8; ++j) b |= ((w >> dropout_nib_pos(j)) & 1u) << j;
+  return b;
+}
+
+// Byte mode (any other thr): byte b of the group hash decides column 4g + b (kept iff >= thr).
 __device__ __forceinline__ unsigned bytes_to_mask(unsigned x) { return (x << 8) - x; }
-
-// Byte k of the result is 0xFF iff byte k of the group hash is >= thr (element 4g+k kept).
-// thr = 64 / 128 / 192 (p = 0.25 — the reference's rate — / 0.5 / 0.75) is a function of the
-// top two bits of each byte: 4 bit ops instead of 4 compares + selects.
 __device__ __forceinline__ unsigned keep_bytes(unsigned h, int thr) {
-  unsigned b;
-  if (thr == 64) {
-    b = ((h | (h << 1)) >> 7) & 0x01010101u;
-  } else if (thr == 128) {
-    b = (h >> 7) & 0x01010101u;
-  } else if (thr == 192) {
-    b = ((h & (h << 1)) >> 7) & 0x01010101u;
-  } else {
-    b = 0u;
+  unsigned b = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) b |= ((int)((h >> (8 * k)) & 0xFFu) >= thr ? 1u : 0u) << (8 * k);
-  }
+  for (int k = 0; k < 4; ++k) b |= ((int)((h >> (8 * k)) & 0xFFu) >= thr ? 1u : 0u) << (8 * k);
   return bytes_to_mask(b);
 }
 
@@ -83,31 +135,16 @@ __device__ __forceinline__ unsigned keep_pair(unsigned kb, int j) {
 
 // Element-dropout AND-masks for the 8 bf16 columns 8q..8q+7 (one 16-byte piece) of a row
 // with row hash hrow (ops/reference.py dropout_keep_mask is the specification):
-//  * thr % 16 == 0 (p = k/16, incl. the reference's 0.25): ONE group hash per piece, nibble
-//    k decides column 8q+k (kept iff nibble >= thr/16);
+//  * thr % 16 == 0: ONE group hash per piece; the keep word's bits 15 / 31 (shifted by the
+//    pair index) become the two halves of each pair mask through v_perm_b32 — at p = 0.25
+//    one v_lshl_or + three shifts + four perms after the hash;
 //  * otherwise two byte-wise group hashes (groups 2q, 2q+1, byte k decides column 4g+k).
 __device__ __forceinline__ u32x4 keep_piece(unsigned hrow, int q, int thr) {
   if ((thr & 15) == 0) {
-    const unsigned h = dropout_group_hash(hrow, (unsigned)q);
-    const int t = thr >> 4;
-    unsigned b;  // bit 0 of nibble k = keep column k
-    if (t == 2) {  // nibble >= 2: any of bits 1..3
-      b = ((h >> 1) | (h >> 2) | (h >> 3)) & 0x11111111u;
-    } else if (t == 4) {
-      b = ((h | (h >> 1)) >> 2) & 0x11111111u;
-    } else if (t == 8) {
-      b = (h >> 3) & 0x11111111u;
-    } else if (t == 12) {
-      b = ((h & (h >> 1)) >> 2) & 0x11111111u;
-    } else {
-      b = 0u;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b |= (((h >> (4 * k)) & 0xFu) >= (unsigned)t ? 1u : 0u) << (4 * k);
-    }
-    const unsigned lo = bytes_to_mask(b & 0x01010101u);         // byte j: column 2j (even nibbles)
-    const unsigned hi = bytes_to_mask((b >> 4) & 0x01010101u);  // byte j: column 2j+1
-    return u32x4{__builtin_amdgcn_perm(hi, lo, 0x04040000u), __builtin_amdgcn_perm(hi, lo, 0x05050101u),
-                 __builtin_amdgcn_perm(hi, lo, 0x06060202u), __builtin_amdgcn_perm(hi, lo, 0x07070303u)};
+    const unsigned w0 = dropout_keep_word(dropout_group_hash(hrow, (unsigned)q), thr >> 4);
+    const unsigned w1 = w0 << 1, w2 = w0 << 2, w3 = w0 << 3;
+    return u32x4{__builtin_amdgcn_perm(w1, w0, 0x09090808u), __builtin_amdgcn_perm(w1, w0, 0x0B0B0A0Au),
+                 __builtin_amdgcn_perm(w3, w2, 0x09090808u), __builtin_amdgcn_perm(w3, w2, 0x0B0B0A0Au)};
   }
   const unsigned k0 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q)), thr);
   const unsigned k1 = keep_bytes(dropout_group_hash(hrow, (unsigned)(2 * q + 1)), thr);

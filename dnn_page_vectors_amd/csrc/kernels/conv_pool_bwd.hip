@@ -32,28 +32,33 @@ constexpr int FW = 150;
 
 // ---- dW, db -----------------------------------------------------------------------
 // grid (2*FW, nsplit), block 256 (4 waves).  Each wave takes its samples 64 at a time:
-// lane l loads sample (base+l)'s g / ReLU flag / argmax and the k token ids of its
-// argmax window (independent loads, issued together), then the wave walks the live
-// samples with v_readlane broadcasts.  Lane l owns the 16-byte piece l of the (k x EP)
-// window (row l / 13, columns 8*(l % 13) .. +7): one 16-byte table load, the dropout mask
-// of the piece from keep_piece (one group hash in the nibble mode), 8 FMAs.  The k row
-// hashes of a sample are computed once by lanes 0..k-1 and fetched with ds_bpermute.
-// Table loads for 4 samples are issued before use.
+// lane l loads sample (base+l)'s g / ReLU flag / argmax and the k token ids of its argmax
+// window, hashes the k dropout rows of that window itself (k full-wave lowbias32 rounds per 64
+// samples) and parks {token, row hash} per window row in a wave-private LDS table; the wave then
+// walks the live samples 4 per round: lane l owns the 16-byte piece l of the (k x EP) window
+// (row l / 13, columns 8*(l % 13) .. +7) and reads its row's {token, hash} with ONE ds_read_b64
+// per sample — one 16-byte table load, the dropout mask of the piece from keep_piece, 8 FMAs.
+// (Round 5 hashed the rows inside each round — 16 active lanes, a bpermute -> lowbias32 ->
+// bpermute chain in front of every mask — and moved the ids with 4 + 1 bpermutes per sample:
+// dW 1.10 ms per step with dropout against 0.61 without, profiles/r6_first/.)
 constexpr int PIECES_ROW = EP / 8;  // 13
 template <int K, int DM>
 __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const float* __restrict__ pooled,
                                           const int* __restrict__ argmax, const int* __restrict__ ids,
                                           const unsigned short* __restrict__ table, float* __restrict__ dw,
-                                          float* __restrict__ db, float* red, int L, int E, int V, int fg, int fl,
-                                          int n0, int n1, unsigned seed, unsigned row_offset, int thr, int token_mode,
-                                          float scale, long long* fxw, long long* fxb) {
+                                          float* __restrict__ db, float* red, int2* trow, int L, int E, int V,
+                                          int fg, int fl, int n0, int n1, unsigned seed, unsigned row_offset,
+                                          int thr, int token_mode, float scale, long long* fxw, long long* fxb) {
   constexpr int NP = K * PIECES_ROW;  // pieces per window (39 / 52)
+  constexpr bool DROP = DM != 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int2* tw = trow + wave * (64 * 4);  // this wave's {token, row hash} table: [sample lane][window row]
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float gsum = 0.f;
   const int jj = lane / PIECES_ROW, pc = lane - jj * PIECES_ROW;
   const bool pv_ = lane < NP && pc * 8 < E;
   const int jsel = jj < K ? jj : 0;
+  const unsigned hseed = DROP ? mix32(seed) : 0u;  // dropout_row_hash(seed, r) = mix32(r ^ mix32(seed))
   for (int base = n0 + wave * 64; base < n1; base += 256) {
     const int n = base + lane;
     float g = 0.f;
@@ -71,6 +76,12 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
       }
     }
     gsum += live ? g : 0.f;
+    const unsigned rbase = row_offset + (unsigned)n * (unsigned)L + (unsigned)a;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const unsigned hr = DROP ? mix32((rbase + (unsigned)j) ^ hseed) : 0u;
+      tw[lane * 4 + j] = int2{tok[j], (int)hr};
+    }
     unsigned long long m = __ballot(live);
     while (m) {
       int sl[4];
@@ -80,42 +91,23 @@ __device__ __forceinline__ void dw_filter(const float* __restrict__ gpool, const
         sl[u] = m ? (int)__builtin_ctzll(m) : -1;
         if (m) { m &= m - 1; ++cnt; }
       }
-      u32x4 raw[4];
-      // dropout row hashes of the (up to) 4 samples of this round in ONE pass: lane 4u + j
-      // hashes row (n_u, a_u + j), then every lane fetches its row's hash with a bpermute
-      // ... and the same lanes fetch the window's token ids of those samples (4 bpermutes for
-      // the round instead of 4 readlanes + 3 selects per sample)
-      unsigned hq = 0u;
-      int tq;
-      {
-        const int uu = (lane >> 2) & 3, jq = lane & 3;
-        int su = sl[0];
-        su = uu == 1 ? sl[1] : su;
-        su = uu == 2 ? sl[2] : su;
-        su = uu == 3 ? sl[3] : su;
-        su = su < 0 ? sl[0] : su;
-        int tv[4];
+      int2 th[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) tv[j] = __builtin_amdgcn_ds_bpermute(su * 4, tok[j]);
-        tq = jq == 0 ? tv[0] : jq == 1 ? tv[1] : jq == 2 ? tv[2] : tv[3];
-        if (DM < 0 ? thr > 0 : DM != 0) {
-          const int au = __builtin_amdgcn_ds_bpermute(su * 4, a);
-          hq = (lane < 16 && jq < K) ? dropout_row_hash(seed, row_offset + (unsigned)((base + su) * L + au + jq)) : 0u;
-        }
-      }
+      for (int u = 0; u < 4; ++u) th[u] = tw[(u < cnt ? sl[u] : sl[0]) * 4 + jsel];
+      u32x4 raw[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u >= cnt) break;
-        const int t = __builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, tq);
+        const int t = th[u].x;
         const bool ok = pv_ && t >= 0 && t < V;
         // 32-bit element offset (V * EP < 2^31): no 64-bit multiply per piece
         raw[u] = ok ? *reinterpret_cast<const u32x4*>(table + (unsigned)(t * EP + pc * 8)) : u32x4{0u, 0u, 0u, 0u};
-        if (DM < 0 ? thr > 0 : DM != 0) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
-          const unsigned hr = (unsigned)__builtin_amdgcn_ds_bpermute((4 * u + jsel) * 4, (int)hq);
+        if constexpr (DROP) {  // dropout mask of this lane's piece (ops/reference.py dropout_keep_mask)
+          const unsigned hr = (unsigned)th[u].y;
           if (DM == 3 || (DM < 0 && token_mode)) {
             const unsigned k = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
             raw[u] &= u32x4{k, k, k, k};
-          } else {
+          } else if (DM > 0 || thr > 0) {
             raw[u] &= keep_piece(hr, pc, dm_thr(DM, thr));
           }
         }
@@ -173,28 +165,20 @@ __global__ __launch_bounds__(256) void conv_bwd_dw_kernel(const float* gpool, co
                                                           int nsplit,
                                                           unsigned seed, const unsigned* seed_ptr,
                                                           unsigned row_offset, int thr, int token_mode, float scale,
-                                                          int xcd_map, long long* fx) {
+                                                          long long* fx) {
   __shared__ float red[4 * 4 * EP];
+  __shared__ int2 trow[4 * 64 * 4];  // per wave: {token, dropout row hash} of 64 samples x 4 window rows
   if (seed_ptr) seed += *seed_ptr;  // device seed offset (captured hipGraph steps)
-  // XCD-aware work mapping: workgroups are dealt round-robin to the 8 XCDs (each with its
-  // own L2).  The natural (f = blockIdx.x, split = blockIdx.y) order puts filters f, f+1 of
-  // one sample range on different XCDs, so every L2 fetches the same gpool / argmax /
-  // pooled / id lines (rows of 2*FW floats hold all filters of a sample).  Remapped, the
-  // 2*FW filter blocks of a split run on ONE XCD and share those lines in its L2.
-  int f = blockIdx.x, split = blockIdx.y;
-  if (xcd_map && (nsplit & 7) == 0) {
-    const int b = blockIdx.x + gridDim.x * blockIdx.y;
-    const int logical = (b & 7) * (gridDim.x * (nsplit >> 3)) + (b >> 3);
-    f = logical % (int)gridDim.x;
-    split = logical / (int)gridDim.x;
-  }
+  // (an XCD-aware remap of (filter, split) blocks — a split's filter blocks on one XCD sharing
+  // its L2 — measured neutral in round 4 and was removed in round 6)
+  const int f = blockIdx.x, split = blockIdx.y;
   const int per = ((N + nsplit - 1) / nsplit + 255) / 256 * 256;
   const int n0 = split * per, n1 = min(N, n0 + per);
   if (f < FW)
-    dw_filter<3, DM>(gpool, pooled, argmax, ids, table, dw3, db3, red, L, E, V, f, f, n0, n1, seed, row_offset, thr,
+    dw_filter<3, DM>(gpool, pooled, argmax, ids, table, dw3, db3, red, trow, L, E, V, f, f, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx, fx ? fx + (size_t)7 * FW * E : nullptr);
   else
-    dw_filter<4, DM>(gpool, pooled, argmax, ids, table, dw4, db4, red, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
+    dw_filter<4, DM>(gpool, pooled, argmax, ids, table, dw4, db4, red, trow, L, E, V, f, f - FW, n0, n1, seed, row_offset, thr,
                  token_mode, scale, fx ? fx + (size_t)3 * FW * E : nullptr, fx ? fx + (size_t)7 * FW * E : nullptr);
 }
 
@@ -422,220 +406,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   if (cur != UV) reduce4_flush(slab, acc, g, p, lane, E, cur, dtable, fx);
 }
 
-// ---- dTable for short sequences (query towers: L <= DENSE_MAXL) ------------------------------
-// A 45-token query has ~45 touched embedding rows but 1050 (f, j) gradient entries, so the
-// entry-level emit -> sort -> reduce moves 23x more entries than there are rows.  Instead:
-//  dx_dense : one workgroup per sample builds the sample's dense input gradient in LDS,
-//               dX[t, :] = s * sum_{(f, j): argmax[n,f] + j == t, live} g[n,f] * W[f, j, :]
-//             (LDS float atomics: the (f, j) of a sample collide on the same t), applies the
-//             regenerated dropout mask and writes each touched row (fp32, stride EP) plus its
-//             token key (sentinel V for untouched / fully dropped rows);
-//  sort     : the row keys (radix_sort.hip), values = row index;
-//  rows_reduce: each wave sums EPW consecutive sorted rows per token in registers, one
-//             row-atomic per (wave, token) run.  Summing per token BEFORE the global atomics
-//             matters: direct per-row atomics from dx_dense serialise on the Zipf-hot rows
-//             (measured 2.4 ms vs 0.49 ms for the sort path at 4096 x 45).
-constexpr int DENSE_MAXL = 256;  // LDS: L * EP fp32 (104 KB at L = 256)
-
-// dx_dense, one workgroup per sample, no atomics:
-//  1. per-filter {g*scale (0 = dead), argmax} -> LDS;
-//  2. wave 0 ranks the (f, j) entries by their position t = argmax + j in entry order (one
-//     ballot per bit of t finds the lanes of a round with the same t; per-t running counts in
-//     LDS): bucket position = stable, so each row sums its entries in a fixed order;
-//  3. exclusive scan of the per-t counts, scatter of the entry ids into their buckets;
-//  4. wave w sums rows t = w, w+4, ...: lane c < 52 owns columns 2c, 2c+1 (one 4-byte load of
-//     the bf16 weight row per entry, 4 entries in flight), applies the dropout mask of those
-//     columns and writes the row (fp32, stride EP) + its token key.
-constexpr int DX_ENT = 2 * FW * 4;  // entry ids f*4 + j (k=3 filters leave j = 3 unused)
-constexpr int DX_BATCH = 8;          // entries per load batch in the row sums
-constexpr int DX_THREADS = 512;      // 8 waves: rows t = wave, wave + 8, ...
-
-template <typename KT, int DM>
-__global__ __launch_bounds__(DX_THREADS) void conv_bwd_dx_dense_kernel(const float* __restrict__ gpool,
-                                                                const float* __restrict__ pooled,
-                                                                const int* __restrict__ argmax,
-                                                                const int* __restrict__ ids,
-                                                                const unsigned short* __restrict__ wrow,
-                                                                float* __restrict__ rows, KT* __restrict__ keys,
-                                                                int L, int V, unsigned seed,
-                                                                const unsigned* seed_ptr, unsigned row_offset,
-                                                                int thr, int token_mode, float scale) {
-  __shared__ float gsl[2 * FW];
-  __shared__ int al[2 * FW];
-  __shared__ unsigned cnt[DENSE_MAXL];
-  __shared__ unsigned start[DENSE_MAXL];
-  __shared__ unsigned short rnk[DX_ENT];
-  __shared__ unsigned short ent[DX_ENT];
-  __shared__ unsigned ws[DX_THREADS / 64];
-  if (seed_ptr) seed += *seed_ptr;
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const size_t rb = (size_t)n * (2 * FW);
-  for (int f = tid; f < 2 * FW; f += DX_THREADS) {
-    const float g = gpool[rb + f];
-    const int a = argmax[rb + f];
-    const bool live = pooled[rb + f] > 0.f && g != 0.f && PV_OK(a >= 0 && a < L, PV_ERR_ARGMAX);
-    gsl[f] = live ? g * scale : 0.f;
-    al[f] = a;
-  }
-  for (int t = tid; t < DENSE_MAXL; t += DX_THREADS) cnt[t] = 0u;
-  __syncthreads();
-  // (2) stable ranks by t, wave 0
-  int nb = 0;  // bits of t
-  while ((1 << nb) < L) ++nb;
-  if (wave == 0) {
-    for (int e0 = 0; e0 < DX_ENT; e0 += 64) {
-      const int e = e0 + lane;
-      const int f = e >> 2, j = e & 3;
-      int t = -1;
-      if (e < DX_ENT && (j < 3 || f >= FW) && gsl[f] != 0.f) {
-        t = al[f] + j;
-        if (t >= L) t = -1;
-      }
-      const bool valid = t >= 0;
-      unsigned long long m = __ballot(valid);
-      for (int b = 0; b < nb; ++b) {
-        const bool bit = valid && ((t >> b) & 1);
-        const unsigned long long bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
-      }
-      m = valid ? m : 0ull;
-      const unsigned long long lt = (1ull << lane) - 1ull;
-      const unsigned old = valid ? cnt[t] : 0u;
-      if (e < DX_ENT) rnk[e] = valid ? (unsigned short)(old + __popcll(m & lt)) : (unsigned short)0xFFFF;
-      if (valid && (m & lt) == 0ull) cnt[t] = old + (unsigned)__popcll(m);
-    }
-  }
-  __syncthreads();
-  {  // (3) scan of the per-t counts (L <= 256 <= threads)
-    const unsigned v = tid < L ? cnt[tid] : 0u;
-    unsigned x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) ws[wave] = x;
-    __syncthreads();
-    unsigned base = 0;
-    for (int i = 0; i < wave; ++i) base += ws[i];
-    if (tid < L) start[tid] = base + x - v;
-  }
-  __syncthreads();
-  for (int e = tid; e < DX_ENT; e += DX_THREADS) {
-    const unsigned r = rnk[e];
-    if (r != 0xFFFFu) {
-      const int t = al[e >> 2] + (e & 3);
-      ent[start[t] + r] = (unsigned short)e;
-    }
-  }
-  __syncthreads();
-  // (4) rows
-  const int c = lane;          // column pair (2c, 2c+1)
-  const bool act = c < EP / 2;  // 52 pairs
-  for (int t = wave; t < L; t += DX_THREADS / 64) {
-    const size_t r = (size_t)n * L + t;
-    const int tok = ids[r];
-    PV_CHECK(tok >= 0 && tok < V, PV_ERR_ID);
-    const int b0 = (int)start[t], b1 = b0 + (int)cnt[t];
-    float x0 = 0.f, x1 = 0.f;
-    for (int i = b0; i < b1; i += DX_BATCH) {  // DX_BATCH weight-row loads in flight per lane
-      unsigned w[DX_BATCH];
-      float g[DX_BATCH];
-#pragma unroll
-      for (int u = 0; u < DX_BATCH; ++u) {
-        const int e = ent[i + u < b1 ? i + u : b0];
-        g[u] = i + u < b1 ? gsl[e >> 2] : 0.f;
-        w[u] = act ? *reinterpret_cast<const unsigned*>(wrow + (size_t)e * EP + 2 * c) : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < DX_BATCH; ++u) {
-        x0 += g[u] * __uint_as_float(w[u] << 16);
-        x1 += g[u] * __uint_as_float(w[u] & 0xFFFF0000u);
-      }
-    }
-    bool keep_row = tok >= 0 && tok < V && b1 > b0;
-    if (keep_row && (DM < 0 ? thr > 0 : DM != 0)) {
-      const unsigned hr = dropout_row_hash(seed, row_offset + (unsigned)n * (unsigned)L + (unsigned)t);
-      if (DM == 3 || (DM < 0 && token_mode)) {
-        keep_row = (int)(hr & 0xFFu) >= thr;
-      } else {
-        const u32x4 k = keep_piece(hr, c >> 2, dm_thr(DM, thr));
-        const unsigned kw = k[c & 3];
-        x0 = (kw & 1u) ? x0 : 0.f;
-        x1 = (kw & 0x10000u) ? x1 : 0.f;
-      }
-    }
-    if (lane == 0) keys[r] = (KT)(keep_row ? (unsigned)tok : (unsigned)V);
-    if (keep_row && act) *reinterpret_cast<f32x2*>(rows + r * EP + 2 * c) = f32x2{x0, x1};
-  }
-}
-
-// Sorted rows -> dTable: wave w sums entries [w*EPW, (w+1)*EPW) run by run (sentinel keys V
-// sort last and end the walk); rows are loaded 4 entries ahead.
-template <typename KT>
-__global__ __launch_bounds__(256) void conv_bwd_rows_reduce_kernel(const KT* __restrict__ skeys,
-                                                                   const unsigned* __restrict__ svals,
-                                                                   const float* __restrict__ rows,
-                                                                   float* __restrict__ dtable, long M, int EPW,
-                                                                   int E, int V, long long* fx) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long wbeg = ((long)blockIdx.x * 4 + wave) * EPW;
-  if (wbeg >= M) return;
-  const long wend = min(M, wbeg + (long)EPW);
-  const int c0 = lane, c1 = lane + 64;
-  const unsigned UV = (unsigned)V;
-  unsigned cur = UV;
-  float a0 = 0.f, a1 = 0.f;
-  auto flush = [&]() {
-    if (cur < UV) {
-      if (fx) {  // deterministic mode
-        if (c0 < E) fx_add(fx, (size_t)cur * E + c0, a0);
-        if (c1 < E) fx_add(fx, (size_t)cur * E + c1, a1);
-      } else {
-        float* drow = dtable + (size_t)cur * E;
-        if (c0 < E) atomicAdd(&drow[c0], a0);
-        if (c1 < E) atomicAdd(&drow[c1], a1);
-      }
-    }
-    a0 = 0.f;
-    a1 = 0.f;
-  };
-  for (long i0 = wbeg; i0 < wend; i0 += 64) {
-    // this sub-chunk's keys / row ids: one per lane, broadcast by readlane
-    const long il = i0 + lane;
-    const unsigned kl = il < wend ? (unsigned)skeys[il] : UV;
-    const unsigned rl = (il < wend && kl < UV) ? svals[il] : 0u;
-    const int n = __popcll(__ballot(kl < UV));  // live entries are a prefix (sorted)
-    for (int e0 = 0; e0 < n; e0 += 8) {
-      float x0[8], x1[8];
-      unsigned kk[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u < n ? e0 + u : e0;
-        kk[u] = (unsigned)__builtin_amdgcn_readlane((int)kl, e);
-        const unsigned row = (unsigned)__builtin_amdgcn_readlane((int)rl, e);
-        PV_CHECK((long)row < M, PV_ERR_SLOT);
-        const float* src = rows + (size_t)row * EP;
-        x0[u] = src[c0];
-        x1[u] = c1 < E ? src[c1] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (e0 + u >= n) break;
-        if (kk[u] != cur) {
-          flush();
-          cur = kk[u];
-        }
-        a0 += x0[u];
-        a1 += x1[u];
-      }
-    }
-    if (n < 64) break;
-  }
-  flush();
-}
-
 PV_DEBUG_EXPORT(convbwd)
 }  // namespace convbwd
 }  // namespace pv
@@ -668,10 +438,6 @@ PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const i
   int nsplit = (N + 255) / 256;
   if (nsplit > 64) nsplit = 64;
   if (nsplit < 1) nsplit = 1;
-  static const int xcd_map = [] {  // PAGEVEC_DW_XCD=0: natural block order (A/B switch)
-    const char* e = getenv("PAGEVEC_DW_XCD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
   hipStream_t st = (hipStream_t)stream;
   // deterministic mode: fixed-point accumulators [dW3 | dW4 | db], flushed in order below
   const size_t nfx = (size_t)7 * FW * E + 2 * FW;
@@ -681,7 +447,7 @@ PV_API int pv_conv_pool_bwd_dw2(const float* gpool, const float* pooled, const i
 #define PV_DW(DMV)                                                                                               \
   hipLaunchKernelGGL((conv_bwd_dw_kernel<DMV>), dim3(2 * FW, nsplit), dim3(256), 0, st, gpool, pooled, argmax, ids, \
                      (const unsigned short*)table, dw3, dw4, db3, db4, N, L, E, V, nsplit, seed, seed_ptr,           \
-                     row_offset, thr, token_mode, scale, xcd_map, fx)
+                     row_offset, thr, token_mode, scale, fx)
   if (dm == 0) PV_DW(0);
   else if (dm == 1) PV_DW(1);
   else if (dm == 4) PV_DW(4);
@@ -809,59 +575,4 @@ PV_API int pv_conv_pool_bwd_reduce7(const void* skeys, const unsigned* svals, co
                                     void* stream) {
   return launch_reduce7<unsigned>(skeys, svals, rec, wrow, dtable, M, epw, L, E, V, seed, seed_ptr, row_offset, thr,
                                   token_mode, (hipStream_t)stream);
-}
-
-// Short-sequence dTable, step 1: rows (N*L, EP) fp32 (touched rows written), keys (N*L) u16
-// (V < 65535) or u32 with sentinel V; wrow as for the reduce kernels; L <= pv_conv_dx_dense_maxl().
-PV_API int pv_conv_dx_dense_maxl() { return pv::convbwd::DENSE_MAXL; }
-
-PV_API int pv_conv_pool_bwd_dx_dense(const float* gpool, const float* pooled, const int* argmax, const int* ids,
-                                     const void* wrow, float* rows, void* keys, int key_bytes, int N, int L, int V,
-                                     unsigned seed, const unsigned* seed_ptr, unsigned row_offset, int thr,
-                                     int token_mode, float scale, void* stream) {
-  using namespace pv::convbwd;
-  if (L > DENSE_MAXL || L < 4 || N <= 0 || (key_bytes == 2 && V >= 65535)) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  const int dm = dm_of(thr, token_mode);
-#define PV_DX_LAUNCH(KT, DMV)                                                                                   \
-  hipLaunchKernelGGL((conv_bwd_dx_dense_kernel<KT, DMV>), dim3(N), dim3(DX_THREADS), 0, st, gpool, pooled, argmax, ids, \
-                     (const unsigned short*)wrow, rows, (KT*)keys, L, V, seed, seed_ptr, row_offset, thr,        \
-                     token_mode, scale)
-  if (key_bytes == 2) {
-    switch (dm) {
-      case 0: PV_DX_LAUNCH(unsigned short, 0); break;
-      case 1: PV_DX_LAUNCH(unsigned short, 1); break;
-      case 3: PV_DX_LAUNCH(unsigned short, 3); break;
-      default: PV_DX_LAUNCH(unsigned short, 2); break;
-    }
-  } else {
-    switch (dm) {
-      case 0: PV_DX_LAUNCH(unsigned, 0); break;
-      case 1: PV_DX_LAUNCH(unsigned, 1); break;
-      case 3: PV_DX_LAUNCH(unsigned, 3); break;
-      default: PV_DX_LAUNCH(unsigned, 2); break;
-    }
-  }
-#undef PV_DX_LAUNCH
-  PV_LAUNCH_CHECK();
-  return 0;
-}
-
-// Short-sequence dTable, step 3 (after sorting keys with values = row ids): dtable += rows.
-PV_API int pv_conv_bwd_rows_reduce(const void* skeys, int key_bytes, const unsigned* svals, const float* rows,
-                                   float* dtable, long M, int epw, int E, int V, void* stream) {
-  using namespace pv::convbwd;
-  if (E > EP || epw < 64 || (epw & 63)) return -1;
-  const long waves = (M + epw - 1) / epw;
-  hipStream_t st = (hipStream_t)stream;
-  const DetAcc det((size_t)V * E, st);
-  if (det.err) return det.err;
-  if (key_bytes == 2)
-    hipLaunchKernelGGL(conv_bwd_rows_reduce_kernel<unsigned short>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                       st, (const unsigned short*)skeys, svals, rows, dtable, M, epw, E, V, det.fx);
-  else
-    hipLaunchKernelGGL(conv_bwd_rows_reduce_kernel<unsigned>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                       (const unsigned*)skeys, svals, rows, dtable, M, epw, E, V, det.fx);
-  PV_LAUNCH_CHECK();
-  return det.finish(dtable, (size_t)V * E, st);
 }

@@ -69,10 +69,9 @@ __device__ __forceinline__ u32x4 keep4(unsigned hr, int pc, int thr, int token_m
   }
   u32x4 k;
   if ((thr & 15) == 0) {
-    const unsigned h = dropout_group_hash(hr, (unsigned)(pc >> 1)) >> (16 * (pc & 1));
-    const unsigned t = (unsigned)thr >> 4;
+    const unsigned b = dropout_keep_bits8(dropout_group_hash(hr, (unsigned)(pc >> 1)), thr >> 4) >> (4 * (pc & 1));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) k[i] = ((h >> (4 * i)) & 0xFu) >= t ? 0xFFFFFFFFu : 0u;
+    for (int i = 0; i < 4; ++i) k[i] = 0u - ((b >> i) & 1u);
   } else {
     const unsigned h = dropout_group_hash(hr, (unsigned)pc);
 #pragma unroll
@@ -84,10 +83,7 @@ __device__ __forceinline__ u32x4 keep4(unsigned hr, int pc, int thr, int token_m
 // keep bit of column e (the same specification, one element)
 __device__ __forceinline__ bool keep1(unsigned hr, int e, int thr, int token_mode) {
   if (token_mode) return (int)(hr & 0xFFu) >= thr;
-  if ((thr & 15) == 0) {
-    const unsigned h = dropout_group_hash(hr, (unsigned)(e >> 3));
-    return ((h >> (4 * (e & 7))) & 0xFu) >= ((unsigned)thr >> 4);
-  }
+  if ((thr & 15) == 0) return dropout_nibble(dropout_group_hash(hr, (unsigned)(e >> 3)), e & 7) >= ((unsigned)thr >> 4);
   const unsigned h = dropout_group_hash(hr, (unsigned)(e >> 2));
   return (int)((h >> (8 * (e & 3))) & 0xFFu) >= thr;
 }
@@ -601,13 +597,8 @@ __global__ __launch_bounds__(256) void conv_f32_mask_kernel(unsigned* __restrict
   if (token_mode) {
     bits = ((int)(hr & 0xFFu) >= thr) ? 0xFFFFFFFFu : 0u;
   } else if ((thr & 15) == 0) {
-    const unsigned t = (unsigned)thr >> 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const unsigned h = dropout_group_hash(hr, (unsigned)(4 * w + q));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bits |= (((h >> (4 * j)) & 0xFu) >= t ? 1u : 0u) << (8 * q + j);
-    }
+    for (int q = 0; q < 4; ++q) bits |= dropout_keep_bits8(dropout_group_hash(hr, (unsigned)(4 * w + q)), thr >> 4) << (8 * q);
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {

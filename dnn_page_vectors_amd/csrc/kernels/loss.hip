@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(256) void ib_pos_kernel(const unsigned short* __res
   }
 }
 
-// Wide vectors, fallback path (D > 192 that ibw_kernel does not cover, or PAGEVEC_IB_WIDE=0):
+// Wide vectors, fallback path (D > 192 that ibw_kernel does not cover, e.g. DP = 640 / 896):
 // the narrow flash kernels keep a query row's D accumulators in registers, which D = 768 does
 // not fit, so the logits are tiled at the GEMM level instead — S is produced one column block (B x Mb, bounded memory) at a time by
 // a bf16 x bf16 -> fp32 library GEMM and never exists whole.  Per block, one wave per row:
@@ -1240,21 +1240,13 @@ PV_API int pv_ib_fwd(const void* X, const void* Y, float* sumexp, float* ws, int
   return 0;
 }
 
-// Kernel generation (PAGEVEC_IB / pv_ib_set_version), read once per process so the
-// workspace queries and the launches always agree:
-//   7 (default): ib7 (ib5 software-pipelined) for every pass at DP = 160 / 128, ib3 for the rest
-//                (fused forward -15 %, dD pass -3 % vs gens 5 / 3: profiles/r5_ib7/)
-//   5: ib5 (32x32x16) for the fused forward / query-row pass at DP = 160 / 128, ib3 for the rest
-//   3: ib3 everywhere (A/B and the ib5-vs-ib3 numerics test)
-static int g_ib_version = -1;
-static int ib_version() {
-  if (g_ib_version < 0) {
-    const char* e = getenv("PAGEVEC_IB");
-    const int v = e ? atoi(e) : 7;
-    g_ib_version = (v == 3 || v == 5) ? v : 7;
-  }
-  return g_ib_version;
-}
+// Kernel generation (pv_ib_set_version; the production generation is 7):
+//   7: ib7 (ib5 software-pipelined) for every pass at DP = 160 / 128, ib3 for the other widths
+//      (fused forward -15 %, dD pass -3 % vs gens 5 / 3: profiles/r5_ib7/)
+//   5, 3: the earlier generations, kept as the numerics oracles of the ib7 tests (ib7 is
+//      bit-identical to ib5) and for tools/ib_micro.py; no environment switch selects them
+static int g_ib_version = 7;
+static int ib_version() { return g_ib_version; }
 
 PV_API int pv_ib_version() { return ib_version(); }
 // A/B and tests: switch the kernel version (between steps only: workspaces are sized per version)

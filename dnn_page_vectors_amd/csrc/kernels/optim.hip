@@ -27,20 +27,11 @@ __device__ __forceinline__ float warmup_scale(const float* tdev) {
   return w > 0.f ? fminf(1.f, tdev[0] / w) : 1.f;
 }
 
-// NT: non-temporal loads / stores (the update streams 28-30 B per parameter once per step,
-// far beyond the L2 / Infinity Cache: no reuse to keep); A/B via pv_adam_set_nt
-template <int NT>
-__device__ __forceinline__ f32x4 ld4(const float* b, long i) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(b) + i);
-  else return reinterpret_cast<const f32x4*>(b)[i];
-}
-template <int NT>
-__device__ __forceinline__ void st4(float* b, long i, const f32x4& x) {
-  if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(b) + i);
-  else reinterpret_cast<f32x4*>(b)[i] = x;
-}
+// (non-temporal loads / stores were measured as an A/B arm in round 5 — 16 M parameters 86.5
+// vs 67.7 us — and removed: docs/PERF.md "Dense Adam streams")
+__device__ __forceinline__ f32x4 ld4(const float* b, long i) { return reinterpret_cast<const f32x4*>(b)[i]; }
+__device__ __forceinline__ void st4(float* b, long i, const f32x4& x) { reinterpret_cast<f32x4*>(b)[i] = x; }
 
-template <int NT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr_t,
                                                    float b1, float b2, float eps, float wd, int torch_style,
@@ -76,33 +67,33 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   long i = i4;
   for (; i + stride < n4; i += 2 * stride) {
     const long j = i + stride;
-    f32x4 p0 = ld4<NT>(p, i), p1 = ld4<NT>(p, j);
-    f32x4 g0 = ld4<NT>(g, i), g1 = ld4<NT>(g, j);
-    f32x4 m0 = ld4<NT>(m, i), m1 = ld4<NT>(m, j);
-    f32x4 v0 = ld4<NT>(v, i), v1 = ld4<NT>(v, j);
+    f32x4 p0 = ld4(p, i), p1 = ld4(p, j);
+    f32x4 g0 = ld4(g, i), g1 = ld4(g, j);
+    f32x4 m0 = ld4(m, i), m1 = ld4(m, j);
+    f32x4 v0 = ld4(v, i), v1 = ld4(v, j);
     upd(p0, g0, m0, v0);
     upd(p1, g1, m1, v1);
     if (p16) {  // bf16 compute copy of the updated weights (consumers skip their cast kernel)
       store_bf16x4(p16 + 4 * i, p0);
       store_bf16x4(p16 + 4 * j, p1);
     }
-    st4<NT>(p, i, p0);
-    st4<NT>(m, i, m0);
-    st4<NT>(v, i, v0);
-    st4<NT>(p, j, p1);
-    st4<NT>(m, j, m1);
-    st4<NT>(v, j, v1);
+    st4(p, i, p0);
+    st4(m, i, m0);
+    st4(v, i, v0);
+    st4(p, j, p1);
+    st4(m, j, m1);
+    st4(v, j, v1);
   }
   for (; i < n4; i += stride) {
-    f32x4 pp = ld4<NT>(p, i);
-    f32x4 gg = ld4<NT>(g, i);
-    f32x4 mm = ld4<NT>(m, i);
-    f32x4 vv = ld4<NT>(v, i);
+    f32x4 pp = ld4(p, i);
+    f32x4 gg = ld4(g, i);
+    f32x4 mm = ld4(m, i);
+    f32x4 vv = ld4(v, i);
     upd(pp, gg, mm, vv);
     if (p16) store_bf16x4(p16 + 4 * i, pp);
-    st4<NT>(p, i, pp);
-    st4<NT>(m, i, mm);
-    st4<NT>(v, i, vv);
+    st4(p, i, pp);
+    st4(m, i, mm);
+    st4(v, i, vv);
   }
   for (long i = n4 * 4 + i4; i < n; i += stride) {
     float gk = g[i] + wd * p[i];
@@ -266,24 +257,12 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
 
 using namespace pv;
 
-static int g_adam_nt = -1, g_adam_grid = 16384;  // 16384: -2..4 % vs 4096 (tools/adam_stream_micro.py)
-static int adam_nt() {
-  if (g_adam_nt < 0) {
-    const char* e = getenv("PAGEVEC_ADAM_NT");
-    g_adam_nt = (e && atoi(e) == 1) ? 1 : 0;
-  }
-  return g_adam_nt;
-}
-// dense Adam launch (plain / non-temporal streams)
+static int g_adam_grid = 16384;  // 16384: -2..4 % vs 4096 (tools/adam_stream_micro.py)
 static void launch_adam(dim3 grid, hipStream_t st, float* p, const float* g, float* m, float* v, long n, float lr,
                         float b1, float b2, float eps, float wd, int torch_style, float bc2i, const float* skip,
                         const float* tdev, unsigned short* p16) {
-  if (adam_nt())
-    hipLaunchKernelGGL(pv::optim::adam_kernel<1>, grid, dim3(256), 0, st, p, g, m, v, n, lr, b1, b2, eps, wd,
-                       torch_style, bc2i, skip, tdev, p16);
-  else
-    hipLaunchKernelGGL(pv::optim::adam_kernel<0>, grid, dim3(256), 0, st, p, g, m, v, n, lr, b1, b2, eps, wd,
-                       torch_style, bc2i, skip, tdev, p16);
+  hipLaunchKernelGGL(pv::optim::adam_kernel, grid, dim3(256), 0, st, p, g, m, v, n, lr, b1, b2, eps, wd, torch_style,
+                     bc2i, skip, tdev, p16);
 }
 
 static unsigned grid_for(long n, int per_thread) {
@@ -309,9 +288,8 @@ PV_API int pv_adam_dev(float* p, const float* g, float* m, float* v, long n, flo
 // Segmented step (lazy embedding rows): pv_step_inc once, then one pv_adam_seg per range of
 // the flat buffer — row_len 0: dense update of n elements; row_len > 0: lazy rows of an
 // (n / row_len, row_len) table.
-// A/B: non-temporal Adam streams (nt 0 / 1) and the dense launch's workgroup cap
-PV_API int pv_adam_set_nt(int nt, int grid_cap) {
-  g_adam_nt = nt ? 1 : 0;
+// A/B: the dense launch's workgroup cap
+PV_API int pv_adam_set_grid(int grid_cap) {
   if (grid_cap >= 256 && grid_cap <= 65536) g_adam_grid = grid_cap;
   return 0;
 }

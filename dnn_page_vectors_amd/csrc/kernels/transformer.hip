@@ -137,14 +137,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const unsigned short
 
 // Dropout keep decisions of columns c..c+3 (c % 4 == 0) of a row, bit k = column c+k kept:
 // the same counter hash as the conv kernels and ops/reference.py::dropout_keep_mask
-// (thr % 16 == 0: nibble b of mix(h_row + g8*phi) decides column 8*g8+b; otherwise byte b of
-// mix(h_row + g4*phi) decides column 4*g4+b).  thr = round(256 p), scale = 256 / (256 - thr).
+// (thr % 16 == 0: nibble j of the group hash of g8 decides column 8*g8+j, common.h
+// dropout_nibble; otherwise byte b of the group hash of g4 decides column 4*g4+b).  thr = round(256 p), scale = 256 / (256 - thr).
 __device__ __forceinline__ unsigned keep4(unsigned hrow, int c, int thr) {
   unsigned bits = 0u;
   if ((thr & 15) == 0) {
-    const unsigned h = dropout_group_hash(hrow, (unsigned)(c >> 3)) >> (4 * (c & 7));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) bits |= (((h >> (4 * k)) & 0xFu) >= (unsigned)(thr >> 4) ? 1u : 0u) << k;
+    bits = (dropout_keep_bits8(dropout_group_hash(hrow, (unsigned)(c >> 3)), thr >> 4) >> (c & 7)) & 0xFu;
   } else {
     const unsigned h = dropout_group_hash(hrow, (unsigned)(c >> 2));
 #pragma unroll

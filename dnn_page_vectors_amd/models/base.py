@@ -78,8 +78,6 @@ class TwoTowerModel(nn.Module):
         B, S, Ld = d_ids.shape
         training = self.training
         side = self._query_stream(q_ids)
-        if side is not None and getattr(self, "query_first", False) and getattr(self.cfg, "share_doc_tower", True):
-            return self._forward_query_first(q_ids, d_ids, seed, doc_hook, side)
         if getattr(self.cfg, "share_doc_tower", True):
             d = self.tower_forward("doc", d_ids.reshape(B * S, Ld), training, seed * 2 + 2).view(B, S, -1)
         else:  # v1: independent towers per document slot (dssm_cnn/cnn_dssm.py:160-164)
@@ -101,25 +99,6 @@ class TwoTowerModel(nn.Module):
             q = self.tower_forward("query", q_ids, training, seed * 2 + 1)
         main.wait_stream(side)
         q.record_stream(main)
-        return q, d
-
-    def _forward_query_first(self, q_ids, d_ids, seed, doc_hook, side):
-        """The query tower (side stream) BEFORE the page tower, which waits for it.  With no
-        cross-GPU page gather to hide (the trainer sets ``query_first`` when the doc hook starts
-        no collective), the page tower's persistent all-CU conv otherwise runs first and the
-        query conv queues behind it on the critical path to the loss; the backward still
-        overlaps on the two streams."""
-        B, S, Ld = d_ids.shape
-        main = torch.cuda.current_stream(q_ids.device)
-        side.wait_stream(main)
-        q_ids.record_stream(side)
-        with torch.cuda.stream(side):
-            q = self.tower_forward("query", q_ids, self.training, seed * 2 + 1)
-        main.wait_stream(side)
-        q.record_stream(main)
-        d = self.tower_forward("doc", d_ids.reshape(B * S, Ld), self.training, seed * 2 + 2).view(B, S, -1)
-        if doc_hook is not None:
-            doc_hook(d)
         return q, d
 
     def _query_stream(self, q_ids: torch.Tensor) -> Optional[torch.cuda.Stream]:

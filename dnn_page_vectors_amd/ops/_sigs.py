@@ -41,9 +41,6 @@ SIGS = {
     "pv_conv_pool_bwd_dw2": "ppppp" "pppp" "iiii" "upuiif" "p",
     "pv_conv_pool_bwd_emit3": "ppppppp" "iii" "f" "p",
     "pv_conv_bwd_slots_per_sample": "",
-    "pv_conv_dx_dense_maxl": "",
-    "pv_conv_pool_bwd_dx_dense": "ppppppp" "iiii" "upuii" "f" "p",
-    "pv_conv_bwd_rows_reduce": "pippp" "liii" "p",
     # conv_pool_bwd.hip: dTable reduce
     "pv_conv_pool_bwd_emit3_u16": "pppppp" "iii" "f" "p",
     "pv_conv_pool_bwd_reduce7_u16": "ppppp" "liiii" "upuii" "p",
@@ -97,8 +94,6 @@ SIGS = {
     "pv_layernorm_bwd": "ppppppppp" "ii" "p",
     "pv_bias_gelu_fwd": "ppp" "li" "p",
     # lt_gemm.hip (hipBLASLt with fused epilogues)
-    "pv_lt_gemm": "ii" "iii" "pi" "pi" "pi" "i" "f" "pi" "p" "i" "pl" "p",
-    "pv_lt_set_tune": "i",
     "pv_attn_set_qg": "iii",
     "pv_attn_set_fwd_dma": "i",
     "pv_gemm_mx8_set_stages": "i",
@@ -126,7 +121,7 @@ SIGS = {
     "pv_loss_stats": "pp" "i" "pp" "p",
     "pv_ib_grad_scale": "p" "i" "f" "p" "i" "f" "p" "i" "ppp" "p",
     "pv_colsum": "p" "i" "lll" "p" "i" "pp" "ii" "p",
-    "pv_adam_set_nt": "ii",
+    "pv_adam_set_grid": "i",
     "pv_step_inc": "p" "p",
     "pv_adam_seg": "pppp" "li" "p" "fffff" "i" "pp" "p",
     "pv_adam_rows": "pppp" "i" "pl" "p" "fffff" "i" "pp" "p",

@@ -62,11 +62,13 @@ _grid_cache = {}
 
 # sorted dTable entries per wave in the reduce (conv_bwd_reduce7_kernel; multiple of 64)
 REDUCE_EPW = int(os.environ.get("PAGEVEC_REDUCE_EPW", "512"))
-# 4-byte sort keys even when the vocabulary fits 2-byte keys (tests: u16 vs u32 reduce)
-KEYS32 = os.environ.get("PAGEVEC_KEYS32", "0") != "0"
+
+
+KEYS32 = False  # tests: the 4-byte-key instantiation at a small vocabulary (no env switch)
 
 
 def _k16(V: int) -> bool:
+    """2-byte dTable sort keys (token ids < 65535, sentinel V); 4-byte keys above."""
     return V < 65535 and not KEYS32
 
 # dW/db kernel on a side HIP stream, concurrent with the dTable emit -> sort -> reduce chain
@@ -134,15 +136,6 @@ def sort_pairs_iota(keys: torch.Tensor, skeys: torch.Tensor, svals: torch.Tensor
     check(L_.pv_rsort_pairs(P(temp), tb, P(keys), P(skeys), None, P(svals), M, end_bit, kb, s), "pv_rsort_pairs")
 
 
-# dTable of short sequences (the query towers) from per-sample dense dX rows (N*L rows sorted by
-# token) instead of N*1050 (f, j) entries through emit -> sort -> reduce.  Same-process A/B
-# (tools/qbwd_micro.py, whole conv backward incl. dW): 4096 x 45 0.445 vs 0.459 ms, but
-# 1024 x 250 0.293 vs 0.265 ms — so only up to DENSE_DX_MAXL tokens.  Since the faster
-# reduce7 / templated dW kernels the entry path wins for the headline query tower too
-# (same box, headline step 7.637 / 7.595 vs 7.650 / 7.638 ms), so the dense-dX path is
-# now opt-in: PAGEVEC_DENSE_DX=1.
-DENSE_DX = os.environ.get("PAGEVEC_DENSE_DX", "0") != "0"
-DENSE_DX_MAXL = 64
 # the dTable sort keys written by the conv FORWARD's loader waves, one sample behind the MFMA
 # waves (each filter's argmax window and ReLU liveness are known then): the backward only
 # writes the {g * scale, argmax} records instead of running the emit kernel's id gathers on
@@ -172,10 +165,6 @@ V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5, 16384 + 128 + 
 
 def _conv_dbg() -> int:
     return int(lib().pv_conv_get_dbg())
-
-
-def _dense_dx(L: int) -> bool:
-    return DENSE_DX and L <= min(DENSE_DX_MAXL, lib().pv_conv_dx_dense_maxl())
 
 
 def _weight_rows(w3: torch.Tensor, w4: torch.Tensor, ep: int) -> torch.Tensor:
@@ -215,8 +204,7 @@ class _ConvPoolFn(torch.autograd.Function):
         # needs_input_grad reflects requires_grad, not grad mode, and forward() itself runs with
         # grad disabled: the caller's grad mode (_CALLER_GRAD) says whether a backward can
         # follow.  Under no_grad (eval, Recall / encode batches) no keys are emitted or sorted.
-        if _CALLER_GRAD.on and ctx.needs_input_grad[1] and FWD_EMIT and not _dense_dx(L) \
-                and _conv_dbg() in (0,) + V7_DBG:
+        if _CALLER_GRAD.on and ctx.needs_input_grad[1] and FWD_EMIT and _conv_dbg() in (0,) + V7_DBG:
             k16 = _k16(V)
             keys = torch.empty(N * SLOTS_PER_SAMPLE, dtype=torch.int16 if k16 else torch.int32, device=ids.device)
         check(lib().pv_conv_pool_fwd2(P(ids), P(tbl16), P(wpack), P(b3c), P(b4c), P(pooled), P(argmax), N, L, V,
@@ -277,9 +265,8 @@ class _ConvPoolFn(torch.autograd.Function):
         L_ = lib()
         # every buffer the side stream touches is allocated on the main stream above/before
         # and the main stream joins the side stream before returning: no cross-stream reuse
-        dense_dx = ctx.needs_input_grad[1] and _dense_dx(L)
         # the page tower's dW beside its table chain (not inside a hipGraph capture: one stream)
-        side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1] and not dense_dx
+        side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1]
                 and not torch.cuda.is_current_stream_capturing() and not determinism.enabled() else None)
         if side is not None:
             main = torch.cuda.current_stream(dev)
@@ -299,23 +286,7 @@ class _ConvPoolFn(torch.autograd.Function):
         if side is not None:
             launch_dw()
         dtable = None
-        if dense_dx:
-            # short sequences (query towers): per-sample dense dX rows (LDS), sorted by token,
-            # summed per token run: N*L rows instead of N*1050 (f, j) entries
-            R = N * L
-            k16 = V < 65535
-            keys = torch.empty(R, dtype=torch.int16 if k16 else torch.int32, device=dev)
-            rows = torch.empty(R, EP, dtype=torch.float32, device=dev)
-            check(L_.pv_conv_pool_bwd_dx_dense(P(gpool), P(pooled), P(argmax), P(ids), P(_weight_rows(w3, w4, EP)),
-                                               P(rows), P(keys), 2 if k16 else 4, N, L, V, seed, P(sp), row_offset,
-                                               thr, tok, scale, s), "pv_conv_pool_bwd_dx_dense")
-            skeys = torch.empty_like(keys)
-            svals = torch.empty(R, dtype=torch.int32, device=dev)
-            sort_pairs_iota(keys, skeys, svals, max(1, int(V).bit_length()))
-            dtable = t_tab if t_tab is not None else torch.zeros(V, E, dtype=torch.float32, device=dev)
-            check(L_.pv_conv_bwd_rows_reduce(P(skeys), 2 if k16 else 4, P(svals), P(rows), P(dtable), R, 256, E, V, s),
-                  "pv_conv_bwd_rows_reduce")
-        elif ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:
             M = N * SLOTS_PER_SAMPLE  # k3 filters 3 slots, k4 filters 4 (conv_bwd_emit3_kernel)
             u32 = torch.int32
             end_bit = max(1, int(V).bit_length())

@@ -145,8 +145,11 @@ _BAG_SPLITK = int(os.environ.get("PAGEVEC_BAG_SPLITK", "0"))  # override of the 
 BAG_EPW = int(os.environ.get("PAGEVEC_BAG_EPW", "64"))  # sorted entries per wave (>= 8)
 FP8_BAG = os.environ.get("PAGEVEC_FP8_BAG", "1") != "0"  # 0: fp8 towers keep the bf16 counts GEMM (A/B)
 # fp8 bag weight gradient: C^T G on the MX fp8 MFMA too (e4m3 counts transposed, G per-tensor
-# scaled e4m3) instead of the exact bf16 counts + hipBLASLt
-FP8_BWD = os.environ.get("PAGEVEC_FP8_BWD", "1") != "0"
+# scaled e4m3) instead of the exact bf16 counts + hipBLASLt.  Opt-in: the product is within
+# ~8 % of the exact gradient (per-row gradients below amax * 2^-9 / 448 flush to zero), and
+# the step-level A/B did not show a gain (chunked 1.737 vs 1.683 ms median,
+# profiles/r5_lt/chunked_fp8bwd_ab.txt) although the isolated micro is faster
+FP8_BWD = os.environ.get("PAGEVEC_FP8_BWD", "0") != "0"
 
 
 _BAG_ACT = {"none": 0, "relu": 1, "tanh": 3}
@@ -349,7 +352,7 @@ def embedding_bag(ids: torch.Tensor, W: torch.Tensor, W16: Optional[torch.Tensor
     ``fp8``: long bags (the counts plan) multiply e4m3 counts by the per-tensor-scaled e4m3
     table on the block-scaled fp8 MFMA (``w8`` = ops.fp8.quantize_t(W) of this step, else
     quantised here); the weight gradient is e4m3 C^T x the per-tensor e4m3 gradient on the same
-    MFMA (PAGEVEC_FP8_BWD, default), or the exact bf16 C^T G (straight-through)."""
+    MFMA (PAGEVEC_FP8_BWD=1, opt-in), or the exact bf16 C^T G (straight-through, default)."""
     note_rows(W, ids)  # sparse-gradient tables (parallel/sparse_rows.py) record their rows
     if use_hip(ids, W) and act in _BAG_ACT:
         if W16 is None:

@@ -185,7 +185,7 @@ class _InBatchFn(torch.autograd.Function):
 
 
 # column-block size of the wide-vector path: B x ROWS_BLOCK_ELEMS / B fp32 logits per block
-ROWS_BLOCK_ELEMS = int(os.environ.get("PAGEVEC_IB_ROWS_BLOCK", str(1 << 25)))
+ROWS_BLOCK_ELEMS = 1 << 25
 
 
 def _col_blocks(B: int, M: int):
@@ -197,7 +197,7 @@ class _InBatchRowsFn(torch.autograd.Function):
     """Wide vectors (D > 192, e.g. BERT's 768; the narrow flash kernels hold D accumulators per
     query row in registers).  Default: the wide flash kernel (loss.hip::ibw_kernel, _wide_ok):
     S reduced over D across a workgroup's 4 waves, the gradient products on the same tile, no
-    S block in HBM and no library GEMM.  Fallback (other D, PAGEVEC_IB_WIDE=0): the logits are
+    S block in HBM and no library GEMM.  Fallback (the widths ibw does not cover): the logits are
     tiled over page-column blocks at the GEMM level — each
     (B x Mb) block of S comes from a bf16 x bf16 -> fp32 library GEMM, is reduced by
     loss.hip::ib_rows_blk_kernel and dropped, so memory stays O(B * Mb) for any M; the
@@ -240,7 +240,7 @@ class _InBatchRowsFn(torch.autograd.Function):
 
 # Wide vectors on the flash kernel (loss.hip::ibw_kernel, DP % 128 == 0, 256..1024): no S block
 # in HBM, no library GEMM; "0" = the column-block path below (fp32 S blocks + hipBLASLt)
-IB_WIDE = os.environ.get("PAGEVEC_IB_WIDE", "1") != "0"
+IB_WIDE = True  # tests switch it off to exercise the column-block fallback at a covered width
 
 
 def _wide_ok(DP: int) -> bool:

@@ -35,6 +35,25 @@ def _mix32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+_GROUP_STEP = 0x9E3779  # 24-bit golden-ratio step between a row's groups
+# nibble mode: element j of a group reads h[P] h[P-8] h[P-4] h[P-12] (MSB first), P = 15 - j//2 + 16 (j%2)
+_NIB_POS = [15 - (j >> 1) + 16 * (j & 1) for j in range(8)]
+
+
+def _mix24(x: torch.Tensor) -> torch.Tensor:
+    """The group-hash mixer (common.h mix24): two xorshift + 24-bit-multiply rounds."""
+    x = x & _M32
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * 0xED5AD5) & _M32
+    x = x ^ (x >> 15)
+    return ((x & 0xFFFFFF) * 0x9E3779) & _M32
+
+
+def _group_hash(h_row: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """(n,) row hashes x (ng,) group ids -> (n, ng) group hashes (common.h dropout_group_hash)."""
+    return _mix24(h_row.unsqueeze(1) + ((g & 0xFFFFFF) * _GROUP_STEP).unsqueeze(0))
+
+
 def dropout_threshold(p: float) -> int:
     """Keep an element when its 8-bit hash byte >= round(p*256) (p quantised to 1/256)."""
     return int(round(p * 256.0))
@@ -45,10 +64,14 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     """Bool keep-mask of shape (n_rows, width) for flat row ids ``row_offset + r`` (r < n_rows,
     or r in ``rows`` when given: any local row ids, n_rows = rows.numel()).
 
-    element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25):
-             h_row = mix(row ^ mix(seed)); nibble b of mix(h_row + g*0x9E3779B9) decides column
-             8g+b (kept iff nibble >= thr/16) — one hash per 8 columns;
-    element, other thr: byte b of mix(h_row + g*0x9E3779B9) decides column 4g+b (>= thr);
+    h_row = mix32(row ^ mix32(seed)) (lowbias32); the group hash of group g of a row is
+    h = mix24(h_row + g * 0x9E3779) (two xorshift / 24-bit multiply rounds, full-rate on the GPU).
+
+    element, thr = round(256p) a multiple of 16 (p = k/16, e.g. the reference's 0.25): column
+             8g + j is kept iff the 4-bit value h[P] h[P-8] h[P-4] h[P-12] (MSB first),
+             P = 15 - j//2 + 16 (j%2), is >= thr/16 — one hash per 8 columns (the layout lets
+             the kernels build the bf16 pair masks with v_perm_b32, common.h keep_piece);
+    element, other thr: byte b of the group hash of g decides column 4g+b (>= thr);
     token:   one decision per row: byte 0 of h_row.
     """
     thr = dropout_threshold(p)
@@ -64,13 +87,13 @@ def dropout_keep_mask(seed: int, n_rows: int, width: int, p: float, row_offset: 
     if thr % 16 == 0:
         ng = (width + 7) // 8
         g = torch.arange(ng, dtype=torch.int64, device=device)
-        h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
-        shifts = torch.arange(0, 32, 4, dtype=torch.int64, device=device)
-        nib = (h.unsqueeze(2) >> shifts) & 0xF  # (n, ng, 8)
+        h = _group_hash(h_row, g).unsqueeze(2)  # (n, ng, 1)
+        P = torch.tensor(_NIB_POS, dtype=torch.int64, device=device)
+        nib = (((h >> P) & 1) << 3) | (((h >> (P - 8)) & 1) << 2) | (((h >> (P - 4)) & 1) << 1) | ((h >> (P - 12)) & 1)
         return nib.reshape(n_rows, ng * 8)[:, :width] >= thr // 16
     ng = (width + 3) // 4
     g = torch.arange(ng, dtype=torch.int64, device=device)
-    h = _mix32(h_row.unsqueeze(1) + ((g * 0x9E3779B9) & _M32).unsqueeze(0))  # (n, ng)
+    h = _group_hash(h_row, g)  # (n, ng)
     shifts = torch.tensor([0, 8, 16, 24], dtype=torch.int64, device=device)
     bytes_ = (h.unsqueeze(2) >> shifts) & 0xFF  # (n, ng, 4)
     return (bytes_.reshape(n_rows, ng * 4)[:, :width] >= thr)

@@ -483,11 +483,6 @@ def wgrad_f32(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] =
     ``out``: fp32 destination (a flat-gradient view, ops/grad_sink.py), overwritten.
     """
     T = dy2.shape[0]
-    if WGRAD_LT and dy2.is_cuda:
-        o = out if out is not None else torch.empty(dy2.shape[1], x2.shape[1], dtype=torch.float32,
-                                                    device=dy2.device)
-        check(lt_mm(dy2, x2, o, ta=True), "pv_lt_gemm(wgrad)")
-        return o
     sk = _wgrad_splits(T)
     try:
         if sk == 1:
@@ -507,11 +502,7 @@ class _Linear16Fn(torch.autograd.Function):
     def forward(ctx, x, w, b, w16, res=None, blink=None):
         x = x.to(torch.bfloat16)
         x2 = x.reshape(-1, x.shape[-1])
-        if LINEAR_LT and x2.is_cuda and x2.is_contiguous():
-            y = torch.empty(x2.shape[0], w16.shape[0], dtype=torch.bfloat16, device=x2.device)
-            check(lt_mm(x2, w16, y, tb=True, epi=1 if b is not None else 0,
-                        bias=b.detach().float().contiguous() if b is not None else None), "pv_lt_gemm(linear)")
-        elif b is not None:
+        if b is not None:
             y = torch.addmm(b.to(torch.bfloat16), x2, w16.t())
         else:
             y = x2 @ w16.t()
@@ -562,161 +553,24 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
     return F.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
 
 
-# FFN on hipBLASLt fused epilogues (lt_gemm.hip): "1" = GELU_AUX_BIAS forward / DGELU_BGRAD
-# backward where the library has solutions (probed once per shape), "0" = plain GEMMs + the
-# bias_gelu kernels.  torch 2.10's hipBLASLt on gfx950 has none for bf16 (tools/lt_probe.py:
-# GELU / GELU_BIAS only, no AUX / DGELU variants), so the probe falls back there.
-FFN_LT = os.environ.get("PAGEVEC_FFN_LT", "1") != "0"
-# hipBLASLt candidate autotuning (lt_gemm.hip): time the heuristic's top 16 once per problem
-LT_TUNE = os.environ.get("PAGEVEC_LT_TUNE", "0") != "0"
-_LT_TUNE_SET = [None]
-# the linear layers' forward / dX GEMMs through lt_gemm.hip too (bias epilogue, in-place
-# residual dX) instead of torch.addmm / mm; WGRAD_LT: the fp32 weight gradient as one lt GEMM
-# instead of the split-K bmm (measured slower: profiles/r5_lt/)
-LINEAR_LT = os.environ.get("PAGEVEC_LINEAR_LT", "0") != "0"
-WGRAD_LT = os.environ.get("PAGEVEC_WGRAD_LT", "0") != "0"
-_LT_WS = {}
-_LT_BAD = set()  # (shape, epilogue) keys hipBLASLt has no solution for
-LT_WS_BYTES = 64 << 20
-
-
-def _lt_ws(dev: torch.device) -> torch.Tensor:
-    if _LT_TUNE_SET[0] != LT_TUNE:
-        lib().pv_lt_set_tune(int(LT_TUNE))
-        _LT_TUNE_SET[0] = LT_TUNE
-    ws = _LT_WS.get(dev)
-    if ws is None:
-        ws = _LT_WS[dev] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=dev)
-    return ws
-
-
-def lt_mm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, ta: bool = False, tb: bool = False, epi: int = 0,
-          bias: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None, beta: float = 0.0) -> int:
-    """Row-major out (M x N) [= beta out +] op(a) @ op(b) on hipBLASLt (lt_gemm.hip), op = transpose
-    when ta / tb (a stored K x M, b stored N x K).  bf16 operands; out bf16 or fp32.  Epilogue
-    ``epi``: 1 = + bias, 2 = gelu(. + bias) with the pre-activation written to aux, 4 = . * gelu'(aux)
-    with the bias gradient (fp32, length N) written to bias.  hipBLASLt is column-major, so it
-    computes out^T = op(b)^T op(a)^T.  Returns the launcher status (-3: no library solution)."""
-    M, N = out.shape
-    K = a.shape[0] if ta else a.shape[1]
-    for t in (a, b, out):
-        if t.stride(-1) != 1:
-            raise ValueError("lt_mm operands need unit column stride")
-    ws = _lt_ws(out.device)
-    return lib().pv_lt_gemm(int(tb), int(ta), N, M, K, P(b), b.stride(0), P(a), a.stride(0), P(out), out.stride(0),
-                            int(out.dtype == torch.float32), float(beta), P(bias),
-                            int(bias is not None and bias.dtype == torch.float32), P(aux), epi, P(ws), ws.numel(),
-                            stream(out.device))
-
-
 def _dx_residual(res: Optional[ResidualLink], dy2: torch.Tensor, w16: torch.Tensor, shape) -> torch.Tensor:
     """dX = dY W (+ the residual branch's gradient parked in ``res``, added in the GEMM epilogue)."""
     rg = res.grad if res is not None else None
     if rg is None:
-        if LINEAR_LT and dy2.is_cuda:
-            dx = torch.empty(dy2.shape[0], w16.shape[1], dtype=torch.bfloat16, device=dy2.device)
-            check(lt_mm(dy2, w16, dx), "pv_lt_gemm(dx)")
-            return dx.view(shape)
         return (dy2 @ w16).view(shape)
     res.grad = None
     if rg.dtype == dy2.dtype and rg.is_contiguous():
-        if LINEAR_LT and dy2.is_cuda:
-            check(lt_mm(dy2, w16, rg.view(-1, rg.shape[-1]), beta=1.0), "pv_lt_gemm(dx+res)")
-            return rg.view(shape)
         return rg.view(-1, rg.shape[-1]).addmm_(dy2, w16).view(shape)
     return torch.addmm(rg.reshape(-1, rg.shape[-1]).to(dy2.dtype), dy2, w16).view(shape)
-
-
-class _FfnFn(torch.autograd.Function):
-    """f2 = gelu(x W1^T + b1) W2^T (tanh GELU) with the bias + GELU in the first GEMM's
-    epilogue (which also writes the pre-activation h for the backward) and the GELU backward
-    + b1 gradient in the epilogue of the dF GEMM (dH = (dY2 W2) * gelu'(h), db1 = colsum dH):
-    no separate pass over the (T x I) activation in either direction (lt_gemm.hip)."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, w1_16, w2_16, res=None):
-        x2 = x.to(torch.bfloat16).reshape(-1, x.shape[-1]).contiguous()
-        T, I = x2.shape[0], w1_16.shape[0]
-        h = torch.empty(T, I, dtype=torch.bfloat16, device=x.device)
-        f = torch.empty_like(h)
-        check(lt_mm(x2, w1_16, f, tb=True, epi=2, bias=b1.detach().float().contiguous(), aux=h), "pv_lt_gemm(gelu)")
-        if LINEAR_LT:
-            y = torch.empty(T, w2_16.shape[0], dtype=torch.bfloat16, device=x.device)
-            check(lt_mm(f, w2_16, y, tb=True), "pv_lt_gemm(ffn2)")
-        else:
-            y = f @ w2_16.t()
-        ctx.save_for_backward(x2, h, f, w1_16, w2_16)
-        ctx.shape = x.shape
-        ctx.params = (w1, b1, w2)
-        ctx.res = res
-        return y.view(*x.shape[:-1], w2_16.shape[0])
-
-    @staticmethod
-    def backward(ctx, dy):
-        x2, h, f, w1_16, w2_16 = ctx.saved_tensors
-        pw1, pb1, pw2 = ctx.params
-        dy2 = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
-        dh = torch.empty_like(h)
-        tb = grad_sink.write_target(pb1) if ctx.needs_input_grad[2] else None
-        db1 = tb if tb is not None else torch.empty(h.shape[1], dtype=torch.float32, device=h.device)
-        # dH = (dY2 W2) * gelu'(h), W2 stored (H x I) row-major = the GEMM's K x N
-        check(lt_mm(dy2, w2_16, dh, epi=4, bias=db1, aux=h), "pv_lt_gemm(dgelu)")
-        if tb is not None:
-            grad_sink.done(pb1)
-            db1 = None
-        dw1 = dw2 = None
-        if ctx.needs_input_grad[3]:
-            t = grad_sink.write_target(pw2)
-            dw2 = wgrad_f32(dy2, f, out=t)
-            if t is not None:
-                grad_sink.done(pw2)
-                dw2 = None
-        if ctx.needs_input_grad[1]:
-            t = grad_sink.write_target(pw1)
-            dw1 = wgrad_f32(dh, x2, out=t)
-            if t is not None:
-                grad_sink.done(pw1)
-                dw1 = None
-        dx = _dx_residual(ctx.res, dh, w1_16, ctx.shape) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1 if ctx.needs_input_grad[2] else None, dw2, None, None, None
-
-
-def _ffn_lt_ok(x: torch.Tensor, w1: torch.Tensor) -> bool:
-    key = (x.shape[-1], w1.shape[0], x.device)
-    if key in _LT_BAD:
-        return False
-    T = x.numel() // x.shape[-1]
-    # one probe per shape class: hipBLASLt may have no GELU_AUX_BIAS / DGELU_BGRAD solution
-    xb = torch.zeros(T, x.shape[-1], dtype=torch.bfloat16, device=x.device)
-    w = torch.zeros(w1.shape, dtype=torch.bfloat16, device=x.device)
-    h = torch.empty(T, w1.shape[0], dtype=torch.bfloat16, device=x.device)
-    f = torch.empty_like(h)
-    b = torch.zeros(w1.shape[0], dtype=torch.float32, device=x.device)
-    wt = torch.zeros(x.shape[-1], w1.shape[0], dtype=torch.bfloat16, device=x.device)
-    r1 = lt_mm(xb, w, f, tb=True, epi=2, bias=b, aux=h)
-    r2 = lt_mm(xb, wt, h, epi=4, bias=b, aux=f) if r1 == 0 else r1
-    if r1 != 0 or r2 != 0:
-        if r1 not in (0, -3) or r2 not in (0, -3):
-            check(r1 if r1 not in (0, -3) else r2, "pv_lt_gemm(probe)")
-        _LT_BAD.add(key)
-        return False
-    return True
-
-
-_LT_OK = {}
 
 
 def ffn(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
         res: Optional[ResidualLink] = None) -> torch.Tensor:
     """The transformer FFN without its output bias: gelu(x W1^T + b1) W2^T (the output bias
-    is added by the following add_layernorm)."""
-    if use_hip(x) and FFN_LT and torch.is_grad_enabled():
-        key = (tuple(x.shape), w1.shape, x.device)
-        ok = _LT_OK.get(key)
-        if ok is None:
-            ok = _LT_OK[key] = _ffn_lt_ok(x, w1)
-        if ok:
-            return _FfnFn.apply(x, w1, b1, w2, weight_bf16(w1), weight_bf16(w2), res)
+    is added by the following add_layernorm).  The bias + GELU pair runs as one kernel in
+    each direction (bias_gelu / its backward); the hipBLASLt GELU_AUX_BIAS / DGELU_BGRAD
+    epilogues that would fold them into the GEMMs have no gfx950 bf16 solutions in torch
+    2.10's hipBLASLt (round-5 probe, docs/PERF.md), so no GEMM-epilogue arm is kept."""
     return linear(bias_gelu(linear(x, w1, res=res), b1), w2)
 
 

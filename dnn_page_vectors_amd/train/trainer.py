@@ -50,12 +50,6 @@ def _restore_det(prev) -> None:
     determinism.restore(prev)
 
 
-# 1: on one rank the query tower runs before the page tower (models/base.py
-# _forward_query_first).  Off: no measurable gain at the headline shape (same process, interleaved:
-# 7.311 vs 7.304 ms, tools/step_flag_ab.py; alternated processes on one
-# box: 7.09 / 7.12 / 7.01 vs 6.79 / 7.14 / 7.04 ms, profiles/r4_prune/qfirst_ab.txt)
-QUERY_FIRST = os.environ.get("PAGEVEC_QUERY_FIRST", "0") != "0"
-
 class InjectedFault(RuntimeError):
     pass
 
@@ -212,8 +206,6 @@ class Trainer:
                 pre["dn"] = dops.l2_normalize(d_.reshape(B * S, -1))
                 if cfg.loss_mode == "cross_gpu" and self.info.enabled:
                     pre["gather"] = lops.start_page_gather(pre["dn"])
-            # no collective to hide behind the query tower: run it before the page tower
-            self.model.query_first = QUERY_FIRST and not (cfg.loss_mode == "cross_gpu" and self.info.enabled)
             q, d = self.model(q_ids, d_ids, seed=seed, doc_hook=doc_hook)
             dn = pre["dn"]
         qn = dops.l2_normalize(q)

@@ -24,12 +24,9 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_CONV_DBG": ("ab", "0", "conv forward variant / timing ablation (0 = v7 production)"),
     "PAGEVEC_REDUCE_EPW": ("ab", "512", "sorted dTable entries per wave in reduce7"),
     "PAGEVEC_R7_OCC": ("ab", "8", "reduce7 register cap (waves per SIMD)"),
-    "PAGEVEC_KEYS32": ("ab", "0", "4-byte dTable sort keys even for V < 65535"),
     "PAGEVEC_DW_STREAM": ("ab", "0", "page-tower dW on a side stream"),
-    "PAGEVEC_DW_XCD": ("ab", "0", "XCD-aware dW block order"),
     "PAGEVEC_BIAS_SINK": ("ab", "1", "conv bias gradients written by the dW kernel"),
     "PAGEVEC_SIDE_PER_STREAM": ("ab", "1", "one side stream per calling stream"),
-    "PAGEVEC_DENSE_DX": ("ab", "0", "dense dX rows for short sequences (query tower)"),
     "PAGEVEC_FWD_EMIT": ("ab", "1", "dTable sort keys emitted by the forward's loader waves"),
     "PAGEVEC_EARLY_SORT": ("ab", "1", "dTable key sort right after the forward, side stream"),
     "PAGEVEC_EARLY_SORT_SKIP": ("ab", "1", "no early sort for 128 < L < 1024"),
@@ -47,23 +44,14 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_BAG_COUNTS16": ("ab", "1", "16-bit packed LDS counts histogram"),
     "PAGEVEC_BAG_GEMM": ("ab", "lib", "long-bag GEMMs: hipBLASLt on the count matrix (lib) or bag_gemm.hip (hip)"),
     "PAGEVEC_FP8_BAG": ("ab", "1", "fp8 towers: page bag on the MX fp8 MFMA"),
-    "PAGEVEC_FP8_BWD": ("ab", "1", "fp8 towers: bag weight gradient on the MX fp8 MFMA (e4m3 counts^T x e4m3 G)"),
-    "PAGEVEC_LT_TUNE": ("ab", "0", "time hipBLASLt's top candidates once per problem (lt_gemm.hip)"),
-    "PAGEVEC_LINEAR_LT": ("ab", "0", "BERT linear forward / dX GEMMs on lt_gemm.hip instead of torch mm / addmm"),
-    "PAGEVEC_WGRAD_LT": ("ab", "0", "BERT weight gradients as one lt_gemm.hip GEMM instead of the split-K bmm"),
+    "PAGEVEC_FP8_BWD": ("ab", "0", "fp8 towers: bag weight gradient on the MX fp8 MFMA (e4m3 counts^T x e4m3 G)"),
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),
     "PAGEVEC_DIRECT_GRAD": ("ab", "1", "kernels write the flat gradient buffer directly"),
     "PAGEVEC_RESID_FUSE": ("ab", "1", "BERT residual gradients fused into dX GEMMs"),
-    "PAGEVEC_ADAM_NT": ("ab", "0", "dense Adam with non-temporal loads / stores"),
     "PAGEVEC_CONV_SHORT": ("ab", "1", "conv forward: one 48-row chunk for sequences up to 50 tokens (query tower)"),
     "PAGEVEC_ATTN_BGRAD": ("ab", "1", "qkv bias gradient from the attention backward's partial column sums"),
     "PAGEVEC_BERT_EMBED": ("ab", "1", "BERT embedding front end as one fused gather + add kernel"),
-    "PAGEVEC_FFN_LT": ("ab", "1", "BERT FFN bias + GELU (and its backward) in hipBLASLt GEMM epilogues"),
-    "PAGEVEC_IB": ("ab", "7", "in-batch loss kernel generation (7 pipelined ib7, 5 ib5 + ib3, 3 ib3)"),
-    "PAGEVEC_IB_WIDE": ("ab", "1", "wide-vector (D = 768) loss on the ibw flash kernel (0: fp32 S blocks + GEMMs)"),
-    "PAGEVEC_IB_ROWS_BLOCK": ("ab", str(1 << 25), "wide-vector loss column block (elements)"),
     "PAGEVEC_NO_MIRROR": ("ab", "0", "no bf16 mirror written by the Adam kernel"),
-    "PAGEVEC_QUERY_FIRST": ("ab", "0", "query tower before the page tower on one rank"),
     # process plumbing
     "PAGEVEC_HIP_LIB": ("runtime", "", "path of the kernel library to load"),
     "PAGEVEC_DEBUG_KERNELS": ("runtime", "0", "load the PV_CHECK debug kernel library"),

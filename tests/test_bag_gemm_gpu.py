@@ -145,7 +145,7 @@ def test_chunked_fp8_bag_backward_uses_segment_lists(monkeypatch):
 
 @pytest.mark.parametrize("N,L", [(256, 512), (4096, 512), (300, 700)])
 def test_chunked_fp8_bag_backward_on_mx_fp8(N, L, monkeypatch):
-    """PAGEVEC_FP8_BWD (config 5 default): the bag weight gradient as e4m3 counts^T x e4m3
+    """PAGEVEC_FP8_BWD=1 (opt-in arm): the bag weight gradient as e4m3 counts^T x e4m3
     (per-tensor scaled) dz / len on the MX fp8 MFMA, against an fp64 reference of exactly that
     quantised product (emulate_e4m3 = the device's RNE saturating conversion), and within fp8
     rounding of the exact gradient."""

@@ -1174,37 +1174,6 @@ def test_hipgraph_cdssm_unfenced_fresh_batches():
     assert all(v == v and v < 50 for v in vals), vals[-5:]
 
 
-@pytest.mark.parametrize("L,p,mode", [(45, 0.25, "element"), (20, 0.0, "element"), (250, 0.25, "element"),
-                                      (64, 0.25, "token"), (37, 0.3, "element")])
-def test_dense_dx_matches_sort_path(L, p, mode):
-    """Short-sequence dTable (per-sample dense dX in LDS + row atomics) == the emit / sort /
-    reduce path on Zipf-skewed ids (fp32 atomics both ways: equal up to summation order)."""
-    torch.manual_seed(2)
-    V, E, F, N = 700, 100, 150, 96
-    ranks = torch.arange(1, V, dtype=torch.float64)
-    probs = ranks.pow(-1.1)
-    ids = (torch.multinomial(probs / probs.sum(), N * L, replacement=True) + 1).view(N, L).to(torch.int32).to(DEV)
-    table = bf(torch.randn(V, E, device=DEV) * 0.5)
-    w3, w4 = bf(torch.randn(F, 3, E, device=DEV) * 0.1), bf(torch.randn(F, 4, E, device=DEV) * 0.1)
-    b = [torch.zeros(F, device=DEV), torch.zeros(F, device=DEV)]
-    grads = []
-    saved = cops.DENSE_DX, cops.DENSE_DX_MAXL
-    cops.DENSE_DX_MAXL = 256
-    try:
-        for dense in (False, True):
-            cops.DENSE_DX = dense
-            t = table.clone().requires_grad_(True)
-            pooled, _ = cops.conv_relu_maxpool_fused(ids, t, [w3, w4], b, p, 77, True, mode)
-            (pooled * torch.linspace(-1, 1, pooled.numel(), device=DEV).view_as(pooled)).sum().backward()
-            grads.append(t.grad)
-    finally:
-        cops.DENSE_DX, cops.DENSE_DX_MAXL = saved
-    # fp32 sums of hundreds of terms in different orders (hot Zipf rows): absolute tolerance
-    # relative to the largest gradient entry
-    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=2e-5 * float(grads[0].abs().max()))
-    assert grads[0].abs().sum() > 0
-
-
 @pytest.mark.parametrize("model", ["cdssm", "mlp", "bert"])
 def test_direct_flat_grad_writes_match_autograd(model, monkeypatch):
     """ops/grad_sink.py: ops writing parameter gradients straight into the flat buffer give
@@ -1831,9 +1800,9 @@ def test_fp8_bag_matches_reference():
     print(f"fp8 bag vs reference-quantised {err:.2e}, vs exact fp32 (quantisation) {qerr:.3f}")
     assert qerr < 0.08
     gw = float((Wd.grad.cpu() - W.grad).abs().max() / W.grad.abs().max())
-    # FP8_BWD (default): both sides quantise the gradient to e4m3 per tensor — the odd
-    # rounding tie differs (fp32 dz computed with / without FMAs); else the exact C^T G with
-    # bf16 dz on the GPU
+    # FP8_BWD (opt-in arm): both sides quantise the gradient to e4m3 per tensor — the odd
+    # rounding tie differs (fp32 dz computed with / without FMAs); default: the exact C^T G
+    # on both sides (bf16 dz on the GPU)
     assert gw < (5e-3 if eops.FP8_BWD else 1e-2), gw
     torch.testing.assert_close(bd.grad.cpu(), b.grad, rtol=1e-4, atol=1e-4)
 
@@ -1974,9 +1943,9 @@ def test_inbatch_loss_ib7_matches_ib5(B, M, clip, D, ver):
     torch.testing.assert_close(res[ver][2], res[5][2], rtol=1e-4, atol=1e-6)
 
 
-def test_adam_nontemporal_bit_identical():
-    """optim.hip::adam_kernel<1> (non-temporal loads / stores) and a larger workgroup cap
-    change only the memory path: the update is bit-identical to the default kernel."""
+def test_adam_grid_cap_bit_identical():
+    """The dense Adam launch's workgroup cap changes only how the stream is split over
+    workgroups: the update is bit-identical."""
     from dnn_page_vectors_amd.ops._common import P, lib, stream
 
     L_ = lib()
@@ -1986,8 +1955,8 @@ def test_adam_nontemporal_bit_identical():
     base[3].abs_()
     outs = []
     try:
-        for nt, cap in ((0, 4096), (1, 4096), (1, 16384)):
-            L_.pv_adam_set_nt(nt, cap)
+        for cap in (4096, 1024, 16384):
+            L_.pv_adam_set_grid(cap)
             p, g, m, v = (x.clone() for x in base)
             t = torch.zeros(1, device=DEV)
             for _ in range(3):
@@ -1996,22 +1965,17 @@ def test_adam_nontemporal_bit_identical():
             torch.cuda.synchronize()
             outs.append((p, m, v))
     finally:
-        L_.pv_adam_set_nt(0, 16384)  # the defaults
+        L_.pv_adam_set_grid(16384)  # the default
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
 
 
-def test_loss_generation_default_matches_knob_registry():
-    """The loss-kernel generation in effect by default is the one utils/knobs.py records in
-    the bench JSON (7: ib7), unless PAGEVEC_IB overrides it."""
-    import os
-
+def test_loss_generation_default_is_ib7():
+    """The loss-kernel generation in effect by default is ib7 (no environment switch)."""
     from dnn_page_vectors_amd.ops._common import lib as _lib
-    from dnn_page_vectors_amd.utils.knobs import KNOBS
 
-    want = int(os.environ.get("PAGEVEC_IB", KNOBS["PAGEVEC_IB"][1]))
-    assert _lib().pv_ib_version() == (want if want in (3, 5, 7) else 7)
+    assert _lib().pv_ib_version() == 7
 
 
 @pytest.mark.parametrize("L", [45, 50, 20, 4])

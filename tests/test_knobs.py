@@ -28,10 +28,10 @@ def test_every_env_knob_is_registered():
 
 
 def test_in_effect_and_non_default(monkeypatch):
-    monkeypatch.setenv("PAGEVEC_IB_WIDE", "0")
+    monkeypatch.setenv("PAGEVEC_CONV_SHORT", "0")
     monkeypatch.setenv("PAGEVEC_SOMETHING_UNREGISTERED", "x")
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
     eff = knobs.in_effect()
-    assert eff["PAGEVEC_IB_WIDE"] == "0" and eff["PAGEVEC_SOMETHING_UNREGISTERED"] == "x"
+    assert eff["PAGEVEC_CONV_SHORT"] == "0" and eff["PAGEVEC_SOMETHING_UNREGISTERED"] == "x"
     assert eff["GPU_MAX_HW_QUEUES"] == "4 (unset)"
-    assert knobs.non_default().get("PAGEVEC_IB_WIDE") == "0"
+    assert knobs.non_default().get("PAGEVEC_CONV_SHORT") == "0"

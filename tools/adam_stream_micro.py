@@ -23,7 +23,7 @@ def main():
     from dnn_page_vectors_amd.ops._common import lib, P, stream
     L = lib()
     dev = torch.device("cuda")
-    arms = [(0, 4096), (1, 4096), (0, 16384), (1, 16384)]
+    arms = [4096, 16384]
     out = {}
     for n in [int(float(x)) for x in a.n.split(",")]:
         p, g, m, v = (torch.randn(n, device=dev) * 0.01 for _ in range(4))
@@ -32,8 +32,8 @@ def main():
         s = stream(dev)
         res = {arm: [] for arm in arms}
         for _ in range(a.rounds):
-            for nt, cap in arms:
-                L.pv_adam_set_nt(nt, cap)
+            for cap in arms:
+                L.pv_adam_set_grid(cap)
                 for _ in range(3):
                     L.pv_adam_dev(P(p), P(g), P(m), P(v), n, P(t), 1e-4, 0.9, 0.999, 1e-7, 0.0, 0, None, s)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,11 +42,11 @@ def main():
                     L.pv_adam_dev(P(p), P(g), P(m), P(v), n, P(t), 1e-4, 0.9, 0.999, 1e-7, 0.0, 0, None, s)
                 e1.record()
                 torch.cuda.synchronize()
-                res[(nt, cap)].append(e0.elapsed_time(e1) / a.iters * 1e3)
-        for (nt, cap), xs in res.items():
+                res[cap].append(e0.elapsed_time(e1) / a.iters * 1e3)
+        for cap, xs in res.items():
             us = statistics.median(xs)
-            out[f"n{n}_nt{nt}_cap{cap}"] = {"us": round(us, 1), "TBps": round(28 * n / us / 1e6, 2)}
-    L.pv_adam_set_nt(0, 16384)  # the defaults
+            out[f"n{n}_cap{cap}"] = {"us": round(us, 1), "TBps": round(28 * n / us / 1e6, 2)}
+    L.pv_adam_set_grid(16384)  # the default
     print(json.dumps(out))
 
 

@@ -16,7 +16,8 @@ from dnn_page_vectors_amd import _build as B  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--src", default="conv_pool_fwd.hip")
+    ap.add_argument("--src", nargs="+", default=["conv_pool_fwd.hip"],
+                    help="sources compiled with the define (e.g. every user of a common.h switch)")
     ap.add_argument("--define", nargs="+", required=True)
     a = ap.parse_args()
     B.build_hip()  # the release objects of every other source
@@ -31,10 +32,13 @@ def main():
     os.makedirs(vdir, exist_ok=True)
     for d in a.define:
         tag = d.replace("=", "_")
-        obj = os.path.join(vdir, f"{tag}.o")
-        src = os.path.join(kdir, a.src)
-        B._run([B.HIPCC] + list(B.HIP_FLAGS) + [f"-D{d}", "-I", kdir, "-c", src, "-o", obj], True)
-        objs = [obj if os.path.basename(s) == a.src else o for s, o in base]
+        vobj = {}
+        for sname in a.src:
+            obj = os.path.join(vdir, f"{tag}_{os.path.splitext(sname)[0]}.o")
+            B._run([B.HIPCC] + list(B.HIP_FLAGS) + [f"-D{d}", "-I", kdir, "-c", os.path.join(kdir, sname), "-o", obj],
+                   True)
+            vobj[sname] = obj
+        objs = [vobj.get(os.path.basename(s), o) for s, o in base]
         out = os.path.join(vdir, f"libpagevec_hip_{tag}.so")
         B._run([B.HIPCC, f"--offload-arch={B.ARCH}", "-fPIC", "-shared", "-o", out] + objs, True)
         print(out)

@@ -1,7 +1,7 @@
 """Same-process A/B of a trainer-level module flag on the headline step (interleaved rounds,
 CUDA-event timed), e.g. the query-tower-first forward order:
 
-    python tools/step_flag_ab.py --module dnn_page_vectors_amd.train.trainer --flag QUERY_FIRST
+    python tools/step_flag_ab.py --module dnn_page_vectors_amd.ops.conv_pool --flag DW_SIDE_STREAM
 """
 import argparse
 import importlib
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--module", default="dnn_page_vectors_amd.train.trainer")
-    ap.add_argument("--flag", default="QUERY_FIRST")
+    ap.add_argument("--flag", default="DW_SIDE_STREAM")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=15)
     ap.add_argument("--vals", default="0,1", help="the two values A/B'd (Python literals); 0/1 -> False/True")
