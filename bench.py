@@ -161,6 +161,60 @@ def _spawn_ranks(a) -> int:
     return launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], a.gpus, env=env)
 
 
+def _rank_stats(trainer, marks, local_dt, steps, dev, pdist):
+    """Per-rank step-time spread and exposed communication, gathered to every rank: the numbers
+    that tell stragglers, RCCL and compute apart when a multi-GPU run scales poorly.
+
+    step_ms: GPU time from a step's first to its last enqueued work (CUDA events; host clock on
+    the CPU); exposed_allreduce_ms: GPU time the step's stream spends after its backward waiting
+    for the bucketed gradient all-reduces to land (0 at one rank, None when not measured)."""
+    import statistics
+
+    ev = trainer.step_events
+    trainer.step_events = None
+    if ev:
+        step_ms = [e0.elapsed_time(e3) for e0, _, _, e3 in ev]
+        comm = [e1.elapsed_time(e2) for _, e1, e2, _ in ev if e1 is not None]
+    else:
+        step_ms = [1e3 * (b - a_) for a_, b in zip(marks[:-1], marks[1:])]
+        comm = []
+    med_comm = statistics.median(comm) if comm else -1.0
+    local = [statistics.median(step_ms), min(step_ms), max(step_ms), med_comm, 1e3 * local_dt / steps]
+    g = pdist.gather_floats(local, dev)  # (world, 5)
+    col = lambda j: [round(float(x), 3) for x in g[:, j]]  # noqa: E731
+    med = col(0)
+    out = {
+        "step_ms_median_per_rank": med,
+        "step_ms_min_per_rank": col(1),
+        "step_ms_max_per_rank": col(2),
+        "wall_ms_per_step_per_rank": col(4),
+        "step_ms_rank_spread": {"min": min(med), "median": round(statistics.median(med), 3), "max": max(med)},
+        "exposed_allreduce_ms_median_per_rank": None if float(g[:, 3].min()) < 0 else col(3),
+        "step_probe": "cuda events" if ev else "host clock",
+    }
+    return out
+
+
+def _lib_stamp(backend):
+    """Link stamp of the kernel library this run loaded (and whether it matches the sources)."""
+    if backend != "hip":
+        return None
+    from dnn_page_vectors_amd import _build
+
+    path = os.environ.get("PAGEVEC_HIP_LIB")
+    if path:
+        return {"path": path, "variant": True}
+    return {"stamp": _build.hip_stamp(), "matches_sources": not _build.hip_stale()}
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - informational
+        return None
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -245,17 +299,27 @@ def main():
     _sync(dev)
     pdist.barrier()
     _sync(dev)
+    # per-step probes: GPU events around every timed step and around the wait for the bucketed
+    # gradient all-reduces (the exposed communication of the step); host marks on the CPU
+    probe = dev.type == "cuda"
+    if probe:
+        trainer.step_events = []
+    marks = []
     t0 = time.perf_counter()
     for i in range(a.steps):
+        marks.append(time.perf_counter())
         m = step(a.warmup + i)
     _sync(dev)
+    marks.append(time.perf_counter())
     pdist.barrier()
     _sync(dev)
     dt = time.perf_counter() - t0
+    local_dt = dt
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     pdist.all_reduce_max_(t)
     dt = float(t[0])
     final_loss = float(m["loss"])
+    rank_stats = _rank_stats(trainer, marks, local_dt, a.steps, dev, pdist)
 
     # quality phase (untimed): continue on fresh batches so Recall@10 reflects a trained model
     done = a.warmup + a.steps
@@ -356,6 +420,11 @@ def main():
             "train_model_tflops": round(flops * train_mult / 1e12, 1) if train_mult else None,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else None,
             "hip_graph": graph_used,
+            "graph_status": trainer.graph_status,
+            "per_rank": rank_stats,
+            "ranks_seen": W,
+            "rccl_version": _rccl_version() if info.backend == "nccl" else None,
+            "native_lib_stamp": _lib_stamp(a.backend),
             "runtime_knobs": knobs.in_effect(),
         }
         if a.model in ("mlp", "chunked"):

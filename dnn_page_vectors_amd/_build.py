@@ -71,18 +71,47 @@ def _run(cmd: List[str], verbose: bool) -> None:
         print(r.stdout)
 
 
+def _objects(srcs: List[str], compiler: str, flags: List[str], incdir: str, tag: str) -> List[str]:
+    """Object paths of the sources: each keyed by a digest of its source, the shared headers and
+    the flags, so the list (and the link stamp over it) changes with any input."""
+    hdrs = _headers(incdir)
+    return [os.path.join(OBJ, f"{tag}_{os.path.splitext(os.path.basename(s))[0]}_{_digest([s] + hdrs, flags + [compiler])}.o")
+            for s in srcs]
+
+
+def _stamp_of(objs: List[str]) -> str:
+    return hashlib.sha1("\n".join(objs).encode()).hexdigest()
+
+
+def _hip_inputs(debug: bool):
+    srcs = _sources(os.path.join(CSRC, "kernels"), ".hip")
+    flags = list(HIP_FLAGS) + (["-DPAGEVEC_DEBUG=1"] if debug else [])
+    return srcs, flags, os.path.join(CSRC, "kernels"), "hipdbg" if debug else "hip"
+
+
+def hip_stale(debug: bool = False) -> bool:
+    """True when the kernel library is missing or was linked from other sources than the ones in
+    the tree (its link stamp differs from the stamp the current sources / headers / flags give)."""
+    out = HIP_DEBUG_LIB if debug else HIP_LIB
+    stamp = out + ".stamp"
+    if not (os.path.exists(out) and os.path.exists(stamp)):
+        return True
+    srcs, flags, incdir, tag = _hip_inputs(debug)
+    with open(stamp) as f:
+        return f.read().strip() != _stamp_of(_objects(srcs, HIPCC, flags, incdir, tag))
+
+
+def hip_stamp(debug: bool = False) -> str:
+    """The link stamp of the built kernel library ('' if none)."""
+    stamp = (HIP_DEBUG_LIB if debug else HIP_LIB) + ".stamp"
+    return open(stamp).read().strip() if os.path.exists(stamp) else ""
+
+
 def _compile_all(srcs: List[str], compiler: str, flags: List[str], incdir: str, tag: str,
                  jobs: int, verbose: bool) -> List[str]:
     os.makedirs(OBJ, exist_ok=True)
-    hdrs = _headers(incdir)
-    objs = []
-    todo = []
-    for s in srcs:
-        key = _digest([s] + hdrs, flags + [compiler])
-        o = os.path.join(OBJ, f"{tag}_{os.path.splitext(os.path.basename(s))[0]}_{key}.o")
-        objs.append(o)
-        if not os.path.exists(o):
-            todo.append((s, o))
+    objs = _objects(srcs, compiler, flags, incdir, tag)
+    todo = [(s, o) for s, o in zip(srcs, objs) if not os.path.exists(o)]
     def one(so):
         s, o = so
         tmp = o + ".tmp.o"
@@ -101,7 +130,7 @@ def _compile_all(srcs: List[str], compiler: str, flags: List[str], incdir: str, 
 
 def _link(objs: List[str], out: str, linker: List[str], verbose: bool) -> bool:
     stamp = out + ".stamp"
-    key = hashlib.sha1("\n".join(objs).encode()).hexdigest()
+    key = _stamp_of(objs)
     if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
         return False
     tmp = out + ".tmp"
@@ -124,11 +153,9 @@ def build_hip(verbose: bool = False, jobs: int = 4, debug: bool = False) -> str:
     PV_CHECK precondition flags (out-of-range ids / keys, LDS indices) compiled in."""
     if not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    srcs = _sources(os.path.join(CSRC, "kernels"), ".hip")
-    flags = list(HIP_FLAGS) + (["-DPAGEVEC_DEBUG=1"] if debug else [])
+    srcs, flags, incdir, tag = _hip_inputs(debug)
     out = HIP_DEBUG_LIB if debug else HIP_LIB
-    objs = _compile_all(srcs, HIPCC, flags, os.path.join(CSRC, "kernels"), "hipdbg" if debug else "hip", jobs,
-                        verbose)
+    objs = _compile_all(srcs, HIPCC, flags, incdir, tag, jobs, verbose)
     _link(objs, out, [HIPCC, f"--offload-arch={ARCH}", "-fPIC"], verbose)
     return out
 

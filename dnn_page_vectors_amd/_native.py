@@ -110,7 +110,10 @@ def hip_debug() -> ctypes.CDLL:
         if _hip_debug is None:
             import torch  # noqa: F401
 
-            if _autobuild():
+            if _build.hip_stale(debug=True):
+                if not _autobuild():
+                    raise NativeUnavailable(f"{_build.HIP_DEBUG_LIB} is missing or stale; run python -m "
+                                            "dnn_page_vectors_amd._build --debug")
                 _build.build_hip(debug=True)
             if not os.path.exists(_build.HIP_DEBUG_LIB):
                 raise NativeUnavailable(f"{_build.HIP_DEBUG_LIB} missing; run python -m dnn_page_vectors_amd._build "
@@ -153,7 +156,12 @@ def hip(required: bool = True) -> Optional[ctypes.CDLL]:
                 import torch  # noqa: F401  (single HIP runtime, see module docstring)
 
                 path = os.environ.get("PAGEVEC_HIP_LIB") or _build.HIP_LIB  # variant A/B builds (tools/)
-                if path == _build.HIP_LIB and _autobuild() and not os.path.exists(path):
+                if path == _build.HIP_LIB and _build.hip_stale():
+                    # missing, or linked from other sources than the tree's (the .so is git-ignored
+                    # but travels with the snapshot): rebuild, or refuse to run a stale binary
+                    if not _autobuild():
+                        raise NativeUnavailable(f"{path} is missing or stale (its link stamp does not match the "
+                                                "kernel sources); run python -m dnn_page_vectors_amd._build --hip")
                     _build.build_hip()
                 if not os.path.exists(path):
                     raise NativeUnavailable(f"{path} missing")

@@ -135,8 +135,11 @@ class Configuration:
     grad_bucket_mb: float = 32.0
     lr_warmup_steps: int = 0              # linear learning-rate warmup (0 = none; Keras had none)
     # graph mode on a data-parallel run captures the whole step INCLUDING its RCCL collectives
-    # (page / query gathers, bucketed gradient all-reduces) in the hipGraph; False = eager there
-    graph_distributed: bool = True
+    # (page / query gathers, bucketed gradient all-reduces) in the hipGraph.  Opt-in (round 6):
+    # it is verified on a world-1 RCCL group only (tests/test_rccl_gpu.py), no multi-rank run has
+    # replayed it yet; when on, the ranks agree on the capture outcome and all fall back to eager
+    # steps if any rank's capture failed (Trainer._capture_agreed)
+    graph_distributed: bool = False
     query_stream: bool = True             # query tower (fwd, hence bwd) on a side HIP stream
     deterministic: bool = False           # order-free (fixed-point) GPU reductions, one stream (ops/determinism.py)
     placement: str = "dp"                # dp (data parallel) | tower (slots over ranks, cnn_dssm_tf.py:139-158)

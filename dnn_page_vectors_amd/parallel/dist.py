@@ -155,3 +155,29 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if active():
         dist.broadcast(t, src)
     return t
+
+
+def all_agree(ok: bool, device=None) -> bool:
+    """True iff ``ok`` holds on EVERY rank (one MIN all-reduce; the local value on one rank).
+
+    Used where ranks must take the same branch, e.g. the hipGraph capture of a data-parallel
+    step: a rank whose capture failed would otherwise replay eagerly while its peers replay
+    captured collectives in a different order."""
+    if not active():
+        return bool(ok)
+    dev = device if device is not None else info().device
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()) == 1)
+
+
+def gather_floats(values, device=None):
+    """All ranks' equal-length float lists -> a (world, n) float64 CPU tensor (rank order);
+    the local values as a (1, n) tensor without a process group."""
+    dev = device if device is not None else info().device
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+    if not active():
+        return t.view(1, -1).cpu()
+    out = torch.empty(dist.get_world_size() * t.numel(), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return out.view(dist.get_world_size(), -1).cpu()

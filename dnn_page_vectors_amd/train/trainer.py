@@ -50,6 +50,14 @@ def _restore_det(prev) -> None:
     determinism.restore(prev)
 
 
+# The eager step on a HIGH-priority HIP stream: the query tower (its own stream, models/base.py)
+# and the side streams stay at normal priority, so when both towers' backward chains are queued
+# the dispatcher feeds the page tower's (the critical path: dense / loss backward -> dTable
+# reduce -> dW) first, and the query tower's fills the CUs that are left (round-6 timeline: the
+# page tower's small bias column sum waited 110 us behind the query tower's dTable reduce).
+STEP_PRIORITY = os.environ.get("PAGEVEC_STEP_PRIORITY", "1") != "0"
+
+
 class InjectedFault(RuntimeError):
     pass
 
@@ -154,7 +162,7 @@ class Trainer:
         # fixed-capacity row exchange too, not the exact one (sparse_rows_capacity 0 sizes
         # itself with a host sync); not tower placement
         self.graph_mode = (bool(graph) and self.device.type == "cuda"
-                           and (not self.info.enabled or (bool(getattr(cfg, "graph_distributed", True))
+                           and (not self.info.enabled or (bool(getattr(cfg, "graph_distributed", False))
                                                           and self.placement == "dp"))
                            and not self.deterministic
                            and (self.sparse is None or self.sparse.capacity != 0))
@@ -170,6 +178,10 @@ class Trainer:
         self._graph = None
         self._graph_key = None
         self._graph_warm = 0
+        self.graph_status = "off" if not self.graph_mode else "pending"
+        # optional per-step GPU probes (bench.py): list of (start, before_allreduce_wait,
+        # after_allreduce_wait, end) CUDA events per step; replays record (start, end) only
+        self.step_events: Optional[list] = None
 
     def close(self) -> None:
         """Restore the process-wide deterministic mode this trainer switched on (if any)."""
@@ -268,10 +280,61 @@ class Trainer:
             if self._graph is not None and key == self._graph_key:
                 return self._replay(q_ids, d_ids)
             if self._graph_warm >= self.GRAPH_WARMUP and self._graph is None:
-                self._capture(q_ids, d_ids, key)
-                return self._replay(q_ids, d_ids)
+                if self._capture_agreed(q_ids, d_ids, key):
+                    return self._replay(q_ids, d_ids)
+                return self._eager_step(q_ids, d_ids)
             self._graph_warm += 1
-        return self._eager_step(q_ids, d_ids)
+        return self._prio_step(q_ids, d_ids)
+
+    def _prio_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """The eager step, on this trainer's high-priority stream when STEP_PRIORITY (GPU, not
+        deterministic mode, not inside a capture); ordered after and before the caller's stream."""
+        if not (STEP_PRIORITY and self.device.type == "cuda" and not self.deterministic
+                and not torch.cuda.is_current_stream_capturing()):
+            return self._eager_step(q_ids, d_ids)
+        hp = getattr(self, "_hp_stream", None)
+        if hp is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            hp = self._hp_stream = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+        cur = torch.cuda.current_stream(self.device)
+        hp.wait_stream(cur)
+        for t in (q_ids, d_ids):
+            if t.is_cuda:
+                t.record_stream(hp)  # the caller may free its batch while the step still reads it
+        with torch.cuda.stream(hp):
+            out = self._eager_step(q_ids, d_ids)
+        cur.wait_stream(hp)
+        for t in out.values():
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(cur)
+        return out
+
+    def _capture_agreed(self, q_ids: torch.Tensor, d_ids: torch.Tensor, key) -> bool:
+        """Capture the step, then agree on the outcome across ranks (one MIN all-reduce, outside
+        any capture): if the capture failed on ANY rank, every rank drops its graph and stays
+        eager — a mixed job (some ranks replaying captured collectives, others issuing them
+        eagerly in a different order) would deadlock.  The outcome is logged on every rank and
+        kept in ``graph_status`` (reported by bench.py)."""
+        err = None
+        try:
+            self._capture(q_ids, d_ids, key)
+        except Exception as e:  # noqa: BLE001 - any capture failure falls back to eager
+            err = f"{type(e).__name__}: {e}"
+            self._graph = None
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+        ok = pdist.all_agree(err is None, self.device)
+        if ok:
+            self.graph_status = "captured" + (" (dp, RCCL collectives in the graph)" if self.info.enabled else "")
+            log.info("rank %d: training step captured in a hipGraph (world %d)", self.info.rank,
+                     self.info.world_size)
+            return True
+        self._graph, self._graph_key = None, None
+        self.graph_mode = False
+        self.graph_status = "eager (capture failed on " + ("this rank: " + err if err else "another rank") + ")"
+        log.warning("rank %d: hipGraph capture abandoned on every rank, eager steps from here: %s", self.info.rank,
+                    err or "failed on another rank")
+        return False
 
     # ------------------------------------------------------------------ hipGraph
     def _capture(self, q_ids: torch.Tensor, d_ids: torch.Tensor, key) -> None:
@@ -293,7 +356,13 @@ class Trainer:
         self.step, self.opt.step_count = step0, count0
         self._graph, self._graph_key = g, key
 
+    def _event(self) -> torch.cuda.Event:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
     def _replay(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        e0 = self._event() if self.step_events is not None else None
         self._gq.copy_(q_ids, non_blocking=True)
         self._gd.copy_(d_ids, non_blocking=True)
         seed = (self._base_seed() + self.info.rank * 104729) & 0x7FFFFFFF
@@ -304,6 +373,8 @@ class Trainer:
         d = (2 * seed) & 0xFFFFFFFF
         self._seed_dev.fill_(d - (1 << 32) if d >= (1 << 31) else d)
         self._graph.replay()
+        if e0 is not None:
+            self.step_events.append((e0, None, None, self._event()))
         if self.graph_fence:
             torch.cuda.synchronize(self.device)
         self.opt.step_count += 1
@@ -315,6 +386,8 @@ class Trainer:
     def _eager_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor, seed_override: Optional[int] = None,
                     timing: bool = True) -> Dict[str, torch.Tensor]:
         self.model.train()
+        probe = self.step_events is not None and timing and self.device.type == "cuda"
+        ev0 = self._event() if probe else None
         le = self.cfg.log_every
         timer = PhaseTimer(self.device) if (timing and self.metrics and self.metrics.enabled and le and
                                             (self.step + 1) % le == 0) else None
@@ -355,8 +428,10 @@ class Trainer:
         if timer:
             timer.mark()
         range_push("allreduce")
+        ev1 = self._event() if probe else None
         if self.buckets is not None:
             self.buckets.finish()
+        ev2 = self._event() if probe else None
         range_pop()
         if timer:
             timer.mark()
@@ -374,6 +449,8 @@ class Trainer:
         if timer:
             timer.mark()
             self._timer = timer
+        if probe:
+            self.step_events.append((ev0, ev1, ev2, self._event()))
         self.step += 1
         acc = self._acc if self._acc is not None else (P > 0.5).float().mean()
         return {"loss": loss.detach(), "acc": acc, "grad_sumsq": stats[0],

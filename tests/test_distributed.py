@@ -384,3 +384,48 @@ def test_unique_rows_fixed_size():
     torch.testing.assert_close(got, want[:10])
     assert int(ov) == want.numel() - 10
     assert unique_rows(ids[:0], 50, 4).tolist() == [-1] * 4
+
+
+def _agree_worker(rank, world, port, q):
+    """Capture agreement (Trainer._capture_agreed): rank 1's capture fails, every rank must fall
+    back to eager steps together; pdist.all_agree itself for all-true / one-false inputs."""
+    _env(rank, world, port)
+    from dnn_page_vectors_amd.config import preset_config
+    from dnn_page_vectors_amd.models import build_model
+    from dnn_page_vectors_amd.parallel import dist as pdist
+    from dnn_page_vectors_amd.train.trainer import Trainer
+
+    pdist.init_distributed(device="cpu")
+    res = {"all_true": pdist.all_agree(True), "one_false": pdist.all_agree(rank != world - 1)}
+    cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=4, query_length=8, document_length=16,
+                                                    vocab_hash_size=200)
+    tr = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), torch.device("cpu"))
+    tr.graph_mode = True  # as on a GPU run with graph_distributed=True
+
+    def fake_capture(q_, d_, key):
+        if rank == 1:
+            raise RuntimeError("capture failed (injected)")
+        tr._graph = object()  # rank 0 'captured' its graph
+
+    tr._capture = fake_capture
+    ok = tr._capture_agreed(None, None, ("k",))
+    res.update(ok=ok, graph_mode=tr.graph_mode, graph=tr._graph is not None, status=tr.graph_status)
+    q.put((rank, res))
+    pdist.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_capture_outcome_agreed_across_ranks(world):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    res = dict(q.get(timeout=180) for _ in ps)
+    [p.join(timeout=60) for p in ps]
+    for r in range(world):
+        x = res[r]
+        assert x["all_true"] is True and x["one_false"] is False
+        assert x["ok"] is False and x["graph_mode"] is False and x["graph"] is False, (r, x)
+        assert x["status"].startswith("eager (capture failed on"), x["status"]
+    assert "injected" in res[1]["status"] and "another rank" in res[0]["status"]

@@ -4,6 +4,8 @@ import subprocess
 import sys
 import textwrap
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -40,23 +42,32 @@ def test_launch_propagates_failure(tmp_path):
     assert r.returncode == 7
 
 
-def test_bench_spawns_ranks_for_gpus_n():
-    """`python bench.py --gpus 2` without torchrun: the bench itself spawns 2 rank processes
-    (the driver's multi-GPU invocation); CPU dry run over gloo — one JSON line, n_gpus 2."""
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_bench_spawns_ranks_for_gpus_n(W):
+    """`python bench.py --gpus W` without torchrun: the bench itself spawns W rank processes
+    (the driver's multi-GPU invocation); CPU dry run over gloo — one JSON line, n_gpus W, and
+    the per-rank step-time spread the scaling run is read with."""
     import json
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["OMP_NUM_THREADS"] = "1"
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
-                        "--warmup", "1"], env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(W), "--dry-run", "--steps", "2",
+                        "--warmup", "1"], env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["n_gpus"] == W and out["config"]["parallelism"] == f"dp{W}"
     assert out["config"]["dist_backend"] == "gloo" and out["config"]["launch"] == "bench-spawn"
     assert out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
-    assert out["recall_candidates"] == 2 * 64 and out["dry_run"] is True
+    assert out["recall_candidates"] == W * 64 and out["dry_run"] is True
+    pr = out["per_rank"]
+    for k in ("step_ms_median_per_rank", "step_ms_min_per_rank", "step_ms_max_per_rank", "wall_ms_per_step_per_rank"):
+        assert len(pr[k]) == W and all(v > 0 for v in pr[k]), (k, pr[k])
+    sp = pr["step_ms_rank_spread"]
+    assert sp["min"] <= sp["median"] <= sp["max"]
+    assert pr["step_probe"] == "host clock" and pr["exposed_allreduce_ms_median_per_rank"] is None
+    assert out["ranks_seen"] == W and out["graph_status"] == "off" and out["rccl_version"] is None
     # the driver's JSON contract
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):

@@ -43,3 +43,13 @@ def test_debug_kernel_library_builds_with_checks():
         assert f"pv_debug_{unit}".encode() in blob
     with open(_build.HIP_LIB, "rb") as f:
         assert b"pv_debug_convfwd" not in f.read()  # compiled out of the release library
+
+
+def test_stale_library_detected(monkeypatch):
+    """_native.hip() rebuilds (or, with PAGEVEC_NO_AUTOBUILD=1, refuses) a kernel library whose
+    link stamp does not match the tree's sources / headers / flags: any change of an input
+    changes the expected stamp."""
+    _build.build_hip()
+    assert not _build.hip_stale() and _build.hip_stamp()
+    monkeypatch.setattr(_build, "HIP_FLAGS", list(_build.HIP_FLAGS) + ["-DPV_STAMP_PROBE=1"])
+    assert _build.hip_stale()

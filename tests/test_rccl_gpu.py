@@ -161,7 +161,7 @@ def _graph_worker(port, models, steps, out):
         dev = info.device
         res = {}
         for model in models:
-            cfg = _cfg(model)
+            cfg = _cfg(model).replace(graph_distributed=True)  # opt-in: capture the collectives too
             data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=1024), dev, seed=3)
             batches = [data.batch(cfg.batch_size) for _ in range(steps)]
             runs = {}
