@@ -1160,6 +1160,164 @@ __global__ __launch_bounds__(256) void ib_grad_scale_kernel(const float* __restr
   }
 }
 
+// ---- fused glue of the in-batch loss (round 6) ------------------------------------------------
+// Forward finish, one wave per query row, after the fused ib7 forward + dQ-part pass:
+//   the positive logit (ib_pos's forward half: raw cosine s -> sraw, g*clip(s)), the split
+//   partial sums -> sumexp -> loss = g + log(sumexp) - g*clip(s) and P+ (ib_rowsum), the split
+//   partials of U -> U (ib_split_reduce), and the batch mean loss / accuracy (loss_stats): each
+//   workgroup stores its partial sums, and the workgroup that takes the last ticket of an
+//   agent-scope counter sums the partials in workgroup order (deterministic) and re-arms the
+//   counter for the next launch (capturable: no memset node).  Four launches -> one.
+__global__ __launch_bounds__(256) void ib_fin_fwd_kernel(const unsigned short* __restrict__ X,
+                                                         const unsigned short* __restrict__ Y,
+                                                         const int* __restrict__ pos,
+                                                         const float* __restrict__ part, int ns,
+                                                         const float* __restrict__ ws_u, float* __restrict__ U,
+                                                         int nx, int DP, float gamma, int clip,
+                                                         float* __restrict__ sumexp, float* __restrict__ loss,
+                                                         float* __restrict__ prob, float* __restrict__ sraw,
+                                                         float* __restrict__ bpart, unsigned* __restrict__ ticket,
+                                                         float* __restrict__ out_loss, float* __restrict__ out_acc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  __shared__ float sl[4], sa[4];
+  __shared__ int last;
+  float lrow = 0.f, arow = 0.f;
+  if (row < nx) {
+    const int p = pos[row];
+    float d = 0.f;
+    for (int f = lane; f < DP; f += 64) d += bf16_to_f32(X[(size_t)row * DP + f]) * bf16_to_f32(Y[(size_t)p * DP + f]);
+    d = wave_sum(d);
+    float a = lane < ns ? part[(size_t)lane * nx + row] : 0.f;  // ns <= 64 (ib3_splits)
+    a = wave_sum(a);
+    const float spos = gamma * (clip ? fminf(fmaxf(d, 0.f), 1.f) : d);
+    const float l = gamma + __logf(a) - spos;
+    const float pr = __expf(-l);
+    if (lane == 0) {
+      sumexp[row] = a;
+      loss[row] = l;
+      prob[row] = pr;
+      sraw[row] = d;
+    }
+    lrow = l;
+    arow = pr > 0.5f ? 1.f : 0.f;
+    if (ws_u && ns > 1) {
+      const size_t plane = (size_t)nx * DP;
+      for (int c = lane; c < DP / 4; c += 64) {
+        const size_t o = (size_t)row * DP + 4 * c;
+        f32x4 u = *reinterpret_cast<const f32x4*>(ws_u + o);
+        for (int sp = 1; sp < ns; ++sp) u += *reinterpret_cast<const f32x4*>(ws_u + sp * plane + o);
+        *reinterpret_cast<f32x4*>(U + o) = u;
+      }
+    }
+  }
+  if (!ticket) return;
+  if (lane == 0) {
+    sl[w] = lrow;
+    sa[w] = arow;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<f32x2*>(bpart + 2 * blockIdx.x) = f32x2{(sl[0] + sl[1]) + (sl[2] + sl[3]),
+                                                              (sa[0] + sa[1]) + (sa[2] + sa[3])};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = atomicAdd(ticket, 1u);
+    const int is_last = t == gridDim.x - 1;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last = is_last;
+  }
+  __syncthreads();
+  if (!last) return;
+  // the last workgroup: every partial, summed in workgroup order by thread i (stride 256), then
+  // the 256 per-thread sums in thread order
+  float s = 0.f, a = 0.f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
+    const f32x2 v = *reinterpret_cast<const f32x2*>(bpart + 2 * b);
+    s += v[0];
+    a += v[1];
+  }
+  __shared__ float ts[256], ta[256];
+  ts[threadIdx.x] = s;
+  ta[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float S = 0.f, A = 0.f;
+    for (int i = 0; i < 256; ++i) {
+      S += ts[i];
+      A += ta[i];
+    }
+    const float inv = 1.f / (float)nx;
+    *out_loss = S * inv;
+    if (out_acc) *out_acc = A * inv;
+    *ticket = 0u;  // re-armed for the next launch
+  }
+}
+
+// dD finish, thread = (page row, 4 columns): the split partials of the dD pass (ib_split_reduce;
+// ns = 1: in place) plus the positive pair's one-hot term for the rows that are some query's
+// positive (ib_pos's backward half on the page side): dD_m += h_b X_b with b = inv[m],
+// h_b = -grow_b * gamma where clip(s_b) passes its gradient.
+__global__ __launch_bounds__(256) void ib_fin_dd_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                        int nrows, int DP, int ns, const int* __restrict__ inv,
+                                                        const unsigned short* __restrict__ Q,
+                                                        const float* __restrict__ grow, const float* __restrict__ sraw,
+                                                        float gamma, int clip) {
+  const int per = DP / 4;
+  const long n4 = (long)nrows * per;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 a = reinterpret_cast<const f32x4*>(ws)[i];
+    for (int sp = 1; sp < ns; ++sp) a += reinterpret_cast<const f32x4*>(ws)[(size_t)sp * n4 + i];
+    const int m = (int)(i / per), c = 4 * (int)(i - (long)m * per);
+    const int b = inv[m];
+    if (b >= 0) {
+      const float sb = sraw[b];
+      if (!clip || (sb >= 0.f && sb <= 1.f)) {
+        const float h = -grow[b] * gamma;
+        const unsigned short* q = Q + (size_t)b * DP + c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += h * bf16_to_f32(q[k]);
+      }
+    }
+    reinterpret_cast<f32x4*>(out)[i] = a;
+  }
+}
+
+// Backward prologue with the query side of the positive pair folded in: ib_grad_scale's scale /
+// per-row gradient / dQ = scale * U, plus dQ_i += h_i * Y_pos(i) (h_i as in ib_fin_dd_kernel).
+__global__ __launch_bounds__(256) void ib_grad_scale_pos_kernel(const float* __restrict__ gl, int scalar, float invB,
+                                                                const float* __restrict__ sumexp, int B, float gamma,
+                                                                const float* __restrict__ U, int DP,
+                                                                float* __restrict__ dq, float* __restrict__ scale,
+                                                                float* __restrict__ grow,
+                                                                const unsigned short* __restrict__ Y,
+                                                                const int* __restrict__ pos,
+                                                                const float* __restrict__ sraw, int clip) {
+  const int per = DP / 4;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)B * per) return;
+  const int i = (int)(t / per), c4 = (int)(t - (long)i * per);
+  const float g = scalar ? gl[0] * invB : gl[i];
+  const float sc = g * gamma / sumexp[i];
+  if (c4 == 0) {
+    scale[i] = sc;
+    grow[i] = g;
+  }
+  f32x4 u = *reinterpret_cast<const f32x4*>(U + (size_t)i * DP + 4 * c4) * sc;
+  const float sb = sraw[i];
+  if (!clip || (sb >= 0.f && sb <= 1.f)) {
+    const float h = -g * gamma;
+    const unsigned short* y = Y + (size_t)pos[i] * DP + 4 * c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] += h * bf16_to_f32(y[k]);
+  }
+  *reinterpret_cast<f32x4*>(dq + (size_t)i * DP + 4 * c4) = u;
+}
+
 PV_DEBUG_EXPORT(loss)
 }  // namespace loss
 }  // namespace pv
@@ -1486,3 +1644,99 @@ PV_API int pv_ibw(const void* O, int no, const void* It, int ni, int DP, const f
   }
   return 0;
 }
+
+// ---- fused in-batch loss glue (round 6): see ib_fin_fwd_kernel / ib_fin_dd_kernel ----------
+// Forward: the ib7 (or ib5 / ib3) forward + dQ-part pass, then ONE finish launch.  pos (nx)
+// positive page per query; sraw (nx) receives the raw positive cosines the backward needs;
+// bpart: 2 * ceil(nx / 4) floats; ticket: one zero-initialised u32 per concurrent use (re-armed
+// by the kernel); out_loss / out_acc: 0-dim outputs (null ticket: no batch statistics).
+PV_API int pv_ib_fwd_dq2(const void* X, const void* Y, const int* pos, float* sumexp, float* U, float* ws_u,
+                         float* part, int nx, int ny, int DP, float gamma, int clip, float* sraw, float* loss,
+                         float* prob, float* bpart, unsigned* ticket, float* out_loss, float* out_acc, void* stream) {
+  using namespace pv::loss;
+  if (DP % 32 || DP > 192 || nx < 1) return -2;
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
+  if ((ns > 1 && !ws_u) || ns > 64) return -3;
+  hipStream_t s = (hipStream_t)stream;
+  const int nrb = (nx + 255) / 256;
+  const dim3 grid3(nrb * ns);
+#define PV_IB_FWDDQ2(CLIPV)                                                                                     \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib7_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 7 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib7_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 5 && DP == 160) {                                                                  \
+    hipLaunchKernelGGL((ib5_kernel<5, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else if (ib_version() == 5 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib5_kernel<4, true, CLIPV, true>), grid3, dim3(512), 0, s, (const unsigned short*)X,    \
+                       (const unsigned short*)Y, nullptr, U, ws_u, nx, ny, per, nrb, gamma, part);              \
+  } else {                                                                                                      \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, true, CLIPV, true>), grid3, dim3(512), 0, s,        \
+                                            (const unsigned short*)X, (const unsigned short*)Y, nullptr, U,     \
+                                            ws_u, nx, ny, per, nrb, gamma, part));                              \
+  }
+  if (clip) { PV_IB_FWDDQ2(true); } else { PV_IB_FWDDQ2(false); }
+#undef PV_IB_FWDDQ2
+  PV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ib_fin_fwd_kernel, dim3((nx + 3) / 4), dim3(256), 0, s, (const unsigned short*)X,
+                     (const unsigned short*)Y, pos, part, ns, ns > 1 ? ws_u : nullptr, U, nx, DP, gamma, clip, sumexp,
+                     loss, prob, sraw, bpart, ticket, out_loss, out_acc);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward prologue (dQ = scale * U + the positive pair's query term), see ib_grad_scale_pos_kernel.
+PV_API int pv_ib_grad_scale_pos(const float* gl, int scalar, float invB, const float* sumexp, int B, float gamma,
+                                const float* U, int DP, float* dq, float* scale, float* grow, const void* Y,
+                                const int* pos, const float* sraw, int clip, void* stream) {
+  if (B < 1 || DP % 4 || !U || !dq) return -1;
+  const long n = (long)B * (DP / 4);
+  hipLaunchKernelGGL(pv::loss::ib_grad_scale_pos_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, gl, scalar, invB, sumexp, B, gamma, U, DP, dq, scale, grow,
+                     (const unsigned short*)Y, pos, sraw, clip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// dD pass (X = pages, Y = queries, scale indexed by the query) + ONE finish launch that sums the
+// split partials and adds the positive pair's page term: inv (nx) = the query whose positive
+// page row m is (-1: none).
+PV_API int pv_ib_bwd_dd_pos(const void* X, const void* Y, const float* scale, float* out, float* ws, int nx, int ny,
+                            int DP, float gamma, int clip, const int* inv, const float* grow, const float* sraw,
+                            void* stream) {
+  using namespace pv::loss;
+  if (DP % 32 || DP > 192) return -2;
+  int ns, per;
+  ib_split_plan(nx, ny, ns, per);
+  if (ns > 1 && !ws) return -3;
+  hipStream_t s = (hipStream_t)stream;
+  const int nrb = (nx + 255) / 256;
+  const dim3 grid3(nrb * ns);
+#define PV_IB_DD(CLIPV)                                                                                         \
+  if (ib_version() == 7 && DP == 160) {                                                                         \
+    hipLaunchKernelGGL((ib7_kernel<5, false, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,         \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else if (ib_version() == 7 && DP == 128) {                                                                  \
+    hipLaunchKernelGGL((ib7_kernel<4, false, CLIPV>), grid3, dim3(512), 0, s, (const unsigned short*)X,         \
+                       (const unsigned short*)Y, scale, out, ws, nx, ny, per, nrb, gamma);                      \
+  } else {                                                                                                      \
+    IB_DISPATCH(DP / 32, hipLaunchKernelGGL((ib3_kernel<KS, false, CLIPV>), grid3, dim3(512), 0, s,             \
+                                            (const unsigned short*)X, (const unsigned short*)Y, scale, out, ws, \
+                                            nx, ny, per, nrb, gamma));                                          \
+  }
+  if (clip) { PV_IB_DD(true); } else { PV_IB_DD(false); }
+#undef PV_IB_DD
+  PV_LAUNCH_CHECK();
+  const long n4 = (long)nx * DP / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(ib_fin_dd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ns > 1 ? ws : out, out, nx, DP,
+                     ns > 1 ? ns : 1, inv, (const unsigned short*)Y, grow, sraw, gamma, clip);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+

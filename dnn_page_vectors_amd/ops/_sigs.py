@@ -77,6 +77,9 @@ SIGS = {
     "pv_ib_rows_blk": "p" "iii" "pp" "fi" "p",
     "pv_ib_rowsum": "pp" "ii" "ppp" "f" "p",
     "pv_ib_version": "",
+    "pv_ib_fwd_dq2": "ppppppp" "iii" "f" "i" "ppppppp" "p",
+    "pv_ib_grad_scale_pos": "pifpifpipppppp" "ip",
+    "pv_ib_bwd_dd_pos": "ppppp" "iii" "f" "i" "ppp" "p",
     "pv_ib_set_version": "i",
     # embedding.hip
     "pv_trigram_hash": "ppp" "iiii" "p",

@@ -140,7 +140,43 @@ def _grad_prologue(gl: torch.Tensor, reduce: bool, B: int, gamma: float, sumexp:
     return scale, grow, dq
 
 
+FUSED_GLUE = True  # tests: False runs the round-5 glue launches (the fused path's oracle)
+_TICKETS = {}  # device -> u32 counter of the fused forward finish's last-workgroup reduction
+
+
+def _ticket(dev: torch.device) -> torch.Tensor:
+    t = _TICKETS.get(dev)
+    if t is None:
+        t = _TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
+def _pos_inverse(pos: torch.Tensor, M: int) -> Optional[torch.Tensor]:
+    """inv (M,) int32: the query whose positive page row m is, -1 for none; None when two queries
+    share a positive (the fused dD finish needs a one-to-one map).  Cached on the pos tensor (the
+    trainer keeps one per shape); built eagerly, never inside a capture."""
+    key = (M, pos.data_ptr(), pos.numel())
+    hit = getattr(pos, "_pv_inv", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    p = pos.long()
+    inv = None
+    if p.numel() == 0 or (int(p.min()) >= 0 and int(p.max()) < M and torch.unique(p).numel() == p.numel()):
+        inv = torch.full((M,), -1, dtype=torch.int32, device=pos.device)
+        inv[p] = torch.arange(p.numel(), dtype=torch.int32, device=pos.device)
+    pos._pv_inv = (key, inv)
+    return inv
+
+
 class _InBatchFn(torch.autograd.Function):
+    """Flash in-batch softmax loss.  Training (query gradient wanted): the fused ib7 forward + dQ
+    part, ONE finish launch (positive logit, loss / P+, U, batch mean loss / accuracy), then in
+    the backward the prologue with the query side of the positive pair folded in, the dD pass and
+    ONE finish launch (split sum + the page side of the positive pair) — five glue launches of
+    round 5 (ib_pos x 2, ib_rowsum, ib_split_reduce x 2 ... loss_stats) fold into the three."""
+
     @staticmethod
     def forward(ctx, qn, dn, pos, gamma, clip, reduce=False):
         B, D = qn.shape
@@ -151,14 +187,39 @@ class _InBatchFn(torch.autograd.Function):
         qb = _pad_bf16(qn, DP)
         db = _pad_bf16(dn, DP)
         pos = pos.to(torch.int32).contiguous()
-        loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
-        ctx.save_for_backward(qb, db, pos, sumexp, U)
-        ctx.meta = (B, M, D, DP, float(gamma), int(clip))
+        inv = _pos_inverse(pos, M) if ctx.needs_input_grad[0] and FUSED_GLUE else None
         ctx.reduce = bool(reduce)
+        ctx.meta = (B, M, D, DP, float(gamma), int(clip))
+        if inv is not None:
+            dev = qb.device
+            L_ = lib()
+            sumexp = torch.empty(B, dtype=torch.float32, device=dev)
+            loss = torch.empty(B, dtype=torch.float32, device=dev)
+            prob = torch.empty(B, dtype=torch.float32, device=dev)
+            sraw = torch.empty(B, dtype=torch.float32, device=dev)
+            U = torch.empty(B, DP, dtype=torch.float32, device=dev)
+            ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), 1), dtype=torch.float32, device=dev)
+            part = torch.empty(L_.pv_ib_fwd_dq_parts(B, M), dtype=torch.float32, device=dev)
+            lm = acc = bpart = tk = None
+            if reduce:
+                lm = torch.empty((), dtype=torch.float32, device=dev)
+                acc = torch.empty((), dtype=torch.float32, device=dev)
+                bpart = torch.empty(2 * ((B + 3) // 4), dtype=torch.float32, device=dev)
+                tk = _ticket(dev)
+            check(L_.pv_ib_fwd_dq2(P(qb), P(db), P(pos), P(sumexp), P(U), P(ws), P(part), B, M, DP, float(gamma),
+                                   int(clip), P(sraw), P(loss), P(prob), P(bpart), P(tk), P(lm), P(acc),
+                                   stream(dev)), "pv_ib_fwd_dq2")
+            ctx.save_for_backward(qb, db, pos, sumexp, U, sraw, inv)
+            ctx.fused = True
+        else:
+            loss, prob, sumexp, U = _ib_forward(qb, db, pos, B, M, DP, gamma, clip, ctx.needs_input_grad[0])
+            ctx.save_for_backward(qb, db, pos, sumexp, U)
+            ctx.fused = False
+            if reduce:
+                lm, acc = _loss_stats(loss, prob)
         ctx.mark_non_differentiable(prob)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for prob / acc
         if reduce:
-            lm, acc = _loss_stats(loss, prob)
             ctx.mark_non_differentiable(acc)
             return lm, prob, acc
         return loss, prob
@@ -167,8 +228,24 @@ class _InBatchFn(torch.autograd.Function):
     def backward(ctx, gl, _gp, _ga=None):
         if gl is None:  # materialize_grads is off: the loss output was not used
             return (None,) * len(ctx.needs_input_grad)
-        qb, db, pos, sumexp, U = ctx.saved_tensors
         B, M, D, DP, gamma, clip = ctx.meta
+        if ctx.fused:
+            qb, db, pos, sumexp, U, sraw, inv = ctx.saved_tensors
+            dev = qb.device
+            L_ = lib()
+            s = stream(dev)
+            g_in = gl.contiguous().float()
+            scale = torch.empty(B, dtype=torch.float32, device=dev)
+            grow = torch.empty(B, dtype=torch.float32, device=dev)
+            dq = torch.empty(B, DP, dtype=torch.float32, device=dev)
+            check(L_.pv_ib_grad_scale_pos(P(g_in), int(ctx.reduce), 1.0 / B, P(sumexp), B, gamma, P(U), DP, P(dq),
+                                          P(scale), P(grow), P(db), P(pos), P(sraw), clip, s), "pv_ib_grad_scale_pos")
+            dd = torch.empty(M, DP, dtype=torch.float32, device=dev)
+            ws = torch.empty(max(L_.pv_ib_bwd_ws(M, B, DP), 1), dtype=torch.float32, device=dev)
+            check(L_.pv_ib_bwd_dd_pos(P(db), P(qb), P(scale), P(dd), P(ws), M, B, DP, gamma, clip, P(inv), P(grow),
+                                      P(sraw), s), "pv_ib_bwd_dd_pos")
+            return dq[:, :D], dd[:, :D], None, None, None, None
+        qb, db, pos, sumexp, U = ctx.saved_tensors
         s = stream(qb.device)
         L_ = lib()
         scale, g, dq = _grad_prologue(gl, ctx.reduce, B, gamma, sumexp, U, DP)

@@ -2011,3 +2011,37 @@ def test_conv_short_chunk_bit_identical(L, p, mode):
     assert torch.equal(outs[0][1], outs[1][1])
     for a, c in zip(outs[0][2:], outs[1][2:]):
         torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,M,clip,D", [(4096, 16384, True, 150), (700, 5000, False, 128), (300, 1200, True, 150)])
+def test_inbatch_fused_glue_matches_unfused(B, M, clip, D, monkeypatch):
+    """ops/loss.py FUSED_GLUE: the one-launch forward finish (positive logit, loss / P+, U split
+    sum, batch mean loss + accuracy by a last-workgroup ticket) and the backward with the
+    positive pair folded into the prologue and the dD split sum equal the round-5 launches
+    (ib_pos x 2, ib_rowsum, ib_split_reduce x 2, loss_stats, ib_grad_scale) to fp32 rounding;
+    a second call re-uses the re-armed ticket."""
+    torch.manual_seed(21)
+    q = torch.randn(B, D, device=DEV)
+    dd = torch.randn(M, D, device=DEV)
+    dd[::4][:B] = q + 2.0 * dd[::4][:B]
+    if clip:
+        q, dd = q.abs(), dd.abs()
+    qn0 = bf(ref.l2_normalize(q))
+    dn0 = bf(ref.l2_normalize(dd))
+    pos = torch.arange(B, device=DEV, dtype=torch.int32) * 4
+    res = {}
+    for fused in (False, True, True):
+        monkeypatch.setattr(lops, "FUSED_GLUE", fused)
+        qn = qn0.clone().requires_grad_(True)
+        dn = dn0.clone().requires_grad_(True)
+        lm, P, acc = lops.inbatch_loss(qn, dn, pos, 10.0, clip, reduce=True)
+        lm.backward()
+        torch.cuda.synchronize()
+        res.setdefault(fused, []).append((float(lm), float(acc), P.detach(), qn.grad, dn.grad))
+    base = res[False][0]
+    for got in res[True]:
+        assert abs(got[0] - base[0]) <= 1e-5 * abs(base[0]) and got[1] == base[1]
+        torch.testing.assert_close(got[2], base[2], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(got[3], base[3], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(got[4], base[4], rtol=1e-4, atol=1e-6)
+    assert res[True][0][0] == res[True][1][0]  # deterministic finish, ticket re-armed
