@@ -294,6 +294,10 @@ def main():
         q, d = pool[i % len(pool)]
         return trainer.train_step(q, d)
 
+    # the whole loop on the trainer's high-priority stream (Trainer.stream_context): the query
+    # tower and side streams keep normal priority, and consecutive steps need no stream hand-off
+    sctx = trainer.stream_context()
+    sctx.__enter__()
     for i in range(a.warmup):
         m = step(i)
     _sync(dev)
@@ -329,6 +333,8 @@ def main():
         if info.rank == 0 and (i + 1) % 100 == 0:
             print(f"quality step {done + i + 1}: loss {float(m['loss']):.4f}", file=sys.stderr, flush=True)
     quality_loss = float(m["loss"])
+    _sync(dev)
+    sctx.__exit__(None, None, None)
 
     recall = recall_local = None
     if a.recall > 0:

@@ -80,7 +80,9 @@ def _objects(srcs: List[str], compiler: str, flags: List[str], incdir: str, tag:
 
 
 def _stamp_of(objs: List[str]) -> str:
-    return hashlib.sha1("\n".join(objs).encode()).hexdigest()
+    # object BASENAMES (each carries its source digest): the stamp is the same wherever the tree
+    # lives (the GPU box unpacks the snapshot under another absolute path)
+    return hashlib.sha1("\n".join(os.path.basename(o) for o in objs).encode()).hexdigest()
 
 
 def _hip_inputs(debug: bool):
@@ -148,7 +150,30 @@ def build_runtime(verbose: bool = False, jobs: int = 4) -> str:
     return RT_LIB
 
 
+class _BuildLock:
+    """Inter-process lock around a build (ranks of one job may find the library stale together)."""
+
+    def __enter__(self):
+        import fcntl
+
+        os.makedirs(LIB, exist_ok=True)
+        self.f = open(os.path.join(LIB, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
 def build_hip(verbose: bool = False, jobs: int = 4, debug: bool = False) -> str:
+    with _BuildLock():
+        return _build_hip(verbose, jobs, debug)
+
+
+def _build_hip(verbose: bool = False, jobs: int = 4, debug: bool = False) -> str:
     """Release kernels -> libpagevec_hip.so; debug=True -> libpagevec_hip_debug.so with the
     PV_CHECK precondition flags (out-of-range ids / keys, LDS indices) compiled in."""
     if not os.path.exists(HIPCC):

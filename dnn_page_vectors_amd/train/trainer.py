@@ -286,17 +286,36 @@ class Trainer:
             self._graph_warm += 1
         return self._prio_step(q_ids, d_ids)
 
-    def _prio_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """The eager step, on this trainer's high-priority stream when STEP_PRIORITY (GPU, not
-        deterministic mode, not inside a capture); ordered after and before the caller's stream."""
-        if not (STEP_PRIORITY and self.device.type == "cuda" and not self.deterministic
-                and not torch.cuda.is_current_stream_capturing()):
-            return self._eager_step(q_ids, d_ids)
+    def priority_stream(self) -> Optional[torch.cuda.Stream]:
+        """This trainer's high-priority stream (None when STEP_PRIORITY is off, on the CPU or in
+        deterministic mode)."""
+        if not (STEP_PRIORITY and self.device.type == "cuda" and not self.deterministic):
+            return None
         hp = getattr(self, "_hp_stream", None)
         if hp is None:
             lo, hi = torch.cuda.Stream.priority_range()
             hp = self._hp_stream = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+        return hp
+
+    def stream_context(self):
+        """``with trainer.stream_context(): <training loop>`` — the loop's own work (batches,
+        metrics) on the high-priority stream too, so consecutive steps need no cross-stream
+        hand-off (each hand-off is a queue-to-queue dependency: ~0.2 ms of idle GPU per step
+        when the step ran on its own stream and the caller's on the default one)."""
+        import contextlib
+
+        hp = self.priority_stream()
+        return torch.cuda.stream(hp) if hp is not None else contextlib.nullcontext()
+
+    def _prio_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """The eager step, on this trainer's high-priority stream when STEP_PRIORITY (GPU, not
+        deterministic mode, not inside a capture); ordered after and before the caller's stream."""
+        hp = self.priority_stream()
+        if hp is None or torch.cuda.is_current_stream_capturing():
+            return self._eager_step(q_ids, d_ids)
         cur = torch.cuda.current_stream(self.device)
+        if cur == hp:  # the caller already runs on it (stream_context)
+            return self._eager_step(q_ids, d_ids)
         hp.wait_stream(cur)
         for t in (q_ids, d_ids):
             if t.is_cuda:
@@ -525,6 +544,16 @@ class Trainer:
             if hasattr(cb, "on_train_begin"):
                 cb.on_train_begin(self)
         start_epoch = self.epoch
+        with self.stream_context():
+            self._fit_epochs(train_batches, nb_epoch, steps_per_epoch, validation_batches, validation_steps,
+                             callbacks, history, start_epoch)
+        for cb in callbacks:
+            if hasattr(cb, "on_train_end"):
+                cb.on_train_end(self, history)
+        return {k: v for k, v in history.items() if v}
+
+    def _fit_epochs(self, train_batches, nb_epoch, steps_per_epoch, validation_batches, validation_steps, callbacks,
+                    history, start_epoch) -> None:
         for ep in range(start_epoch, nb_epoch):
             tr = self._run_epoch(iter(train_batches(ep)), steps_per_epoch, True)
             history["loss"].append(tr.get("loss", float("nan")))
@@ -542,10 +571,6 @@ class Trainer:
             for cb in callbacks:
                 if hasattr(cb, "on_epoch_end"):
                     cb.on_epoch_end(self, ep, logs)
-        for cb in callbacks:
-            if hasattr(cb, "on_train_end"):
-                cb.on_train_end(self, history)
-        return {k: v for k, v in history.items() if v}
 
     # ------------------------------------------------------------------ state
     def state(self) -> Dict[str, object]:
