@@ -490,9 +490,11 @@ class _CrossGpuRowsFn(torch.autograd.Function):
     """Cross-GPU negatives for wide vectors (D > 192: BERT's 768) with the same communication
     design as _CrossGpuFn — the page gather started after the doc tower, the bf16 queries and
     the per-query softmax scales gathered asynchronously, and NO reduce-scatter in backward:
-    dQ = local queries x all pages, dD of the LOCAL pages = all W*B queries x local pages —
-    with the logits tiled over column blocks at the GEMM level (_rows_forward / _rows_backward)
-    instead of the register-resident flash kernels."""
+    dQ = local queries x all pages, dD of the LOCAL pages = all W*B queries x local pages.  The
+    passes (_rows_forward / _rows_backward) run on the ``ibw`` flash kernel (loss.hip, DP a
+    multiple of 128 in 256..1024: the row's d-slices split over a workgroup's 4 waves, no logits
+    in HBM); only the widths ibw does not cover fall back to column blocks of library-GEMM
+    logits."""
 
     @staticmethod
     def forward(ctx, qn, dn, pos_local, gamma, clip, group, pre, reduce=False):

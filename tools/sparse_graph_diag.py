@@ -11,7 +11,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29533")
-os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", PAGEVEC_FORCE_DIST="1")
+os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+os.environ.setdefault("PAGEVEC_FORCE_DIST", "1")
 import torch  # noqa: E402
 
 
@@ -19,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=22)
     ap.add_argument("--runs", default="e,e,g,g")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="configuration overrides (bisecting the row-sparse / lazy-Adam / query-stream arms)")
     a = ap.parse_args()
     from dnn_page_vectors_amd.config import preset_config
     from dnn_page_vectors_amd.data.synthetic import SyntheticPairs, spec_from_config
@@ -30,6 +33,10 @@ def main():
     dev = info.device
     cfg = preset_config("cdssm_ngram_bf16").replace(batch_size=64, document_length=256, grad_bucket_mb=1.0,
                                                     sparse_embedding_grad=True, lazy_embedding_adam=True)
+    if a.set:
+        cfg = cfg.override(a.set)
+    print("config:", {k: getattr(cfg, k) for k in ("sparse_embedding_grad", "lazy_embedding_adam", "query_stream")},
+          "force_dist:", os.environ.get("PAGEVEC_FORCE_DIST"), flush=True)
     data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=1024), dev, seed=3)
     batches = [data.batch(cfg.batch_size) for _ in range(a.steps)]
     ref = None
