@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=22)
     ap.add_argument("--runs", default="e,e,g,g")
+    ap.add_argument("--burn", type=int, default=0, help="throwaway eager trainers run first (first-run effects)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="configuration overrides (bisecting the row-sparse / lazy-Adam / query-stream arms)")
     a = ap.parse_args()
@@ -39,6 +40,13 @@ def main():
           "force_dist:", os.environ.get("PAGEVEC_FORCE_DIST"), flush=True)
     data = SyntheticPairs(spec_from_config(cfg, cfg.vocab_hash_size, num_pages=1024), dev, seed=3)
     batches = [data.batch(cfg.batch_size) for _ in range(a.steps)]
+    for _ in range(a.burn):
+        torch.manual_seed(1234)
+        tb = Trainer(cfg, build_model(cfg, cfg.vocab_hash_size), dev, graph=False)
+        for q, d in batches:
+            tb.train_step(q, d)
+        torch.cuda.synchronize()
+        del tb
     ref = None
     for i, kind in enumerate(a.runs.split(",")):
         torch.manual_seed(1234)
