@@ -22,6 +22,12 @@ from ..ops import dense as dops
 from ..ops import determinism
 from ..ops._common import precision_scope
 
+# experiment (round 6): keep the query tower / early sort / dW side streams inside a
+# hipGraph capture (the capture forks into them and joins back)
+CAPTURE_STREAMS = os.environ.get("PAGEVEC_CAPTURE_STREAMS", "0") != "0"
+# cuda_stream handles of the query-tower streams (a fork of the capture stream inside a capture)
+QUERY_STREAM_IDS = set()
+
 _GENERATION = [0]
 
 
@@ -106,7 +112,7 @@ class TwoTowerModel(nn.Module):
             return None
         if os.environ.get("PAGEVEC_QUERY_STREAM", "1") == "0":  # A/B switch
             return None
-        if torch.cuda.is_current_stream_capturing():  # hipGraph capture: one stream
+        if torch.cuda.is_current_stream_capturing() and not CAPTURE_STREAMS:  # hipGraph capture: one stream
             return None
         if determinism.enabled():  # deterministic mode: one stream (ops/determinism.py)
             return None
@@ -121,6 +127,7 @@ class TwoTowerModel(nn.Module):
         dev = q_ids.device.index
         if dev not in st:
             st[dev] = torch.cuda.Stream(device=q_ids.device)
+            QUERY_STREAM_IDS.add(st[dev].cuda_stream)
         return st[dev]
 
     def _towers_share_params(self) -> bool:

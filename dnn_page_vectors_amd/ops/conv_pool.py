@@ -163,6 +163,21 @@ V7_DBG = (16384 + 64 + 5 + 1024, 16384 + 64 + 5, 16384 + 128 + 5, 16384 + 128 + 
           16384 + 192 + 5 + 1024)  # pv_conv_set_dbg variants with the loader key emit (every v7 arm)
 
 
+def _capture_streams() -> bool:
+    """Side streams inside a hipGraph capture (models/base.py CAPTURE_STREAMS) — except a fork
+    of a fork: the query tower's early sort (a side stream of the query stream, itself forked
+    from the capture stream) made hipStreamEndCapture segfault (round 6: query stream alone and
+    early sort alone capture fine, both together crash), so inside a capture the query tower
+    sorts in its backward."""
+    from ..models.base import CAPTURE_STREAMS, QUERY_STREAM_IDS
+
+    if not CAPTURE_STREAMS:
+        return False
+    if torch.cuda.is_current_stream_capturing() and torch.cuda.current_stream().cuda_stream in QUERY_STREAM_IDS:
+        return False
+    return True
+
+
 def _conv_dbg() -> int:
     return int(lib().pv_conv_get_dbg())
 
@@ -213,7 +228,7 @@ class _ConvPoolFn(torch.autograd.Function):
               "pv_conv_pool_fwd2")
         ctx.keys = keys
         ctx.sorted = None
-        if keys is not None and _early_sort(L) and not torch.cuda.is_current_stream_capturing() \
+        if keys is not None and _early_sort(L) and (_capture_streams() or not torch.cuda.is_current_stream_capturing()) \
                 and not determinism.enabled():
             # the sort of the table-gradient keys depends on the forward alone: run it now on
             # the side stream, beside the rest of the forward and the loss, instead of on the
@@ -267,7 +282,8 @@ class _ConvPoolFn(torch.autograd.Function):
         # and the main stream joins the side stream before returning: no cross-stream reuse
         # the page tower's dW beside its table chain (not inside a hipGraph capture: one stream)
         side = (_side_stream(dev) if DW_SIDE_STREAM and ctx.needs_input_grad[1]
-                and not torch.cuda.is_current_stream_capturing() and not determinism.enabled() else None)
+                and (_capture_streams() or not torch.cuda.is_current_stream_capturing()) and not determinism.enabled()
+                else None)
         if side is not None:
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
