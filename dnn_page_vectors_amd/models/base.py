@@ -22,9 +22,12 @@ from ..ops import dense as dops
 from ..ops import determinism
 from ..ops._common import precision_scope
 
-# experiment (round 6): keep the query tower / early sort / dW side streams inside a
-# hipGraph capture (the capture forks into them and joins back)
-CAPTURE_STREAMS = os.environ.get("PAGEVEC_CAPTURE_STREAMS", "0") != "0"
+# hipGraph captures keep the query tower / early-sort side streams (the capture forks into them
+# and joins back; round 6): graph steps MLP 1.148 -> 1.078 ms, chunked fp8 1.047 ->
+# 0.997, chunked CDSSM 1.125 -> 1.048 (profiles/r6/capture_streams_ab.txt).  The round-5 segfault
+# in capture_end came from a fork of a fork — the query tower's early sort on a side stream of
+# the query stream — which conv_pool._capture_streams keeps out of captures.  0: one stream.
+CAPTURE_STREAMS = os.environ.get("PAGEVEC_CAPTURE_STREAMS", "1") != "0"
 # cuda_stream handles of the query-tower streams (a fork of the capture stream inside a capture)
 QUERY_STREAM_IDS = set()
 

@@ -51,6 +51,7 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_CONV_SHORT": ("ab", "1", "conv forward: one 48-row chunk for sequences up to 50 tokens (query tower)"),
     "PAGEVEC_ATTN_BGRAD": ("ab", "1", "qkv bias gradient from the attention backward's partial column sums"),
     "PAGEVEC_BERT_EMBED": ("ab", "1", "BERT embedding front end as one fused gather + add kernel"),
+    "PAGEVEC_CAPTURE_STREAMS": ("ab", "1", "hipGraph captures keep the query-tower / early-sort side streams"),
     "PAGEVEC_STEP_PRIORITY": ("ab", "1", "eager step on a high-priority stream (query tower / side streams normal)"),
     "PAGEVEC_NO_MIRROR": ("ab", "0", "no bf16 mirror written by the Adam kernel"),
     # process plumbing
