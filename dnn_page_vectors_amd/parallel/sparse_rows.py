@@ -60,6 +60,7 @@ class _Table:
     pending: Optional[Tuple] = None          # in-flight all-gathers
     prev_buf: Optional[torch.Tensor] = None  # persistent copy of ``prev`` (stable address under capture)
     cap: int = 0                             # agreed exchange capacity (rows), 0 = not yet agreed
+    cap_basis: int = 0                       # this rank's noted-id count the capacity was agreed for
 
 
 def unique_rows(ids: torch.Tensor, V: int, cap: int,
@@ -144,10 +145,15 @@ class SparseTables:
             cnt = (u >= 0).sum().reshape(1)
             dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
             return max(1, int(cnt.item()))
-        if t.cap == 0:  # auto: agreed once, from the noted-id counts (no per-step sync)
-            cnt = torch.tensor([min(t.V, ids.numel())], dtype=torch.int64, device=ids.device)
+        # auto: agreed from the noted-id counts (host-known shapes) — once, and again whenever a
+        # step notes more ids than the count the capacity was agreed for (a larger batch shape),
+        # so a later, larger step does not overflow a capacity sized for the first
+        n_ids = min(t.V, ids.numel())
+        if t.cap == 0 or n_ids > t.cap_basis:
+            cnt = torch.tensor([n_ids], dtype=torch.int64, device=ids.device)
             dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
-            t.cap = max(1, int(cnt.item()))
+            t.cap = max(t.cap, 1, int(cnt.item()))
+            t.cap_basis = max(t.cap_basis, n_ids)
         return t.cap
 
     def launch(self, t: _Table, group=None) -> None:
@@ -235,6 +241,14 @@ class SparseTables:
                 g = torch.where(rows.unsqueeze(1) >= 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
                 out[0] += torch.where(fin, g, torch.zeros_like(g)).pow(2).sum()
                 out[1] = torch.maximum(out[1], (~fin).any().float())
+        # a step whose distinct rows overflowed the exchange capacity dropped some rows' gradients:
+        # flag it like a non-finite gradient, so the optimizer skips it on the device (no update of
+        # the rows that WERE exchanged with a partial picture) and check() reports it
+        seen = getattr(self, "_overflow_seen", None)
+        if seen is None:
+            seen = self._overflow_seen = torch.zeros_like(self.overflow)
+        out[1] = torch.maximum(out[1], (self.overflow > seen).float())
+        seen.copy_(self.overflow)
         out[1] = (out[1] > 0).float()
         return out
 

@@ -501,6 +501,8 @@ class Trainer:
             if train:
                 nf = m["nonfinite"]
                 tot["nonfinite"] = tot.get("nonfinite", 0.0) + nf
+                if self.sparse is not None and self.cfg.log_every and self.step % self.cfg.log_every == 0:
+                    self.sparse.check()  # a host read at the logging cadence: fail early
                 if self.metrics and self.cfg.log_every and self.step % self.cfg.log_every == 0:
                     rec = dict(step=self.step, loss=float(m["loss"]), acc=float(m["acc"]),
                                grad_norm=math.sqrt(max(0.0, float(m["grad_sumsq"]))), hbm_gb=round(hbm_used_gb(), 3))

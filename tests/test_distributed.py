@@ -303,6 +303,7 @@ def _sparse_worker(rank, world, port, q, V, sparse, cap=-1):
     cfg = _cfg("cross_gpu", B // world).replace(sparse_embedding_grad=sparse, lazy_embedding_adam=True,
                                                 sparse_rows_capacity=cap)
     tr = Trainer(cfg, CDSSM(cfg, V))
+    init = tr.flat.data.detach().clone()
     if sparse:
         assert tr.buckets.sparse_bucket  # the tables' buckets are row exchanges
     for qa, da in _sparse_data(B, V):
@@ -314,6 +315,8 @@ def _sparse_worker(rank, world, port, q, V, sparse, cap=-1):
             tr.sparse.check()
         except RuntimeError as e:
             err = str(e)
+    if err:  # every step overflowed: each was skipped like a non-finite one (no partial update)
+        assert torch.equal(tr.flat.data, init), "an overflowing step updated the parameters"
     q.put((rank, tr.flat.data.detach().numpy().copy(), err))
     pdist.destroy()
 
@@ -358,7 +361,8 @@ def test_sparse_embedding_grad_dp_equals_dense(world):
 def test_sparse_rows_capacity_modes():
     """The exchange's padding (Configuration.sparse_rows_capacity): exact per-step sizing (0,
     host sync) and a fixed capacity with room give the auto mode's parameters; a capacity below
-    the distinct-row count drops rows and every rank's check() says so."""
+    the distinct-row count drops rows, the step is skipped on the device (parameters unchanged)
+    and every rank's check() says so."""
     V, world = 200_000, 2
     auto = _run_sparse(world, V, True, -1)[0][0]
     for cap in (0, 4096):
