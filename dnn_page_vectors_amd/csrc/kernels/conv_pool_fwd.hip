@@ -792,10 +792,8 @@ using namespace pv;
 
 // Pack conv weights (fp32, [F][k][E] per width) into MFMA B fragments (bf16).
 // w3: (150,3,E) ; w4: (150,4,E). out: 20 tiles' fragments (NT*S3 + NT*S4) * 64 lanes * 8.
-__global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E, bf16x8* out) {
+__device__ __forceinline__ bf16x8 pack_fragment(const float* w3, const float* w4, int E, int frag, int lane) {
   using namespace pv::convpool;
-  int frag = blockIdx.x;  // fragment index
-  int lane = threadIdx.x;
   int T, s;
   if (frag < NT * S3) { T = frag / S3; s = frag % S3; }
   else { T = NT + (frag - NT * S3) / S4; s = (frag - NT * S3) % S4; }
@@ -817,7 +815,11 @@ __global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E
     if (col < FW && jj < k && e < E) x = w[((size_t)col * k + jj) * E + e];
     v[j] = (short)f32_to_bf16(x);
   }
-  out[(size_t)frag * 64 + lane] = v;
+  return v;
+}
+
+__global__ void pack_conv_weights_kernel(const float* w3, const float* w4, int E, bf16x8* out) {
+  out[(size_t)blockIdx.x * 64 + threadIdx.x] = pack_fragment(w3, w4, E, blockIdx.x, threadIdx.x);
 }
 
 PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* out, void* stream) {
@@ -826,6 +828,68 @@ PV_API int pv_conv_pack_weights(const float* w3, const float* w4, int E, void* o
   int nfrag = NT * S3 + NT * S4 + S4;  // + the mixed tile of v4
   hipLaunchKernelGGL(pack_conv_weights_kernel, dim3(nfrag), dim3(64), 0, (hipStream_t)stream, w3, w4, E,
                      (bf16x8*)out);
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// The per-step bf16 operands of up to 4 conv towers in ONE launch (round 6): each tower's table
+// cast to the padded (V, EP) bf16 layout and its filters packed into MFMA fragments — what
+// pv_cast_pad_bf16 + pv_conv_pack_weights did in two launches per tower at the start of every
+// forward.  Blocks [0, cast_blocks) of a tower cast its table (grid-stride), the next
+// pack_blocks blocks pack 4 fragments each (64 lanes per fragment).
+struct PrepTower {
+  const float* table;      // (V, E) fp32
+  unsigned short* tbl16;   // (V, EP) bf16
+  const float* w3;         // (FW, 3, E)
+  const float* w4;         // (FW, 4, E)
+  bf16x8* pack;            // pv_conv_packed_size() bf16
+  int V;
+};
+struct PrepArgs {
+  PrepTower t[4];
+  int n, E, cast_blocks;
+};
+
+__global__ __launch_bounds__(256) void conv_prep_multi_kernel(PrepArgs a) {
+  using namespace pv::convpool;
+  constexpr int NFRAG = NT * S3 + NT * S4 + S4;
+  constexpr int PACK_BLOCKS = (NFRAG + 3) / 4;
+  const int per = a.cast_blocks + PACK_BLOCKS;
+  const int ti = blockIdx.x / per, b = blockIdx.x - ti * per;
+  if (ti >= a.n) return;
+  const PrepTower& t = a.t[ti];
+  if (b < a.cast_blocks) {
+    const long total = (long)t.V * EP;
+    for (long i = (long)b * 256 + threadIdx.x; i < total; i += (long)a.cast_blocks * 256) {
+      const long r = i / EP;
+      const int c = (int)(i - r * EP);
+      t.tbl16[i] = c < a.E ? f32_to_bf16(t.table[r * a.E + c]) : (unsigned short)0;
+    }
+    return;
+  }
+  const int frag = (b - a.cast_blocks) * 4 + (threadIdx.x >> 6);
+  if (frag < NFRAG) t.pack[(size_t)frag * 64 + (threadIdx.x & 63)] = pack_fragment(t.w3, t.w4, a.E, frag, threadIdx.x & 63);
+}
+
+// tables / tbl16 / w3 / w4 / packs: arrays of n (<= 4) device pointers; Vs: n vocabulary sizes
+PV_API int pv_conv_prep_multi(int n, const void* const* tables, void* const* tbl16, const void* const* w3s,
+                              const void* const* w4s, void* const* packs, const int* Vs, int E, void* stream) {
+  using namespace pv::convpool;
+  if (n < 1 || n > 4 || E > EP) return -1;
+  PrepArgs a{};
+  a.n = n;
+  a.E = E;
+  long vmax = 0;
+  for (int i = 0; i < n; ++i) {
+    a.t[i] = PrepTower{(const float*)tables[i], (unsigned short*)tbl16[i], (const float*)w3s[i], (const float*)w4s[i],
+                       (bf16x8*)packs[i], Vs[i]};
+    vmax = Vs[i] > vmax ? Vs[i] : vmax;
+  }
+  long cb = (vmax * EP / 4 + 255) / 256;  // ~4 elements per thread
+  a.cast_blocks = (int)(cb < 1 ? 1 : cb > 4096 ? 4096 : cb);
+  constexpr int NFRAG = NT * S3 + NT * S4 + S4;
+  const int per = a.cast_blocks + (NFRAG + 3) / 4;
+  hipLaunchKernelGGL(conv_prep_multi_kernel, dim3(n * per), dim3(256), 0, (hipStream_t)stream, a);
   PV_LAUNCH_CHECK();
   return 0;
 }

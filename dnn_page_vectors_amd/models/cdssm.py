@@ -62,8 +62,11 @@ class CDSSMTower(nn.Module):
     def fast_ok(self) -> bool:
         return cops.fast_path_supported(self.embedding.shape[1], self.widths, self.conv_w[0].shape[0])
 
+    def build_cache_ok(self) -> bool:
+        return self.embedding.is_cuda and self.fast_ok() and cops.use_hip(self.embedding)
+
     def build_cache(self):
-        if self.embedding.is_cuda and self.fast_ok() and cops.use_hip(self.embedding):
+        if self.build_cache_ok():
             return (cops.table_bf16(self.embedding.detach()),
                     cops.pack_weights(self.conv_w[0].detach(), self.conv_w[1].detach()))
         return None
@@ -102,6 +105,11 @@ class CDSSM(TwoTowerModel):
         return self.cfg.hidden_dims
 
     def build_cache(self) -> Dict[str, object]:
+        towers = [("query", self.query_tower)] + [(f"doc{i}", t) for i, t in enumerate(self.doc_towers)]
+        if cops.PREP_MULTI and all(t.build_cache_ok() for _, t in towers):  # every tower's copies in one launch
+            res = cops.prep_towers([(t.embedding.detach(), t.conv_w[0].detach(), t.conv_w[1].detach())
+                                    for _, t in towers])
+            return {k: r for (k, _), r in zip(towers, res)}
         c = {"query": self.query_tower.build_cache()}
         for i, t in enumerate(self.doc_towers):
             c[f"doc{i}"] = t.build_cache()

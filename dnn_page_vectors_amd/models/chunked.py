@@ -34,6 +34,7 @@ import torch.nn as nn
 
 from ..ops import dense as dops
 from .base import TwoTowerModel
+from ..ops import conv_pool as cops
 from .cdssm import CDSSMTower
 from .mlp_dssm import MLPTower
 
@@ -73,7 +74,12 @@ class ChunkedPageEncoder(TwoTowerModel):
     def build_cache(self):
         if not self.query_tower.embedding.is_cuda:
             return {}
-        return {"query": self.query_tower.build_cache(), "doc0": self.doc_towers[0].build_cache()}
+        q, d = self.query_tower, self.doc_towers[0]
+        if self.encoder == "cdssm" and cops.PREP_MULTI and q.build_cache_ok() and d.build_cache_ok():
+            res = cops.prep_towers([(t.embedding.detach(), t.conv_w[0].detach(), t.conv_w[1].detach())
+                                    for t in (q, d)])
+            return {"query": res[0], "doc0": res[1]}
+        return {"query": q.build_cache(), "doc0": d.build_cache()}
 
     def _tower(self, t, ids, training, seed, cache):
         if self.encoder == "cdssm":

@@ -9,6 +9,7 @@ _T = {"p": ctypes.c_void_p, "i": ctypes.c_int, "u": ctypes.c_uint, "l": ctypes.c
 
 SIGS = {
     # conv_pool_fwd.hip
+    "pv_conv_prep_multi": "ippppppip",
     "pv_conv_pack_weights": "ppipp",
     "pv_conv_weight_rows": "ppipp",
     "pv_conv_packed_size": "",

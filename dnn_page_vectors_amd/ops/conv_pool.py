@@ -51,6 +51,32 @@ def pack_weights(w3: torch.Tensor, w4: torch.Tensor) -> torch.Tensor:
     return out
 
 
+PREP_MULTI = True  # A/B switch (tools/step_flag_ab.py --flag PREP_MULTI): one-launch tower prep
+
+
+def prep_towers(towers) -> list:
+    """[(table (V,E), w3, w4), ...] -> [(table_bf16, packed weights), ...] — the per-step compute
+    copies of every conv tower in one launch per 4 towers (pv_conv_prep_multi) instead of two per
+    tower (table_bf16 + pack_weights)."""
+    import ctypes
+    out = []
+    n_pack = lib().pv_conv_packed_size()
+    for g in range(0, len(towers), 4):
+        grp = [(t.contiguous(), w3.contiguous(), w4.contiguous()) for t, w3, w4 in towers[g:g + 4]]
+        E = grp[0][0].shape[1]
+        res = [(torch.empty(t.shape[0], EP, dtype=torch.bfloat16, device=t.device),
+                torch.empty(n_pack, dtype=torch.bfloat16, device=t.device)) for t, _, _ in grp]
+        n = len(grp)
+        arrs = [(ctypes.c_void_p * n)(*[P(x) for x in col]) for col in
+                ([t for t, _, _ in grp], [r[0] for r in res], [w for _, w, _ in grp], [w for _, _, w in grp],
+                 [r[1] for r in res])]
+        Vs = (ctypes.c_int * n)(*[t.shape[0] for t, _, _ in grp])
+        check(lib().pv_conv_prep_multi(n, *[ctypes.addressof(a) for a in arrs], ctypes.addressof(Vs), E,
+                                       stream(grp[0][0].device)), "pv_conv_prep_multi")
+        out.extend(res)
+    return out
+
+
 def _dropout_args(p: float, training: bool, mode: str) -> Tuple[int, int, float]:
     if not training or p <= 0.0 or mode == "none":
         return 0, 0, 1.0

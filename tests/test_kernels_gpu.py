@@ -199,6 +199,19 @@ def test_conv_forward_role_split_bit_identical(variant, N, L, p, mode):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("n,E", [(2, 100), (6, 100), (3, 37)])
+def test_prep_towers_matches_per_tower_copies(n, E):
+    """One-launch tower prep (pv_conv_prep_multi) == table_bf16 + pack_weights per tower, bit for bit
+    (6 towers: two launches, the unshared-doc-tower v1 layout)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    towers = [(torch.randn(1000 + 777 * i, E, device=DEV, generator=g), torch.randn(150, 3, E, device=DEV, generator=g),
+               torch.randn(150, 4, E, device=DEV, generator=g)) for i in range(n)]
+    got = cops.prep_towers(towers)
+    for (t, w3, w4), (tb, pk) in zip(towers, got):
+        assert torch.equal(tb, cops.table_bf16(t))
+        assert torch.equal(pk, cops.pack_weights(w3, w4))
+
+
 def test_conv_pool_eval_mode_no_dropout():
     V, E, F, N, L = 50, 100, 150, 4, 20
     ids = torch.randint(0, V, (N, L), dtype=torch.int32, device=DEV)
