@@ -400,6 +400,103 @@ __global__ __launch_bounds__(256) void colsum_kernel(const TX* __restrict__ x, l
   else out[c] = s4[0];
 }
 
+// ---- reference precision (dtype = "fp32"): fp32-exact GEMM on the fp32 MFMA ----------------
+// C (M, N) = A (M, K) . B (K, N) [+ bias[n], act] with A(m, k) = A[m sam + k sak] and
+// B(k, n) = B[k sbk + n sbn]: one kernel for the forward X W^T, the dgrad dZ W and the wgrad
+// dZ^T X of the dense layers (reference Dense + Activation in fp32, cnn_dssm_th.py:136-138).
+// v_mfma_f32_16x16x4_f32 (fp32 products and sums; no bf16 operand anywhere), 64 x 64 tiles,
+// K-steps of 16 staged k-major in LDS (a fragment read is 16 consecutive m / n per lane group:
+// conflict-free), 4 waves of 32 x 32, the next K-step fetched into registers during this one's
+// MFMAs (one barrier per step).  blockIdx.z = split-K slice: slice z writes its own (M, N) slab
+// at C + z M ldc without the epilogue (the column-sum kernel reduces the slabs in order).
+// AK: sak == 1 (an A row is contiguous in k); BN1: sbn == 1 (a B row is contiguous in n): the
+// staging map puts consecutive threads on the contiguous axis.
+constexpr int FB = 64, FK = 16;
+template <bool AK, bool BN1>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, long sam, long sak,
+                                                       const float* __restrict__ B, long sbk, long sbn,
+                                                       const float* __restrict__ bias, float* __restrict__ C, long ldc,
+                                                       int M, int N, int K, int kper, int act, int accumulate) {
+  __shared__ float As[2][FK][FB + 4];
+  __shared__ float Bs[2][FK][FB + 4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = blockIdx.x * FB, n0 = blockIdx.y * FB;
+  const int kb = blockIdx.z * kper, ke = min(K, kb + kper);
+  // staging coordinates of this thread's 4 elements per operand (tile-relative)
+  const int am = AK ? t >> 2 : (t & 15) * 4, ak = AK ? (t & 3) * 4 : t >> 4;
+  const int bn = BN1 ? (t & 15) * 4 : t >> 2, bk = BN1 ? t >> 4 : (t & 3) * 4;
+  float ra[4], rb[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gm = m0 + am + (AK ? 0 : e), gk = k0 + ak + (AK ? e : 0);
+      ra[e] = (gm < M && gk < ke) ? A[(long)gm * sam + (long)gk * sak] : 0.f;
+      const int gn = n0 + bn + (BN1 ? e : 0), gk2 = k0 + bk + (BN1 ? 0 : e);
+      rb[e] = (gn < N && gk2 < ke) ? B[(long)gk2 * sbk + (long)gn * sbn] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      As[buf][ak + (AK ? e : 0)][am + (AK ? 0 : e)] = ra[e];
+      Bs[buf][bk + (BN1 ? 0 : e)][bn + (BN1 ? e : 0)] = rb[e];
+    }
+  };
+  const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32, r16 = lane & 15, kq = lane >> 4;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (kb < ke) {
+    fetch(kb);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kb; k0 < ke; k0 += FK) {
+    const bool more = k0 + FK < ke;
+    if (more) fetch(k0 + FK);
+#pragma unroll
+    for (int s = 0; s < FK / 4; ++s) {
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[buf][4 * s + kq][wm + 16 * i + r16];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[buf][4 * s + kq][wn + 16 * j + r16];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
+    buf ^= 1;
+  }
+  const bool split = gridDim.z > 1;
+  float* Cz = C + (size_t)blockIdx.z * M * ldc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm + 16 * i + 4 * kq + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn + 16 * j + r16;
+        if (n >= N) continue;
+        float v = acc[i][j][r];
+        float* o = Cz + (size_t)m * ldc + n;
+        if (!split) {
+          if (bias) v += bias[n];
+          v = act_fn(v, act);
+          if (accumulate) v += *o;
+        }
+        *o = v;
+      }
+    }
+}
+
 }  // namespace dense
 }  // namespace pv
 
@@ -564,7 +661,7 @@ PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* ou
   const bool vec = C % 4 == 0 && ldx % 4 == 0 && !((uintptr_t)out & 15) && !((uintptr_t)x & (xdt ? 7 : 15));
   const int V = vec ? 4 : 1;
   const long units = C / V;
-  const bool narrow = units <= 1024;
+  const bool narrow = units <= 1024 || !vec;  // the element-load variant exists at 16 quads only
   const int QB = narrow ? 16 : 64, RG = 256 / QB;
   const long gx = (units + QB - 1) / QB;
   long splits = 1;
@@ -594,6 +691,32 @@ PV_API int pv_colsum(const void* x, int xdt, long R, long C, long ldx, float* ou
     else PV_COLSUM(float, 64, 4);
   }
 #undef PV_COLSUM
+  PV_LAUNCH_CHECK();
+  return 0;
+}
+
+// fp32-exact GEMM (gemm_f32_kernel): C = A . B [+ bias, act], element strides as above; splits
+// > 1: C holds `splits` (M, ldc) slabs of partial sums over K slices (no epilogue, no
+// accumulate).  Both the A and B operands: one unit stride required (sak or sam, sbn or sbk).
+PV_API int pv_gemm_f32(const float* A, long sam, long sak, const float* B, long sbk, long sbn, const float* bias,
+                       float* C, long ldc, int M, int N, int K, int splits, int act, int accumulate, void* stream) {
+  using namespace pv::dense;
+  if (M < 1 || N < 1 || K < 1 || splits < 1 || ldc < N) return -1;
+  if (splits > 1 && (accumulate || bias || act)) return -2;
+  if ((sak != 1 && sam != 1) || (sbn != 1 && sbk != 1)) return -3;
+  const int kper = ((K + splits - 1) / splits + FK - 1) / FK * FK;
+  splits = (K + kper - 1) / kper;
+  const dim3 grid((M + FB - 1) / FB, (N + FB - 1) / FB, splits);
+  hipStream_t s = (hipStream_t)stream;
+#define PV_GF(AKV, BNV)                                                                                     \
+  hipLaunchKernelGGL((gemm_f32_kernel<AKV, BNV>), grid, dim3(256), 0, s, A, sam, sak, B, sbk, sbn, bias, C, ldc, \
+                     M, N, K, kper, act, accumulate)
+  if (sak == 1) {
+    if (sbn == 1) PV_GF(true, true); else PV_GF(true, false);
+  } else {
+    if (sbn == 1) PV_GF(false, true); else PV_GF(false, false);
+  }
+#undef PV_GF
   PV_LAUNCH_CHECK();
   return 0;
 }

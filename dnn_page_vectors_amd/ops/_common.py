@@ -36,8 +36,11 @@ def precision_scope(cfg):
     weights and optimizer state.  ``fp32``: the reference's precision (Keras/Theano trains in
     fp32, dssm_cnn_v2/cnn_dssm_th.py:182) — inside this scope no bf16 HIP kernel runs: the CDSSM
     conv tower runs its fp32 HIP kernels (csrc/kernels/conv_pool_f32.hip, fp32 MFMA; see
-    ``ref_precision``), every other op its fp32 PyTorch implementation (rocBLAS on the GPU);
-    the fused Adam kernel is fp32 already.  CPU runs are fp32 either way."""
+    ``ref_precision``), the dense layers the fp32-MFMA GEMM (dense.hip gemm_f32_kernel), the
+    L2 normalisation / explicit loss / column sums / activation backward their fp32 kernels
+    (``use_hip_exact``); the remaining ops (in-batch losses, transformer and LSTM towers, bag
+    GEMMs) their fp32 PyTorch implementation.  The fused Adam kernel is fp32 already.  CPU runs
+    are fp32 either way."""
     global _FORCE
     if getattr(cfg, "dtype", "bf16") != "fp32" or _FORCE == "torch":
         yield
@@ -62,6 +65,18 @@ F32_NATIVE = os.environ.get("PAGEVEC_F32_NATIVE", "1") != "0"
 def ref_precision() -> bool:
     """Inside a dtype="fp32" precision scope with the native fp32 kernels enabled."""
     return _REF_PREC[0] > 0 and F32_NATIVE
+
+
+def use_hip_exact(*tensors: torch.Tensor) -> bool:
+    """``use_hip`` for kernels whose arithmetic is fp32 end to end (no bf16 operand: L2
+    normalisation, column sums, activation backward, the explicit loss): inside a dtype="fp32"
+    scope they run too, beside the fp32-MFMA dense / conv kernels (``ref_precision``)."""
+    if ref_precision():
+        if any(t is not None and t.is_cuda for t in tensors):
+            _native.hip(required=True)
+            return True
+        return False
+    return use_hip(*tensors)
 
 
 def use_hip(*tensors: torch.Tensor) -> bool:

@@ -54,6 +54,7 @@ SIGS = {
     # w2v.hip
     "pv_w2v_train": "pppppp" "ll" "iiii" "u" "f" "i" "p",
     # dense.hip
+    "pv_gemm_f32": "pll" "pll" "p" "pl" "iiii" "ii" "p",
     "pv_linear_act": "pipippp" "iiiiii" "p",
     "pv_linear_wgrad": "pipip" "iiiii" "p",
     "pv_linear_dgrad": "pipip" "iii" "p",

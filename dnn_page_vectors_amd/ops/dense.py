@@ -17,7 +17,7 @@ import torch
 
 from . import grad_sink
 from . import reference as ref
-from ._common import P, check, lib, stream, use_hip
+from ._common import P, check, lib, ref_precision, stream, use_hip, use_hip_exact
 
 _ACT = {"none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 
@@ -107,7 +107,7 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool
         C *= int(d)
     epi = scale is not None or bias is not None or act != "none"
     x2 = x.reshape(R, C) if x.is_contiguous() else x.contiguous().reshape(R, C)
-    if use_hip(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.dtype == torch.float32)):
+    if use_hip_exact(x) and _colsum_ok(x2, C, C) and (out is None or (out.is_contiguous() and out.dtype == torch.float32)):
         E = int(tail[-1]) if len(tail) else 1
         if epi:
             mode = 3 if (scale_is_len and scale is not None) else 2
@@ -205,7 +205,105 @@ def dgrad_hip(dz: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dx
 
 
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
+             bias: Optional[torch.Tensor] = None, act: str = "none", out: Optional[torch.Tensor] = None,
+             accumulate: bool = False, splits: int = 1) -> torch.Tensor:
+    """op(a) @ op(b) [+ bias, act] in exact fp32 on the fp32 MFMA (dense.hip::gemm_f32_kernel), the
+    dense layers' GEMM at the reference precision.  ``a_t`` / ``b_t``: the operand is stored
+    transposed (read through strides, no copy).  ``splits`` > 1: split-K partial slabs reduced by
+    the column-sum kernel (no epilogue: bias / act / accumulate need splits == 1)."""
+    a, b = a.contiguous(), b.contiguous()
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise TypeError("gemm_f32: fp32 operands")
+    M, K = (a.shape[1], a.shape[0]) if a_t else a.shape
+    Kb, N = (b.shape[1], b.shape[0]) if b_t else b.shape
+    if K != Kb:
+        raise ValueError(f"gemm_f32: inner dims {K} vs {Kb}")
+    sam, sak = (1, M) if a_t else (K, 1)
+    sbk, sbn = (1, K) if b_t else (N, 1)
+    bb = bias.contiguous().float() if bias is not None else None
+    if splits > 1:
+        kper = -(-(-(-K // splits)) // 16) * 16
+        ns = -(-K // kper)
+        ws = torch.empty(ns, M, N, dtype=torch.float32, device=a.device)
+        check(lib().pv_gemm_f32(P(a), sam, sak, P(b), sbk, sbn, None, P(ws), N, M, N, K, ns, 0, 0, stream(a.device)),
+              "pv_gemm_f32")
+        if ns > 1:
+            if bias is not None or act != "none" or accumulate:
+                raise ValueError("gemm_f32: split-K partials take no epilogue")
+            return colsum(ws, out=out)
+        part = ws[0]
+        return part if out is None else out.copy_(part)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    elif not (out.is_contiguous() and out.shape == (M, N) and out.dtype == torch.float32):
+        raise ValueError("gemm_f32: out must be a contiguous fp32 (M, N) tensor")
+    check(lib().pv_gemm_f32(P(a), sam, sak, P(b), sbk, sbn, P(bb), P(out), N, M, N, K, 1, _ACT[act], int(accumulate),
+                            stream(a.device)), "pv_gemm_f32")
+    return out
+
+
+def _wgrad_splits_f32(M: int, N: int, K: int) -> int:
+    tiles = -(-N // 64) * -(-K // 64)
+    return max(1, min(64, -(-512 // tiles), M // 256))
+
+
+class _LinearF32Fn(torch.autograd.Function):
+    """Dense + activation at the reference precision (dtype="fp32"): forward, dgrad and wgrad on
+    the fp32-MFMA GEMM, the activation backward and bias column sum on their fp32 kernels; the
+    weight / bias gradients written straight into the flat gradient like _LinearActFn."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous().float()
+        wf = w.contiguous().float()
+        y = gemm_f32(x2, wf, b_t=True, bias=b, act=act)
+        ctx.save_for_backward(x2, wf, y if act in ("relu", "tanh") else None, b)
+        ctx.act = act
+        ctx.xshape = x.shape
+        ctx.params = (w, b)
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wf, y, b = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous().float()
+        if ctx.act in ("relu", "tanh"):
+            dz = torch.empty_like(dy2)
+            check(lib().pv_act_bwd(P(y), P(dy2), P(dz), dy2.numel(), _ACT[ctx.act], stream(dy.device)), "pv_act_bwd")
+        elif ctx.act == "none":
+            dz = dy2
+        else:  # gelu: the pre-activation recomputed on the same GEMM
+            pre = gemm_f32(x2, wf, b_t=True, bias=b)
+            with torch.enable_grad():
+                pre.requires_grad_(True)
+                dz = torch.autograd.grad(torch.nn.functional.gelu(pre, approximate="tanh"), pre, dy2)[0]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_f32(dz, wf).view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            M, N = dz.shape
+            sk = _wgrad_splits_f32(M, N, x2.shape[1])
+            tw = grad_sink.write_target(ctx.params[0])
+            if tw is not None:
+                gemm_f32(dz, x2, a_t=True, out=tw, splits=sk)
+                grad_sink.done(ctx.params[0])
+            else:
+                dw = gemm_f32(dz, x2, a_t=True, splits=sk)
+        if b is not None and ctx.needs_input_grad[2]:
+            tb = grad_sink.write_target(ctx.params[1])
+            if tb is not None:
+                colsum(dz, out=tb, accumulate=True)
+                grad_sink.done(ctx.params[1])
+            else:
+                db = colsum(dz)
+        return dx, dw, db, None
+
+
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: str = "relu") -> torch.Tensor:
+    if ref_precision() and x.is_cuda:  # dtype="fp32": exact fp32 on the fp32 MFMA
+        use_hip_exact(x)
+        return _LinearF32Fn.apply(x, w, b, act)
     if use_hip(x, w):
         return _LinearActFn.apply(x, w, b, act)
     return ref.linear_act(x, w, b, act)
@@ -247,7 +345,7 @@ class _L2NormFn(torch.autograd.Function):
 
 
 def l2_normalize(x: torch.Tensor) -> torch.Tensor:
-    if use_hip(x):
+    if use_hip_exact(x):
         return _L2NormFn.apply(x)
     return ref.l2_normalize(x)
 

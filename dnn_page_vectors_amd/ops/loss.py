@@ -27,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import reference as ref
-from ._common import P, check, lib, stream, use_hip
+from ._common import P, check, lib, stream, use_hip, use_hip_exact
 
 
 class _ExplicitFn(torch.autograd.Function):
@@ -68,8 +68,9 @@ def dssm_explicit_loss(qn: torch.Tensor, dn: torch.Tensor, gamma: float, clip: b
     """qn (B, D), dn (B, 1+J, D) normalised -> (per-row loss (B,), P(D+|Q) (B,)).
 
     GPU: the fused HIP kernel (1+J <= 64, D <= 1024: covers the BERT tower's D = 768); beyond
-    that the loss is rejected on the GPU rather than silently run as eager torch."""
-    if use_hip(qn, dn):
+    that the loss is rejected on the GPU rather than silently run as eager torch.  fp32 end to
+    end, so it also runs at dtype="fp32" (``use_hip_exact``)."""
+    if use_hip_exact(qn, dn):
         if dn.shape[1] > EXPLICIT_MAX_J1 or qn.shape[1] > EXPLICIT_MAX_D:
             raise NotImplementedError(f"explicit loss kernel supports 1+J <= {EXPLICIT_MAX_J1} and D <= "
                                       f"{EXPLICIT_MAX_D}; got 1+J = {dn.shape[1]}, D = {qn.shape[1]}")

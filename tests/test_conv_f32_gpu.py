@@ -83,9 +83,40 @@ def test_conv_f32_eval_and_row_offset(monkeypatch):
     torch.testing.assert_close(po, pro, rtol=1e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("M,N,K,a_t,b_t,act,splits", [
+    (300, 150, 300, False, True, "relu", 1),    # forward X W^T (CDSSM head)
+    (77, 45, 130, False, True, "tanh", 1),      # ragged edges
+    (300, 300, 150, False, False, "none", 1),   # dgrad dZ W
+    (150, 300, 4096, True, False, "none", 8),   # wgrad dZ^T X, split-K
+    (64, 64, 1000, True, True, "gelu", 1),      # both transposed
+    (513, 129, 17, False, False, "none", 3),    # split-K with a short last slice
+])
+def test_gemm_f32_matches_fp64(M, N, K, a_t, b_t, act, splits):
+    from dnn_page_vectors_amd.ops import dense as dops
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(*((K, M) if a_t else (M, K)), device=DEV, generator=g)
+    b = torch.randn(*((N, K) if b_t else (K, N)), device=DEV, generator=g)
+    bias = torch.randn(N, device=DEV, generator=g) if splits == 1 else None
+    out = dops.gemm_f32(a, b, a_t=a_t, b_t=b_t, bias=bias, act=act, splits=splits)
+    A = (a.t() if a_t else a).double()
+    B = (b.t() if b_t else b).double()
+    r = A @ B + (bias.double() if bias is not None else 0.0)
+    r = {"relu": torch.relu, "tanh": torch.tanh, "none": lambda t: t,
+         "gelu": lambda t: torch.nn.functional.gelu(t, approximate="tanh")}[act](r)
+    # exact fp32 products and sums: K-length rounding only (the bf16 path would be ~1e-2)
+    torch.testing.assert_close(out.double(), r, rtol=2e-5, atol=2e-5 * K ** 0.5)
+    if splits == 1:  # accumulate into an existing output
+        acc = torch.ones(M, N, device=DEV)
+        dops.gemm_f32(a, b, a_t=a_t, b_t=b_t, out=acc, accumulate=True)
+        torch.testing.assert_close(acc.double(), A @ B + 1.0, rtol=2e-5, atol=2e-5 * K ** 0.5)
+
+
 def test_cdssm_fp32_step_native_matches_torch_ops(monkeypatch):
-    """One dtype="fp32" CDSSM training step: the native fp32 conv tower gives the loss and the
-    flat gradient of the all-PyTorch fp32 path (PAGEVEC_F32_NATIVE=0)."""
+    """One dtype="fp32" CDSSM training step: the native fp32 conv tower, dense layers (fp32 MFMA
+    GEMM), L2 normalisation and explicit loss give the loss and the flat gradient of the
+    all-PyTorch fp32 path (PAGEVEC_F32_NATIVE=0)."""
+    from dnn_page_vectors_amd.ops import dense as dops
+    from dnn_page_vectors_amd.ops import loss as lops
     from dnn_page_vectors_amd.config import Configuration
     from dnn_page_vectors_amd.models import build_model
     from dnn_page_vectors_amd.parallel import dist as pdist
@@ -102,11 +133,16 @@ def test_cdssm_fp32_step_native_matches_torch_ops(monkeypatch):
     for native in (False, True):
         monkeypatch.setattr(_common, "F32_NATIVE", native)
         calls = _spy(monkeypatch)
+        lin, exp = [], []
+        orig_lin, orig_exp = dops._LinearF32Fn.apply, lops._ExplicitFn.apply
+        monkeypatch.setattr(dops._LinearF32Fn, "apply", lambda *a, o=orig_lin: lin.append(1) or o(*a))
+        monkeypatch.setattr(lops._ExplicitFn, "apply", lambda *a, o=orig_exp: exp.append(1) or o(*a))
         torch.manual_seed(0)
         tr = Trainer(cfg, build_model(cfg, V), torch.device(DEV))
         m = tr.train_step(q, d)
         torch.cuda.synchronize()
         assert bool(calls) == native
+        assert bool(lin) == native and bool(exp) == native, (len(lin), len(exp))
         out.append((float(m["loss"]), tr.flat.grad.clone()))
     (la, ga), (lb, gb) = out
     assert abs(la - lb) <= 1e-5 * max(1.0, abs(la))

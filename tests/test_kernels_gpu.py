@@ -1302,7 +1302,9 @@ def test_lazy_embedding_adam_matches_cpu(torch_style, E):
 @pytest.mark.parametrize("R,shape,dt", [(4096, (512,), torch.float32), (65536, (768,), torch.bfloat16),
                                         (8, (4096, 512), torch.float32), (3, (100,), torch.float32),
                                         (1000, (36,), torch.bfloat16), (16384, (150,), torch.float32),
-                                        (777, (3, 50), torch.float32), (65, (30,), torch.bfloat16)])
+                                        (777, (3, 50), torch.float32), (65, (30,), torch.bfloat16),
+                                        # wide and not 4-aligned: element loads at 16 quads per block
+                                        (2, (513, 129), torch.float32), (3, (4099,), torch.bfloat16)])
 def test_colsum_modes(R, shape, dt):
     """dense.hip::colsum_kernel (bias gradients, split-K sums) vs the fp32 torch sum:
     overwrite, accumulate into a non-zero buffer, and the scale / bias / activation epilogue."""
