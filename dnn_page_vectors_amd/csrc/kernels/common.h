@@ -67,15 +67,11 @@ __host__ __device__ __forceinline__ unsigned mix24(unsigned x) {
   x ^= x >> 15;
   return umul24(x, 0x9E3779u);
 }
-#ifdef PV_DROP_HASH_LEGACY  // quality A/B build only (tools/conv_variant_build.py): the round-5 mask stream
-__host__ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
-  return mix32(hrow + g * 0x9E3779B9u);
-}
-#else
+// (the round-5 stream, mix32(hrow + g * 0x9E3779B9) with nibble j = bits 4j..4j+3, was the A arm
+// of the quality A/B, profiles/r6/hash_quality_ab.txt; its build switch was removed after it)
 __host__ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, unsigned g) {
   return mix24(hrow + umul24(g, DROP_GROUP_STEP));
 }
-#endif
 
 // Nibble mode (thr % 16 == 0, p = k/16 — the reference's 0.25 is k = 4): element j (column
 // 8g + j) of a group reads the 4-bit value  h[P] h[P-8] h[P-4] h[P-12]  (MSB first) with
@@ -86,9 +82,6 @@ __host__ __device__ __forceinline__ unsigned dropout_group_hash(unsigned hrow, u
 // turn bits 15 / 31 of a word into the two 16-bit halves of a bf16-pair AND mask.
 __host__ __device__ __forceinline__ int dropout_nib_pos(int j) { return 15 - (j >> 1) + 16 * (j & 1); }
 __host__ __device__ __forceinline__ unsigned dropout_nibble(unsigned h, int j) {
-#ifdef PV_DROP_HASH_LEGACY
-  return (h >> (4 * j)) & 0xFu;
-#endif
   const int P = dropout_nib_pos(j);
   return (((h >> P) & 1u) << 3) | (((h >> (P - 8)) & 1u) << 2) | (((h >> (P - 4)) & 1u) << 1) | ((h >> (P - 12)) & 1u);
 }
@@ -98,11 +91,6 @@ __host__ __device__ __forceinline__ unsigned dropout_nibble(unsigned h, int j) {
 __device__ __forceinline__ unsigned rotl32(unsigned h, int r) { return __builtin_amdgcn_alignbit(h, h, 32 - r); }
 // word whose bit P_j is the keep decision of element j (other bits: don't care)
 __device__ __forceinline__ unsigned dropout_keep_word(unsigned h, int t) {
-#ifdef PV_DROP_HASH_LEGACY
-  unsigned lw = 0u;
-  for (int j = 0; j < 8; ++j) lw |= (dropout_nibble(h, j) >= (unsigned)t ? 1u : 0u) << dropout_nib_pos(j);
-  return lw;
-#endif
   if (t == 4) return h | rotl32(h, 8);                   // value >= 4: either of the two top bits
   if (t == 2) return h | rotl32(h, 8) | rotl32(h, 4);    // value >= 2: any of the three top bits
   if (t == 8) return h;                                  // value >= 8: the top bit

@@ -132,6 +132,7 @@ SIGS = {
     "pv_adam_rows": "pppp" "i" "pl" "p" "fffff" "i" "pp" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
+    "pv_sumsq_ticket": "p" "l" "ppp" "p",
     "pv_sumsq": "p" "l" "p" "p",
     "pv_scale": "p" "lf" "p",
     # gemm_mx8.hip

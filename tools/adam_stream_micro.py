@@ -28,7 +28,7 @@ def main():
     for n in [int(float(x)) for x in a.n.split(",")]:
         p, g, m, v = (torch.randn(n, device=dev) * 0.01 for _ in range(4))
         v.abs_()
-        t = torch.zeros(1, device=dev)
+        t = torch.zeros(2, device=dev)  # {step, warmup steps}
         s = stream(dev)
         res = {arm: [] for arm in arms}
         for _ in range(a.rounds):
