@@ -30,6 +30,22 @@ PV_DEBUG_FLAG
 
 constexpr float BCE_EPS = 1e-7f;
 
+// sum over the ns split planes of a partial-sum buffer at float4 index i (plane stride `plane`
+// float4s), in plane order — the loads issued eight at a time (a plane-at-a-time loop keeps one
+// load per lane in flight: the split sums of the loss glue ran at ~1.3 TB/s, latency-bound);
+// out-of-range loads read as zero, and x + 0 == x, so the sum is the sequential one bit for bit
+__device__ __forceinline__ f32x4 split_sum4(const f32x4* __restrict__ ws, size_t plane, size_t i, int ns) {
+  f32x4 a = ws[i];
+  for (int sp = 1; sp < ns; sp += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = sp + k < ns ? ws[(size_t)(sp + k) * plane + i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += v[k];
+  }
+  return a;
+}
+
 // q: (B, D) normalised, d: (B, 1+J, D) normalised (positive first).  One wave per row; the
 // query row lives in registers (MAXD floats per lane: D <= 64 MAXD), the 1+J raw cosines in
 // wave-uniform registers (J1 <= MAXJ); compile-time (MAXD, MAXJ) in {2, 4, 8, 16} x {16, 64}
@@ -907,9 +923,7 @@ __global__ __launch_bounds__(256) void ib_split_reduce_kernel(const float* __res
                                                               long n4, int ns) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 a = reinterpret_cast<const f32x4*>(ws)[i];
-    for (int sp = 1; sp < ns; ++sp) a += reinterpret_cast<const f32x4*>(ws)[(size_t)sp * n4 + i];
-    reinterpret_cast<f32x4*>(out)[i] = a;
+    reinterpret_cast<f32x4*>(out)[i] = split_sum4(reinterpret_cast<const f32x4*>(ws), (size_t)n4, (size_t)i, ns);
   }
 }
 
@@ -1164,10 +1178,12 @@ __global__ __launch_bounds__(256) void ib_grad_scale_kernel(const float* __restr
 // Forward finish, one wave per query row, after the fused ib7 forward + dQ-part pass:
 //   the positive logit (ib_pos's forward half: raw cosine s -> sraw, g*clip(s)), the split
 //   partial sums -> sumexp -> loss = g + log(sumexp) - g*clip(s) and P+ (ib_rowsum), the split
-//   partials of U -> U (ib_split_reduce), and the batch mean loss / accuracy (loss_stats): each
-//   workgroup stores its partial sums, and the workgroup that takes the last ticket of an
-//   agent-scope counter sums the partials in workgroup order (deterministic) and re-arms the
-//   counter for the next launch (capturable: no memset node).  Four launches -> one.
+//   partials of U -> U (ib_split_reduce), and each workgroup's partial sums of the batch mean
+//   loss / accuracy, which ib_stats_final_kernel (one workgroup) adds in workgroup order
+//   (deterministic, capturable).  Four launches -> two.  (A first version finished the batch sums
+//   in the workgroup that took the last ticket of an agent-scope counter: the release fence each
+//   workgroup needs before its ticket writes back its XCD's L2 — 74 vs 25 us per launch on the
+//   headline shape, step 7.007 vs 6.948 ms, profiles/r6/glue3/.)
 __global__ __launch_bounds__(256) void ib_fin_fwd_kernel(const unsigned short* __restrict__ X,
                                                          const unsigned short* __restrict__ Y,
                                                          const int* __restrict__ pos,
@@ -1176,12 +1192,10 @@ __global__ __launch_bounds__(256) void ib_fin_fwd_kernel(const unsigned short* _
                                                          int nx, int DP, float gamma, int clip,
                                                          float* __restrict__ sumexp, float* __restrict__ loss,
                                                          float* __restrict__ prob, float* __restrict__ sraw,
-                                                         float* __restrict__ bpart, unsigned* __restrict__ ticket,
-                                                         float* __restrict__ out_loss, float* __restrict__ out_acc) {
+                                                         float* __restrict__ bpart) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
   __shared__ float sl[4], sa[4];
-  __shared__ int last;
   float lrow = 0.f, arow = 0.f;
   if (row < nx) {
     const int p = pos[row];
@@ -1202,40 +1216,30 @@ __global__ __launch_bounds__(256) void ib_fin_fwd_kernel(const unsigned short* _
     lrow = l;
     arow = pr > 0.5f ? 1.f : 0.f;
     if (ws_u && ns > 1) {
-      const size_t plane = (size_t)nx * DP;
+      const size_t plane4 = (size_t)nx * DP / 4;
       for (int c = lane; c < DP / 4; c += 64) {
-        const size_t o = (size_t)row * DP + 4 * c;
-        f32x4 u = *reinterpret_cast<const f32x4*>(ws_u + o);
-        for (int sp = 1; sp < ns; ++sp) u += *reinterpret_cast<const f32x4*>(ws_u + sp * plane + o);
-        *reinterpret_cast<f32x4*>(U + o) = u;
+        const size_t o4 = (size_t)row * (DP / 4) + c;
+        reinterpret_cast<f32x4*>(U)[o4] = split_sum4(reinterpret_cast<const f32x4*>(ws_u), plane4, o4, ns);
       }
     }
   }
-  if (!ticket) return;
+  if (!bpart) return;
   if (lane == 0) {
     sl[w] = lrow;
     sa[w] = arow;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0)
     *reinterpret_cast<f32x2*>(bpart + 2 * blockIdx.x) = f32x2{(sl[0] + sl[1]) + (sl[2] + sl[3]),
                                                               (sa[0] + sa[1]) + (sa[2] + sa[3])};
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = atomicAdd(ticket, 1u);
-    const int is_last = t == gridDim.x - 1;
-    if (is_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    last = is_last;
-  }
-  __syncthreads();
-  if (!last) return;
-  // the last workgroup: every partial, summed in workgroup order by thread i (stride 256), then
-  // the 256 per-thread sums in thread order
+}
+
+// batch mean loss / accuracy from ib_fin_fwd_kernel's per-workgroup partials, summed in
+// workgroup order (thread i: workgroups i, i + 256, ...; then the 256 sums in thread order)
+__global__ __launch_bounds__(256) void ib_stats_final_kernel(const float* __restrict__ bpart, int nb, int nx,
+                                                             float* __restrict__ out_loss, float* __restrict__ out_acc) {
   float s = 0.f, a = 0.f;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
+  for (int b = threadIdx.x; b < nb; b += 256) {
     const f32x2 v = *reinterpret_cast<const f32x2*>(bpart + 2 * b);
     s += v[0];
     a += v[1];
@@ -1253,7 +1257,6 @@ __global__ __launch_bounds__(256) void ib_fin_fwd_kernel(const unsigned short* _
     const float inv = 1.f / (float)nx;
     *out_loss = S * inv;
     if (out_acc) *out_acc = A * inv;
-    *ticket = 0u;  // re-armed for the next launch
   }
 }
 
@@ -1270,8 +1273,7 @@ __global__ __launch_bounds__(256) void ib_fin_dd_kernel(const float* __restrict_
   const long n4 = (long)nrows * per;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 a = reinterpret_cast<const f32x4*>(ws)[i];
-    for (int sp = 1; sp < ns; ++sp) a += reinterpret_cast<const f32x4*>(ws)[(size_t)sp * n4 + i];
+    f32x4 a = split_sum4(reinterpret_cast<const f32x4*>(ws), (size_t)n4, (size_t)i, ns);
     const int m = (int)(i / per), c = 4 * (int)(i - (long)m * per);
     const int b = inv[m];
     if (b >= 0) {
@@ -1648,11 +1650,11 @@ PV_API int pv_ibw(const void* O, int no, const void* It, int ni, int DP, const f
 // ---- fused in-batch loss glue (round 6): see ib_fin_fwd_kernel / ib_fin_dd_kernel ----------
 // Forward: the ib7 (or ib5 / ib3) forward + dQ-part pass, then ONE finish launch.  pos (nx)
 // positive page per query; sraw (nx) receives the raw positive cosines the backward needs;
-// bpart: 2 * ceil(nx / 4) floats; ticket: one zero-initialised u32 per concurrent use (re-armed
-// by the kernel); out_loss / out_acc: 0-dim outputs (null ticket: no batch statistics).
+// bpart: 2 * ceil(nx / 4) floats of workgroup partials; out_loss / out_acc: 0-dim outputs (null
+// bpart / out_loss: no batch statistics).
 PV_API int pv_ib_fwd_dq2(const void* X, const void* Y, const int* pos, float* sumexp, float* U, float* ws_u,
                          float* part, int nx, int ny, int DP, float gamma, int clip, float* sraw, float* loss,
-                         float* prob, float* bpart, unsigned* ticket, float* out_loss, float* out_acc, void* stream) {
+                         float* prob, float* bpart, float* out_loss, float* out_acc, void* stream) {
   using namespace pv::loss;
   if (DP % 32 || DP > 192 || nx < 1) return -2;
   int ns, per;
@@ -1682,10 +1684,16 @@ PV_API int pv_ib_fwd_dq2(const void* X, const void* Y, const int* pos, float* su
   if (clip) { PV_IB_FWDDQ2(true); } else { PV_IB_FWDDQ2(false); }
 #undef PV_IB_FWDDQ2
   PV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ib_fin_fwd_kernel, dim3((nx + 3) / 4), dim3(256), 0, s, (const unsigned short*)X,
+  const int nb = (nx + 3) / 4;
+  const bool stats = bpart && out_loss;
+  hipLaunchKernelGGL(ib_fin_fwd_kernel, dim3(nb), dim3(256), 0, s, (const unsigned short*)X,
                      (const unsigned short*)Y, pos, part, ns, ns > 1 ? ws_u : nullptr, U, nx, DP, gamma, clip, sumexp,
-                     loss, prob, sraw, bpart, ticket, out_loss, out_acc);
+                     loss, prob, sraw, stats ? bpart : nullptr);
   PV_LAUNCH_CHECK();
+  if (stats) {
+    hipLaunchKernelGGL(ib_stats_final_kernel, dim3(1), dim3(256), 0, s, (const float*)bpart, nb, nx, out_loss, out_acc);
+    PV_LAUNCH_CHECK();
+  }
   return 0;
 }
 

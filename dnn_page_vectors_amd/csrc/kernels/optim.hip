@@ -246,74 +246,6 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   }
 }
 
-// The same sums without a zeroed output or atomics on it (round 6): each workgroup stores its
-// (sum, flag) pair, the workgroup that takes the last ticket (agent-scope release fence, ticket
-// add, acquire fence) adds the pairs in workgroup order, writes out2 and re-arms the ticket —
-// deterministic, capturable, and the output needs no fill kernel before the launch.
-__global__ __launch_bounds__(256) void sumsq_ticket_kernel(const float* __restrict__ x, long n, float* __restrict__ out2,
-                                                           float* __restrict__ part, unsigned* __restrict__ ticket) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long stride = (long)gridDim.x * blockDim.x;
-  const long n4 = ((uintptr_t)x & 15) ? 0 : n / 4;
-  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
-  float s = 0.f, bad = 0.f;
-  long i = t;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    const f32x4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
-    sq_acc(a, s, bad);
-    sq_acc(b, s, bad);
-    sq_acc(c, s, bad);
-    sq_acc(d, s, bad);
-  }
-  for (; i < n4; i += stride) sq_acc(x4[i], s, bad);
-  for (long j = n4 * 4 + t; j < n; j += stride) {
-    const float v = x[j];
-    if (!isfinite(v)) bad = 1.f;
-    else s += v * v;
-  }
-  s = wave_sum(s);
-  bad = wave_max(bad);
-  __shared__ float ws[4], wb[4];
-  __shared__ int last;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) { ws[w] = s; wb[w] = bad; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    *reinterpret_cast<f32x2*>(part + 2 * blockIdx.x) =
-        f32x2{(ws[0] + ws[1]) + (ws[2] + ws[3]), fmaxf(fmaxf(wb[0], wb[1]), fmaxf(wb[2], wb[3]))};
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned tk = atomicAdd(ticket, 1u);
-    const int is_last = tk == gridDim.x - 1;
-    if (is_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    last = is_last;
-  }
-  __syncthreads();
-  if (!last) return;
-  float S = 0.f, B = 0.f;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
-    const f32x2 v = *reinterpret_cast<const f32x2*>(part + 2 * b);
-    S += v[0];
-    B = fmaxf(B, v[1]);
-  }
-  __shared__ float ts[256], tb[256];
-  ts[threadIdx.x] = S;
-  tb[threadIdx.x] = B;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float tot = 0.f, fl = 0.f;
-    for (int k = 0; k < 256; ++k) {
-      tot += ts[k];
-      fl = fmaxf(fl, tb[k]);
-    }
-    *reinterpret_cast<f32x2*>(out2) = f32x2{tot, fl};
-    *ticket = 0u;  // re-armed for the next launch
-  }
-}
-
 __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long stride = (long)gridDim.x * blockDim.x;
@@ -446,18 +378,6 @@ PV_API int pv_adam(float* p, const float* g, float* m, float* v, long n, int ste
 PV_API int pv_cast_pad_bf16(const float* in, void* out, long rows, int cols, int ldo, void* stream) {
   hipLaunchKernelGGL(pv::optim::cast_pad_bf16_kernel, dim3(grid_for(rows * ldo, 4)), dim3(256), 0,
                      (hipStream_t)stream, in, (unsigned short*)out, rows, cols, ldo);
-  PV_LAUNCH_CHECK();
-  return 0;
-}
-
-// out2 (2 floats, any content) = {sum x^2, non-finite flag}; part: 2 * 512 floats of scratch;
-// ticket: one zero-initialised u32 per concurrent use (re-armed by the kernel)
-PV_API int pv_sumsq_ticket(const float* x, long n, float* out2, float* part, unsigned* ticket, void* stream) {
-  if (n < 1 || !part || !ticket) return -1;
-  unsigned blocks = grid_for(n, 16);
-  if (blocks > 512) blocks = 512;
-  hipLaunchKernelGGL(pv::optim::sumsq_ticket_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, out2, part,
-                     ticket);
   PV_LAUNCH_CHECK();
   return 0;
 }

@@ -79,7 +79,7 @@ SIGS = {
     "pv_ib_rows_blk": "p" "iii" "pp" "fi" "p",
     "pv_ib_rowsum": "pp" "ii" "ppp" "f" "p",
     "pv_ib_version": "",
-    "pv_ib_fwd_dq2": "ppppppp" "iii" "f" "i" "ppppppp" "p",
+    "pv_ib_fwd_dq2": "ppppppp" "iii" "f" "i" "pppppp" "p",
     "pv_ib_grad_scale_pos": "pifpifpipppppp" "ip",
     "pv_ib_bwd_dd_pos": "ppppp" "iii" "f" "i" "ppp" "p",
     "pv_ib_set_version": "i",
@@ -132,7 +132,6 @@ SIGS = {
     "pv_adam_rows": "pppp" "i" "pl" "p" "fffff" "i" "pp" "p",
     "pv_adam": "pppp" "li" "fffff" "i" "p" "p",
     "pv_cast_pad_bf16": "pp" "lii" "p",
-    "pv_sumsq_ticket": "p" "l" "ppp" "p",
     "pv_sumsq": "p" "l" "p" "p",
     "pv_scale": "p" "lf" "p",
     # gemm_mx8.hip

@@ -142,14 +142,6 @@ def _grad_prologue(gl: torch.Tensor, reduce: bool, B: int, gamma: float, sumexp:
 
 
 FUSED_GLUE = True  # tests: False runs the round-5 glue launches (the fused path's oracle)
-_TICKETS = {}  # device -> u32 counter of the fused forward finish's last-workgroup reduction
-
-
-def _ticket(dev: torch.device) -> torch.Tensor:
-    t = _TICKETS.get(dev)
-    if t is None:
-        t = _TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-    return t
 
 
 def _pos_inverse(pos: torch.Tensor, M: int) -> Optional[torch.Tensor]:
@@ -201,14 +193,13 @@ class _InBatchFn(torch.autograd.Function):
             U = torch.empty(B, DP, dtype=torch.float32, device=dev)
             ws = torch.empty(max(L_.pv_ib_bwd_ws(B, M, DP), 1), dtype=torch.float32, device=dev)
             part = torch.empty(L_.pv_ib_fwd_dq_parts(B, M), dtype=torch.float32, device=dev)
-            lm = acc = bpart = tk = None
+            lm = acc = bpart = None
             if reduce:
                 lm = torch.empty((), dtype=torch.float32, device=dev)
                 acc = torch.empty((), dtype=torch.float32, device=dev)
                 bpart = torch.empty(2 * ((B + 3) // 4), dtype=torch.float32, device=dev)
-                tk = _ticket(dev)
             check(L_.pv_ib_fwd_dq2(P(qb), P(db), P(pos), P(sumexp), P(U), P(ws), P(part), B, M, DP, float(gamma),
-                                   int(clip), P(sraw), P(loss), P(prob), P(bpart), P(tk), P(lm), P(acc),
+                                   int(clip), P(sraw), P(loss), P(prob), P(bpart), P(lm), P(acc),
                                    stream(dev)), "pv_ib_fwd_dq2")
             ctx.save_for_backward(qb, db, pos, sumexp, U, sraw, inv)
             ctx.fused = True
