@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--D", type=int, default=150)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ib", default="5,3", help="kernel generations to time (loss.hip pv_ib_set_version)")
+    ap.add_argument("--glue", default="1", help="ops/loss.py FUSED_GLUE values to time (1 fused finish kernels, "
+                                                 "0 the round-5 glue launches)")
     a = ap.parse_args()
     from dnn_page_vectors_amd.ops._common import lib
     dev = torch.device("cuda")
@@ -47,8 +49,9 @@ def main():
         d = dn.clone().requires_grad_(True)
         lr, _ = ref.inbatch_softmax_loss(q, d, pos, 10.0, True)
         lr.sum().backward()
-        for ver in [int(v) for v in a.ib.split(",")]:
+        for ver, glue in [(int(v), int(gl)) for v in a.ib.split(",") for gl in a.glue.split(",")]:
             assert lib().pv_ib_set_version(ver) == 0
+            L.FUSED_GLUE = bool(glue)
             l, gq, gd = run(qn, dn, pos)
             e = [float((l - lr.detach()).abs().max()), float((gq - q.grad).abs().max() / q.grad.abs().max()),
                  float((gd - d.grad).abs().max() / d.grad.abs().max())]
@@ -82,7 +85,7 @@ def main():
             torch.cuda.synchronize()
             tg = ev0.elapsed_time(ev1) / a.iters / 1e3
             fl = 2.0 * a.B * M * 160 * 5
-            print(f"ib{ver} M={M}: fwd+bwd {t*1e3:.3f} ms host-synced per call incl. clones ({fl / t / 1e12:.0f} TF/s), "
+            print(f"ib{ver}{'' if glue else ' (round-5 glue)'} M={M}: fwd+bwd {t*1e3:.3f} ms host-synced per call incl. clones ({fl / t / 1e12:.0f} TF/s), "
                   f"{tg*1e3:.3f} ms GPU back to back ({fl / tg / 1e12:.0f} TF/s); "
                   f"err loss {e[0]:.2e} dq {e[1]:.2e} dd {e[2]:.2e}", flush=True)
 
