@@ -144,12 +144,14 @@ def _grad_prologue(gl: torch.Tensor, reduce: bool, B: int, gamma: float, sumexp:
 FUSED_GLUE = True  # tests: False runs the round-5 glue launches (the fused path's oracle)
 
 
-def _pos_inverse(pos: torch.Tensor, M: int) -> Optional[torch.Tensor]:
+def _pos_inverse(pos: torch.Tensor, M: int, owner: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """inv (M,) int32: the query whose positive page row m is, -1 for none; None when two queries
-    share a positive (the fused dD finish needs a one-to-one map).  Cached on the pos tensor (the
-    trainer keeps one per shape); built eagerly, never inside a capture."""
-    key = (M, pos.data_ptr(), pos.numel())
-    hit = getattr(pos, "_pv_inv", None)
+    share a positive (the fused dD finish needs a one-to-one map).  Cached on ``owner`` (the
+    caller's index tensor, before any dtype conversion; the trainer keeps one per shape): a miss
+    costs host syncs (min / max / unique); built eagerly, never inside a capture."""
+    owner = pos if owner is None else owner
+    key = (M, owner.data_ptr(), owner.numel(), owner.dtype)
+    hit = getattr(owner, "_pv_inv", None)
     if hit is not None and hit[0] == key:
         return hit[1]
     if torch.cuda.is_current_stream_capturing():
@@ -159,7 +161,7 @@ def _pos_inverse(pos: torch.Tensor, M: int) -> Optional[torch.Tensor]:
     if p.numel() == 0 or (int(p.min()) >= 0 and int(p.max()) < M and torch.unique(p).numel() == p.numel()):
         inv = torch.full((M,), -1, dtype=torch.int32, device=pos.device)
         inv[p] = torch.arange(p.numel(), dtype=torch.int32, device=pos.device)
-    pos._pv_inv = (key, inv)
+    owner._pv_inv = (key, inv)
     return inv
 
 
@@ -179,8 +181,9 @@ class _InBatchFn(torch.autograd.Function):
             raise ValueError("in-batch loss kernel supports D <= 192")
         qb = _pad_bf16(qn, DP)
         db = _pad_bf16(dn, DP)
+        pos_in = pos
         pos = pos.to(torch.int32).contiguous()
-        inv = _pos_inverse(pos, M) if ctx.needs_input_grad[0] and FUSED_GLUE else None
+        inv = _pos_inverse(pos, M, pos_in) if ctx.needs_input_grad[0] and FUSED_GLUE else None
         ctx.reduce = bool(reduce)
         ctx.meta = (B, M, D, DP, float(gamma), int(clip))
         if inv is not None:

@@ -43,7 +43,7 @@ def main():
         dn[: a.B] = torch.nn.functional.normalize(qn + 0.5 * dn[: a.B], dim=1)  # positives correlated
         qn = qn.bfloat16().float()
         dn = dn.bfloat16().float()
-        pos = torch.arange(a.B, device=dev)
+        pos = torch.arange(a.B, device=dev, dtype=torch.int32)  # as the trainer keeps it
         # fp32 oracle
         q = qn.clone().requires_grad_(True)
         d = dn.clone().requires_grad_(True)
@@ -66,13 +66,14 @@ def main():
             # GPU time of the same fwd + bwd back to back (CUDA events, no host sync between
             # iterations: the launch latency overlaps as it does inside a training step; the
             # leaves are built once, their .grad reset to None)
-            q = qn.clone().requires_grad_(True)
-            d = dn.clone().requires_grad_(True)
+            # (own leaves: q / d keep the fp32 oracle's gradients for the next generation's errors)
+            qt = qn.clone().requires_grad_(True)
+            dt = dn.clone().requires_grad_(True)
 
             def step():
-                q.grad = None
-                d.grad = None
-                loss, _ = L.inbatch_loss(q, d, pos, 10.0, True)
+                qt.grad = None
+                dt.grad = None
+                loss, _ = L.inbatch_loss(qt, dt, pos, 10.0, True)
                 loss.sum().backward()
 
             step()
