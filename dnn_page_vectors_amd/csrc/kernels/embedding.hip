@@ -268,6 +268,10 @@ __global__ void bag_counts_kernel(const int* __restrict__ ids, unsigned short* _
 // LDS atomics (no CAS loops on global bf16 cells, no contention between bags), then
 // writes the WHOLE bf16 row (zeros included) with 8-byte stores — the caller does not
 // have to clear the (N, ldc) matrix.
+// Vocabularies wider than HIST_MAX (word level): blockIdx.y walks windows of HIST_MAX ids, each
+// block re-reading its page's ids (round 6: the previous wide-vocabulary kernel added bf16 +1.0
+// by compare-and-swap on the count matrix, so a count stuck at 256 — 256 + 1 rounds to 256 in
+// bf16 — for any id repeated more than 256 times in a page).
 constexpr int HIST_MAX = 38912;  // 152 KB of u32 counters
 __global__ __launch_bounds__(1024) void bag_counts_lds_kernel(const int* __restrict__ ids,
                                                               unsigned short* __restrict__ counts,
@@ -276,7 +280,8 @@ __global__ __launch_bounds__(1024) void bag_counts_lds_kernel(const int* __restr
   extern __shared__ unsigned hist[];
   __shared__ int part[16];
   const int n = blockIdx.x;
-  for (int c = threadIdx.x; c < ldc; c += blockDim.x) hist[c] = 0u;
+  const int v0 = blockIdx.y * HIST_MAX, w = min(HIST_MAX, ldc - v0);  // this window's ids
+  for (int c = threadIdx.x; c < w; c += blockDim.x) hist[c] = 0u;
   __syncthreads();
   const int* row = ids + (size_t)n * L;
   int local = 0;
@@ -285,18 +290,18 @@ __global__ __launch_bounds__(1024) void bag_counts_lds_kernel(const int* __restr
     PV_CHECK(v == pad || (v >= 0 && v < V), PV_ERR_ID);
     if (v != pad && v >= 0 && v < V) {
       ++local;
-      atomicAdd(&hist[v], 1u);
+      if (v >= v0 && v < v0 + w) atomicAdd(&hist[v - v0], 1u);
     }
   }
   for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
   __syncthreads();
-  uint2* crow = reinterpret_cast<uint2*>(counts + (size_t)n * ldc);
-  for (int c4 = threadIdx.x; c4 < ldc / 4; c4 += blockDim.x) {
+  uint2* crow = reinterpret_cast<uint2*>(counts + (size_t)n * ldc + v0);
+  for (int c4 = threadIdx.x; c4 < w / 4; c4 += blockDim.x) {
     const unsigned* h = hist + 4 * c4;
     crow[c4] = uint2{pack_bf16x2((float)h[0], (float)h[1]), pack_bf16x2((float)h[2], (float)h[3])};
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && blockIdx.y == 0) {
     int s = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
     lens[n] = (float)s;
@@ -476,6 +481,22 @@ PV_API int pv_bag_counts(const int* ids, void* counts, float* lens, int N, int L
     }
     hipLaunchKernelGGL(pv::embed::bag_counts_lds_kernel, dim3(N), dim3(1024), ldc * sizeof(unsigned),
                        (hipStream_t)stream, ids, (unsigned short*)counts, lens, N, L, V, ldc, pad);
+    PV_LAUNCH_CHECK();
+    return 0;
+  }
+  if ((ldc & 3) == 0) {  // wide vocabularies: windows of HIST_MAX ids (every element written)
+    static bool attrw = false;
+    if (!attrw) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&pv::embed::bag_counts_lds_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              pv::embed::HIST_MAX * (int)sizeof(unsigned)) != hipSuccess)
+        return -3;
+      attrw = true;
+    }
+    const int nwin = (ldc + pv::embed::HIST_MAX - 1) / pv::embed::HIST_MAX;
+    hipLaunchKernelGGL(pv::embed::bag_counts_lds_kernel, dim3(N, nwin), dim3(1024),
+                       pv::embed::HIST_MAX * sizeof(unsigned), (hipStream_t)stream, ids, (unsigned short*)counts,
+                       lens, N, L, V, ldc, pad);
     PV_LAUNCH_CHECK();
     return 0;
   }

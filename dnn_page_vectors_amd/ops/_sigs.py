@@ -144,6 +144,9 @@ SIGS = {
     "pv_bag_set_dbg": "i",
     "pv_bag_groups": "i",
     "pv_bag_rle": "pppppppp" "iiii" "p",
+    "pv_bagd_fwd": "pipp" "iiii" "p",
+    "pv_bagd_splits": "iiiii",
+    "pv_bagd_wgrad": "pippp" "ii" "iii" "p",
     "pv_bag_mm_fwd": "pppp" "iii" "i" "p",
     "pv_bag_mm_wgrad": "pppp" "ii" "iii" "p",
 }

@@ -37,10 +37,11 @@ _HIST_MAX = 38912  # csrc/kernels/embedding.hip HIST_MAX
 def _counts(ids: torch.Tensor, V: int, pad: int):
     N, L = ids.shape
     ldc = (V + 63) // 64 * 64
-    small = ldc <= _HIST_MAX  # LDS-histogram kernel writes every element itself (ldc % 64 == 0)
-    C = (torch.empty if small else torch.zeros)(N, ldc, dtype=torch.bfloat16, device=ids.device)
+    # the LDS-histogram kernels write every element (ldc % 64 == 0; vocabularies wider than
+    # _HIST_MAX in windows of it): no zero fill
+    C = torch.empty(N, ldc, dtype=torch.bfloat16, device=ids.device)
     lens = torch.empty(N, dtype=torch.float32, device=ids.device)
-    check(lib().pv_bag_counts(P(ids), P(C), P(lens), N, L, V, ldc, pad, int(not small), stream(ids.device)),
+    check(lib().pv_bag_counts(P(ids), P(C), P(lens), N, L, V, ldc, pad, 0, stream(ids.device)),
           "pv_bag_counts")
     return C, lens
 
@@ -93,11 +94,43 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor
 # in-tree MFMA products that build each count tile in LDS (no N x V matrix).  Measured at the
 # MLP shape (tools/bag_gemm_micro.py, profiles/r5_bag/README.md): forward 134 vs 145 us, weight
 # gradient 243 vs 136 us, list build 300 vs 45 us (counts) — the library plan stays the default.
+# "dense" (round 6) = the same dense bf16 count matrix as "lib", multiplied on in-tree MFMA
+# kernels that stream both operands by LDS-DMA (bag_gemm.hip bagd_mm_kernel): forward C W and
+# weight gradient (Gt C)^T with no library GEMM.
 BAG_GEMM = os.environ.get("PAGEVEC_BAG_GEMM", "lib")
 
 
 def _rle_ok(N: int, L: int, V: int, E: int) -> bool:
     return BAG_GEMM == "hip" and L <= 8192 and E % 8 == 0 and V <= 65536
+
+
+def _dense_ok(C: torch.Tensor, W16: torch.Tensor, V: int, E: int) -> bool:
+    return (BAG_GEMM == "dense" and E % 8 == 0 and C.dtype == torch.bfloat16 and C.shape[1] % 64 == 0
+            and W16 is not None and W16.dtype == torch.bfloat16 and W16.is_contiguous() and tuple(W16.shape) == (V, E))
+
+
+def _dense_forward_partials(C: torch.Tensor, W16: torch.Tensor, V: int) -> torch.Tensor:
+    """(splits, N, E) fp32 partial products C[:, slice] @ W16[slice] on bagd_mm_kernel (~256
+    workgroups: split-K over the vocabulary)."""
+    N, ldc = C.shape
+    E = W16.shape[1]
+    tiles = -(-N // 256) * -(-E // 128)
+    want = max(1, min(ldc // 64, round(256 / tiles)))
+    ns = int(lib().pv_bagd_splits(N, V, E, ldc, want))
+    part = torch.empty(ns, N, E, dtype=torch.float32, device=C.device)
+    check(lib().pv_bagd_fwd(P(C), ldc, P(W16), P(part), N, V, E, want, stream(C.device)), "pv_bagd_fwd")
+    return part
+
+
+def _dense_weight_grad(C: torch.Tensor, gs: torch.Tensor, V: int, out: torch.Tensor) -> None:
+    """out (V, E) fp32 (row stride out.stride(0)) = C[:, :V]^T gs on bagd_mm_kernel (gs (N, E) bf16
+    transposed to a zero-padded (E, ceil64(N)) scratch first)."""
+    N, ldc = C.shape
+    E = gs.shape[1]
+    Np = -(-N // 64) * 64
+    ws = torch.empty(E, Np, dtype=torch.bfloat16, device=C.device)
+    check(lib().pv_bagd_wgrad(P(C), ldc, P(gs.contiguous()), P(ws), P(out), int(out.stride(0)), 0, N, V, E,
+                              stream(C.device)), "pv_bagd_wgrad")
 
 
 class _Rle:
@@ -216,7 +249,12 @@ class _BagFn(torch.autograd.Function):
             keys = None
         else:
             C, lens = _counts(ids, V, pad)
-            out = _counts_gemm(C[:, :V], W16, lens if mean else None, bf, act)
+            if _dense_ok(C, W16, V, E):  # in-tree MFMA product, split-K partials + fused epilogue
+                out = dops.colsum(_dense_forward_partials(C, W16, V), scale=lens if mean else None, bias=bf,
+                                  act=act, scale_is_len=True)
+                ctx.dense = True
+            else:
+                out = _counts_gemm(C[:, :V], W16, lens if mean else None, bf, act)
             keys = None
         ctx.rle = rle
         ctx.sparse = (L, E) if C is None and rle is None else None
@@ -314,6 +352,16 @@ def _counts_backward(ctx, g, C, lens, y, rle=None):
         dW = torch.empty(V, E, dtype=torch.float32, device=g.device)
         rle.weight_grad(gs, dW, accumulate=False)
         return None, dW, None, None, None, None, db, None, None
+    if getattr(ctx, "dense", False):  # bag_gemm.hip bagd_mm_kernel: (Gt C)^T stored as dW rows
+        tw = grad_sink.write_target(W)
+        if tw is not None and tw.is_contiguous() and tw.data_ptr() % 16 == 0:
+            _dense_weight_grad(C, gs, V, tw)
+            grad_sink.done(W)
+            return None, None, None, None, None, None, db, None, None
+        if tw is None:
+            dW = torch.empty(V, gs.shape[1], dtype=torch.float32, device=g.device)
+            _dense_weight_grad(C, gs, V, dW)
+            return None, dW, None, None, None, None, db, None, None
     Ct = C[:, :V].t()
     tw = grad_sink.write_target(W)  # fp32-output GEMM straight into the flat gradient
     if tw is not None:

@@ -82,6 +82,32 @@ def test_bag_rle_and_products_match_fp64(N, L, V, E):
     close(acc, base.double() + ref_dw)
 
 
+@pytest.mark.parametrize("N,L,V,E", [(4096, 2000, 30000, 512), (300, 130, 1000, 72), (37, 512, 65000, 128),
+                                     (513, 300, 30000, 256)])
+def test_bag_dense_products_match_fp64(N, L, V, E):
+    """The dense-count in-tree arm (PAGEVEC_BAG_GEMM=dense, bagd_mm_kernel): the histogram's bf16
+    count matrix times W (split-K partials) and C^T Gs into a strided dW, vs fp64."""
+    torch.manual_seed(1)
+    ids = _ids(N, L, V, seed=N + 2 * V)
+    C16, lens = eops._counts(ids, V, 0)
+    Cb = _dense_counts(ids, V).float().bfloat16().double()
+    torch.testing.assert_close(C16[:, :V].double(), Cb, rtol=0, atol=0)
+
+    def close(got, want):
+        err = float((got.double() - want).abs().max())
+        assert err <= 2e-6 * float(want.abs().max()) + 1e-5, (err, float(want.abs().max()))
+
+    W = torch.randn(V, E, device=DEV).bfloat16()
+    part = eops._dense_forward_partials(C16, W, V)
+    close(part.double().sum(0), Cb @ W.double())
+    gs = torch.randn(N, E, device=DEV).bfloat16()
+    base = torch.full((V, E + 8), 7.0, device=DEV)
+    out = base[:, :E]  # strided target, padding untouched
+    eops._dense_weight_grad(C16, gs, V, out)
+    close(out, Cb.t() @ gs.double())
+    assert bool((base[:, E:] == 7.0).all())
+
+
 def test_bag_hip_matches_library_plan_end_to_end(monkeypatch):
     """The MLP page bag (mean, bias, tanh) with its W / bias gradients: in-tree kernels vs the
     hipBLASLt counts plan vs fp32 torch."""
@@ -91,7 +117,7 @@ def test_bag_hip_matches_library_plan_end_to_end(monkeypatch):
     b0 = torch.randn(E, device=DEV) * 0.3
     gy = torch.randn(N, E, device=DEV)
     res = {}
-    for arm in ("hip", "lib"):
+    for arm in ("hip", "lib", "dense"):
         monkeypatch.setattr(eops, "BAG_GEMM", arm)
         W = W0.clone().requires_grad_(True)
         b = b0.clone().requires_grad_(True)
@@ -103,7 +129,7 @@ def test_bag_hip_matches_library_plan_end_to_end(monkeypatch):
     cnt = (ids != 0).sum(1, keepdim=True).clamp(min=1).float()
     yr = torch.tanh(ref.embedding_bag_sum(ids, Wr, 0) / cnt + br)
     (yr * gy).sum().backward()
-    for arm in ("hip", "lib"):
+    for arm in ("hip", "lib", "dense"):
         y, gW, gb = res[arm]
         torch.testing.assert_close(y, yr, rtol=2e-2, atol=2e-2)
         for got, want in ((gW, Wr.grad), (gb, br.grad)):
@@ -111,6 +137,12 @@ def test_bag_hip_matches_library_plan_end_to_end(monkeypatch):
             assert err < 2e-2, (arm, err)
     # the two device arms agree far tighter than either does with fp32 (same bf16 operands)
     torch.testing.assert_close(res["hip"][0], res["lib"][0], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(res["dense"][0], res["lib"][0], rtol=1e-4, atol=1e-4)
+    # dW: the two in-tree arms (both checked against fp64 above) agree to fp32 summation order;
+    # the library GEMM's own rounding sits further off (~4e-3 of an element, 1e-3 of the max)
+    torch.testing.assert_close(res["dense"][1], res["hip"][1], rtol=1e-4, atol=1e-5)
+    err = float((res["dense"][1] - res["lib"][1]).abs().max() / res["lib"][1].abs().max())
+    assert err < 2e-3, err
 
 
 def test_chunked_fp8_bag_backward_uses_segment_lists(monkeypatch):
