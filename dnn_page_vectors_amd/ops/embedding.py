@@ -18,6 +18,7 @@ token's run of dY rows into dW (MLP query tower, N 4096 x L 45: ~0.19 ms of coun
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Optional
 
@@ -96,8 +97,34 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor
 # gradient 243 vs 136 us, list build 300 vs 45 us (counts) — the library plan stays the default.
 # "dense" (round 6) = the same dense bf16 count matrix as "lib", multiplied on in-tree MFMA
 # kernels that stream both operands by LDS-DMA (bag_gemm.hip bagd_mm_kernel): forward C W and
-# weight gradient (Gt C)^T with no library GEMM.
-BAG_GEMM = os.environ.get("PAGEVEC_BAG_GEMM", "lib")
+# weight gradient (Gt C)^T with no library GEMM.  Measured (profiles/r6/bagd/): the eager MLP
+# step 1.485 -> 1.356 and 1.294 -> 1.207 ms (same process, two boxes: the library calls' host
+# cost sits on the step), but inside a captured graph the library GEMMs are faster (kernel time
+# 160 + 129 vs 172 + 152 us; bench 1.033-1.050 vs 1.063-1.072 ms alternated on one box).
+# "auto" (default): dense for eager steps, lib inside a hipGraph capture.
+BAG_GEMM = os.environ.get("PAGEVEC_BAG_GEMM", "auto")
+
+
+_BAG_SCOPE = [None]
+
+
+@contextlib.contextmanager
+def bag_gemm_scope(plan: Optional[str]):
+    """Fix the "auto" choice for a block (the trainer: "lib" for graph-mode trainers, whose eager
+    warm-up steps must initialise the library before the capture)."""
+    prev, _BAG_SCOPE[0] = _BAG_SCOPE[0], plan
+    try:
+        yield
+    finally:
+        _BAG_SCOPE[0] = prev
+
+
+def _bag_gemm() -> str:
+    if BAG_GEMM != "auto":
+        return BAG_GEMM
+    if _BAG_SCOPE[0] is not None:
+        return _BAG_SCOPE[0]
+    return "lib" if torch.cuda.is_current_stream_capturing() else "dense"
 
 
 def _rle_ok(N: int, L: int, V: int, E: int) -> bool:
@@ -105,7 +132,7 @@ def _rle_ok(N: int, L: int, V: int, E: int) -> bool:
 
 
 def _dense_ok(C: torch.Tensor, W16: torch.Tensor, V: int, E: int) -> bool:
-    return (BAG_GEMM == "dense" and E % 8 == 0 and C.dtype == torch.bfloat16 and C.shape[1] % 64 == 0
+    return (_bag_gemm() == "dense" and E % 8 == 0 and C.dtype == torch.bfloat16 and C.shape[1] % 64 == 0
             and W16 is not None and W16.dtype == torch.bfloat16 and W16.is_contiguous() and tuple(W16.shape) == (V, E))
 
 
@@ -229,6 +256,8 @@ class _BagFn(torch.autograd.Function):
             fp8_bwd = want and FP8_BWD and E % 4 == 0
             use_rle = want and not fp8_bwd and _rle_ok(N, L, V, E)
             C8, C, lens = _counts8(ids, V, pad, want and not use_rle and not fp8_bwd)
+            if C is not None and not fp8_bwd and _bag_gemm() == "dense" and E % 8 == 0 and C.shape[1] % 64 == 0:
+                ctx.dense = True  # the bf16 weight gradient C^T G on bagd_mm_kernel
             if use_rle:  # the weight gradient's counts as segment lists (bag_gemm.hip), not bf16 C
                 rle = _Rle(ids, V, pad)
             if fp8_bwd:  # the e4m3 counts serve the weight gradient too (no bf16 N x V matrix)

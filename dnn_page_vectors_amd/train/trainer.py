@@ -33,6 +33,7 @@ from ..ops import determinism
 from ..ops import grad_sink
 from ..ops import loss as lops
 from ..ops._common import precision_scope
+from ..ops import embedding as eops
 from ..ops.optim import FlatAdam, FlatParams, grad_sumsq_and_finite
 from ..parallel import dist as pdist
 from ..parallel import placement
@@ -272,6 +273,13 @@ class Trainer:
     GRAPH_WARMUP = 2
 
     def train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
+        # long-bag GEMMs (ops/embedding.py PAGEVEC_BAG_GEMM=auto): the library inside graphs and
+        # in the eager steps that warm a capture up (its first call may not happen in a capture),
+        # the in-tree kernels for eager-only trainers
+        with eops.bag_gemm_scope("lib" if self.graph_mode else None):
+            return self._train_step(q_ids, d_ids)
+
+    def _train_step(self, q_ids: torch.Tensor, d_ids: torch.Tensor) -> Dict[str, torch.Tensor]:
         if self.step == self._fault_step:
             raise InjectedFault(f"injected fault at step {self.step}")
         determinism.ensure(self.deterministic)
