@@ -140,15 +140,9 @@ SIGS = {
     "pv_amax_quant_fp8_t": "p" "ii" "ppp" "i" "p",
     "pv_bag_counts8": "p" "p" "i" "p" "i" "p" "iiii" "p",
     # bag_gemm.hip (long-bag products with on-the-fly counts)
-    "pv_bag_segments": "i",
-    "pv_bag_set_dbg": "i",
-    "pv_bag_groups": "i",
-    "pv_bag_rle": "pppppppp" "iiii" "p",
     "pv_bagd_fwd": "pipp" "iiii" "p",
     "pv_bagd_splits": "iiiii",
     "pv_bagd_wgrad": "pippp" "ii" "iii" "p",
-    "pv_bag_mm_fwd": "pppp" "iii" "i" "p",
-    "pv_bag_mm_wgrad": "pppp" "ii" "iii" "p",
 }
 
 _RESTYPE = {"pv_rsort_temp_bytes": ctypes.c_long, "pv_ib_fwd_dq_parts": ctypes.c_long, "pv_ib_bwd_ws": ctypes.c_long, "pv_ib_fwd_ws": ctypes.c_long,

@@ -90,18 +90,16 @@ def _counts_gemm(C: torch.Tensor, W16: torch.Tensor, lens: Optional[torch.Tensor
     return dops._torch_act(out, act)
 
 
-# Long bags (the counts plan): "lib" = the dense N x V bf16 count matrix (one LDS-histogram
-# kernel) + hipBLASLt GEMMs; "hip" = csrc/kernels/bag_gemm.hip — atom-major count lists and
-# in-tree MFMA products that build each count tile in LDS (no N x V matrix).  Measured at the
-# MLP shape (tools/bag_gemm_micro.py, profiles/r5_bag/README.md): forward 134 vs 145 us, weight
-# gradient 243 vs 136 us, list build 300 vs 45 us (counts) — the library plan stays the default.
-# "dense" (round 6) = the same dense bf16 count matrix as "lib", multiplied on in-tree MFMA
-# kernels that stream both operands by LDS-DMA (bag_gemm.hip bagd_mm_kernel): forward C W and
-# weight gradient (Gt C)^T with no library GEMM.  Measured (profiles/r6/bagd/): the eager MLP
-# step 1.485 -> 1.356 and 1.294 -> 1.207 ms (same process, two boxes: the library calls' host
-# cost sits on the step), but inside a captured graph the library GEMMs are faster (kernel time
-# 160 + 129 vs 172 + 152 us; bench 1.033-1.050 vs 1.063-1.072 ms alternated on one box).
-# "auto" (default): dense for eager steps, lib inside a hipGraph capture.
+# Long bags (the counts plan): the dense N x V bf16 count matrix (one LDS-histogram kernel)
+# times W.  "lib" = hipBLASLt GEMMs; "dense" (round 6) = in-tree MFMA kernels that stream both
+# operands by LDS-DMA (bag_gemm.hip bagd_mm_kernel): forward C W and weight gradient (Gt C)^T.
+# Measured (profiles/r6/bagd/): the eager MLP step 1.485 -> 1.356 and 1.294 -> 1.207 ms (same
+# process, two boxes: the library calls' host cost sits on the step), but inside a captured graph
+# the library kernels are faster (160 + 129 vs 172 + 152 us; bench 1.033-1.050 vs 1.063-1.072
+# ms alternated on one box).  "auto" (default): dense for eager steps, lib inside a graph.  (The
+# round-5 segment-list arm — count tiles built in LDS from per-atom lists — lost to both on the
+# list build, 300 vs 45-58 us, and its weight gradient, 243 us, and was removed in round 6:
+# profiles/r5_bag/.)
 BAG_GEMM = os.environ.get("PAGEVEC_BAG_GEMM", "auto")
 
 
@@ -125,10 +123,6 @@ def _bag_gemm() -> str:
     if _BAG_SCOPE[0] is not None:
         return _BAG_SCOPE[0]
     return "lib" if torch.cuda.is_current_stream_capturing() else "dense"
-
-
-def _rle_ok(N: int, L: int, V: int, E: int) -> bool:
-    return BAG_GEMM == "hip" and L <= 8192 and E % 8 == 0 and V <= 65536
 
 
 def _dense_ok(C: torch.Tensor, W16: torch.Tensor, V: int, E: int) -> bool:
@@ -158,46 +152,6 @@ def _dense_weight_grad(C: torch.Tensor, gs: torch.Tensor, V: int, out: torch.Ten
     ws = torch.empty(E, Np, dtype=torch.bfloat16, device=C.device)
     check(lib().pv_bagd_wgrad(P(C), ldc, P(gs.contiguous()), P(ws), P(out), int(out.stride(0)), 0, N, V, E,
                               stream(C.device)), "pv_bagd_wgrad")
-
-
-class _Rle:
-    """Atom-major count lists of a batch of bags (bag_gemm.hip): an atom is the block of 64
-    pages x 64 vocabulary ids; its non-zero counts are contiguous u32 entries
-    bf16(count) << 16 | page-in-group << 6 | (id & 63), atoms ordered segment-major
-    (ao[s * Q + q] .. ao[s * Q + q + 1]); non-pad lengths per bag."""
-
-    def __init__(self, ids: torch.Tensor, V: int, pad: int):
-        N, L = ids.shape
-        S = int(lib().pv_bag_segments(V))
-        Q = int(lib().pv_bag_groups(N))
-        dev = ids.device
-        self.N, self.L, self.V = N, L, V
-        self.ent = torch.empty(N * L, dtype=torch.int32, device=dev)
-        self.ao = torch.empty(S * Q + 1, dtype=torch.int32, device=dev)
-        self.lens = torch.empty(N, dtype=torch.float32, device=dev)
-        dist = torch.empty(N * L, dtype=torch.int32, device=dev)
-        cseg = torch.empty(N * S, dtype=torch.uint8, device=dev)
-        within = torch.empty(N * S, dtype=torch.int16, device=dev)
-        tot = torch.empty(S * Q, dtype=torch.int32, device=dev)
-        check(lib().pv_bag_rle(P(ids), P(self.ent), P(self.ao), P(dist), P(cseg), P(within), P(tot), P(self.lens),
-                               N, L, V, pad, stream(dev)), "pv_bag_rle")
-
-    def forward_partials(self, W16: torch.Tensor) -> torch.Tensor:
-        """(splits, N, E) fp32 partial products C[:, split] @ W16[split] (a ~256-workgroup grid)."""
-        N, E = self.N, W16.shape[1]
-        tiles = -(-N // 256) * -(-E // 128)
-        S = int(lib().pv_bag_segments(self.V))
-        splits = max(1, min(S, round(256 / tiles)))
-        part = torch.empty(splits, N, E, dtype=torch.float32, device=W16.device)
-        check(lib().pv_bag_mm_fwd(P(self.ent), P(self.ao), P(W16), P(part), N, self.V, E, splits,
-                                  stream(W16.device)), "pv_bag_mm_fwd")
-        return part
-
-    def weight_grad(self, gs: torch.Tensor, out: torch.Tensor, accumulate: bool) -> None:
-        """out (V, E) fp32 (row stride out.stride(0)) = (or +=) C^T gs, gs (N, E) bf16."""
-        E = gs.shape[1]
-        check(lib().pv_bag_mm_wgrad(P(self.ent), P(self.ao), P(gs), P(out), int(out.stride(0)), int(accumulate),
-                                    self.N, self.V, E, stream(gs.device)), "pv_bag_mm_wgrad")
 
 
 SPARSE_BWD = os.environ.get("PAGEVEC_BAG_SPARSE_BWD", "1") != "0"
@@ -232,7 +186,6 @@ class _BagFn(torch.autograd.Function):
         ctx.mean = bool(mean)
         bf = bias.float().contiguous() if bias is not None else None
         C = None
-        rle = None
         if plan == "gather":
             # short bags: row gather forward; the backward is sparse (sort the (token, slot)
             # entries, sum each token's run of dY rows) -- no N x V counts matrix at all
@@ -254,12 +207,9 @@ class _BagFn(torch.autograd.Function):
             W8t, amax = w8
             want = ctx.needs_input_grad[1]
             fp8_bwd = want and FP8_BWD and E % 4 == 0
-            use_rle = want and not fp8_bwd and _rle_ok(N, L, V, E)
-            C8, C, lens = _counts8(ids, V, pad, want and not use_rle and not fp8_bwd)
+            C8, C, lens = _counts8(ids, V, pad, want and not fp8_bwd)
             if C is not None and not fp8_bwd and _bag_gemm() == "dense" and E % 8 == 0 and C.shape[1] % 64 == 0:
                 ctx.dense = True  # the bf16 weight gradient C^T G on bagd_mm_kernel
-            if use_rle:  # the weight gradient's counts as segment lists (bag_gemm.hip), not bf16 C
-                rle = _Rle(ids, V, pad)
             if fp8_bwd:  # the e4m3 counts serve the weight gradient too (no bf16 N x V matrix)
                 C = C8
                 ctx.fp8_bwd = True
@@ -267,14 +217,6 @@ class _BagFn(torch.autograd.Function):
             if part.dim() == 2:
                 part = part.unsqueeze(0)
             out = dops.colsum(part, scale=lens if mean else None, bias=bf, act=act, scale_is_len=True)
-            keys = None
-        elif _rle_ok(N, L, V, E):
-            # segment lists + in-tree MFMA product, split-K partials summed by the column-sum
-            # kernel with the bag mean / bias / activation (no N x V matrix anywhere)
-            rle = _Rle(ids, V, pad)
-            lens = rle.lens
-            out = dops.colsum(rle.forward_partials(W16), scale=lens if mean else None, bias=bf, act=act,
-                              scale_is_len=True)
             keys = None
         else:
             C, lens = _counts(ids, V, pad)
@@ -285,8 +227,7 @@ class _BagFn(torch.autograd.Function):
             else:
                 out = _counts_gemm(C[:, :V], W16, lens if mean else None, bf, act)
             keys = None
-        ctx.rle = rle
-        ctx.sparse = (L, E) if C is None and rle is None else None
+        ctx.sparse = (L, E) if C is None else None
         ctx.save_for_backward(keys if C is None else C, lens, out if act != "none" else None)
         return out
 
@@ -296,7 +237,7 @@ class _BagFn(torch.autograd.Function):
         first, lens, y = ctx.saved_tensors
         g = g.contiguous().float()
         if ctx.sparse is None and ctx.needs_input_grad[1]:
-            return _counts_backward(ctx, g, first, lens, y, ctx.rle)
+            return _counts_backward(ctx, g, first, lens, y)
         if y is not None:  # activation mask: dpre = dy * act'(y)
             dz = torch.empty_like(g)
             check(lib().pv_act_bwd(P(y), P(g), P(dz), g.numel(), _BAG_ACT[ctx.act], stream(g.device)), "pv_act_bwd")
@@ -342,7 +283,7 @@ class _BagFn(torch.autograd.Function):
         return None, (Ct @ gs).float(), None, None, None, None, db, None, None
 
 
-def _counts_backward(ctx, g, C, lens, y, rle=None):
+def _counts_backward(ctx, g, C, lens, y):
     """Backward of the counts-GEMM bag (long bags): ONE prologue kernel computes the
     activation mask, the fp32 dz for the bias column sum and bf16(dz / len) for the C^T G
     weight-gradient GEMM (was act_bwd + clamp + reciprocal + mul + cast)."""
@@ -371,15 +312,6 @@ def _counts_backward(ctx, g, C, lens, y, rle=None):
         if tw is not None:
             grad_sink.done(W)
             dW = None
-        return None, dW, None, None, None, None, db, None, None
-    if rle is not None:  # bag_gemm.hip weight gradient: count tiles built in LDS, dW rows stored
-        tw = grad_sink.write_target(W)
-        if tw is not None:
-            rle.weight_grad(gs, tw, accumulate=False)
-            grad_sink.done(W)
-            return None, None, None, None, None, None, db, None, None
-        dW = torch.empty(V, E, dtype=torch.float32, device=g.device)
-        rle.weight_grad(gs, dW, accumulate=False)
         return None, dW, None, None, None, None, db, None, None
     if getattr(ctx, "dense", False):  # bag_gemm.hip bagd_mm_kernel: (Gt C)^T stored as dW rows
         tw = grad_sink.write_target(W)

@@ -42,9 +42,8 @@ KNOBS: Dict[str, tuple] = {
     "PAGEVEC_WGRAD_WG": ("ab", "512", "dense-layer weight-gradient workgroup target"),
     "PAGEVEC_QUERY_STREAM": ("ab", "1", "query tower on its own stream beside the page tower"),
     "PAGEVEC_BAG_COUNTS16": ("ab", "1", "16-bit packed LDS counts histogram"),
-    "PAGEVEC_BAG_GEMM": ("ab", "auto", "long-bag GEMMs on the count matrix: in-tree bagd_mm_kernel (dense), "
-                                         "hipBLASLt (lib), segment lists + bag_mm_kernel (hip); auto = dense "
-                                         "eager, lib inside a graph capture"),
+    "PAGEVEC_BAG_GEMM": ("ab", "auto", "long-bag GEMMs on the count matrix: in-tree bagd_mm_kernel (dense) or "
+                                         "hipBLASLt (lib); auto = dense eager, lib inside a graph capture"),
     "PAGEVEC_FP8_BAG": ("ab", "1", "fp8 towers: page bag on the MX fp8 MFMA"),
     "PAGEVEC_FP8_BWD": ("ab", "0", "fp8 towers: bag weight gradient on the MX fp8 MFMA (e4m3 counts^T x e4m3 G)"),
     "PAGEVEC_DENSE_BWD": ("ab", "hip", "dense-layer backward on HIP kernels or the library"),

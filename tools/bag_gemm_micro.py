@@ -1,12 +1,12 @@
-"""Long-bag products of the MLP / chunked towers: in-tree bag_gemm.hip (segment lists +
-on-the-fly-count MFMA products) against the library plan (dense bf16 count matrix + hipBLASLt),
-on synthetic Zipf pages of the bench distribution.  CUDA-event timed, same process.
+"""Long-bag products of the MLP / chunked towers on the dense bf16 count matrix: in-tree
+bag_gemm.hip (bagd_mm_kernel) against hipBLASLt, on synthetic Zipf pages of the bench
+distribution.  CUDA-event timed, same process.
 
     python tools/bag_gemm_micro.py [--N 4096] [--L 2000] [--V 30000] [--E 512]
 
-Reported per call (ms): rle (segment lists), hip_fwd (partials), hip_wgrad, lib_counts (dense
-count matrix), lib_fwd (split-K bmm), lib_wgrad (C^T G), dense_fwd / dense_wgrad (the same count
-matrix on bagd_mm_kernel, PAGEVEC_BAG_GEMM=dense); plus max relative differences.
+Reported per call (ms): lib_counts (dense count matrix), lib_fwd (split-K bmm), lib_wgrad
+(C^T G), dense_fwd / dense_wgrad (the same count matrix on bagd_mm_kernel,
+PAGEVEC_BAG_GEMM=dense); plus max relative differences.
 """
 import argparse
 import json
@@ -48,12 +48,6 @@ def main():
     W16 = torch.randn(a.V, a.E, device=dev).bfloat16()
     G16 = torch.randn(a.N, a.E, device=dev).bfloat16()
     r = {"shape": [a.N, a.L, a.V, a.E]}
-    rle = eops._Rle(ids, a.V, 0)
-    r["rle"] = ev(lambda: eops._Rle(ids, a.V, 0))
-    part = rle.forward_partials(W16)
-    r["hip_fwd"] = ev(lambda: rle.forward_partials(W16))
-    dW = torch.empty(a.V, a.E, device=dev)
-    r["hip_wgrad"] = ev(lambda: rle.weight_grad(G16, dW, False))
     C, lens = eops._counts(ids, a.V, 0)
     r["lib_counts"] = ev(lambda: eops._counts(ids, a.V, 0))
     ref = eops._counts_gemm(C[:, :a.V], W16)
@@ -61,7 +55,6 @@ def main():
     Ct = C[:, :a.V].t()
     out = torch.empty(a.V, a.E, device=dev)
     r["lib_wgrad"] = ev(lambda: torch.mm(Ct, G16, out_dtype=torch.float32, out=out))
-    r["fwd_rel_diff"] = float((part.sum(0) - ref).abs().max() / ref.abs().max())
     # the dense-count in-tree arm (PAGEVEC_BAG_GEMM=dense): same count matrix, bagd_mm_kernel
     from dnn_page_vectors_amd.ops import dense as dops
     dref = dops.colsum(eops._dense_forward_partials(C, W16, a.V))
@@ -69,19 +62,10 @@ def main():
     out2 = torch.empty(a.V, a.E, device=dev)
     r["dense_wgrad"] = ev(lambda: eops._dense_weight_grad(C, G16, a.V, out2))
     r["dense_fwd_rel_diff"] = float((dref - ref).abs().max() / ref.abs().max())
-    from dnn_page_vectors_amd.ops._common import lib
-    if os.environ.get("BAG_MICRO_DBG") == "1":  # round-5 timing ablations (bag_gemm.hip DBG bits;
-        # wrong results by design — a round-6 run of them faulted, so they are opt-in)
-        for d in (1, 2, 3, 4, 8, 12, 15):
-            lib().pv_bag_set_dbg(d)
-            r[f"fwd_dbg{d}"] = ev(lambda: rle.forward_partials(W16))
-        lib().pv_bag_set_dbg(0)
-    r["wgrad_rel_diff"] = float((dW - out).abs().max() / out.abs().max())
     r["dense_wgrad_rel_diff"] = float((out2 - out).abs().max() / out.abs().max())
     flops = 2.0 * a.N * a.V * a.E
-    r["hip_fwd_tflops"] = round(flops / r["hip_fwd"] / 1e9, 1)
-    r["hip_wgrad_tflops"] = round(flops / r["hip_wgrad"] / 1e9, 1)
-    r["nnz_per_page"] = float(rle.ao[-1]) / a.N
+    r["dense_fwd_tflops"] = round(flops / r["dense_fwd"] / 1e9, 1)
+    r["dense_wgrad_tflops"] = round(flops / r["dense_wgrad"] / 1e9, 1)
     print(json.dumps(r), flush=True)
 
 
