@@ -25,11 +25,15 @@ def main():
     ap.add_argument("--pages", type=int, default=65536)
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"], help="override the preset's dtype "
+                    "(reference_char is fp32: the fp32-MFMA conv kernels)")
     a = ap.parse_args()
     preset = {"cdssm": "cdssm_ngram_bf16", "mlp": "mlp_xgpu", "bert": "bert_dp8", "cdssm_char": "reference_char"}[a.model]
     cfg = preset_config(preset)
     if a.model == "cdssm_char":
         cfg = cfg.replace(vocab_hash_size=100)
+    if a.dtype:
+        cfg = cfg.replace(dtype=a.dtype)
     if a.model == "bert":
         a.pages, a.batch = min(a.pages, 4096), min(a.batch, 1024)
     dev = torch.device("cuda")
@@ -45,7 +49,7 @@ def main():
         out = model.encode(ids, "doc", batch_size=a.batch)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
-    print(json.dumps({"model": a.model, "pages": int(ids.shape[0]), "page_len": int(ids.shape[1]),
+    print(json.dumps({"model": a.model, "dtype": cfg.dtype, "pages": int(ids.shape[0]), "page_len": int(ids.shape[1]),
                       "dim": int(out.shape[1]), "batch": a.batch, "ms": round(1e3 * dt, 3),
                       "pages_per_s": round(ids.shape[0] / dt, 1),
                       "tokens_per_s": round(ids.numel() / dt), "norm_check": round(float(out[0].norm()), 4)}),
