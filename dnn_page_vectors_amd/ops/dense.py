@@ -222,6 +222,8 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = Fa
     sam, sak = (1, M) if a_t else (K, 1)
     sbk, sbn = (1, K) if b_t else (N, 1)
     bb = bias.contiguous().float() if bias is not None else None
+    if splits > 1 and (bias is not None or act != "none" or accumulate):
+        raise ValueError("gemm_f32: split-K partials take no epilogue")
     if splits > 1:
         kper = -(-(-(-K // splits)) // 16) * 16
         ns = -(-K // kper)
@@ -229,8 +231,6 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = Fa
         check(lib().pv_gemm_f32(P(a), sam, sak, P(b), sbk, sbn, None, P(ws), N, M, N, K, ns, 0, 0, stream(a.device)),
               "pv_gemm_f32")
         if ns > 1:
-            if bias is not None or act != "none" or accumulate:
-                raise ValueError("gemm_f32: split-K partials take no epilogue")
             return colsum(ws, out=out)
         part = ws[0]
         return part if out is None else out.copy_(part)
